@@ -1,0 +1,181 @@
+// Python bindings of the pgdist native library (_pgdist_C).
+//
+// Deliberately torch-header-free: every device buffer crosses the boundary as a
+// raw address (tensor.data_ptr()) and the HIP stream as its handle
+// (torch.cuda.current_stream().cuda_stream).  Shape/dtype validation lives in
+// the typed Python wrappers (pgdist/ops/kernels.py) that call these entry points,
+// so this translation unit compiles in seconds and has no ABI coupling to a
+// particular PyTorch build.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/numpy.h>
+
+#include <cstdint>
+#include <string>
+
+#include "runtime/runtime.h"
+
+namespace py = pybind11;
+typedef unsigned short bf16_t;
+typedef uintptr_t P;
+
+// ---- kernel launchers (defined in kernels/*.hip) ----
+void launch_bn_fwd_finalize(const float *, int, int, float, const float *, const float *, float,
+                            float, float *, float *, long long *, float *, float *, float *, float *,
+                            hipStream_t);
+void launch_bn_bwd_finalize(const float *, int, int, float, const float *, const float *,
+                            const float *, float *, float *, float *, hipStream_t);
+void launch_bn_apply(const bf16_t *, const bf16_t *, const float *, const float *, bf16_t *,
+                     long long, int, bool, hipStream_t);
+void launch_adam_flat(float *, const float *, float *, float *, bf16_t *, long long, const float *,
+                      float, float, float, float, float, hipStream_t);
+void launch_f32_to_bf16(const float *, bf16_t *, long long, hipStream_t);
+int dw_fwd_num_partials(int, int, int, int, int);
+int dw_dgrad_num_partials(int, int, int, int, int);
+int dw_wgrad_num_partials(int, int, int, int, int);
+void launch_dw_fwd(const bf16_t *, const float *, const float *, int, const bf16_t *, bf16_t *,
+                   float *, int, int, int, int, int, hipStream_t);
+void launch_dw_dgrad(const bf16_t *, const bf16_t *, const float *, const bf16_t *, const bf16_t *,
+                     const float *, const float *, bf16_t *, float *, int, int, int, int, int,
+                     hipStream_t);
+void launch_dw_wgrad(const bf16_t *, const bf16_t *, const float *, const bf16_t *, const float *,
+                     const float *, float *, float *, int, int, int, int, int, hipStream_t);
+int pw_gemm_num_partials(int, int);
+void launch_pw_gemm(int, int, const bf16_t *, const bf16_t *, const float *, const float *,
+                    const float *, const bf16_t *, bf16_t *, const bf16_t *, const float *,
+                    const float *, const bf16_t *, float *, int, int, int, hipStream_t);
+long long pw_wgrad_workspace_floats(int, int, int);
+void launch_pw_wgrad(const bf16_t *, const bf16_t *, const float *, const float *, const float *,
+                     const bf16_t *, const float *, const float *, int, float *, float *, int, int,
+                     int, hipStream_t);
+long long stem_wgrad_workspace_floats(int, int);
+void launch_stem_wgrad(const bf16_t *, const bf16_t *, const float *, const float *, const float *,
+                       const bf16_t *, float *, float *, int, int, int, int, hipStream_t);
+int stem_fwd_num_partials(int, int, int);
+void launch_stem_fwd(const bf16_t *, const bf16_t *, bf16_t *, float *, int, int, int, hipStream_t);
+void launch_head(const bf16_t *, const float *, const float *, const float *, const float *,
+                 const long long *, int, int, int, int, float, unsigned long long, const float *,
+                 int, float, float *, float *, float *, float *, float *, bf16_t *, float *, float *,
+                 float *, hipStream_t);
+void launch_augment(const unsigned char *, const long long *, const long long *, int, int, int,
+                    int, int, const float *, unsigned long long, const float *, int, bf16_t *,
+                    long long *, float *, hipStream_t);
+void launch_step_begin(float *, hipStream_t);
+void launch_reduce_metrics(const float *, const float *, int, double *, hipStream_t);
+
+template <typename T>
+static T *ptr(P p) { return reinterpret_cast<T *>(p); }
+static hipStream_t S(P s) { return reinterpret_cast<hipStream_t>(s); }
+
+static std::string last_error() {
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? std::string() : std::string(hipGetErrorString(e));
+}
+
+PYBIND11_MODULE(_pgdist_C, m) {
+  m.doc() = "pgdist native library: gfx950 HIP kernels + C++ runtime";
+  m.attr("arch") = "gfx950";
+  m.def("last_error", &last_error);
+
+  // ---- BatchNorm ----
+  m.def("bn_fwd_finalize", [](P part, int Pn, int C, float count, P gamma, P beta, float eps,
+                              float mom, P rm, P rv, P nbt, P mean, P rstd, P scale, P shift, P s) {
+    launch_bn_fwd_finalize(ptr<float>(part), Pn, C, count, ptr<float>(gamma), ptr<float>(beta), eps,
+                           mom, ptr<float>(rm), ptr<float>(rv), ptr<long long>(nbt), ptr<float>(mean),
+                           ptr<float>(rstd), ptr<float>(scale), ptr<float>(shift), S(s));
+  });
+  m.def("bn_bwd_finalize", [](P part, int Pn, int C, float count, P mean, P rstd, P gamma, P coef,
+                              P dgamma, P dbeta, P s) {
+    launch_bn_bwd_finalize(ptr<float>(part), Pn, C, count, ptr<float>(mean), ptr<float>(rstd),
+                           ptr<float>(gamma), ptr<float>(coef), ptr<float>(dgamma), ptr<float>(dbeta),
+                           S(s));
+  });
+  m.def("bn_apply", [](P y, P res, P scale, P shift, P out, long long M, int C, bool relu6, P s) {
+    launch_bn_apply(ptr<bf16_t>(y), ptr<bf16_t>(res), ptr<float>(scale), ptr<float>(shift),
+                    ptr<bf16_t>(out), M, C, relu6, S(s));
+  });
+  // ---- optimizer ----
+  m.def("adam_flat", [](P p, P g, P mm, P v, P pb, long long n, P hyper, float b1, float b2,
+                        float eps, float wd, float gscale, P s) {
+    launch_adam_flat(ptr<float>(p), ptr<float>(g), ptr<float>(mm), ptr<float>(v), ptr<bf16_t>(pb),
+                     n, ptr<float>(hyper), b1, b2, eps, wd, gscale, S(s));
+  });
+  m.def("f32_to_bf16", [](P x, P y, long long n, P s) {
+    launch_f32_to_bf16(ptr<float>(x), ptr<bf16_t>(y), n, S(s));
+  });
+  m.def("step_begin", [](P hyper, P s) { launch_step_begin(ptr<float>(hyper), S(s)); });
+  m.def("reduce_metrics", [](P loss, P correct, int B, P acc, P s) {
+    launch_reduce_metrics(ptr<float>(loss), ptr<float>(correct), B, ptr<double>(acc), S(s));
+  });
+  // ---- depthwise ----
+  m.def("dw_fwd_num_partials", &dw_fwd_num_partials);
+  m.def("dw_dgrad_num_partials", &dw_dgrad_num_partials);
+  m.def("dw_wgrad_num_partials", &dw_wgrad_num_partials);
+  m.def("dw_fwd", [](P x, P is, P it, int act, P w, P y, P part, int B, int H, int W, int C,
+                     int stride, P s) {
+    launch_dw_fwd(ptr<bf16_t>(x), ptr<float>(is), ptr<float>(it), act, ptr<bf16_t>(w), ptr<bf16_t>(y),
+                  ptr<float>(part), B, H, W, C, stride, S(s));
+  });
+  m.def("dw_dgrad", [](P g, P ys, P coef, P w, P yp, P ps, P pt, P gout, P part, int B, int H,
+                       int W, int C, int stride, P s) {
+    launch_dw_dgrad(ptr<bf16_t>(g), ptr<bf16_t>(ys), ptr<float>(coef), ptr<bf16_t>(w),
+                    ptr<bf16_t>(yp), ptr<float>(ps), ptr<float>(pt), ptr<bf16_t>(gout),
+                    ptr<float>(part), B, H, W, C, stride, S(s));
+  });
+  m.def("dw_wgrad", [](P g, P ys, P coef, P yp, P ps, P pt, P part, P grad, int B, int H, int W,
+                       int C, int stride, P s) {
+    launch_dw_wgrad(ptr<bf16_t>(g), ptr<bf16_t>(ys), ptr<float>(coef), ptr<bf16_t>(yp),
+                    ptr<float>(ps), ptr<float>(pt), ptr<float>(part), ptr<float>(grad), B, H, W, C,
+                    stride, S(s));
+  });
+  // ---- pointwise ----
+  m.def("pw_gemm_num_partials", &pw_gemm_num_partials);
+  m.def("pw_gemm", [](int pro, int epi, P A, P A2, P pa, P pb, P pc, P W, P out, P Yt, P es, P et,
+                      P R, P part, int M, int N, int K, P s) {
+    launch_pw_gemm(pro, epi, ptr<bf16_t>(A), ptr<bf16_t>(A2), ptr<float>(pa), ptr<float>(pb),
+                   ptr<float>(pc), ptr<bf16_t>(W), ptr<bf16_t>(out), ptr<bf16_t>(Yt), ptr<float>(es),
+                   ptr<float>(et), ptr<bf16_t>(R), ptr<float>(part), M, N, K, S(s));
+  });
+  m.def("pw_wgrad_workspace_floats", &pw_wgrad_workspace_floats);
+  m.def("pw_wgrad", [](P G, P Y, P ga, P gb, P gc, P X, P xs, P xt, int xact, P part, P grad, int M,
+                       int N, int K, P s) {
+    launch_pw_wgrad(ptr<bf16_t>(G), ptr<bf16_t>(Y), ptr<float>(ga), ptr<float>(gb), ptr<float>(gc),
+                    ptr<bf16_t>(X), ptr<float>(xs), ptr<float>(xt), xact, ptr<float>(part),
+                    ptr<float>(grad), M, N, K, S(s));
+  });
+  // ---- stem ----
+  m.def("stem_fwd_num_partials", &stem_fwd_num_partials);
+  m.def("stem_fwd", [](P img, P w, P y, P part, int B, int H, int W, P s) {
+    launch_stem_fwd(ptr<bf16_t>(img), ptr<bf16_t>(w), ptr<bf16_t>(y), ptr<float>(part), B, H, W, S(s));
+  });
+  m.def("stem_wgrad_workspace_floats", &stem_wgrad_workspace_floats);
+  m.def("stem_wgrad", [](P G, P Y, P ga, P gb, P gc, P img, P part, P grad, int B, int H, int W,
+                         int O, P s) {
+    launch_stem_wgrad(ptr<bf16_t>(G), ptr<bf16_t>(Y), ptr<float>(ga), ptr<float>(gb), ptr<float>(gc),
+                      ptr<bf16_t>(img), ptr<float>(part), ptr<float>(grad), B, H, W, O, S(s));
+  });
+  // ---- head ----
+  m.def("head", [](P y, P sc, P sh, P Wl, P bl, P labels, int B, int HW, int C, int NC, float p,
+                   unsigned long long seed, P hyper, int train, float loss_scale, P logits, P loss,
+                   P correct, P dlogits, P pd, P g, P part, P dW, P db, P s) {
+    launch_head(ptr<bf16_t>(y), ptr<float>(sc), ptr<float>(sh), ptr<float>(Wl), ptr<float>(bl),
+                ptr<long long>(labels), B, HW, C, NC, p, seed, ptr<float>(hyper), train, loss_scale,
+                ptr<float>(logits), ptr<float>(loss), ptr<float>(correct), ptr<float>(dlogits),
+                ptr<float>(pd), ptr<bf16_t>(g), ptr<float>(part), ptr<float>(dW), ptr<float>(db), S(s));
+  });
+  // ---- data ----
+  m.def("augment", [](P src, P idx, P labels_src, int nsrc, int B, int out_hw, int train,
+                      int double_resize, P params, unsigned long long seed, P hyper, int epoch_ctr,
+                      P out, P labels_out, P params_out, P s) {
+    launch_augment(ptr<unsigned char>(src), ptr<long long>(idx), ptr<long long>(labels_src), nsrc, B,
+                   out_hw, train, double_resize, ptr<float>(params), seed, ptr<float>(hyper),
+                   epoch_ctr, ptr<bf16_t>(out), ptr<long long>(labels_out), ptr<float>(params_out), S(s));
+  });
+
+  // ---- native runtime (host) ----
+  m.def("read_cifar10_bin", &pgdist_rt::read_cifar10_bin, py::arg("paths"), py::arg("num_threads") = 4,
+        "Read CIFAR-10 binary batches -> (uint8 NHWC [N,32,32,3], int64 labels [N])");
+  m.def("shard_indices", &pgdist_rt::shard_indices, py::arg("perm"), py::arg("num_replicas"),
+        py::arg("rank"), py::arg("drop_last") = false,
+        "DistributedSampler index math on a given permutation (pad by wrap-around, stride by rank)");
+}

@@ -1,0 +1,92 @@
+// Shared device helpers for the pgdist gfx950 (MI355X / CDNA4) kernels.
+//
+// Conventions used by every kernel in csrc/kernels:
+//   * activations are NHWC bf16, viewed as row-major [M = N*H*W][C]
+//   * bf16 values travel as raw 16-bit patterns (uint16) in memory and are
+//     converted with the gfx950 v_cvt_pk_bf16_f32 instruction (RNE, NaN-safe)
+//   * all global traffic of streaming kernels is 16 B per lane (8 x bf16)
+//   * wave = 64 lanes; workgroups are multiples of 64 threads
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef unsigned short bf16_t;  // raw bf16 bits
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short s16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+
+#define PG_DEVICE __device__ __forceinline__
+
+PG_DEVICE float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+PG_DEVICE bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
+
+// 8 x bf16 packed in a uint4 (16 bytes)
+struct alignas(16) bf16x8_pack { uint4 v; };
+
+PG_DEVICE void unpack8(const uint4 &u, float (&f)[8]) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+PG_DEVICE uint32_t pack2(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+PG_DEVICE uint4 pack8(const float (&f)[8]) {
+  uint4 u;
+  u.x = pack2(f[0], f[1]);
+  u.y = pack2(f[2], f[3]);
+  u.z = pack2(f[4], f[5]);
+  u.w = pack2(f[6], f[7]);
+  return u;
+}
+
+PG_DEVICE uint4 ldg16(const void *p) { return *reinterpret_cast<const uint4 *>(p); }
+PG_DEVICE void stg16(void *p, const uint4 &v) { *reinterpret_cast<uint4 *>(p) = v; }
+
+PG_DEVICE float relu6f(float x) { return fminf(fmaxf(x, 0.f), 6.f); }
+
+// Wave-level reductions (64 lanes)
+PG_DEVICE float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Counter-based RNG (splitmix64 finaliser) — deterministic per (seed, counter).
+PG_DEVICE uint64_t pg_mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+PG_DEVICE float pg_uniform(uint64_t seed, uint64_t ctr) {  // [0,1)
+  return (float)(pg_mix64(seed ^ pg_mix64(ctr)) >> 40) * (1.0f / 16777216.0f);
+}
+
+// Prologue transform applied to an activation operand when it is read.
+enum ActMode : int {
+  ACT_NONE = 0,      // x as stored (materialised tensor)
+  ACT_BN_RELU6 = 1,  // relu6(x * scale[c] + shift[c])  (BN-apply of the producer, fused)
+  ACT_BN = 2,        // x * scale[c] + shift[c]
+};
+
+template <int MODE>
+PG_DEVICE float act_apply(float x, float s, float t) {
+  if constexpr (MODE == ACT_BN_RELU6) return relu6f(fmaf(x, s, t));
+  else if constexpr (MODE == ACT_BN) return fmaf(x, s, t);
+  else return x;
+}
+
+// relu6 pass-through mask on the pre-clamp value a = y*s+t
+PG_DEVICE float relu6_mask(float y, float s, float t) {
+  float a = fmaf(y, s, t);
+  return (a > 0.f && a < 6.f) ? 1.f : 0.f;
+}
+
+#define PG_CHECK_LAUNCH() ((void)hipGetLastError())

@@ -1,0 +1,297 @@
+// Fused GPU data augmentation: uint8 32x32x3 CIFAR images (device resident)
+// -> normalised 224x224 NHWC bf16 (4th channel zero pad) for the stem.
+//
+// Reference (CPU, PIL, per sample in 2 DataLoader workers — the measured
+// bottleneck of every reference run):
+//   train: Resize((224,224)) -> RandomResizedCrop(224, scale=(0.7,1.0)) ->
+//          RandomHorizontalFlip() -> ColorJitter(0.3,0.3,0.3,0.1) ->
+//          RandomRotation(15) -> ToTensor -> Normalize(ImageNet)
+//          (cifar10_serial_mobilenet_224.py:28-40)
+//   test:  Resize((224,224)) -> ToTensor -> Normalize   (:42-47)
+//
+// Here: kernel 1 (one workgroup per image) draws the per-image parameters
+// from a counter-based RNG keyed by (seed, step, image) with torchvision's
+// sampling rules (RRC 10-try rejection sampling + centre-crop fallback, jitter
+// factor ranges and random op order, rotation angle) and measures the grey
+// mean the contrast op needs; kernel 2 renders every output pixel by inverse
+// mapping: rotation (nearest, fill 0, PIL pixel-centre convention) -> flip ->
+// bilinear crop-resize of the 224 upsample, itself a bilinear sample of the
+// 32x32 source (the reference's double resize, composed exactly) -> jitter in
+// the sampled order -> normalise.  Fidelity target: the torchvision
+// distributions, not PIL's intermediate uint8 rounding.
+#include "../common.h"
+
+namespace {
+constexpr int kNP = 16;  // params per image
+// param slots
+enum { P_I = 0, P_J, P_H, P_W, P_FLIP, P_B, P_C, P_S, P_HUE, P_ORDER, P_ANGLE, P_MEAN, P_SRC_HW };
+constexpr float kMean[3] = {0.485f, 0.456f, 0.406f};
+constexpr float kStd[3] = {0.229f, 0.224f, 0.225f};
+
+struct Rng {
+  uint64_t key;
+  uint64_t ctr;
+  PG_DEVICE float u() { return pg_uniform(key, ctr++); }
+};
+
+PG_DEVICE void rgb_to_hsv(float r, float g, float b, float &h, float &s, float &v) {
+  const float mx = fmaxf(r, fmaxf(g, b)), mn = fminf(r, fminf(g, b));
+  v = mx;
+  const float d = mx - mn;
+  s = mx > 0.f ? d / mx : 0.f;
+  if (d <= 0.f) { h = 0.f; return; }
+  float hh;
+  if (mx == r) hh = (g - b) / d;
+  else if (mx == g) hh = 2.f + (b - r) / d;
+  else hh = 4.f + (r - g) / d;
+  hh = hh / 6.f;
+  h = hh - floorf(hh);
+}
+
+PG_DEVICE void hsv_to_rgb(float h, float s, float v, float &r, float &g, float &b) {
+  const float h6 = h * 6.f;
+  const int i = ((int)floorf(h6)) % 6;
+  const float f = h6 - floorf(h6);
+  const float p = v * (1.f - s), q = v * (1.f - s * f), t = v * (1.f - s * (1.f - f));
+  switch (i) {
+    case 0: r = v; g = t; b = p; break;
+    case 1: r = q; g = v; b = p; break;
+    case 2: r = p; g = v; b = t; break;
+    case 3: r = p; g = q; b = v; break;
+    case 4: r = t; g = p; b = v; break;
+    default: r = v; g = p; b = q; break;
+  }
+}
+
+PG_DEVICE float gray(float r, float g, float b) { return 0.299f * r + 0.587f * g + 0.114f * b; }
+
+// bilinear sample of the 32x32 source at continuous coords (half-pixel convention), clamped
+PG_DEVICE void src_bilinear(const float *img, int sh, int sw, float x, float y, float (&o)[3]) {
+  x = fminf(fmaxf(x, 0.f), (float)(sw - 1));
+  y = fminf(fmaxf(y, 0.f), (float)(sh - 1));
+  const int x0 = (int)x, y0 = (int)y;
+  const int x1 = min(x0 + 1, sw - 1), y1 = min(y0 + 1, sh - 1);
+  const float fx = x - x0, fy = y - y0;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float a = img[(y0 * sw + x0) * 3 + c], b = img[(y0 * sw + x1) * 3 + c];
+    const float d = img[(y1 * sw + x0) * 3 + c], e = img[(y1 * sw + x1) * 3 + c];
+    o[c] = (a + (b - a) * fx) + ((d + (e - d) * fx) - (a + (b - a) * fx)) * fy;
+  }
+}
+
+// value of the (virtual) upsampled image R (RH x RW) at integer pixel (p, q)
+PG_DEVICE void r_pixel(const float *img, int sh, int sw, int RH, int RW, int p, int q,
+                       float (&o)[3]) {
+  const float x = (q + 0.5f) * ((float)sw / RW) - 0.5f;
+  const float y = (p + 0.5f) * ((float)sh / RH) - 0.5f;
+  src_bilinear(img, sh, sw, x, y, o);
+}
+
+// F(u, v): the crop-resized, flipped image at integer output pixel (u = column, v = row)
+PG_DEVICE void f_pixel(const float *img, int sh, int sw, int RH, int RW, const float *prm, int S,
+                       int u, int v, bool dbl, float (&o)[3]) {
+  if (prm[P_FLIP] > 0.5f) u = S - 1 - u;
+  const float ci = prm[P_I], cj = prm[P_J], ch = prm[P_H], cw = prm[P_W];
+  float xr = cj + (u + 0.5f) * (cw / S) - 0.5f;
+  float yr = ci + (v + 0.5f) * (ch / S) - 0.5f;
+  if (!dbl) {  // crop directly on the source
+    src_bilinear(img, sh, sw, xr, yr, o);
+    return;
+  }
+  xr = fminf(fmaxf(xr, 0.f), (float)(RW - 1));
+  yr = fminf(fmaxf(yr, 0.f), (float)(RH - 1));
+  const int x0 = (int)xr, y0 = (int)yr;
+  const int x1 = min(x0 + 1, RW - 1), y1 = min(y0 + 1, RH - 1);
+  const float fx = xr - x0, fy = yr - y0;
+  float a[3], b[3], d[3], e[3];
+  r_pixel(img, sh, sw, RH, RW, y0, x0, a);
+  r_pixel(img, sh, sw, RH, RW, y0, x1, b);
+  r_pixel(img, sh, sw, RH, RW, y1, x0, d);
+  r_pixel(img, sh, sw, RH, RW, y1, x1, e);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float top = a[c] + (b[c] - a[c]) * fx, bot = d[c] + (e[c] - d[c]) * fx;
+    o[c] = top + (bot - top) * fy;
+  }
+}
+
+// apply jitter ops in the sampled order; stop_before_contrast -> return the value
+// just before the contrast op (for the mean); mean used by contrast
+PG_DEVICE void jitter(float (&x)[3], const float *prm, float mean, bool stop_before_contrast) {
+  const int order = (int)prm[P_ORDER];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int op = (order >> (2 * k)) & 3;
+    if (op == 0) {  // brightness
+#pragma unroll
+      for (int c = 0; c < 3; ++c) x[c] = fminf(fmaxf(x[c] * prm[P_B], 0.f), 1.f);
+    } else if (op == 1) {  // contrast
+      if (stop_before_contrast) return;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) x[c] = fminf(fmaxf(mean + prm[P_C] * (x[c] - mean), 0.f), 1.f);
+    } else if (op == 2) {  // saturation
+      const float gy = gray(x[0], x[1], x[2]);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) x[c] = fminf(fmaxf(gy + prm[P_S] * (x[c] - gy), 0.f), 1.f);
+    } else {  // hue
+      float h, s, v;
+      rgb_to_hsv(x[0], x[1], x[2], h, s, v);
+      h = h + prm[P_HUE];
+      h = h - floorf(h);
+      hsv_to_rgb(h, s, v, x[0], x[1], x[2]);
+    }
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// kernel 1: per-image parameters (+ contrast mean), one workgroup per image
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void augment_params_kernel(
+    const unsigned char *__restrict__ src, const long long *__restrict__ idx, int B, int S,
+    int train, int dbl, const float *__restrict__ given, unsigned long long seed,
+    const float *__restrict__ hyper, int epoch_ctr, float *__restrict__ params) {
+  __shared__ float img[32 * 32 * 3];
+  __shared__ float prm[kNP];
+  __shared__ float red[4];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const long long si = idx[b];
+  for (int i = tid; i < 32 * 32 * 3; i += 256) img[i] = src[si * 3072 + i] * (1.f / 255.f);
+  const int RH = dbl ? S : 32, RW = dbl ? S : 32;  // image the crop is taken from
+  if (tid == 0) {
+    float *p = prm;
+    for (int k = 0; k < kNP; ++k) p[k] = 0.f;
+    if (given) {
+      for (int k = 0; k < kNP; ++k) p[k] = given[b * kNP + k];
+    } else if (!train) {
+      p[P_I] = 0; p[P_J] = 0; p[P_H] = (float)RH; p[P_W] = (float)RW;
+      p[P_B] = 1.f; p[P_C] = 1.f; p[P_S] = 1.f; p[P_HUE] = 0.f;
+      p[P_ORDER] = (float)(0 | (1 << 2) | (2 << 4) | (3 << 6));
+    } else {
+      const unsigned long long step = hyper ? (unsigned long long)hyper[1] : 0ull;
+      Rng r{pg_mix64(seed ^ pg_mix64(step * 0x100000001B3ull + (unsigned long long)epoch_ctr)), (unsigned long long)b * 64};
+      // RandomResizedCrop.get_params(scale=(0.7,1), ratio=(3/4,4/3))
+      const float area = (float)(RH * RW);
+      const float lr0 = logf(3.f / 4.f), lr1 = logf(4.f / 3.f);
+      bool found = false;
+      for (int t = 0; t < 10 && !found; ++t) {
+        const float ta = area * (0.7f + 0.3f * r.u());
+        const float ar = expf(lr0 + (lr1 - lr0) * r.u());
+        const int w = (int)rintf(sqrtf(ta * ar)), h = (int)rintf(sqrtf(ta / ar));
+        if (w > 0 && w <= RW && h > 0 && h <= RH) {
+          p[P_I] = (float)min((int)(r.u() * (RH - h + 1)), RH - h);
+          p[P_J] = (float)min((int)(r.u() * (RW - w + 1)), RW - w);
+          p[P_H] = (float)h;
+          p[P_W] = (float)w;
+          found = true;
+        }
+      }
+      if (!found) {
+        p[P_H] = (float)RH; p[P_W] = (float)RW; p[P_I] = 0.f; p[P_J] = 0.f;  // ratio within bounds for square input
+      }
+      p[P_FLIP] = r.u() < 0.5f ? 1.f : 0.f;
+      // ColorJitter.get_params: fn_idx = randperm(4) then factors
+      int perm[4] = {0, 1, 2, 3};
+      for (int k = 3; k > 0; --k) {
+        const int j = min((int)(r.u() * (k + 1)), k);
+        const int tmp = perm[k]; perm[k] = perm[j]; perm[j] = tmp;
+      }
+      p[P_ORDER] = (float)(perm[0] | (perm[1] << 2) | (perm[2] << 4) | (perm[3] << 6));
+      p[P_B] = 0.7f + 0.6f * r.u();
+      p[P_C] = 0.7f + 0.6f * r.u();
+      p[P_S] = 0.7f + 0.6f * r.u();
+      p[P_HUE] = -0.1f + 0.2f * r.u();
+      p[P_ANGLE] = -15.f + 30.f * r.u();
+    }
+  }
+  __syncthreads();
+  // contrast mean: grey mean of the image just before the contrast op, over a
+  // 56x56 sub-grid of the 224x224 frame (stride S/56)
+  float acc = 0.f;
+  const bool need_mean = prm[P_C] != 1.f;
+  if (need_mean) {
+    const int G = 56;
+    for (int i = tid; i < G * G; i += 256) {
+      const int v = (i / G) * S / G + S / (2 * G), u = (i % G) * S / G + S / (2 * G);
+      float x[3];
+      f_pixel(img, 32, 32, RH, RW, prm, S, u, v, dbl != 0, x);
+      jitter(x, prm, 0.f, true);
+      acc += gray(x[0], x[1], x[2]);
+    }
+    acc = wave_sum(acc);
+    if ((tid & 63) == 0) red[tid >> 6] = acc;
+  }
+  __syncthreads();
+  if (tid < kNP) {
+    float val = prm[tid];
+    if (tid == P_MEAN) val = need_mean ? (red[0] + red[1] + red[2] + red[3]) / (56.f * 56.f) : 0.f;
+    if (tid == P_SRC_HW) val = (float)RH;
+    params[b * kNP + tid] = val;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// kernel 2: render.  grid (B, S/rows_per_block); thread = one output pixel.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void augment_render_kernel(
+    const unsigned char *__restrict__ src, const long long *__restrict__ idx,
+    const long long *__restrict__ labels_src, int S, int dbl, const float *__restrict__ params,
+    bf16_t *__restrict__ out, long long *__restrict__ labels_out) {
+  __shared__ float img[32 * 32 * 3];
+  __shared__ float prm[kNP];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const long long si = idx[b];
+  for (int i = tid; i < 32 * 32 * 3; i += 256) img[i] = src[si * 3072 + i] * (1.f / 255.f);
+  if (tid < kNP) prm[tid] = params[b * kNP + tid];
+  if (labels_out && blockIdx.y == 0 && tid == 0) labels_out[b] = labels_src[si];
+  __syncthreads();
+  const int RH = (int)prm[P_SRC_HW], RW = RH;
+  const float ang = prm[P_ANGLE] * 0.017453292519943295f;
+  // PIL Image.rotate(angle): inverse affine with theta = -angle about the centre
+  const float ca = cosf(-ang), sa = sinf(-ang);
+  const float cx = S * 0.5f, cy = S * 0.5f;
+  const int rows_per_block = (256 * 8 + S - 1) / S;  // ~8 pixels per thread
+  const int y0 = blockIdx.y * rows_per_block;
+  const int npx = min(rows_per_block, S - y0) * S;
+  for (int i = tid; i < npx; i += 256) {
+    const int y = y0 + i / S, x = i % S;
+    float rgb[3] = {0.f, 0.f, 0.f};
+    int u = x, v = y;
+    bool inside = true;
+    if (prm[P_ANGLE] != 0.f) {
+      const float dx = x + 0.5f - cx, dy = y + 0.5f - cy;
+      const float xin = ca * dx + sa * dy + cx;
+      const float yin = -sa * dx + ca * dy + cy;
+      u = (int)floorf(xin);
+      v = (int)floorf(yin);
+      inside = u >= 0 && u < S && v >= 0 && v < S;
+    }
+    if (inside) {
+      f_pixel(img, 32, 32, RH, RW, prm, S, u, v, dbl != 0, rgb);
+      jitter(rgb, prm, prm[P_MEAN], false);
+    }
+    float o[4];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) o[c] = (rgb[c] - kMean[c]) / kStd[c];
+    o[3] = 0.f;
+    uint2 w;
+    w.x = pack2(o[0], o[1]);
+    w.y = pack2(o[2], o[3]);
+    *reinterpret_cast<uint2 *>(out + (((size_t)b * S + y) * S + x) * 4) = w;
+  }
+}
+
+void launch_augment(const unsigned char *src, const long long *idx, const long long *labels_src,
+                    int nsrc, int B, int S, int train, int dbl, const float *given,
+                    unsigned long long seed, const float *hyper, int epoch_ctr, bf16_t *out,
+                    long long *labels_out, float *params, hipStream_t st) {
+  (void)nsrc;
+  hipLaunchKernelGGL(augment_params_kernel, dim3(B), dim3(256), 0, st, src, idx, B, S, train, dbl,
+                     given, seed, hyper, epoch_ctr, params);
+  const int rows_per_block = (256 * 8 + S - 1) / S;
+  dim3 grid(B, (S + rows_per_block - 1) / rows_per_block);
+  hipLaunchKernelGGL(augment_render_kernel, grid, dim3(256), 0, st, src, idx, labels_src, S, dbl,
+                     params, out, labels_out);
+}

@@ -1,0 +1,48 @@
+// Small step-bookkeeping kernels kept on the device so a whole training step
+// (and its metrics) can be captured in one hipGraph and replayed without any
+// host synchronisation.  The reference pays two .item() device->host syncs per
+// batch for its running loss/accuracy (cifar10_mpi_mobilenet_224.py:182-185);
+// here the per-image loss/correct vectors written by the head kernel are
+// folded into fp64 device accumulators and read once per epoch.
+#include "../common.h"
+
+// hyper[1] = optimizer step / RNG step counter
+__global__ void step_begin_kernel(float *hyper) {
+  if (threadIdx.x == 0) hyper[1] += 1.f;
+}
+
+// acc[0] += sum loss, acc[1] += sum correct, acc[2] += B
+__global__ __launch_bounds__(256) void reduce_metrics_kernel(const float *__restrict__ loss,
+                                                            const float *__restrict__ correct, int B,
+                                                            double *__restrict__ acc) {
+  __shared__ double sh[2][256];
+  double l = 0.0, c = 0.0;
+  for (int i = threadIdx.x; i < B; i += 256) {
+    l += loss[i];
+    c += correct[i];
+  }
+  sh[0][threadIdx.x] = l;
+  sh[1][threadIdx.x] = c;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      sh[0][threadIdx.x] += sh[0][threadIdx.x + s];
+      sh[1][threadIdx.x] += sh[1][threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    acc[0] += sh[0][0];
+    acc[1] += sh[1][0];
+    acc[2] += (double)B;
+  }
+}
+
+void launch_step_begin(float *hyper, hipStream_t st) {
+  hipLaunchKernelGGL(step_begin_kernel, dim3(1), dim3(64), 0, st, hyper);
+}
+
+void launch_reduce_metrics(const float *loss, const float *correct, int B, double *acc,
+                           hipStream_t st) {
+  hipLaunchKernelGGL(reduce_metrics_kernel, dim3(1), dim3(256), 0, st, loss, correct, B, acc);
+}

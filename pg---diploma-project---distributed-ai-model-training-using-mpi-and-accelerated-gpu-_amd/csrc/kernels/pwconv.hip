@@ -1,0 +1,553 @@
+// Pointwise (1x1) convolution as an MFMA bf16 GEMM with fused BatchNorm
+// prologue/epilogue, NHWC:  C[M][N] = act(A)[M][K] . W[N][K]^T,  M = B*H*W.
+//
+// Reference ops: the 16 expand + 17 project + final 1x1 convs of MobileNetV2
+// (shapes M in {6,272 .. 1,605,632}, K,N in {16 .. 1280}).
+// These shapes are memory-bound on MI355X (K and N are tiny next to M), so the
+// kernel is organised as a row stream:
+//
+//  * 256-thread workgroup = 4 waves x 32 rows = 128-row M tile, N tile BN in
+//    {32,64,128}; each wave owns 2 x (BN/16) v_mfma_f32_16x16x32_bf16 tiles;
+//  * the A fragment (lane: row l&15, k = 8*(l>>4)..+7) is one 16-B global load
+//    per lane, transformed in registers by the fused prologue:
+//      ACT_NONE      A as stored (materialised block output)
+//      ACT_BN_RELU6  relu6(A*s[k]+t[k])      -- producer BN + ReLU6 (forward)
+//      PRO_BNBWD     a[k]*G + b[k]*Y + c[k]   -- this layer's BN backward (dgrad;
+//                    the weight is then read as [K][N] and transposed while staged)
+//  * the weight tile [BN][K-chunk] is staged once per workgroup in LDS (padded
+//    rows -> conflict-free ds_read_b128) and reused across the workgroup's
+//    M tiles (grid-stride over M with gridDim.x a multiple of 8, so the N
+//    tiles of one M tile share an XCD L2);
+//  * the epilogue goes through an LDS tile so every global load/store is a
+//    coalesced 16-B row chunk:
+//      EPI_FWD       store y, partial (sum y, sum y^2) for this layer's BN
+//      EPI_BWD_RELU6 g = c * 1[0 < yt*s+t < 6], partial (sum g, sum g*yt)
+//      EPI_BWD_LIN   g = c (+ R residual grad),  partial (sum g, sum g*yt)
+//
+// The weight gradient dW[N][K] = sum_m dy[m][n] x[m][k] reduces over M; it is
+// a split-M MFMA kernel whose operands are staged TRANSPOSED in LDS (4 rows of
+// m packed per ds_write_b64) so both fragments are plain ds_read_b128.
+#include "../common.h"
+
+enum { PRO_BNBWD = 3, IM2COL_STEM = 4 };
+enum { EPI_FWD = 0, EPI_BWD_RELU6 = 1, EPI_BWD_LIN = 2 };
+
+namespace {
+constexpr int kBM = 128;       // rows per M tile
+constexpr int kKC = 160;       // max K chunk staged in LDS (multiple of 32)
+constexpr int kBPad = 8;       // bf16 pad per staged weight row (16 B)
+constexpr int kCPad = 8;       // bf16 pad per staged C row
+
+struct PwArgs {
+  const bf16_t *A;      // [M][K]
+  const bf16_t *A2;     // [M][K] (Y for PRO_BNBWD)
+  const float *pa;      // prologue per-k params: s | a
+  const float *pb;      // t | b
+  const float *pc;      // - | c
+  const bf16_t *W;      // [N][K]
+  bf16_t *out;          // [M][N]
+  const bf16_t *Yt;     // [M][N] epilogue BN input (bwd modes)
+  const float *es;      // epilogue per-n scale (relu6 mask)
+  const float *et;      // epilogue per-n shift
+  const bf16_t *R;      // [M][N] residual gradient (EPI_BWD_LIN, optional)
+  float *part;          // [gridDim.x][2][N]
+  int M, N, K;
+};
+}  // namespace
+
+template <int PRO>
+PG_DEVICE s16x8_t load_a_frag(const PwArgs &p, int row, int k) {
+  s16x8_t r = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (row >= p.M || k >= p.K) return r;
+  const size_t off = (size_t)row * p.K + k;
+  uint4 u = ldg16(p.A + off);
+  if constexpr (PRO == ACT_NONE) {
+    return __builtin_bit_cast(s16x8_t, u);
+  } else {
+    float v[8];
+    unpack8(u, v);
+    if constexpr (PRO == PRO_BNBWD) {
+      float y[8];
+      unpack8(ldg16(p.A2 + off), y);
+      const float4 a0 = *reinterpret_cast<const float4 *>(p.pa + k), a1 = *reinterpret_cast<const float4 *>(p.pa + k + 4);
+      const float4 b0 = *reinterpret_cast<const float4 *>(p.pb + k), b1 = *reinterpret_cast<const float4 *>(p.pb + k + 4);
+      const float4 c0 = *reinterpret_cast<const float4 *>(p.pc + k), c1 = *reinterpret_cast<const float4 *>(p.pc + k + 4);
+      const float aa[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+      const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+      const float cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = fmaf(aa[j], v[j], fmaf(bb[j], y[j], cc[j]));
+    } else {
+      const float4 s0 = *reinterpret_cast<const float4 *>(p.pa + k), s1 = *reinterpret_cast<const float4 *>(p.pa + k + 4);
+      const float4 t0 = *reinterpret_cast<const float4 *>(p.pb + k), t1 = *reinterpret_cast<const float4 *>(p.pb + k + 4);
+      const float ss[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+      const float tt[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = act_apply<PRO>(v[j], ss[j], tt[j]);
+    }
+    return __builtin_bit_cast(s16x8_t, pack8(v));
+  }
+}
+
+template <int PRO, int EPI, int BN>
+__global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
+  constexpr int CT = BN / 16;               // col tiles per wave
+  constexpr int LDB = kKC + kBPad;          // staged weight row pitch (elements)
+  constexpr int LDC = BN + kCPad;           // staged C row pitch (elements)
+  constexpr int CH = BN / 8;                // 16-B chunks per C row
+  constexpr int RSTEP = 256 / CH;           // rows covered per epilogue pass
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t *Bs = reinterpret_cast<bf16_t *>(smem);                       // [BN][LDB]
+  bf16_t *Cs = reinterpret_cast<bf16_t *>(smem + BN * LDB * 2);        // [kBM][LDC]
+  float *Red = reinterpret_cast<float *>(smem + BN * LDB * 2);         // aliases Cs at the end
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.y * BN;
+  const int Kp = (p.K + 31) & ~31;
+  const int nmt = (p.M + kBM - 1) / kBM;
+  const int my_chunk = tid % CH;            // fixed epilogue column chunk
+  const int ncol0 = n0 + my_chunk * 8;
+
+  float st0[8], st1[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) st0[j] = st1[j] = 0.f;
+  float es[8], et[8];
+  if constexpr (EPI == EPI_BWD_RELU6) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      es[j] = ncol0 + j < p.N ? p.es[ncol0 + j] : 0.f;
+      et[j] = ncol0 + j < p.N ? p.et[ncol0 + j] : 0.f;
+    }
+  }
+
+  const bool single_chunk = Kp <= kKC;
+  auto stage_b = [&](int kc0, int kcl) {
+    // weight rows n0..n0+BN, k in [kc0, kc0+kcl) -> Bs (zero padded)
+    const int per_row = kcl / 8;
+    for (int i = tid; i < BN * per_row; i += 256) {
+      const int r = i / per_row, c8 = (i % per_row) * 8;
+      const int n = n0 + r, k = kc0 + c8;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (n < p.N && k < p.K) v = ldg16(p.W + (size_t)n * p.K + k);
+      *reinterpret_cast<uint4 *>(Bs + r * LDB + c8) = v;
+    }
+  };
+  // dgrad: the weight is stored [K][N] (conv weight [Cout][Cin] with GEMM K = Cout):
+  // read 8 consecutive n for one k and scatter them transposed into Bs[n][k]
+  auto stage_b_t = [&](int kc0, int kcl) {
+    const int per_k = BN / 8;
+    for (int i = tid; i < kcl * per_k; i += 256) {
+      const int kk = i / per_k, n8 = (i % per_k) * 8;
+      const int k = kc0 + kk, n = n0 + n8;
+      float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (k < p.K && n < p.N) unpack8(ldg16(p.W + (size_t)k * p.N + n), v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) Bs[(n8 + j) * LDB + kk] = f2bf(v[j]);
+    }
+  };
+  auto stage = [&](int kc0, int kcl) {
+    if constexpr (PRO == PRO_BNBWD) stage_b_t(kc0, kcl);
+    else stage_b(kc0, kcl);
+  };
+  if (single_chunk) {
+    stage(0, Kp);
+    __syncthreads();
+  }
+
+  for (int mt = blockIdx.x; mt < nmt; mt += gridDim.x) {
+    const int m0 = mt * kBM;
+    f32x4_t acc[2][CT];
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int c = 0; c < CT; ++c) acc[r][c] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    for (int kc0 = 0; kc0 < Kp; kc0 += kKC) {
+      const int kcl = min(kKC, Kp - kc0);
+      if (!single_chunk) {
+        __syncthreads();
+        stage(kc0, kcl);
+        __syncthreads();
+      }
+      for (int ks = 0; ks < kcl; ks += 32) {
+        const int kg = kc0 + ks + 8 * (lane >> 4);
+        s16x8_t af[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+          af[r] = load_a_frag<PRO>(p, m0 + wave * 32 + r * 16 + (lane & 15), kg);
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+          const s16x8_t bf = *reinterpret_cast<const s16x8_t *>(
+              Bs + (c * 16 + (lane & 15)) * LDB + ks + 8 * (lane >> 4));
+#pragma unroll
+          for (int r = 0; r < 2; ++r)
+            acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8_t, af[r]), __builtin_bit_cast(bf16x8_t, bf), acc[r][c], 0, 0, 0);
+        }
+      }
+    }
+    // ---- stage C tile (bf16) in LDS: acc[r][c][j] = C[wave*32 + r*16 + 4*(lane>>4) + j][c*16 + (lane&15)]
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int c = 0; c < CT; ++c)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          Cs[(wave * 32 + r * 16 + 4 * (lane >> 4) + j) * LDC + c * 16 + (lane & 15)] = f2bf(acc[r][c][j]);
+    __syncthreads();
+    // ---- row-chunked epilogue
+    if (ncol0 < p.N) {
+      for (int rr = tid / CH; rr < kBM; rr += RSTEP) {
+        const int row = m0 + rr;
+        if (row >= p.M) break;
+        float v[8];
+        unpack8(*reinterpret_cast<const uint4 *>(Cs + rr * LDC + my_chunk * 8), v);
+        const size_t off = (size_t)row * p.N + ncol0;
+        if constexpr (EPI == EPI_FWD) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            st0[j] += v[j];
+            st1[j] = fmaf(v[j], v[j], st1[j]);
+          }
+        } else {
+          float yt[8];
+          unpack8(ldg16(p.Yt + off), yt);
+          if constexpr (EPI == EPI_BWD_RELU6) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] *= relu6_mask(yt[j], es[j], et[j]);
+          } else {
+            if (p.R) {
+              float rv[8];
+              unpack8(ldg16(p.R + off), rv);
+#pragma unroll
+              for (int j = 0; j < 8; ++j) v[j] += rv[j];
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            st0[j] += v[j];
+            st1[j] = fmaf(v[j], yt[j], st1[j]);
+          }
+        }
+        stg16(p.out + off, pack8(v));
+      }
+    }
+    __syncthreads();
+  }
+  // ---- per-workgroup BN partials: reduce the RSTEP threads sharing a column chunk
+  // Red: [RSTEP][BN] floats (RSTEP*BN = 2048 floats) per statistic
+  for (int s = 0; s < 2; ++s) {
+    const int rgrp = tid / CH;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Red[rgrp * BN + my_chunk * 8 + j] = s == 0 ? st0[j] : st1[j];
+    __syncthreads();
+    for (int c = tid; c < BN; c += 256) {
+      float a = 0.f;
+      for (int g = 0; g < RSTEP; ++g) a += Red[g * BN + c];
+      if (n0 + c < p.N) p.part[((size_t)blockIdx.x * 2 + s) * p.N + n0 + c] = a;
+    }
+    __syncthreads();
+  }
+}
+
+// ===========================================================================
+// weight gradient: dW[N][K] += sum_m dy[m][n] * x[m][k]
+//   dy = a[n]*G + b[n]*Y + c[n]   (this layer's BN backward; PRO_BNBWD)
+//   x  = act(X)                   (ACT_NONE or ACT_BN_RELU6 of the producer BN)
+// split-M: blockIdx.z = split; part[split][N][K]
+// ===========================================================================
+namespace {
+struct PwWgArgs {
+  const bf16_t *G, *Y;          // [M][N]
+  const float *ga, *gb, *gc;    // [N]
+  const bf16_t *X;              // [M][K]
+  const float *xs, *xt;         // [K]
+  float *part;                  // [S][N][K]
+  int M, N, K, rows_per_split;
+  int ih, iw, oh, ow;           // IM2COL_STEM geometry (image H/W, output H/W)
+};
+constexpr int kWMK = 32;              // m rows per step
+constexpr int kWLD = kWMK + 8;        // transposed tile row pitch (elements): 80 B, conflict-free b128 reads
+}  // namespace
+
+// stage a [32 m][8*CHN cols] tile transposed into T[col][m] (pitch kWLD).
+// thread item = (m4 group of 4 rows, 8-col chunk); PRO transforms applied per element.
+template <int PRO>
+PG_DEVICE void wg_stage(const bf16_t *__restrict__ src, const bf16_t *__restrict__ src2,
+                        const float *pa, const float *pb, const float *pc, int ld, int ncols,
+                        int col0, int m0, int M, int tcols, bf16_t *T, int item) {
+  // item in [0, 8 * (tcols/8)) : m4 = item % 8, chunk = item / 8
+  const int m4 = item & 7, chunk = item >> 3;
+  const int c = col0 + chunk * 8;
+  float v[4][8];
+  float aa[8], bb[8], cc[8];
+  const bool cvalid = c < ncols;
+  if (PRO != ACT_NONE && cvalid) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      aa[j] = pa[c + j];
+      bb[j] = pb[c + j];
+      cc[j] = (PRO == PRO_BNBWD) ? pc[c + j] : 0.f;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int m = m0 + m4 * 4 + q;
+    if (m < M && cvalid) {
+      const size_t off = (size_t)m * ld + c;
+      unpack8(ldg16(src + off), v[q]);
+      if constexpr (PRO == PRO_BNBWD) {
+        float y[8];
+        unpack8(ldg16(src2 + off), y);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[q][j] = fmaf(aa[j], v[q][j], fmaf(bb[j], y[j], cc[j]));
+      } else if constexpr (PRO == ACT_BN_RELU6) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[q][j] = relu6f(fmaf(v[q][j], aa[j], bb[j]));
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[q][j] = 0.f;
+    }
+  }
+  // write transposed: T[chunk*8 + j][m4*4 .. +3] as one 8-byte store
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    uint2 w;
+    w.x = pack2(v[0][j], v[1][j]);
+    w.y = pack2(v[2][j], v[3][j]);
+    *reinterpret_cast<uint2 *>(T + (chunk * 8 + j) * kWLD + m4 * 4) = w;
+  }
+}
+
+// im2col of the stem input (NHWC, 4 channels incl. one zero pad channel, 3x3 s2 p1):
+// X[m][k], m -> (b, oh, ow), k = tap*4 + c, tap = kh*3 + kw;  K = 36.
+PG_DEVICE void wg_stage_im2col(const PwWgArgs &p, int m0, int M, bf16_t *T, int item) {
+  const int m4 = item & 7, chunk = item >> 3;
+  float v[4][8];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int m = m0 + m4 * 4 + q;
+    const int b = m / (p.oh * p.ow), rem = m % (p.oh * p.ow);
+    const int oh = rem / p.ow, ow = rem % p.ow;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int tap = chunk * 2 + h;
+      float f[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (m < M && tap < 9) {
+        const int ih = oh * 2 - 1 + tap / 3, iw = ow * 2 - 1 + tap % 3;
+        if (ih >= 0 && ih < p.ih && iw >= 0 && iw < p.iw) {
+          const uint2 u = *reinterpret_cast<const uint2 *>(p.X + (((size_t)b * p.ih + ih) * p.iw + iw) * 4);
+          f[0] = __uint_as_float(u.x << 16);
+          f[1] = __uint_as_float(u.x & 0xffff0000u);
+          f[2] = __uint_as_float(u.y << 16);
+          f[3] = __uint_as_float(u.y & 0xffff0000u);
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[q][h * 4 + c] = f[c];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    uint2 w;
+    w.x = pack2(v[0][j], v[1][j]);
+    w.y = pack2(v[2][j], v[3][j]);
+    *reinterpret_cast<uint2 *>(T + (chunk * 8 + j) * kWLD + m4 * 4) = w;
+  }
+}
+
+template <int XPRO, int TN, int TK>
+__global__ __launch_bounds__(256) void pw_wgrad_kernel(PwWgArgs p) {
+  // output tile TN x TK split over 4 waves as 2 x 2 quadrants
+  constexpr int QN = TN / 2, QK = TK / 2;
+  constexpr int RN = QN / 16, RK = QK / 16;
+  __shared__ __attribute__((aligned(16))) bf16_t Tdy[TN * kWLD];
+  __shared__ __attribute__((aligned(16))) bf16_t Tx[TK * kWLD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave >> 1, wk = wave & 1;
+  const int n0 = blockIdx.x * TN, k0 = blockIdx.y * TK;
+  const int mbeg = blockIdx.z * p.rows_per_split;
+  const int mend = min(p.M, mbeg + p.rows_per_split);
+
+  f32x4_t acc[RN][RK];
+#pragma unroll
+  for (int a = 0; a < RN; ++a)
+#pragma unroll
+    for (int b = 0; b < RK; ++b) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  constexpr int ITEMS_DY = 8 * (TN / 8), ITEMS_X = 8 * (TK / 8);
+  for (int m0 = mbeg; m0 < mend; m0 += kWMK) {
+    for (int it = tid; it < ITEMS_DY + ITEMS_X; it += 256) {
+      if (it < ITEMS_DY)
+        wg_stage<PRO_BNBWD>(p.G, p.Y, p.ga, p.gb, p.gc, p.N, p.N, n0, m0, mend, TN, Tdy, it);
+      else if constexpr (XPRO == IM2COL_STEM)
+        wg_stage_im2col(p, m0, mend, Tx, it - ITEMS_DY);
+      else
+        wg_stage<XPRO>(p.X, nullptr, p.xs, p.xt, nullptr, p.K, p.K, k0, m0, mend, TK, Tx, it - ITEMS_DY);
+    }
+    __syncthreads();
+    s16x8_t af[RN], bfr[RK];
+#pragma unroll
+    for (int a = 0; a < RN; ++a)
+      af[a] = *reinterpret_cast<const s16x8_t *>(Tdy + (wn * QN + a * 16 + (lane & 15)) * kWLD + 8 * (lane >> 4));
+#pragma unroll
+    for (int b = 0; b < RK; ++b)
+      bfr[b] = *reinterpret_cast<const s16x8_t *>(Tx + (wk * QK + b * 16 + (lane & 15)) * kWLD + 8 * (lane >> 4));
+#pragma unroll
+    for (int a = 0; a < RN; ++a)
+#pragma unroll
+      for (int b = 0; b < RK; ++b)
+        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[a]),
+                                                           __builtin_bit_cast(bf16x8_t, bfr[b]), acc[a][b], 0, 0, 0);
+    __syncthreads();
+  }
+  // acc[a][b][j] = dW[n0 + wn*QN + a*16 + 4*(lane>>4) + j][k0 + wk*QK + b*16 + (lane&15)]
+  float *dst = p.part + (size_t)blockIdx.z * p.N * p.K;
+#pragma unroll
+  for (int a = 0; a < RN; ++a)
+#pragma unroll
+    for (int b = 0; b < RK; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wn * QN + a * 16 + 4 * (lane >> 4) + j;
+        const int k = k0 + wk * QK + b * 16 + (lane & 15);
+        if (n < p.N && k < p.K) dst[(size_t)n * p.K + k] = acc[a][b][j];
+      }
+}
+
+__global__ __launch_bounds__(256) void split_reduce_kernel(const float *__restrict__ part, int S,
+                                                          long long n, float *__restrict__ out) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < S; ++k) s += part[(size_t)k * n + i];
+    out[i] = s;
+  }
+}
+
+// ===========================================================================
+// host launchers
+// ===========================================================================
+static int pw_bn_for(int N) { return N <= 32 ? 32 : (N <= 64 ? 64 : 128); }
+
+int pw_gemm_num_partials(int M, int N) {
+  const int BN = pw_bn_for(N);
+  const int nt = (N + BN - 1) / BN;
+  const int nmt = (M + kBM - 1) / kBM;
+  int gx = 1024 / nt;
+  gx = (gx + 7) & ~7;
+  if (gx < 8) gx = 8;
+  if (gx > nmt) gx = nmt;
+  return gx;
+}
+
+template <int PRO, int EPI, int BN>
+static void launch_pw_t(const PwArgs &a, hipStream_t st) {
+  const int nt = (a.N + BN - 1) / BN;
+  const int gx = pw_gemm_num_partials(a.M, a.N);
+  const size_t lds = (size_t)BN * (kKC + kBPad) * 2 + (size_t)kBM * (BN + kCPad) * 2;
+  hipLaunchKernelGGL((pw_gemm_kernel<PRO, EPI, BN>), dim3(gx, nt), dim3(256), lds, st, a);
+}
+
+template <int PRO, int EPI>
+static void launch_pw_bn(const PwArgs &a, hipStream_t st) {
+  switch (pw_bn_for(a.N)) {
+    case 32: launch_pw_t<PRO, EPI, 32>(a, st); break;
+    case 64: launch_pw_t<PRO, EPI, 64>(a, st); break;
+    default: launch_pw_t<PRO, EPI, 128>(a, st); break;
+  }
+}
+
+// pro: 0 none, 1 bn+relu6, 3 bnbwd ; epi: 0 fwd, 1 bwd relu6, 2 bwd lin
+void launch_pw_gemm(int pro, int epi, const bf16_t *A, const bf16_t *A2, const float *pa,
+                    const float *pb, const float *pc, const bf16_t *W, bf16_t *out,
+                    const bf16_t *Yt, const float *es, const float *et, const bf16_t *R, float *part,
+                    int M, int N, int K, hipStream_t st) {
+  PwArgs a{A, A2, pa, pb, pc, W, out, Yt, es, et, R, part, M, N, K};
+#define PW_CASE(P, E) \
+  if (pro == P && epi == E) { launch_pw_bn<P, E>(a, st); return; }
+  PW_CASE(ACT_NONE, EPI_FWD)
+  PW_CASE(ACT_BN_RELU6, EPI_FWD)
+  PW_CASE(PRO_BNBWD, EPI_BWD_RELU6)
+  PW_CASE(PRO_BNBWD, EPI_BWD_LIN)
+#undef PW_CASE
+}
+
+static void wgrad_geom(int M, int N, int K, int &TN, int &TK, int &S, int &rps) {
+  TN = N <= 32 ? 32 : (N <= 64 ? 64 : 128);
+  TK = K <= 32 ? 32 : (K <= 64 ? 64 : 128);
+  const int tiles = ((N + TN - 1) / TN) * ((K + TK - 1) / TK);
+  S = 1024 / tiles;
+  if (S < 1) S = 1;
+  const int max_s = (M + 255) / 256;
+  if (S > max_s) S = max_s;
+  rps = ((M + S - 1) / S + kWMK - 1) / kWMK * kWMK;
+  S = (M + rps - 1) / rps;
+}
+
+long long pw_wgrad_workspace_floats(int M, int N, int K) {
+  int TN, TK, S, rps;
+  wgrad_geom(M, N, K, TN, TK, S, rps);
+  return (long long)S * N * K;
+}
+
+template <int XPRO, int TN, int TK>
+static void launch_wg_t(const PwWgArgs &a, int S, hipStream_t st) {
+  dim3 grid((a.N + TN - 1) / TN, (a.K + TK - 1) / TK, S);
+  hipLaunchKernelGGL((pw_wgrad_kernel<XPRO, TN, TK>), grid, dim3(256), 0, st, a);
+}
+
+template <int XPRO>
+static void launch_wg_x(const PwWgArgs &a, int TN, int TK, int S, hipStream_t st) {
+#define WG_CASE(A_, B_) \
+  if (TN == A_ && TK == B_) { launch_wg_t<XPRO, A_, B_>(a, S, st); return; }
+  WG_CASE(32, 32) WG_CASE(32, 64) WG_CASE(32, 128)
+  WG_CASE(64, 32) WG_CASE(64, 64) WG_CASE(64, 128)
+  WG_CASE(128, 32) WG_CASE(128, 64) WG_CASE(128, 128)
+#undef WG_CASE
+}
+
+// reorder [32][36] (k = tap*4 + c) -> torch [32][3][3][3] (o, c, kh, kw)
+__global__ void stem_wgrad_permute_kernel(const float *__restrict__ src, float *__restrict__ grad,
+                                          int O) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= O * 27) return;
+  const int o = i / 27, r = i % 27, c = r / 9, tap = r % 9;
+  grad[i] = src[o * 36 + tap * 4 + c];
+}
+
+long long stem_wgrad_workspace_floats(int M, int O) {
+  int TN, TK, S, rps;
+  wgrad_geom(M, O, 36, TN, TK, S, rps);
+  return (long long)S * O * 36 + (long long)O * 36;
+}
+
+void launch_stem_wgrad(const bf16_t *G, const bf16_t *Y, const float *ga, const float *gb,
+                       const float *gc, const bf16_t *img, float *part, float *grad, int B, int H,
+                       int W, int O, hipStream_t st) {
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  const int M = B * Ho * Wo;
+  int TN, TK, S, rps;
+  wgrad_geom(M, O, 36, TN, TK, S, rps);
+  PwWgArgs a{G, Y, ga, gb, gc, img, nullptr, nullptr, part, M, O, 36, rps, H, W, Ho, Wo};
+  launch_wg_x<IM2COL_STEM>(a, TN, TK, S, st);
+  float *tmp = part + (size_t)S * O * 36;
+  const long long n = (long long)O * 36;
+  hipLaunchKernelGGL(split_reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, st, part, S, n, tmp);
+  hipLaunchKernelGGL(stem_wgrad_permute_kernel, dim3((O * 27 + 255) / 256), dim3(256), 0, st, tmp, grad, O);
+}
+
+void launch_pw_wgrad(const bf16_t *G, const bf16_t *Y, const float *ga, const float *gb,
+                     const float *gc, const bf16_t *X, const float *xs, const float *xt, int xact,
+                     float *part, float *grad, int M, int N, int K, hipStream_t st) {
+  int TN, TK, S, rps;
+  wgrad_geom(M, N, K, TN, TK, S, rps);
+  PwWgArgs a{G, Y, ga, gb, gc, X, xs, xt, part, M, N, K, rps, 0, 0, 0, 0};
+  if (xact == ACT_BN_RELU6) launch_wg_x<ACT_BN_RELU6>(a, TN, TK, S, st);
+  else launch_wg_x<ACT_NONE>(a, TN, TK, S, st);
+  const long long n = (long long)N * K;
+  int grid = (int)((n + 255) / 256);
+  if (grid > 2048) grid = 2048;
+  hipLaunchKernelGGL(split_reduce_kernel, dim3(grid), dim3(256), 0, st, part, S, n, grad);
+}

@@ -1,0 +1,73 @@
+"""Benchmark step builders used by ``bench.py``.
+
+``hip`` backend: the native static-plan executor (HIP kernels, fused Adam,
+bucketed RCCL all-reduce, optional hipGraph capture).
+``torch`` backend: the PyTorch/MIOpen path (channels_last bf16 autocast +
+``torch.nn.parallel.DistributedDataParallel`` + fused torch Adam) — kept as the
+measured baseline the native path has to beat.
+"""
+import torch
+import torch.nn.functional as F
+
+from ..models import build_model
+from ..data.synthetic import synthetic_cifar
+
+
+def _resolve_backend(backend: str, device: torch.device) -> str:
+    if backend == "auto":
+        return "hip" if device.type == "cuda" else "torch"
+    return backend
+
+
+def build_bench_step(model_name: str, batch_size: int, device: torch.device, backend: str = "auto",
+                     img_size: int = 224, use_graph: bool = True, world_size: int = 1, rank: int = 0):
+    backend = _resolve_backend(backend, device)
+    if backend == "hip":
+        from .native_step import NativeTrainStep
+        step = NativeTrainStep.for_benchmark(model_name, batch_size, device, img_size=img_size,
+                                             use_graph=use_graph, world_size=world_size, rank=rank)
+        return step.bench_step, {"backend": "hip", "graph": step.graph_enabled}
+    return _torch_bench_step(model_name, batch_size, device, img_size, world_size, rank)
+
+
+def _torch_bench_step(model_name, batch_size, device, img_size, world_size, rank):
+    torch.manual_seed(42 + rank)
+    n_data = 4096
+    imgs_np, labels_np = synthetic_cifar(n_data, seed=rank)
+    imgs = torch.from_numpy(imgs_np).to(device)            # [N,32,32,3] uint8, device resident
+    labels_all = torch.from_numpy(labels_np).to(device)
+    mean = torch.tensor([0.485, 0.456, 0.406], device=device).view(1, 3, 1, 1)
+    std = torch.tensor([0.229, 0.224, 0.225], device=device).view(1, 3, 1, 1)
+
+    model = build_model(model_name, num_classes=10 if model_name == "mobilenet_v2" else 1000).to(device)
+    if device.type == "cuda":
+        model = model.to(memory_format=torch.channels_last)
+    ddp = model
+    if world_size > 1:
+        ddp = torch.nn.parallel.DistributedDataParallel(
+            model, device_ids=[device.index] if device.type == "cuda" else None)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4, fused=device.type == "cuda")
+    crit = torch.nn.CrossEntropyLoss()
+    amp_dtype = torch.bfloat16
+    state = {"i": 0}
+    n_cls = 10 if model_name == "mobilenet_v2" else 1000
+
+    def step():
+        i = state["i"]
+        state["i"] += 1
+        idx = torch.randint(0, n_data, (batch_size,), device=device)
+        x = imgs.index_select(0, idx).permute(0, 3, 1, 2).float().div_(255.0)
+        x = F.interpolate(x, size=(img_size, img_size), mode="bilinear", align_corners=False)
+        flip = (torch.rand(batch_size, 1, 1, 1, device=device) < 0.5)
+        x = torch.where(flip, x.flip(3), x)
+        x = ((x - mean) / std).contiguous(memory_format=torch.channels_last)
+        y = labels_all.index_select(0, idx) % n_cls
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast(device_type=device.type, dtype=amp_dtype, enabled=device.type == "cuda"):
+            out = ddp(x)
+            loss = crit(out.float(), y)
+        loss.backward()
+        opt.step()
+        return loss
+
+    return step, {"backend": "torch", "graph": False}

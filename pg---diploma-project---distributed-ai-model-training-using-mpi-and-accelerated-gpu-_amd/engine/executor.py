@@ -1,0 +1,320 @@
+"""Static-plan executor: MobileNetV2 training step on the fused gfx950 kernels.
+
+Instead of tracing autograd through ~150 forward / ~300 backward library ops
+(reference call stack: SURVEY.md §3.3), the network is compiled once into a
+fixed schedule of fused HIP kernels over preallocated NHWC bf16 buffers:
+
+forward, per inverted-residual block (BN = training-mode BatchNorm)
+  expand   pw_gemm(ACT_BN_RELU6 | ACT_NONE prologue)  -> y_e + BN_e partials
+  finalize BN_e                                        -> scale/shift (+running stats)
+  dw       dw_fwd(relu6(BN_e(y_e)) prologue)           -> y_d + BN_d partials
+  finalize BN_d
+  project  pw_gemm(relu6(BN_d(y_d)) prologue)          -> y_p + BN_p partials
+  finalize BN_p
+  output   o = BN_p(y_p) (+ o_in)                      (materialised, bf16)
+head: BN_18/ReLU6 + avgpool + dropout + linear + CE + its backward (one kernel)
+
+backward walks the schedule in reverse; every BN backward is split into a
+partial-sum epilogue in the kernel that produces the gradient and a per-channel
+finalize, and the BN-backward elementwise step is fused into the prologues of
+both the dgrad and the wgrad kernels that consume it.  Weight gradients are
+written straight into the flat gradient buffer; after each layer the gradient
+bucket reducer is told which parameters are final so the RCCL all-reduce of a
+complete bucket starts while backward continues.
+
+Every buffer is allocated once, so the whole step can be captured in a hipGraph.
+"""
+from dataclasses import dataclass, field
+from typing import Callable, List, Optional
+
+import torch
+
+from ..models.mobilenet_v2 import MobileNetV2, InvertedResidual
+from ..ops import kernels as K
+from .flat import FlatParams
+
+
+class BNState:
+    """Buffers of one training-mode BatchNorm over an [M, C] activation."""
+
+    def __init__(self, flat: FlatParams, module: torch.nn.BatchNorm2d, prefix: str, M: int, C: int,
+                 device, need_g: bool = True):
+        self.prefix, self.M, self.C = prefix, M, C
+        self.module = module
+        self.eps, self.momentum = module.eps, module.momentum if module.momentum is not None else 0.1
+        self.gamma, self.beta = flat.w(prefix + ".weight"), flat.w(prefix + ".bias")
+        self.dgamma, self.dbeta = flat.g(prefix + ".weight"), flat.g(prefix + ".bias")
+        f32 = dict(dtype=torch.float32, device=device)
+        self.mean = torch.zeros(C, **f32)
+        self.rstd = torch.ones(C, **f32)
+        self.scale = torch.ones(C, **f32)
+        self.shift = torch.zeros(C, **f32)
+        self.coef = torch.zeros(3, C, **f32)
+        self.y = torch.empty(M, C, dtype=torch.bfloat16, device=device)   # pre-BN activation
+        self.g = torch.empty(M, C, dtype=torch.bfloat16, device=device) if need_g else None
+        self.param_names = [prefix + ".weight", prefix + ".bias"]
+
+    def finalize_fwd(self, part, P):
+        K.bn_fwd_finalize(part, P, self.C, self.M, self.gamma, self.beta, self.eps, self.momentum,
+                          self.module.running_mean, self.module.running_var,
+                          self.module.num_batches_tracked, self.mean, self.rstd, self.scale, self.shift)
+
+    def finalize_bwd(self, part, P):
+        K.bn_bwd_finalize(part, P, self.C, self.M, self.mean, self.rstd, self.gamma, self.coef,
+                          self.dgamma, self.dbeta)
+
+    def eval_prepare(self):
+        with torch.no_grad():
+            rs = torch.rsqrt(self.module.running_var + self.eps)
+            self.scale.copy_(self.gamma * rs)
+            self.shift.copy_(self.beta - self.module.running_mean * self.gamma * rs)
+
+    @property
+    def a(self):
+        return self.coef[0]
+
+    @property
+    def b(self):
+        return self.coef[1]
+
+    @property
+    def c(self):
+        return self.coef[2]
+
+
+@dataclass
+class BlockPlan:
+    idx: int
+    prefix: str
+    cin: int
+    cout: int
+    hidden: int
+    stride: int
+    expand: bool
+    residual: bool
+    H: int
+    W: int
+    Ho: int
+    Wo: int
+    w_e: Optional[str]
+    w_d: str
+    w_p: str
+    bn_e: Optional[BNState]
+    bn_d: BNState
+    bn_p: BNState
+    o: torch.Tensor = None          # block output (materialised)
+    G: torch.Tensor = None          # gradient w.r.t. o
+
+
+class MobileNetV2Executor:
+    def __init__(self, model: MobileNetV2, batch: int, img_size: int, device: torch.device,
+                 flat: Optional[FlatParams] = None, dropout_seed: int = 0):
+        assert device.type == "cuda", "the native executor runs on the GPU"
+        self.model = model.to(device)
+        self.B, self.S, self.device = batch, img_size, device
+        self.flat = flat or FlatParams(self.model, device)
+        self.dropout_seed = dropout_seed
+        self.drop_p = float(model.classifier[0].p)
+        B = batch
+        feats = model.features
+        # ---------------- stem
+        H = (img_size - 1) // 2 + 1
+        self.H0 = H
+        self.stem_w = "features.0.0.weight"
+        self.bn0 = BNState(self.flat, feats[0][1], "features.0.1", B * H * H, feats[0][0].out_channels, device)
+        parts = [K.stem_num_partials(B, img_size, img_size)]
+        wg = [K.stem_wgrad_workspace(B, img_size, img_size, 32)]
+        # ---------------- blocks
+        self.blocks: List[BlockPlan] = []
+        cur_h = H
+        for i in range(1, len(feats) - 1):
+            blk: InvertedResidual = feats[i]
+            pre = f"features.{i}.conv"
+            Hin = cur_h
+            Ho = (Hin - 1) // blk.stride + 1
+            Min, Mout = B * Hin * Hin, B * Ho * Ho
+            expand = blk.expand_ratio != 1
+            if expand:
+                bn_e = BNState(self.flat, blk.conv[0][1], f"{pre}.0.1", Min, blk.hidden, device)
+                dwm, w_e = blk.conv[1], f"{pre}.0.0.weight"
+                w_d, bn_d_pre = f"{pre}.1.0.weight", f"{pre}.1.1"
+                w_p, bn_p_mod, bn_p_pre = f"{pre}.2.weight", blk.conv[3], f"{pre}.3"
+            else:
+                bn_e, w_e, dwm = None, None, blk.conv[0]
+                w_d, bn_d_pre = f"{pre}.0.0.weight", f"{pre}.0.1"
+                w_p, bn_p_mod, bn_p_pre = f"{pre}.1.weight", blk.conv[2], f"{pre}.2"
+            bn_d = BNState(self.flat, dwm[1], bn_d_pre, Mout, blk.hidden, device)
+            bn_p = BNState(self.flat, bn_p_mod, bn_p_pre, Mout, blk.oup, device, need_g=False)
+            bp = BlockPlan(i, pre, blk.inp, blk.oup, blk.hidden, blk.stride, expand, blk.use_res_connect,
+                           Hin, Hin, Ho, Ho, w_e, w_d, w_p, bn_e, bn_d, bn_p)
+            bp.o = torch.empty(Mout, blk.oup, dtype=torch.bfloat16, device=device)
+            bp.G = torch.empty(Mout, blk.oup, dtype=torch.bfloat16, device=device)
+            self.blocks.append(bp)
+            if expand:
+                parts.append(K.pw_num_partials(Min, blk.hidden))                       # fwd expand
+                parts.append(K.pw_num_partials(Min, blk.inp))                          # bwd expand dgrad
+                wg.append(K.pw_wgrad_workspace(Min, blk.hidden, blk.inp))
+            parts.append(K.dw_num_partials("fwd", B, Hin, Hin, blk.hidden, blk.stride))
+            parts.append(K.dw_num_partials("dgrad", B, Hin, Hin, blk.hidden, blk.stride))
+            wg.append(K.dw_num_partials("wgrad", B, Hin, Hin, blk.hidden, blk.stride) * 9 * blk.hidden)
+            parts.append(K.pw_num_partials(Mout, blk.oup))                             # fwd project
+            parts.append(K.pw_num_partials(Mout, blk.hidden))                          # bwd project dgrad
+            wg.append(K.pw_wgrad_workspace(Mout, blk.oup, blk.hidden))
+            cur_h = Ho
+        # ---------------- final 1x1 conv + head
+        last = feats[-1]
+        self.Hf = cur_h
+        Mf = B * cur_h * cur_h
+        self.C_last_in = self.blocks[-1].cout
+        self.C_last = last[0].out_channels
+        self.w_last = f"features.{len(feats) - 1}.0.weight"
+        self.bn_last = BNState(self.flat, last[1], f"features.{len(feats) - 1}.1", Mf, self.C_last, device)
+        parts.append(K.pw_num_partials(Mf, self.C_last))
+        parts.append(K.pw_num_partials(Mf, self.C_last_in))
+        parts.append(B)
+        wg.append(K.pw_wgrad_workspace(Mf, self.C_last, self.C_last_in))
+        self.NC = model.classifier[1].out_features
+        self.w_lin, self.b_lin = "classifier.1.weight", "classifier.1.bias"
+        f32 = dict(dtype=torch.float32, device=device)
+        self.logits = torch.zeros(B, self.NC, **f32)
+        self.loss = torch.zeros(B, **f32)
+        self.correct = torch.zeros(B, **f32)
+        self.dlogits = torch.zeros(B, self.NC, **f32)
+        self.pd = torch.zeros(B, self.C_last, **f32)
+        # ---------------- workspaces (stream-ordered reuse)
+        maxC = max([self.C_last] + [b.hidden for b in self.blocks])
+        self.ws_part = torch.zeros(max(parts) * 2 * maxC + 1024, **f32)
+        self.ws_wgrad = torch.zeros(max(wg) + 1024, **f32)
+        self.img = torch.zeros(B, img_size, img_size, 4, dtype=torch.bfloat16, device=device)
+        self.labels = torch.zeros(B, dtype=torch.int64, device=device)
+        self.hyper = torch.zeros(2, **f32)   # [lr, step]
+        self.on_params_ready: Optional[Callable[[List[str]], None]] = None
+
+    # ------------------------------------------------------------------ helpers
+    def _ready(self, names):
+        if self.on_params_ready is not None:
+            self.on_params_ready(names)
+
+    def _fin_fwd(self, bn: BNState, P: int, train: bool):
+        if train:
+            bn.finalize_fwd(self.ws_part, P)
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, train: bool = True):
+        """Runs the forward pass on ``self.img`` (and, when training, the head backward)."""
+        f, B, S = self.flat, self.B, self.S
+        ws = self.ws_part
+        # stem
+        K.stem_fwd(self.img, f.b(self.stem_w), self.bn0.y, ws, B, S, S)
+        self._fin_fwd(self.bn0, K.stem_num_partials(B, S, S), train)
+        inp_bn, inp_t = self.bn0, None   # block input: virtual relu6(bn0(y0))
+        for bp in self.blocks:
+            Hin = bp.H
+            Min = B * Hin * Hin
+            if bp.expand:
+                if inp_t is None:
+                    K.pw_gemm(K.ACT_BN_RELU6, K.EPI_FWD, inp_bn.y, f.b(bp.w_e), bp.bn_e.y, ws, Min, bp.hidden,
+                              bp.cin, pa=inp_bn.scale, pb=inp_bn.shift)
+                else:
+                    K.pw_gemm(K.ACT_NONE, K.EPI_FWD, inp_t, f.b(bp.w_e), bp.bn_e.y, ws, Min, bp.hidden, bp.cin)
+                self._fin_fwd(bp.bn_e, K.pw_num_partials(Min, bp.hidden), train)
+                dw_in = bp.bn_e
+            else:
+                assert inp_t is None, "t=1 block expects the (virtual) stem output"
+                dw_in = inp_bn
+            K.dw_fwd(dw_in.y, dw_in.scale, dw_in.shift, K.ACT_BN_RELU6, f.b(bp.w_d), bp.bn_d.y, ws, B, Hin, Hin,
+                     bp.hidden, bp.stride)
+            self._fin_fwd(bp.bn_d, K.dw_num_partials("fwd", B, Hin, Hin, bp.hidden, bp.stride), train)
+            Mout = B * bp.Ho * bp.Wo
+            K.pw_gemm(K.ACT_BN_RELU6, K.EPI_FWD, bp.bn_d.y, f.b(bp.w_p), bp.bn_p.y, ws, Mout, bp.cout, bp.hidden,
+                      pa=bp.bn_d.scale, pb=bp.bn_d.shift)
+            self._fin_fwd(bp.bn_p, K.pw_num_partials(Mout, bp.cout), train)
+            K.bn_apply(bp.bn_p.y, bp.bn_p.scale, bp.bn_p.shift, bp.o, relu6=False,
+                       res=inp_t if bp.residual else None)
+            inp_bn, inp_t = bp.bn_p, bp.o
+        # final 1x1 conv
+        Mf = B * self.Hf * self.Hf
+        K.pw_gemm(K.ACT_NONE, K.EPI_FWD, inp_t, f.b(self.w_last), self.bn_last.y, ws, Mf, self.C_last,
+                  self.C_last_in)
+        self._fin_fwd(self.bn_last, K.pw_num_partials(Mf, self.C_last), train)
+        # head (+ its backward when training)
+        K.head(self.bn_last.y, self.bn_last.scale, self.bn_last.shift, f.w(self.w_lin), f.w(self.b_lin),
+               self.labels, B, self.Hf * self.Hf, self.C_last, self.NC, self.drop_p, self.dropout_seed,
+               self.hyper, train, 1.0 / B, logits=self.logits, loss=self.loss, correct=self.correct,
+               dlogits=self.dlogits if train else None, pd=self.pd if train else None,
+               g_out=self.bn_last.g if train else None, part=ws if train else None,
+               dW=f.g(self.w_lin) if train else None, db=f.g(self.b_lin) if train else None)
+
+    # ------------------------------------------------------------------ backward
+    def backward(self):
+        f, B, S = self.flat, self.B, self.S
+        ws, wg = self.ws_part, self.ws_wgrad
+        self._ready([self.w_lin, self.b_lin])
+        # BN of the final conv (g produced by the head kernel)
+        bnl = self.bn_last
+        bnl.finalize_bwd(ws, B)
+        self._ready(bnl.param_names)
+        Mf = B * self.Hf * self.Hf
+        last_blk = self.blocks[-1]
+        # dgrad of the final conv -> gradient w.r.t. o_17 (feeds BN_p of block 17, linear)
+        K.pw_gemm(K.PRO_BNBWD, K.EPI_BWD_LIN, bnl.g, f.b(self.w_last), last_blk.G, ws, Mf, self.C_last_in,
+                  self.C_last, A2=bnl.y, pa=bnl.a, pb=bnl.b, pc=bnl.c, Yt=last_blk.bn_p.y, R=None)
+        P_g = K.pw_num_partials(Mf, self.C_last_in)
+        last_blk.bn_p.finalize_bwd(ws, P_g)
+        K.pw_wgrad(bnl.g, bnl.y, bnl.a, bnl.b, bnl.c, last_blk.o, None, None, K.ACT_NONE, wg,
+                   f.g(self.w_last), Mf, self.C_last, self.C_last_in)
+        self._ready([self.w_last] + last_blk.bn_p.param_names)
+
+        for bi in range(len(self.blocks) - 1, -1, -1):
+            bp = self.blocks[bi]
+            prev = self.blocks[bi - 1] if bi > 0 else None
+            Hin = bp.H
+            Min, Mout = B * Hin * Hin, B * bp.Ho * bp.Wo
+            bnp, bnd = bp.bn_p, bp.bn_d
+            # bn_p backward coefficients were finalised by whoever produced bp.G
+            # project dgrad -> g_d (relu6 mask of BN_d) + BN_d partials
+            K.pw_gemm(K.PRO_BNBWD, K.EPI_BWD_RELU6, bp.G, f.b(bp.w_p), bnd.g, ws, Mout, bp.hidden, bp.cout,
+                      A2=bnp.y, pa=bnp.a, pb=bnp.b, pc=bnp.c, Yt=bnd.y, es=bnd.scale, et=bnd.shift)
+            bnd.finalize_bwd(ws, K.pw_num_partials(Mout, bp.hidden))
+            # project wgrad
+            K.pw_wgrad(bp.G, bnp.y, bnp.a, bnp.b, bnp.c, bnd.y, bnd.scale, bnd.shift, K.ACT_BN_RELU6, wg,
+                       f.g(bp.w_p), Mout, bp.cout, bp.hidden)
+            self._ready([bp.w_p] + bnd.param_names)
+            # depthwise: input BN is BN_e (expand) or the stem BN0 (t=1 block)
+            dw_in = bp.bn_e if bp.expand else self.bn0
+            K.dw_dgrad(bnd.g, bnd.y, bnd.coef, f.b(bp.w_d), dw_in.y, dw_in.scale, dw_in.shift, dw_in.g, ws,
+                       B, Hin, Hin, bp.hidden, bp.stride)
+            dw_in.finalize_bwd(ws, K.dw_num_partials("dgrad", B, Hin, Hin, bp.hidden, bp.stride))
+            K.dw_wgrad(bnd.g, bnd.y, bnd.coef, dw_in.y, dw_in.scale, dw_in.shift, wg, f.g(bp.w_d),
+                       B, Hin, Hin, bp.hidden, bp.stride)
+            self._ready([bp.w_d] + dw_in.param_names)
+            if bp.expand:
+                bne = bp.bn_e
+                assert prev is not None
+                # expand dgrad -> gradient w.r.t. the block input o_prev (+ skip gradient)
+                K.pw_gemm(K.PRO_BNBWD, K.EPI_BWD_LIN, bne.g, f.b(bp.w_e), prev.G, ws, Min, bp.cin, bp.hidden,
+                          A2=bne.y, pa=bne.a, pb=bne.b, pc=bne.c, Yt=prev.bn_p.y,
+                          R=bp.G if bp.residual else None)
+                prev.bn_p.finalize_bwd(ws, K.pw_num_partials(Min, bp.cin))
+                K.pw_wgrad(bne.g, bne.y, bne.a, bne.b, bne.c, prev.o, None, None, K.ACT_NONE, wg,
+                           f.g(bp.w_e), Min, bp.hidden, bp.cin)
+                self._ready([bp.w_e] + prev.bn_p.param_names)
+            else:
+                # t=1 block: its input is relu6(BN0(stem)) -> stem weight gradient
+                bn0 = self.bn0
+                K.stem_wgrad(bn0.g, bn0.y, bn0.a, bn0.b, bn0.c, self.img, wg, f.g(self.stem_w), B, S, S, 32)
+                self._ready([self.stem_w])
+
+    # ------------------------------------------------------------------ eval
+    def eval_prepare(self):
+        for bn in self.all_bns():
+            bn.eval_prepare()
+
+    def all_bns(self):
+        out = [self.bn0]
+        for bp in self.blocks:
+            if bp.bn_e is not None:
+                out.append(bp.bn_e)
+            out += [bp.bn_d, bp.bn_p]
+        out.append(self.bn_last)
+        return out

@@ -1,0 +1,82 @@
+"""Flat parameter / gradient / optimizer-state storage.
+
+All trainable tensors of a model live in ONE contiguous fp32 master buffer (the
+module's ``Parameter`` objects are re-pointed to views of it, so
+``state_dict()`` / checkpointing / the torch oracle path see the same memory),
+with a parallel fp32 gradient buffer, Adam ``m``/``v`` buffers and a bf16
+shadow copy that the HIP kernels read.
+
+Layout is *backward-completion order* (reverse of ``named_parameters``: the
+classifier first, the stem last) with every tensor 64-element aligned, so the
+gradient all-reduce buckets are contiguous prefixes/ranges of the gradient
+buffer that become ready in order while backward is still running
+(reference DDP buckets: SURVEY.md §2.7 N6).
+"""
+from typing import Dict, List, Tuple
+
+import torch
+
+ALIGN = 64
+
+
+def _align(n: int, a: int = ALIGN) -> int:
+    return (n + a - 1) // a * a
+
+
+class FlatParams:
+    def __init__(self, model: torch.nn.Module, device: torch.device, with_shadow: bool = True):
+        named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
+        order = list(reversed(named))
+        self.offsets: Dict[str, Tuple[int, int]] = {}
+        self.order: List[str] = []
+        off = 0
+        for name, p in order:
+            off = _align(off)
+            self.offsets[name] = (off, p.numel())
+            self.order.append(name)
+            off += p.numel()
+        self.numel = _align(off)
+        self.device = device
+        self.master = torch.zeros(self.numel, dtype=torch.float32, device=device)
+        self.grad = torch.zeros_like(self.master)
+        self.exp_avg = torch.zeros_like(self.master)
+        self.exp_avg_sq = torch.zeros_like(self.master)
+        self.shadow = torch.zeros(self.numel, dtype=torch.bfloat16, device=device) if with_shadow else None
+        self.params = {}
+        with torch.no_grad():
+            for name, p in order:
+                o, n = self.offsets[name]
+                self.master[o:o + n].copy_(p.detach().reshape(-1).to(device))
+                p.data = self.master[o:o + n].view(p.shape)
+                p.grad = self.grad[o:o + n].view(p.shape)
+                self.params[name] = p
+        self.refresh_shadow()
+
+    # views ---------------------------------------------------------------
+    def w(self, name: str) -> torch.Tensor:
+        o, n = self.offsets[name]
+        return self.master[o:o + n]
+
+    def g(self, name: str) -> torch.Tensor:
+        o, n = self.offsets[name]
+        return self.grad[o:o + n]
+
+    def b(self, name: str) -> torch.Tensor:
+        o, n = self.offsets[name]
+        return self.shadow[o:o + n]
+
+    def range_of(self, name: str) -> Tuple[int, int]:
+        o, n = self.offsets[name]
+        return o, o + n
+
+    def refresh_shadow(self):
+        if self.shadow is None:
+            return
+        if self.device.type == "cuda":
+            from ..ops import kernels as K
+            K.f32_to_bf16(self.master, self.shadow)
+        else:
+            self.shadow.copy_(self.master.to(torch.bfloat16))
+
+    def optimizer_state(self):
+        return {"exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq}

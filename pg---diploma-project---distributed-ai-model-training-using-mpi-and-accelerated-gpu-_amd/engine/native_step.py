@@ -1,0 +1,143 @@
+"""One native training step = GPU augmentation + fused forward/backward +
+bucketed RCCL gradient all-reduce + fused Adam + device-side metrics,
+optionally captured once into a hipGraph and replayed.
+
+Reference per-batch body (``cifar10_mpi_mobilenet_224.py:173-185``):
+``imgs.to(device); zero_grad(); out = ddp_model(imgs); loss = criterion(...);
+loss.backward(); optimizer.step(); torch.max(...); loss.item(); (...).item()``
+— two host syncs per batch and a CPU/PIL data pipeline.  Here the only host
+work per step is one 1 KB index copy and a graph replay.
+"""
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from ..models import build_model
+from ..ops import kernels as K
+from ..parallel.ddp import BucketedGradReducer, broadcast_parameters
+from .executor import MobileNetV2Executor
+
+
+class NativeTrainStep:
+    def __init__(self, model, batch: int, device: torch.device, img_size: int = 224, lr: float = 1e-4,
+                 betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, world_size: int = 1,
+                 rank: int = 0, use_graph: bool = True, seed: int = 0, bucket_mb: float = 4.0,
+                 first_bucket_mb: float = 1.0, reduce_dtype: torch.dtype = torch.float32,
+                 double_resize: bool = True, augment: bool = True):
+        self.device, self.B, self.S = device, batch, img_size
+        self.world, self.rank = world_size, rank
+        self.exe = MobileNetV2Executor(model, batch, img_size, device, dropout_seed=(seed * 7919) ^ rank)
+        self.flat = self.exe.flat
+        self.betas, self.eps, self.wd = betas, eps, weight_decay
+        self.seed = seed
+        self.double_resize = double_resize
+        self.augment_enabled = augment
+        self.hyper = self.exe.hyper
+        self.hyper[0] = lr
+        self.metrics = torch.zeros(3, dtype=torch.float64, device=device)
+        self.idx = torch.zeros(batch, dtype=torch.int64, device=device)
+        self.aug_params = torch.zeros(batch, K.AUG_NPARAMS, dtype=torch.float32, device=device)
+        self.src = None
+        self.src_labels = None
+        self.epoch_ctr = 0
+        # ---- data parallel
+        self.reducer = None
+        if world_size > 1:
+            ranges = [(n,) + self.flat.range_of(n) for n in self.flat.order]
+            self.reducer = BucketedGradReducer(self.flat.grad, ranges, bucket_mb, first_bucket_mb, reduce_dtype)
+            self.exe.on_params_ready = self.reducer.mark_ready
+            self.sync_from_rank0()
+        # RCCL collectives are issued eagerly between graph segments; a single-graph
+        # capture is used on one GPU
+        self.use_graph = use_graph and world_size == 1
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self._eager_runs = 0
+
+    # ------------------------------------------------------------------ setup
+    @classmethod
+    def for_benchmark(cls, model_name: str, batch: int, device, img_size=224, use_graph=True,
+                      world_size=1, rank=0, n_data=50000):
+        if model_name != "mobilenet_v2":
+            raise NotImplementedError("native executor implements mobilenet_v2; use --backend torch for "
+                                      f"{model_name}")
+        torch.manual_seed(42)  # identical random-init weights on every rank (then rank-0 broadcast)
+        model = build_model("mobilenet_v2", num_classes=10)
+        st = cls(model, batch, device, img_size=img_size, world_size=world_size, rank=rank,
+                 use_graph=use_graph, seed=42)
+        g = torch.Generator(device=device).manual_seed(1234 + rank)
+        src = torch.randint(0, 256, (n_data, 32, 32, 3), dtype=torch.uint8, device=device, generator=g)
+        labels = torch.randint(0, 10, (n_data,), dtype=torch.int64, device=device, generator=g)
+        st.set_data(src, labels)
+        st._perm = torch.randperm(n_data, device=device, generator=g)
+        st._pos = 0
+        return st
+
+    def set_data(self, src_u8: torch.Tensor, labels: torch.Tensor):
+        assert src_u8.is_cuda and src_u8.dtype == torch.uint8 and src_u8.shape[1:] == (32, 32, 3)
+        self.src = src_u8.contiguous()
+        self.src_labels = labels.to(self.device, torch.int64).contiguous()
+
+    def sync_from_rank0(self):
+        mods = [m for m in self.exe.model.modules() if isinstance(m, torch.nn.BatchNorm2d)]
+        bufs = [b for m in mods for b in (m.running_mean, m.running_var, m.num_batches_tracked)]
+        broadcast_parameters([self.flat.master] + bufs)
+        self.flat.refresh_shadow()
+
+    def set_lr(self, lr: float):
+        self.hyper[0:1].fill_(float(lr))
+
+    # ------------------------------------------------------------------ step
+    def _body(self):
+        exe = self.exe
+        K.step_begin(self.hyper)
+        if self.augment_enabled:
+            K.augment(self.src, self.idx, self.src_labels, exe.img, exe.labels, self.aug_params, train=True,
+                      double_resize=self.double_resize, seed=self.seed + 17 * self.rank, hyper=self.hyper,
+                      epoch_ctr=0, out_hw=self.S)
+        if self.reducer is not None:
+            self.reducer.begin()
+        exe.forward(train=True)
+        exe.backward()
+        if self.reducer is not None:
+            self.reducer.finish()
+        K.adam_flat(self.flat.master, self.flat.grad, self.flat.exp_avg, self.flat.exp_avg_sq,
+                    self.flat.shadow, self.hyper, self.betas[0], self.betas[1], self.eps, self.wd,
+                    1.0 / self.world)
+        K.reduce_metrics(exe.loss, exe.correct, self.B, self.metrics)
+
+    def run(self, idx: torch.Tensor):
+        """One training step on the batch ``src[idx]`` (idx: int64 [B] on device)."""
+        self.idx.copy_(idx, non_blocking=True)
+        if not self.use_graph:
+            self._body()
+            return
+        if self.graph is None:
+            if self._eager_runs < 2:   # warm-up: module loading / first-touch outside capture
+                self._eager_runs += 1
+                self._body()
+                return
+            torch.cuda.synchronize(self.device)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self._body()
+        self.graph.replay()
+
+    @property
+    def graph_enabled(self) -> bool:
+        return self.use_graph
+
+    def bench_step(self):
+        n = self._perm.numel()
+        if self._pos + self.B > n:
+            self._pos = 0
+        self.run(self._perm[self._pos:self._pos + self.B])
+        self._pos += self.B
+
+    # ------------------------------------------------------------------ metrics
+    def read_metrics(self, reset: bool = True):
+        """(sum loss, sum correct, count) accumulated on device since the last reset."""
+        v = self.metrics.tolist()
+        if reset:
+            self.metrics.zero_()
+        return v

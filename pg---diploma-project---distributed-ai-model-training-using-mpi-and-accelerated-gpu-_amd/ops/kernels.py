@@ -1,0 +1,259 @@
+"""Typed, validated Python entry points of the gfx950 HIP kernels.
+
+Each wrapper checks device / dtype / contiguity / shape invariants the kernel
+and its launch grid assume (a kernel that reads out of bounds can reset the
+whole GPU node, so the checks run on the host before every launch), then calls
+the native launcher on the current HIP stream (graph-capture safe: no
+allocation, no synchronisation inside).
+
+Activations are NHWC bf16 tensors viewed as [M, C]; per-channel BN vectors are
+fp32 [C]; BN partial-sum buffers are fp32 [P, 2, C].
+"""
+from typing import Optional
+
+import torch
+
+from ._lib import lib
+
+ACT_NONE, ACT_BN_RELU6, ACT_BN, PRO_BNBWD = 0, 1, 2, 3
+EPI_FWD, EPI_BWD_RELU6, EPI_BWD_LIN = 0, 1, 2
+AUG_NPARAMS = 16
+
+
+def _s() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t: Optional[torch.Tensor]) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def _chk(t: Optional[torch.Tensor], dtype, numel=None, name="tensor"):
+    if t is None:
+        return
+    if not t.is_cuda:
+        raise ValueError(f"{name}: expected a device tensor")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    if numel is not None and t.numel() < numel:
+        raise ValueError(f"{name}: has {t.numel()} elements, kernel needs {numel}")
+    if t.data_ptr() % 16:
+        raise ValueError(f"{name}: must be 16-byte aligned")
+
+
+BF16, F32 = torch.bfloat16, torch.float32
+
+
+# --------------------------------------------------------------------------- BN
+def bn_fwd_finalize(part, P, C, count, gamma, beta, eps, momentum, rmean, rvar, nbt, mean, rstd,
+                    scale, shift):
+    _chk(part, F32, P * 2 * C, "part")
+    for n, t in (("gamma", gamma), ("beta", beta), ("rmean", rmean), ("rvar", rvar), ("mean", mean),
+                 ("rstd", rstd), ("scale", scale), ("shift", shift)):
+        if t is not None and t.numel() < C:
+            raise ValueError(f"{n}: too small")
+    lib().bn_fwd_finalize(_p(part), P, C, float(count), _p(gamma), _p(beta), float(eps), float(momentum),
+                          _p(rmean), _p(rvar), _p(nbt), _p(mean), _p(rstd), _p(scale), _p(shift), _s())
+
+
+def bn_bwd_finalize(part, P, C, count, mean, rstd, gamma, coef, dgamma=None, dbeta=None):
+    _chk(part, F32, P * 2 * C, "part")
+    _chk(coef, F32, 3 * C, "coef")
+    lib().bn_bwd_finalize(_p(part), P, C, float(count), _p(mean), _p(rstd), _p(gamma), _p(coef),
+                          _p(dgamma), _p(dbeta), _s())
+
+
+def bn_apply(y, scale, shift, out, relu6=False, res=None):
+    M, C = y.shape
+    assert C % 8 == 0
+    _chk(y, BF16, M * C, "y")
+    _chk(out, BF16, M * C, "out")
+    _chk(res, BF16, M * C, "res")
+    lib().bn_apply(_p(y), _p(res), _p(scale), _p(shift), _p(out), M, C, bool(relu6), _s())
+
+
+# --------------------------------------------------------------------------- optimizer
+def adam_flat(p, g, m, v, pb, hyper, beta1, beta2, eps, weight_decay=0.0, grad_scale=1.0):
+    n = p.numel()
+    assert n % 4 == 0 and g.numel() == n and m.numel() == n and v.numel() == n
+    for t, nm in ((p, "p"), (g, "g"), (m, "m"), (v, "v")):
+        _chk(t, F32, n, nm)
+    _chk(pb, BF16, n, "pb")
+    lib().adam_flat(_p(p), _p(g), _p(m), _p(v), _p(pb), n, _p(hyper), float(beta1), float(beta2),
+                    float(eps), float(weight_decay), float(grad_scale), _s())
+
+
+def f32_to_bf16(x, y):
+    assert x.numel() == y.numel()
+    lib().f32_to_bf16(_p(x), _p(y), x.numel(), _s())
+
+
+def step_begin(hyper):
+    lib().step_begin(_p(hyper), _s())
+
+
+def reduce_metrics(loss, correct, B, acc):
+    _chk(acc, torch.float64, 3, "acc")
+    lib().reduce_metrics(_p(loss), _p(correct), B, _p(acc), _s())
+
+
+# --------------------------------------------------------------------------- depthwise
+def dw_out_hw(H, W, stride):
+    return (H - 1) // stride + 1, (W - 1) // stride + 1
+
+
+def dw_num_partials(kind, B, H, W, C, stride):
+    f = {"fwd": lib().dw_fwd_num_partials, "dgrad": lib().dw_dgrad_num_partials,
+         "wgrad": lib().dw_wgrad_num_partials}[kind]
+    return f(B, H, W, C, stride)
+
+
+def _dw_check(B, H, W, C, stride):
+    if C % 8 or C // 8 > 256:
+        raise ValueError(f"depthwise: C={C} must be a multiple of 8 and <= 2048")
+    if stride not in (1, 2):
+        raise ValueError("depthwise: stride must be 1 or 2")
+
+
+def dw_fwd(x, in_s, in_t, act, w, y, part, B, H, W, C, stride):
+    _dw_check(B, H, W, C, stride)
+    Ho, Wo = dw_out_hw(H, W, stride)
+    _chk(x, BF16, B * H * W * C, "x")
+    _chk(w, BF16, C * 9, "w")
+    _chk(y, BF16, B * Ho * Wo * C, "y")
+    _chk(part, F32, dw_num_partials("fwd", B, H, W, C, stride) * 2 * C, "part")
+    lib().dw_fwd(_p(x), _p(in_s), _p(in_t), int(act), _p(w), _p(y), _p(part), B, H, W, C, stride, _s())
+
+
+def dw_dgrad(g, yself, coef, w, yprev, ps, pt, gout, part, B, H, W, C, stride):
+    _dw_check(B, H, W, C, stride)
+    Ho, Wo = dw_out_hw(H, W, stride)
+    _chk(g, BF16, B * Ho * Wo * C, "g")
+    _chk(yself, BF16, B * Ho * Wo * C, "yself")
+    _chk(yprev, BF16, B * H * W * C, "yprev")
+    _chk(gout, BF16, B * H * W * C, "gout")
+    _chk(part, F32, dw_num_partials("dgrad", B, H, W, C, stride) * 2 * C, "part")
+    lib().dw_dgrad(_p(g), _p(yself), _p(coef), _p(w), _p(yprev), _p(ps), _p(pt), _p(gout), _p(part),
+                   B, H, W, C, stride, _s())
+
+
+def dw_wgrad(g, yself, coef, yprev, ps, pt, part, grad, B, H, W, C, stride):
+    _dw_check(B, H, W, C, stride)
+    Ho, Wo = dw_out_hw(H, W, stride)
+    _chk(g, BF16, B * Ho * Wo * C, "g")
+    _chk(yprev, BF16, B * H * W * C, "yprev")
+    _chk(part, F32, dw_num_partials("wgrad", B, H, W, C, stride) * 9 * C, "part")
+    _chk(grad, F32, 9 * C, "grad")
+    lib().dw_wgrad(_p(g), _p(yself), _p(coef), _p(yprev), _p(ps), _p(pt), _p(part), _p(grad),
+                   B, H, W, C, stride, _s())
+
+
+# --------------------------------------------------------------------------- pointwise
+def pw_num_partials(M, N):
+    return lib().pw_gemm_num_partials(M, N)
+
+
+def pw_gemm(pro, epi, A, W, out, part, M, N, K, A2=None, pa=None, pb=None, pc=None, Yt=None,
+            es=None, et=None, R=None):
+    """out[M,N] = prologue(A)[M,K] @ W^T, W [N,K] (fwd) or W [K,N] (pro == PRO_BNBWD)."""
+    if K % 8 or N % 8:
+        raise ValueError(f"pw_gemm: K={K}, N={N} must be multiples of 8")
+    _chk(A, BF16, M * K, "A")
+    _chk(A2, BF16, M * K, "A2")
+    _chk(W, BF16, N * K, "W")
+    _chk(out, BF16, M * N, "out")
+    _chk(Yt, BF16, M * N, "Yt")
+    _chk(R, BF16, M * N, "R")
+    _chk(part, F32, pw_num_partials(M, N) * 2 * N, "part")
+    if pro in (ACT_BN_RELU6, PRO_BNBWD):
+        assert pa is not None and pb is not None and pa.numel() >= K
+    if pro == PRO_BNBWD:
+        assert A2 is not None and pc is not None
+    if epi in (EPI_BWD_RELU6, EPI_BWD_LIN):
+        assert Yt is not None
+    if epi == EPI_BWD_RELU6:
+        assert es is not None and et is not None
+    lib().pw_gemm(int(pro), int(epi), _p(A), _p(A2), _p(pa), _p(pb), _p(pc), _p(W), _p(out), _p(Yt),
+                  _p(es), _p(et), _p(R), _p(part), M, N, K, _s())
+
+
+def pw_wgrad_workspace(M, N, K):
+    return lib().pw_wgrad_workspace_floats(M, N, K)
+
+
+def pw_wgrad(G, Y, ga, gb, gc, X, xs, xt, xact, part, grad, M, N, K):
+    _chk(G, BF16, M * N, "G")
+    _chk(Y, BF16, M * N, "Y")
+    _chk(X, BF16, M * K, "X")
+    _chk(part, F32, pw_wgrad_workspace(M, N, K), "part")
+    _chk(grad, F32, N * K, "grad")
+    lib().pw_wgrad(_p(G), _p(Y), _p(ga), _p(gb), _p(gc), _p(X), _p(xs), _p(xt), int(xact), _p(part),
+                   _p(grad), M, N, K, _s())
+
+
+# --------------------------------------------------------------------------- stem
+def stem_num_partials(B, H, W):
+    return lib().stem_fwd_num_partials(B, H, W)
+
+
+def stem_fwd(img, w, y, part, B, H, W):
+    Ho, Wo = dw_out_hw(H, W, 2)
+    _chk(img, BF16, B * H * W * 4, "img")
+    _chk(w, BF16, 32 * 27, "w")
+    _chk(y, BF16, B * Ho * Wo * 32, "y")
+    _chk(part, F32, stem_num_partials(B, H, W) * 2 * 32, "part")
+    lib().stem_fwd(_p(img), _p(w), _p(y), _p(part), B, H, W, _s())
+
+
+def stem_wgrad_workspace(B, H, W, O=32):
+    Ho, Wo = dw_out_hw(H, W, 2)
+    return lib().stem_wgrad_workspace_floats(B * Ho * Wo, O)
+
+
+def stem_wgrad(G, Y, ga, gb, gc, img, part, grad, B, H, W, O=32):
+    Ho, Wo = dw_out_hw(H, W, 2)
+    _chk(G, BF16, B * Ho * Wo * O, "G")
+    _chk(img, BF16, B * H * W * 4, "img")
+    _chk(part, F32, stem_wgrad_workspace(B, H, W, O), "part")
+    _chk(grad, F32, O * 27, "grad")
+    lib().stem_wgrad(_p(G), _p(Y), _p(ga), _p(gb), _p(gc), _p(img), _p(part), _p(grad), B, H, W, O, _s())
+
+
+# --------------------------------------------------------------------------- head
+def head(y, s, t, Wl, bl, labels, B, HW, C, NC, drop_p, seed, hyper, train, loss_scale,
+         logits=None, loss=None, correct=None, dlogits=None, pd=None, g_out=None, part=None,
+         dW=None, db=None):
+    if NC > 16 or C % 8 or C // 8 > 256:
+        raise ValueError("head kernel supports NC <= 16 and C <= 2048 (C % 8 == 0)")
+    _chk(y, BF16, B * HW * C, "y")
+    _chk(Wl, F32, NC * C, "Wl")
+    if train:
+        for t_, n in ((dlogits, "dlogits"), (pd, "pd"), (g_out, "g_out"), (part, "part"), (dW, "dW"),
+                      (db, "db")):
+            if t_ is None:
+                raise ValueError(f"head(train=True) needs {n}")
+        _chk(g_out, BF16, B * HW * C, "g_out")
+        _chk(part, F32, B * 2 * C, "part")
+    if labels is not None:
+        _chk(labels, torch.int64, B, "labels")
+    lib().head(_p(y), _p(s), _p(t), _p(Wl), _p(bl), _p(labels), B, HW, C, NC, float(drop_p),
+               int(seed) & ((1 << 64) - 1), _p(hyper), int(bool(train)), float(loss_scale), _p(logits),
+               _p(loss), _p(correct), _p(dlogits), _p(pd), _p(g_out), _p(part), _p(dW), _p(db), _s())
+
+
+# --------------------------------------------------------------------------- data
+def augment(src, idx, labels_src, out, labels_out, params_out, train=True, double_resize=True,
+            seed=0, hyper=None, epoch_ctr=0, given_params=None, out_hw=224):
+    """uint8 [N,32,32,3] (device) gathered by idx [B] -> normalised NHWC4 bf16 [B,S,S,4]."""
+    B = idx.numel()
+    if src.dtype != torch.uint8 or tuple(src.shape[1:]) != (32, 32, 3) or not src.is_contiguous():
+        raise ValueError("augment: src must be contiguous uint8 [N,32,32,3]")
+    _chk(idx, torch.int64, B, "idx")
+    _chk(out, BF16, B * out_hw * out_hw * 4, "out")
+    _chk(params_out, F32, B * AUG_NPARAMS, "params_out")
+    _chk(given_params, F32, B * AUG_NPARAMS, "given_params")
+    lib().augment(_p(src), _p(idx), _p(labels_src), src.shape[0], B, out_hw, int(bool(train)),
+                  int(bool(double_resize)), _p(given_params), int(seed) & ((1 << 64) - 1), _p(hyper),
+                  int(epoch_ctr), _p(out), _p(labels_out), _p(params_out), _s())

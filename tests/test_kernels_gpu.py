@@ -1,0 +1,384 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op.
+
+Inputs are bf16-representable (kernels read bf16 storage); the reference runs in
+fp32 on those exact values, so the residual error is the kernels' own bf16
+output rounding and fp32 accumulation order.
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from pgdist.ops import kernels as K  # noqa: E402
+
+
+def bf(t):
+    return t.to(torch.bfloat16)
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def rnd(*shape, dev, scale=1.0, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(dev)
+
+
+def bn_params(C, dev, seed=1):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    s = (torch.rand(C, generator=g) + 0.5).to(dev)
+    t = (torch.rand(C, generator=g) - 0.5).to(dev)
+    return s.contiguous(), t.contiguous()
+
+
+def relu6(x):
+    return x.clamp(0, 6)
+
+
+def sum_parts(part, P, C, nv=2):
+    return part[: P * nv * C].view(P, nv, C).sum(0)
+
+
+# ----------------------------------------------------------------------------- BN
+def test_bn_finalize_and_apply(dev):
+    M, C = 5000, 96
+    y = bf(rnd(M, C, dev=dev) * 2 + 0.3)
+    P = 7
+    chunks = torch.tensor_split(y.float(), P, dim=0)
+    part = torch.stack([torch.stack([c.sum(0), (c * c).sum(0)]) for c in chunks]).contiguous()
+    gamma, beta = bn_params(C, dev, 3)
+    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    nbt = torch.zeros(1, dtype=torch.int64, device=dev)
+    mean, rstd, scale, shift = [torch.empty(C, device=dev) for _ in range(4)]
+    K.bn_fwd_finalize(part, P, C, M, gamma, beta, 1e-5, 0.1, rm, rv, nbt, mean, rstd, scale, shift)
+    ref = torch.nn.BatchNorm2d(C).to(dev)
+    with torch.no_grad():
+        ref.weight.copy_(gamma)
+        ref.bias.copy_(beta)
+    out_ref = ref(y.float().t().reshape(1, C, M, 1)).reshape(C, M).t()
+    torch.cuda.synchronize()
+    assert torch.allclose(rm, ref.running_mean, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(rv, ref.running_var, rtol=1e-4, atol=1e-5)
+    assert int(nbt.item()) == 1
+    out = torch.empty_like(y)
+    K.bn_apply(y, scale, shift, out, relu6=True)
+    assert rel(out, relu6(out_ref)) < 1e-2
+    res = bf(rnd(M, C, dev=dev, seed=5))
+    K.bn_apply(y, scale, shift, out, relu6=False, res=res)
+    assert rel(out, out_ref + res.float()) < 1e-2
+
+
+def test_bn_bwd_finalize_matches_autograd(dev):
+    M, C = 4096, 64
+    y = bf(rnd(M, C, dev=dev) * 1.5 + 0.2).float()
+    gamma, beta = bn_params(C, dev, 4)
+    g = bf(rnd(M, C, dev=dev, seed=9)).float()
+    yy = y.clone().requires_grad_(True)
+    ga = gamma.clone().requires_grad_(True)
+    be = beta.clone().requires_grad_(True)
+    out = F.batch_norm(yy.t().reshape(1, C, M, 1), None, None, ga, be, training=True, eps=1e-5)
+    out.backward(g.t().reshape(1, C, M, 1))
+    mean = y.mean(0)
+    rstd = torch.rsqrt(y.var(0, unbiased=False) + 1e-5)
+    part = torch.stack([g.sum(0), (g * y).sum(0)]).unsqueeze(0).contiguous()
+    coef = torch.empty(3, C, device=dev)
+    dgam, dbet = torch.empty(C, device=dev), torch.empty(C, device=dev)
+    K.bn_bwd_finalize(part, 1, C, M, mean.contiguous(), rstd.contiguous(), gamma, coef, dgam, dbet)
+    dy = coef[0] * g + coef[1] * y + coef[2]
+    assert rel(dy, yy.grad) < 1e-4
+    assert rel(dgam, ga.grad) < 1e-4
+    assert rel(dbet, be.grad) < 1e-4
+
+
+# ----------------------------------------------------------------------------- depthwise
+DW_CASES = [(2, 14, 14, 32, 1), (2, 14, 14, 96, 2), (3, 28, 28, 144, 1), (2, 7, 7, 960, 1),
+            (2, 56, 56, 96, 2), (1, 28, 28, 576, 2), (2, 9, 9, 24, 1), (2, 10, 10, 16, 2)]
+
+
+@pytest.mark.parametrize("B,H,W,C,stride", DW_CASES)
+def test_dw_fwd(dev, B, H, W, C, stride):
+    x = bf(rnd(B, H, W, C, dev=dev, seed=B + C))
+    s, t = bn_params(C, dev)
+    w = bf(rnd(C, 1, 3, 3, dev=dev, seed=3) * 0.3)
+    Ho, Wo = K.dw_out_hw(H, W, stride)
+    y = torch.empty(B, Ho, Wo, C, dtype=torch.bfloat16, device=dev)
+    P = K.dw_num_partials("fwd", B, H, W, C, stride)
+    part = torch.zeros(P * 2 * C, device=dev)
+    K.dw_fwd(x, s, t, K.ACT_BN_RELU6, w, y, part, B, H, W, C, stride)
+    z = relu6(x.float() * s + t).permute(0, 3, 1, 2)
+    ref = F.conv2d(z, w.float(), stride=stride, padding=1, groups=C).permute(0, 2, 3, 1)
+    assert rel(y, ref) < 8e-3
+    st = sum_parts(part, P, C)
+    r2 = ref.reshape(-1, C)
+    assert rel(st[0], r2.sum(0)) < 1e-3
+    assert rel(st[1], (r2 * r2).sum(0)) < 1e-3
+
+
+@pytest.mark.parametrize("B,H,W,C,stride", DW_CASES)
+def test_dw_dgrad_wgrad(dev, B, H, W, C, stride):
+    yprev = bf(rnd(B, H, W, C, dev=dev, seed=11))
+    s, t = bn_params(C, dev, 2)
+    w = bf(rnd(C, 1, 3, 3, dev=dev, seed=3) * 0.3)
+    Ho, Wo = K.dw_out_hw(H, W, stride)
+    g = bf(rnd(B, Ho, Wo, C, dev=dev, seed=12))
+    yself = bf(rnd(B, Ho, Wo, C, dev=dev, seed=13))
+    coef = torch.stack([torch.rand(C, device=dev) + 0.5, torch.rand(C, device=dev) - 0.5,
+                        torch.rand(C, device=dev) - 0.5]).contiguous()
+    dy = (coef[0] * g.float() + coef[1] * yself.float() + coef[2]).permute(0, 3, 1, 2)
+    z = relu6(yprev.float() * s + t).permute(0, 3, 1, 2)
+    dz = torch.nn.grad.conv2d_input(z.shape, w.float(), dy, stride=stride, padding=1, groups=C)
+    a = yprev.float() * s + t
+    mask = ((a > 0) & (a < 6)).float()
+    gref = dz.permute(0, 2, 3, 1) * mask
+    gout = torch.empty(B, H, W, C, dtype=torch.bfloat16, device=dev)
+    P = K.dw_num_partials("dgrad", B, H, W, C, stride)
+    part = torch.zeros(P * 2 * C, device=dev)
+    K.dw_dgrad(g, yself, coef, w, yprev, s, t, gout, part, B, H, W, C, stride)
+    assert rel(gout, gref) < 8e-3
+    st = sum_parts(part, P, C)
+    assert rel(st[0], gref.reshape(-1, C).sum(0)) < 2e-2
+    assert rel(st[1], (gref * yprev.float()).reshape(-1, C).sum(0)) < 2e-2
+    # wgrad
+    wref = torch.nn.grad.conv2d_weight(z, w.shape, dy, stride=stride, padding=1, groups=C)
+    Pw = K.dw_num_partials("wgrad", B, H, W, C, stride)
+    wpart = torch.zeros(Pw * 9 * C, device=dev)
+    grad = torch.empty(C * 9, device=dev)
+    K.dw_wgrad(g, yself, coef, yprev, s, t, wpart, grad, B, H, W, C, stride)
+    assert rel(grad.view(C, 1, 3, 3), wref) < 1e-3
+
+
+# ----------------------------------------------------------------------------- pointwise
+PW_CASES = [(1000, 16, 96), (4096, 24, 144), (777, 96, 24), (3000, 320, 1280), (2048, 160, 960),
+            (513, 32, 32), (6272, 960, 160), (256, 64, 384)]
+
+
+@pytest.mark.parametrize("M,K_,N", PW_CASES)
+@pytest.mark.parametrize("pro", [K.ACT_NONE, K.ACT_BN_RELU6])
+def test_pw_fwd(dev, M, K_, N, pro):
+    A = bf(rnd(M, K_, dev=dev, seed=M))
+    s, t = bn_params(K_, dev)
+    W = bf(rnd(N, K_, dev=dev, seed=5) / math.sqrt(K_))
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    P = K.pw_num_partials(M, N)
+    part = torch.zeros(P * 2 * N, device=dev)
+    K.pw_gemm(pro, K.EPI_FWD, A, W, out, part, M, N, K_, pa=s, pb=t)
+    x = relu6(A.float() * s + t) if pro == K.ACT_BN_RELU6 else A.float()
+    ref = x @ W.float().t()
+    assert rel(out, ref) < 8e-3
+    st = sum_parts(part, P, N)
+    assert rel(st[0], ref.sum(0)) < 1e-2
+    assert rel(st[1], (ref * ref).sum(0)) < 1e-2
+
+
+@pytest.mark.parametrize("M,Kf,Nf", PW_CASES)
+@pytest.mark.parametrize("epi", [K.EPI_BWD_RELU6, K.EPI_BWD_LIN])
+def test_pw_dgrad(dev, M, Kf, Nf, epi):
+    # forward conv: [M,Kf] -> [M,Nf], weight [Nf][Kf]; dgrad produces [M,Kf]
+    G = bf(rnd(M, Nf, dev=dev, seed=1))
+    Y = bf(rnd(M, Nf, dev=dev, seed=2))
+    coef = torch.stack([torch.rand(Nf, device=dev) + 0.5, torch.rand(Nf, device=dev) - 0.5,
+                        torch.rand(Nf, device=dev) - 0.5]).contiguous()
+    W = bf(rnd(Nf, Kf, dev=dev, seed=5) / math.sqrt(Nf))
+    Yt = bf(rnd(M, Kf, dev=dev, seed=6))
+    es, et = bn_params(Kf, dev, 7)
+    R = bf(rnd(M, Kf, dev=dev, seed=8)) if epi == K.EPI_BWD_LIN else None
+    out = torch.empty(M, Kf, dtype=torch.bfloat16, device=dev)
+    P = K.pw_num_partials(M, Kf)
+    part = torch.zeros(P * 2 * Kf, device=dev)
+    K.pw_gemm(K.PRO_BNBWD, epi, G, W, out, part, M, Kf, Nf, A2=Y, pa=coef[0], pb=coef[1], pc=coef[2],
+              Yt=Yt, es=es, et=et, R=R)
+    dy = coef[0] * G.float() + coef[1] * Y.float() + coef[2]
+    ref = dy @ W.float()
+    if epi == K.EPI_BWD_RELU6:
+        a = Yt.float() * es + et
+        ref = ref * ((a > 0) & (a < 6)).float()
+    else:
+        ref = ref + R.float()
+    assert rel(out, ref) < 8e-3
+    st = sum_parts(part, P, Kf)
+    assert rel(st[0], ref.sum(0)) < 2e-2
+    assert rel(st[1], (ref * Yt.float()).sum(0)) < 2e-2
+
+
+@pytest.mark.parametrize("M,Kf,Nf", PW_CASES)
+@pytest.mark.parametrize("xact", [K.ACT_NONE, K.ACT_BN_RELU6])
+def test_pw_wgrad(dev, M, Kf, Nf, xact):
+    G = bf(rnd(M, Nf, dev=dev, seed=1))
+    Y = bf(rnd(M, Nf, dev=dev, seed=2))
+    coef = torch.stack([torch.rand(Nf, device=dev) + 0.5, torch.rand(Nf, device=dev) - 0.5,
+                        torch.rand(Nf, device=dev) - 0.5]).contiguous()
+    X = bf(rnd(M, Kf, dev=dev, seed=3))
+    xs, xt = bn_params(Kf, dev, 4)
+    ws = torch.zeros(K.pw_wgrad_workspace(M, Nf, Kf), device=dev)
+    grad = torch.empty(Nf * Kf, device=dev)
+    K.pw_wgrad(G, Y, coef[0], coef[1], coef[2], X, xs, xt, xact, ws, grad, M, Nf, Kf)
+    dy = coef[0] * G.float() + coef[1] * Y.float() + coef[2]
+    x = relu6(X.float() * xs + xt) if xact == K.ACT_BN_RELU6 else X.float()
+    # bf16 operands inside the MFMA: compare against the bf16-rounded operands
+    ref = bf(dy).float().t() @ bf(x).float()
+    assert rel(grad.view(Nf, Kf), ref) < 2e-3
+
+
+# ----------------------------------------------------------------------------- stem
+@pytest.mark.parametrize("B,S", [(2, 32), (3, 64), (2, 224)])
+def test_stem(dev, B, S):
+    img = torch.zeros(B, S, S, 4, dtype=torch.bfloat16, device=dev)
+    img[..., :3] = bf(rnd(B, S, S, 3, dev=dev, seed=1))
+    w = bf(rnd(32, 3, 3, 3, dev=dev, seed=2) * 0.2)
+    Ho = (S - 1) // 2 + 1
+    y = torch.empty(B, Ho, Ho, 32, dtype=torch.bfloat16, device=dev)
+    P = K.stem_num_partials(B, S, S)
+    part = torch.zeros(P * 2 * 32, device=dev)
+    K.stem_fwd(img, w, y, part, B, S, S)
+    x = img[..., :3].float().permute(0, 3, 1, 2)
+    ref = F.conv2d(x, w.float(), stride=2, padding=1).permute(0, 2, 3, 1)
+    assert rel(y, ref) < 8e-3
+    st = sum_parts(part, P, 32)
+    assert rel(st[0], ref.reshape(-1, 32).sum(0)) < 1e-3
+    # wgrad
+    G = bf(rnd(B, Ho, Ho, 32, dev=dev, seed=3))
+    Y = bf(rnd(B, Ho, Ho, 32, dev=dev, seed=4))
+    coef = torch.stack([torch.rand(32, device=dev) + 0.5, torch.rand(32, device=dev) - 0.5,
+                        torch.rand(32, device=dev) - 0.5]).contiguous()
+    dy = coef[0] * G.float() + coef[1] * Y.float() + coef[2]
+    ws = torch.zeros(K.stem_wgrad_workspace(B, S, S), device=dev)
+    grad = torch.empty(32 * 27, device=dev)
+    K.stem_wgrad(G, Y, coef[0], coef[1], coef[2], img, ws, grad, B, S, S)
+    wref = torch.nn.grad.conv2d_weight(x, w.shape, bf(dy).float().permute(0, 3, 1, 2), stride=2, padding=1)
+    assert rel(grad.view(32, 3, 3, 3), wref) < 2e-3
+
+
+# ----------------------------------------------------------------------------- head
+@pytest.mark.parametrize("train", [True, False])
+def test_head(dev, train):
+    B, HW, C, NC = 6, 49, 1280, 10
+    y = bf(rnd(B, HW, C, dev=dev, seed=1) * 3)
+    s, t = bn_params(C, dev, 2)
+    Wl = (rnd(NC, C, dev=dev, seed=3) * 0.05).contiguous()
+    bl = (rnd(NC, dev=dev, seed=4) * 0.1).contiguous()
+    labels = torch.randint(0, NC, (B,), device=dev)
+    f32 = dict(device=dev, dtype=torch.float32)
+    logits, loss, correct = torch.zeros(B, NC, **f32), torch.zeros(B, **f32), torch.zeros(B, **f32)
+    dlog, pd = torch.zeros(B, NC, **f32), torch.zeros(B, C, **f32)
+    g = torch.empty(B, HW, C, dtype=torch.bfloat16, device=dev)
+    part = torch.zeros(B * 2 * C, **f32)
+    dW, db = torch.zeros(NC * C, **f32), torch.zeros(NC, **f32)
+    K.head(y, s, t, Wl, bl, labels, B, HW, C, NC, 0.0, 0, None, train, 1.0 / B, logits=logits, loss=loss,
+           correct=correct, dlogits=dlog, pd=pd, g_out=g, part=part, dW=dW, db=db)
+    yy = y.float().clone().requires_grad_(True)
+    W_ = Wl.clone().requires_grad_(True)
+    b_ = bl.clone().requires_grad_(True)
+    z = relu6(yy * s + t)
+    pooled = z.mean(1)
+    lg = pooled @ W_.t() + b_
+    L = F.cross_entropy(lg, labels)
+    assert rel(logits, lg) < 1e-4
+    assert abs(loss.mean().item() - L.item()) < 1e-4
+    assert torch.equal(correct.bool(), lg.argmax(1) == labels)
+    if train:
+        L.backward()
+        # g is the gradient w.r.t. the pre-activation a (= relu6 mask applied)
+        a = y.float() * s + t
+        mask = ((a > 0) & (a < 6)).float()
+        dpool = (torch.softmax(lg, 1) - F.one_hot(labels, NC)).detach() / B @ Wl
+        gref = dpool[:, None, :] / HW * mask
+        assert rel(g, gref) < 8e-3
+        assert rel(dW.view(NC, C), W_.grad) < 1e-4
+        assert rel(db, b_.grad) < 1e-4
+        st = sum_parts(part, B, C).float()
+        assert rel(st[0], gref.reshape(-1, C).sum(0)) < 1e-2
+
+
+# ----------------------------------------------------------------------------- adam
+def test_adam_matches_torch(dev):
+    n = 4096
+    p0 = rnd(n, dev=dev, seed=1)
+    p = p0.clone()
+    m, v = torch.zeros(n, device=dev), torch.zeros(n, device=dev)
+    pb = torch.empty(n, dtype=torch.bfloat16, device=dev)
+    ref = p0.clone().requires_grad_(True)
+    opt = torch.optim.Adam([ref], lr=1e-3)
+    hyper = torch.tensor([1e-3, 0.0], device=dev)
+    for it in range(5):
+        g = rnd(n, dev=dev, seed=10 + it)
+        ref.grad = g.clone()
+        opt.step()
+        hyper[1] += 1
+        K.adam_flat(p, g * 2.0, m, v, pb, hyper, 0.9, 0.999, 1e-8, 0.0, grad_scale=0.5)
+    assert rel(p, ref.detach()) < 1e-6
+    assert rel(pb, ref.detach()) < 5e-3
+
+
+# ----------------------------------------------------------------------------- augment
+def test_augment_eval_matches_bilinear_resize(dev):
+    N, B, S = 10, 4, 224
+    src = torch.randint(0, 256, (N, 32, 32, 3), dtype=torch.uint8, device=dev)
+    labels = torch.arange(N, device=dev)
+    idx = torch.tensor([3, 1, 7, 3], device=dev)
+    out = torch.empty(B, S, S, 4, dtype=torch.bfloat16, device=dev)
+    lab = torch.empty(B, dtype=torch.int64, device=dev)
+    prm = torch.empty(B, K.AUG_NPARAMS, device=dev)
+    K.augment(src, idx, labels, out, lab, prm, train=False)
+    x = src[idx].permute(0, 3, 1, 2).float() / 255
+    ref = F.interpolate(x, size=(S, S), mode="bilinear", align_corners=False)
+    mean = torch.tensor([0.485, 0.456, 0.406], device=dev).view(1, 3, 1, 1)
+    std = torch.tensor([0.229, 0.224, 0.225], device=dev).view(1, 3, 1, 1)
+    ref = ((ref - mean) / std).permute(0, 2, 3, 1)
+    assert rel(out[..., :3], ref) < 5e-3
+    assert torch.all(out[..., 3] == 0)
+    assert torch.equal(lab, labels[idx])
+
+
+def test_augment_train_param_distribution(dev):
+    N, B, S = 64, 256, 224
+    src = torch.randint(0, 256, (N, 32, 32, 3), dtype=torch.uint8, device=dev)
+    labels = torch.zeros(N, dtype=torch.int64, device=dev)
+    idx = torch.randint(0, N, (B,), device=dev)
+    out = torch.empty(B, S, S, 4, dtype=torch.bfloat16, device=dev)
+    lab = torch.empty(B, dtype=torch.int64, device=dev)
+    prm = torch.empty(B, K.AUG_NPARAMS, device=dev)
+    hyper = torch.tensor([0.0, 5.0], device=dev)
+    K.augment(src, idx, labels, out, lab, prm, train=True, seed=3, hyper=hyper)
+    p = prm.cpu()
+    area = p[:, 2] * p[:, 3] / (S * S)
+    assert area.min() >= 0.69 and area.max() <= 1.0
+    ratio = p[:, 3] / p[:, 2]
+    assert ratio.min() >= 0.74 and ratio.max() <= 1.34
+    assert (p[:, 0] + p[:, 2] <= S).all() and (p[:, 1] + p[:, 3] <= S).all()
+    assert 0.3 < p[:, 4].mean() < 0.7
+    for col in (5, 6, 7):
+        assert p[:, col].min() >= 0.7 and p[:, col].max() <= 1.3
+    assert p[:, 8].abs().max() <= 0.1 and p[:, 10].abs().max() <= 15
+    assert torch.isfinite(out.float()).all()
+    # same seed + step -> identical params; next step -> different
+    prm2 = torch.empty_like(prm)
+    K.augment(src, idx, labels, out, lab, prm2, train=True, seed=3, hyper=hyper)
+    assert torch.equal(prm, prm2)
+    hyper[1] += 1
+    K.augment(src, idx, labels, out, lab, prm2, train=True, seed=3, hyper=hyper)
+    assert not torch.equal(prm, prm2)
+
+
+def test_augment_flip_identity(dev):
+    N, B, S = 4, 2, 64
+    src = torch.randint(0, 256, (N, 32, 32, 3), dtype=torch.uint8, device=dev)
+    labels = torch.zeros(N, dtype=torch.int64, device=dev)
+    idx = torch.tensor([0, 2], device=dev)
+    ev = torch.empty(B, S, S, 4, dtype=torch.bfloat16, device=dev)
+    tr = torch.empty_like(ev)
+    lab = torch.empty(B, dtype=torch.int64, device=dev)
+    prm = torch.empty(B, K.AUG_NPARAMS, device=dev)
+    K.augment(src, idx, labels, ev, lab, prm, train=False, out_hw=S)
+    given = torch.zeros(B, K.AUG_NPARAMS, device=dev)
+    given[:, 2] = S
+    given[:, 3] = S
+    given[:, 4] = 1.0                       # flip
+    given[:, 5:8] = 1.0                     # identity jitter
+    given[:, 9] = 0 | (1 << 2) | (2 << 4) | (3 << 6)
+    K.augment(src, idx, labels, tr, lab, prm, train=True, given_params=given, out_hw=S)
+    assert rel(tr, ev.flip(2)) < 1e-3
