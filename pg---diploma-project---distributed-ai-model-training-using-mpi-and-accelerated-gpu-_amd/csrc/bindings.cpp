@@ -61,6 +61,7 @@ void launch_augment(const unsigned char *, const long long *, const long long *,
                     int, int, const float *, unsigned long long, const float *, int, bf16_t *,
                     long long *, float *, hipStream_t);
 void launch_step_begin(float *, hipStream_t);
+int colsum_rows(int);
 void launch_reduce_metrics(const float *, const float *, int, double *, hipStream_t);
 
 template <typename T>
@@ -76,6 +77,7 @@ PYBIND11_MODULE(_pgdist_C, m) {
   m.doc() = "pgdist native library: gfx950 HIP kernels + C++ runtime";
   m.attr("arch") = "gfx950";
   m.def("last_error", &last_error);
+  m.def("colsum_rows", &colsum_rows, "rows of level-1 scratch a reduction over R partial rows needs");
 
   // ---- BatchNorm ----
   m.def("bn_fwd_finalize", [](P part, int Pn, int C, float count, P gamma, P beta, float eps,

@@ -120,10 +120,17 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t *__restrict_
 // ---------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------
+void launch_colsum(const float *src, int R, long long n, float *dst, int &rows_out, hipStream_t st);
+
+// part: [P][2][C] followed by scratch for the level-1 fold (colsum_rows(P) * 2C floats)
 void launch_bn_fwd_finalize(const float *part, int P, int C, float count, const float *gamma,
                             const float *beta, float eps, float momentum, float *rmean,
                             float *rvar, long long *nbt, float *mean, float *rstd, float *scale,
                             float *shift, hipStream_t st) {
+  int rows = P;
+  float *tmp = const_cast<float *>(part) + (size_t)P * 2 * C;
+  launch_colsum(part, P, 2LL * C, tmp, rows, st);
+  if (rows != P) { part = tmp; P = rows; }
   hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, st, part, P, C,
                      count, gamma, beta, eps, momentum, rmean, rvar, nbt, mean, rstd, scale, shift);
 }
@@ -131,6 +138,10 @@ void launch_bn_fwd_finalize(const float *part, int P, int C, float count, const 
 void launch_bn_bwd_finalize(const float *part, int P, int C, float count, const float *mean,
                             const float *rstd, const float *gamma, float *coef, float *dgamma,
                             float *dbeta, hipStream_t st) {
+  int rows = P;
+  float *tmp = const_cast<float *>(part) + (size_t)P * 2 * C;
+  launch_colsum(part, P, 2LL * C, tmp, rows, st);
+  if (rows != P) { part = tmp; P = rows; }
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, st, part, P, C,
                      count, mean, rstd, gamma, coef, dgamma, dbeta);
 }

@@ -266,94 +266,91 @@ struct PwWgArgs {
   int M, N, K, rows_per_split;
   int ih, iw, oh, ow;           // IM2COL_STEM geometry (image H/W, output H/W)
 };
-constexpr int kWMK = 32;              // m rows per step
-constexpr int kWLD = kWMK + 8;        // transposed tile row pitch (elements): 80 B, conflict-free b128 reads
+constexpr int kWMK = 64;              // m rows per pipeline step
+constexpr int kWLD = kWMK + 8;        // transposed tile row pitch (elements): 144 B, conflict-free b128 reads
 }  // namespace
 
-// stage a [32 m][8*CHN cols] tile transposed into T[col][m] (pitch kWLD).
-// thread item = (m4 group of 4 rows, 8-col chunk); PRO transforms applied per element.
+// One staging item = 4 consecutive rows (m) x 8 consecutive columns of a [M][ld]
+// bf16 operand; it is loaded raw into registers one step ahead (prefetch) and
+// written transposed into LDS as T[col][m] (4 rows of m packed per 8-B store)
+// after the current step's MFMAs, with the BN transform applied on the way.
+struct WgItem {
+  uint4 a[4];   // rows of G (dy items) or X (x items)
+  uint4 b[4];   // rows of Y (dy items only)
+};
+
+template <bool DY>
+PG_DEVICE void wg_load(WgItem &it, const bf16_t *__restrict__ src, const bf16_t *__restrict__ src2,
+                       int ld, int ncols, int c, int m0, int M) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int m = m0 + q;
+    if (m < M && c < ncols) {
+      const size_t off = (size_t)m * ld + c;
+      it.a[q] = ldg16(src + off);
+      if constexpr (DY) it.b[q] = ldg16(src2 + off);
+    } else {
+      it.a[q] = make_uint4(0, 0, 0, 0);
+      if constexpr (DY) it.b[q] = make_uint4(0, 0, 0, 0);
+    }
+  }
+}
+
+// rows beyond M or columns beyond ncols must contribute exactly 0 after the transform
 template <int PRO>
-PG_DEVICE void wg_stage(const bf16_t *__restrict__ src, const bf16_t *__restrict__ src2,
-                        const float *pa, const float *pb, const float *pc, int ld, int ncols,
-                        int col0, int m0, int M, int tcols, bf16_t *T, int item) {
-  // item in [0, 8 * (tcols/8)) : m4 = item % 8, chunk = item / 8
-  const int m4 = item & 7, chunk = item >> 3;
-  const int c = col0 + chunk * 8;
+PG_DEVICE void wg_write(const WgItem &it, const float *pa, const float *pb, const float *pc, int ncols,
+                        int c, int m0, int M, bf16_t *T, int tcol, int tm) {
   float v[4][8];
   float aa[8], bb[8], cc[8];
   const bool cvalid = c < ncols;
-  if (PRO != ACT_NONE && cvalid) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      aa[j] = pa[c + j];
-      bb[j] = pb[c + j];
-      cc[j] = (PRO == PRO_BNBWD) ? pc[c + j] : 0.f;
-    }
+  for (int j = 0; j < 8; ++j) {
+    aa[j] = (PRO != ACT_NONE && cvalid) ? pa[c + j] : 0.f;
+    bb[j] = (PRO != ACT_NONE && cvalid) ? pb[c + j] : 0.f;
+    cc[j] = (PRO == PRO_BNBWD && cvalid) ? pc[c + j] : 0.f;
   }
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const int m = m0 + m4 * 4 + q;
-    if (m < M && cvalid) {
-      const size_t off = (size_t)m * ld + c;
-      unpack8(ldg16(src + off), v[q]);
-      if constexpr (PRO == PRO_BNBWD) {
-        float y[8];
-        unpack8(ldg16(src2 + off), y);
+    unpack8(it.a[q], v[q]);
+    const bool valid = (m0 + q < M) && cvalid;
+    if constexpr (PRO == PRO_BNBWD) {
+      float y[8];
+      unpack8(it.b[q], y);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[q][j] = fmaf(aa[j], v[q][j], fmaf(bb[j], y[j], cc[j]));
-      } else if constexpr (PRO == ACT_BN_RELU6) {
+      for (int j = 0; j < 8; ++j) v[q][j] = valid ? fmaf(aa[j], v[q][j], fmaf(bb[j], y[j], cc[j])) : 0.f;
+    } else if constexpr (PRO == ACT_BN_RELU6) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[q][j] = relu6f(fmaf(v[q][j], aa[j], bb[j]));
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[q][j] = 0.f;
+      for (int j = 0; j < 8; ++j) v[q][j] = valid ? relu6f(fmaf(v[q][j], aa[j], bb[j])) : 0.f;
     }
   }
-  // write transposed: T[chunk*8 + j][m4*4 .. +3] as one 8-byte store
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     uint2 w;
     w.x = pack2(v[0][j], v[1][j]);
     w.y = pack2(v[2][j], v[3][j]);
-    *reinterpret_cast<uint2 *>(T + (chunk * 8 + j) * kWLD + m4 * 4) = w;
+    *reinterpret_cast<uint2 *>(T + (tcol + j) * kWLD + tm) = w;
   }
 }
 
 // im2col of the stem input (NHWC, 4 channels incl. one zero pad channel, 3x3 s2 p1):
-// X[m][k], m -> (b, oh, ow), k = tap*4 + c, tap = kh*3 + kw;  K = 36.
-PG_DEVICE void wg_stage_im2col(const PwWgArgs &p, int m0, int M, bf16_t *T, int item) {
-  const int m4 = item & 7, chunk = item >> 3;
-  float v[4][8];
+// X[m][k], m -> (b, oh, ow), k = tap*4 + c, tap = kh*3 + kw;  K = 36.  Item = 4 rows x 2 taps.
+PG_DEVICE void wg_load_im2col(WgItem &it, const PwWgArgs &p, int chunk, int m0, int M) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const int m = m0 + m4 * 4 + q;
+    const int m = m0 + q;
     const int b = m / (p.oh * p.ow), rem = m % (p.oh * p.ow);
     const int oh = rem / p.ow, ow = rem % p.ow;
+    uint2 u[2] = {make_uint2(0, 0), make_uint2(0, 0)};
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int tap = chunk * 2 + h;
-      float f[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       if (m < M && tap < 9) {
         const int ih = oh * 2 - 1 + tap / 3, iw = ow * 2 - 1 + tap % 3;
-        if (ih >= 0 && ih < p.ih && iw >= 0 && iw < p.iw) {
-          const uint2 u = *reinterpret_cast<const uint2 *>(p.X + (((size_t)b * p.ih + ih) * p.iw + iw) * 4);
-          f[0] = __uint_as_float(u.x << 16);
-          f[1] = __uint_as_float(u.x & 0xffff0000u);
-          f[2] = __uint_as_float(u.y << 16);
-          f[3] = __uint_as_float(u.y & 0xffff0000u);
-        }
+        if (ih >= 0 && ih < p.ih && iw >= 0 && iw < p.iw)
+          u[h] = *reinterpret_cast<const uint2 *>(p.X + (((size_t)b * p.ih + ih) * p.iw + iw) * 4);
       }
-#pragma unroll
-      for (int c = 0; c < 4; ++c) v[q][h * 4 + c] = f[c];
     }
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    uint2 w;
-    w.x = pack2(v[0][j], v[1][j]);
-    w.y = pack2(v[2][j], v[3][j]);
-    *reinterpret_cast<uint2 *>(T + (chunk * 8 + j) * kWLD + m4 * 4) = w;
+    it.a[q] = make_uint4(u[0].x, u[0].y, u[1].x, u[1].y);
   }
 }
 
@@ -362,8 +359,12 @@ __global__ __launch_bounds__(256) void pw_wgrad_kernel(PwWgArgs p) {
   // output tile TN x TK split over 4 waves as 2 x 2 quadrants
   constexpr int QN = TN / 2, QK = TK / 2;
   constexpr int RN = QN / 16, RK = QK / 16;
-  __shared__ __attribute__((aligned(16))) bf16_t Tdy[TN * kWLD];
-  __shared__ __attribute__((aligned(16))) bf16_t Tx[TK * kWLD];
+  constexpr int M4 = kWMK / 4;                       // 4-row groups per step
+  constexpr int ITEMS_DY = M4 * (TN / 8), ITEMS_X = M4 * (TK / 8);
+  constexpr int ITEMS = ITEMS_DY + ITEMS_X;
+  constexpr int IPT = (ITEMS + 255) / 256;           // items per thread
+  __shared__ __attribute__((aligned(16))) bf16_t Tdy[2][TN * kWLD];
+  __shared__ __attribute__((aligned(16))) bf16_t Tx[2][TK * kWLD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave >> 1, wk = wave & 1;
   const int n0 = blockIdx.x * TN, k0 = blockIdx.y * TK;
@@ -376,31 +377,72 @@ __global__ __launch_bounds__(256) void pw_wgrad_kernel(PwWgArgs p) {
 #pragma unroll
     for (int b = 0; b < RK; ++b) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  constexpr int ITEMS_DY = 8 * (TN / 8), ITEMS_X = 8 * (TK / 8);
-  for (int m0 = mbeg; m0 < mend; m0 += kWMK) {
-    for (int it = tid; it < ITEMS_DY + ITEMS_X; it += 256) {
-      if (it < ITEMS_DY)
-        wg_stage<PRO_BNBWD>(p.G, p.Y, p.ga, p.gb, p.gc, p.N, p.N, n0, m0, mend, TN, Tdy, it);
-      else if constexpr (XPRO == IM2COL_STEM)
-        wg_stage_im2col(p, m0, mend, Tx, it - ITEMS_DY);
-      else
-        wg_stage<XPRO>(p.X, nullptr, p.xs, p.xt, nullptr, p.K, p.K, k0, m0, mend, TK, Tx, it - ITEMS_DY);
+  WgItem items[IPT];
+  auto load_step = [&](int m0) {
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      const int it = tid + i * 256;
+      if (it < ITEMS_DY) {
+        const int m4 = it % M4, chunk = it / M4;
+        wg_load<true>(items[i], p.G, p.Y, p.N, p.N, n0 + chunk * 8, m0 + m4 * 4, mend);
+      } else if (it < ITEMS) {
+        const int xi = it - ITEMS_DY;
+        const int m4 = xi % M4, chunk = xi / M4;
+        if constexpr (XPRO == IM2COL_STEM) wg_load_im2col(items[i], p, chunk, m0 + m4 * 4, mend);
+        else wg_load<false>(items[i], p.X, nullptr, p.K, p.K, k0 + chunk * 8, m0 + m4 * 4, mend);
+      }
     }
-    __syncthreads();
-    s16x8_t af[RN], bfr[RK];
+  };
+  auto write_step = [&](int m0, int buf) {
 #pragma unroll
-    for (int a = 0; a < RN; ++a)
-      af[a] = *reinterpret_cast<const s16x8_t *>(Tdy + (wn * QN + a * 16 + (lane & 15)) * kWLD + 8 * (lane >> 4));
+    for (int i = 0; i < IPT; ++i) {
+      const int it = tid + i * 256;
+      if (it < ITEMS_DY) {
+        const int m4 = it % M4, chunk = it / M4;
+        wg_write<PRO_BNBWD>(items[i], p.ga, p.gb, p.gc, p.N, n0 + chunk * 8, m0 + m4 * 4, mend, Tdy[buf],
+                            chunk * 8, m4 * 4);
+      } else if (it < ITEMS) {
+        const int xi = it - ITEMS_DY;
+        const int m4 = xi % M4, chunk = xi / M4;
+        if constexpr (XPRO == IM2COL_STEM)
+          wg_write<ACT_NONE>(items[i], nullptr, nullptr, nullptr, 36, chunk * 8 < 36 ? 0 : 36, m0 + m4 * 4,
+                             mend, Tx[buf], chunk * 8, m4 * 4);
+        else
+          wg_write<XPRO>(items[i], p.xs, p.xt, nullptr, p.K, k0 + chunk * 8, m0 + m4 * 4, mend, Tx[buf],
+                         chunk * 8, m4 * 4);
+      }
+    }
+  };
+
+  int buf = 0;
+  if (mbeg < mend) {
+    load_step(mbeg);
+    write_step(mbeg, 0);
+  }
+  __syncthreads();
+  for (int m0 = mbeg; m0 < mend; m0 += kWMK) {
+    const bool has_next = m0 + kWMK < mend;
+    if (has_next) load_step(m0 + kWMK);           // global loads in flight during the MFMAs
+    const bf16_t *Td = Tdy[buf], *Tq = Tx[buf];
 #pragma unroll
-    for (int b = 0; b < RK; ++b)
-      bfr[b] = *reinterpret_cast<const s16x8_t *>(Tx + (wk * QK + b * 16 + (lane & 15)) * kWLD + 8 * (lane >> 4));
+    for (int ks = 0; ks < kWMK; ks += 32) {
+      s16x8_t af[RN], bfr[RK];
 #pragma unroll
-    for (int a = 0; a < RN; ++a)
+      for (int a = 0; a < RN; ++a)
+        af[a] = *reinterpret_cast<const s16x8_t *>(Td + (wn * QN + a * 16 + (lane & 15)) * kWLD + ks + 8 * (lane >> 4));
 #pragma unroll
       for (int b = 0; b < RK; ++b)
-        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[a]),
-                                                           __builtin_bit_cast(bf16x8_t, bfr[b]), acc[a][b], 0, 0, 0);
+        bfr[b] = *reinterpret_cast<const s16x8_t *>(Tq + (wk * QK + b * 16 + (lane & 15)) * kWLD + ks + 8 * (lane >> 4));
+#pragma unroll
+      for (int a = 0; a < RN; ++a)
+#pragma unroll
+        for (int b = 0; b < RK; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[a]),
+                                                             __builtin_bit_cast(bf16x8_t, bfr[b]), acc[a][b], 0, 0, 0);
+    }
+    if (has_next) write_step(m0 + kWMK, buf ^ 1);  // other buffer: last read before the previous barrier
     __syncthreads();
+    buf ^= 1;
   }
   // acc[a][b][j] = dW[n0 + wn*QN + a*16 + 4*(lane>>4) + j][k0 + wk*QK + b*16 + (lane&15)]
   float *dst = p.part + (size_t)blockIdx.z * p.N * p.K;
@@ -474,14 +516,19 @@ void launch_pw_gemm(int pro, int epi, const bf16_t *A, const bf16_t *A2, const f
 #undef PW_CASE
 }
 
+void launch_colsum(const float *src, int R, long long n, float *dst, int &rows_out, hipStream_t st);
+int colsum_rows(int R);
+
+// split-M geometry: tiles of TN x TK outputs, S splits of >= kMinRowsPerSplit rows each
+static constexpr int kMinRowsPerSplit = 512;
 static void wgrad_geom(int M, int N, int K, int &TN, int &TK, int &S, int &rps) {
   TN = N <= 32 ? 32 : (N <= 64 ? 64 : 128);
   TK = K <= 32 ? 32 : (K <= 64 ? 64 : 128);
   const int tiles = ((N + TN - 1) / TN) * ((K + TK - 1) / TK);
-  S = 1024 / tiles;
-  if (S < 1) S = 1;
-  const int max_s = (M + 255) / 256;
+  S = (1024 + tiles - 1) / tiles;
+  const int max_s = (M + kMinRowsPerSplit - 1) / kMinRowsPerSplit;
   if (S > max_s) S = max_s;
+  if (S < 1) S = 1;
   rps = ((M + S - 1) / S + kWMK - 1) / kWMK * kWMK;
   S = (M + rps - 1) / rps;
 }
@@ -489,7 +536,7 @@ static void wgrad_geom(int M, int N, int K, int &TN, int &TK, int &S, int &rps) 
 long long pw_wgrad_workspace_floats(int M, int N, int K) {
   int TN, TK, S, rps;
   wgrad_geom(M, N, K, TN, TK, S, rps);
-  return (long long)S * N * K;
+  return (long long)(S + colsum_rows(S)) * N * K;
 }
 
 template <int XPRO, int TN, int TK>
@@ -520,7 +567,7 @@ __global__ void stem_wgrad_permute_kernel(const float *__restrict__ src, float *
 long long stem_wgrad_workspace_floats(int M, int O) {
   int TN, TK, S, rps;
   wgrad_geom(M, O, 36, TN, TK, S, rps);
-  return (long long)S * O * 36 + (long long)O * 36;
+  return (long long)(S + colsum_rows(S) + 1) * O * 36;
 }
 
 void launch_stem_wgrad(const bf16_t *G, const bf16_t *Y, const float *ga, const float *gb,
@@ -532,9 +579,12 @@ void launch_stem_wgrad(const bf16_t *G, const bf16_t *Y, const float *ga, const 
   wgrad_geom(M, O, 36, TN, TK, S, rps);
   PwWgArgs a{G, Y, ga, gb, gc, img, nullptr, nullptr, part, M, O, 36, rps, H, W, Ho, Wo};
   launch_wg_x<IM2COL_STEM>(a, TN, TK, S, st);
-  float *tmp = part + (size_t)S * O * 36;
   const long long n = (long long)O * 36;
-  hipLaunchKernelGGL(split_reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, st, part, S, n, tmp);
+  int rows = S;
+  float *lvl1 = part + (size_t)S * n;
+  launch_colsum(part, S, n, lvl1, rows, st);
+  float *tmp = lvl1 + (size_t)colsum_rows(S) * n;
+  hipLaunchKernelGGL(split_reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, st, rows == S ? part : lvl1, rows, n, tmp);
   hipLaunchKernelGGL(stem_wgrad_permute_kernel, dim3((O * 27 + 255) / 256), dim3(256), 0, st, tmp, grad, O);
 }
 
@@ -547,7 +597,10 @@ void launch_pw_wgrad(const bf16_t *G, const bf16_t *Y, const float *ga, const fl
   if (xact == ACT_BN_RELU6) launch_wg_x<ACT_BN_RELU6>(a, TN, TK, S, st);
   else launch_wg_x<ACT_NONE>(a, TN, TK, S, st);
   const long long n = (long long)N * K;
+  int rows = S;
+  float *lvl1 = part + (size_t)S * n;
+  launch_colsum(part, S, n, lvl1, rows, st);
   int grid = (int)((n + 255) / 256);
   if (grid > 2048) grid = 2048;
-  hipLaunchKernelGGL(split_reduce_kernel, dim3(grid), dim3(256), 0, st, part, S, n, grad);
+  hipLaunchKernelGGL(split_reduce_kernel, dim3(grid), dim3(256), 0, st, rows == S ? part : lvl1, rows, n, grad);
 }

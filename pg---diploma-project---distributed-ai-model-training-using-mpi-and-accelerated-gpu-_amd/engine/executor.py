@@ -122,7 +122,7 @@ class MobileNetV2Executor:
         self.H0 = H
         self.stem_w = "features.0.0.weight"
         self.bn0 = BNState(self.flat, feats[0][1], "features.0.1", B * H * H, feats[0][0].out_channels, device)
-        parts = [K.stem_num_partials(B, img_size, img_size)]
+        parts = [(K.stem_num_partials(B, img_size, img_size), 32)]   # (partial rows, channels)
         wg = [K.stem_wgrad_workspace(B, img_size, img_size, 32)]
         # ---------------- blocks
         self.blocks: List[BlockPlan] = []
@@ -151,14 +151,14 @@ class MobileNetV2Executor:
             bp.G = torch.empty(Mout, blk.oup, dtype=torch.bfloat16, device=device)
             self.blocks.append(bp)
             if expand:
-                parts.append(K.pw_num_partials(Min, blk.hidden))                       # fwd expand
-                parts.append(K.pw_num_partials(Min, blk.inp))                          # bwd expand dgrad
+                parts.append((K.pw_num_partials(Min, blk.hidden), blk.hidden))        # fwd expand
+                parts.append((K.pw_num_partials(Min, blk.inp), blk.inp))               # bwd expand dgrad
                 wg.append(K.pw_wgrad_workspace(Min, blk.hidden, blk.inp))
-            parts.append(K.dw_num_partials("fwd", B, Hin, Hin, blk.hidden, blk.stride))
-            parts.append(K.dw_num_partials("dgrad", B, Hin, Hin, blk.hidden, blk.stride))
-            wg.append(K.dw_num_partials("wgrad", B, Hin, Hin, blk.hidden, blk.stride) * 9 * blk.hidden)
-            parts.append(K.pw_num_partials(Mout, blk.oup))                             # fwd project
-            parts.append(K.pw_num_partials(Mout, blk.hidden))                          # bwd project dgrad
+            parts.append((K.dw_num_partials("fwd", B, Hin, Hin, blk.hidden, blk.stride), blk.hidden))
+            parts.append((K.dw_num_partials("dgrad", B, Hin, Hin, blk.hidden, blk.stride), blk.hidden))
+            wg.append(K.dw_wgrad_workspace(B, Hin, Hin, blk.hidden, blk.stride))
+            parts.append((K.pw_num_partials(Mout, blk.oup), blk.oup))                 # fwd project
+            parts.append((K.pw_num_partials(Mout, blk.hidden), blk.hidden))           # bwd project dgrad
             wg.append(K.pw_wgrad_workspace(Mout, blk.oup, blk.hidden))
             cur_h = Ho
         # ---------------- final 1x1 conv + head
@@ -169,9 +169,9 @@ class MobileNetV2Executor:
         self.C_last = last[0].out_channels
         self.w_last = f"features.{len(feats) - 1}.0.weight"
         self.bn_last = BNState(self.flat, last[1], f"features.{len(feats) - 1}.1", Mf, self.C_last, device)
-        parts.append(K.pw_num_partials(Mf, self.C_last))
-        parts.append(K.pw_num_partials(Mf, self.C_last_in))
-        parts.append(B)
+        parts.append((K.pw_num_partials(Mf, self.C_last), self.C_last))
+        parts.append((K.pw_num_partials(Mf, self.C_last_in), self.C_last_in))
+        parts.append((B, self.C_last))
         wg.append(K.pw_wgrad_workspace(Mf, self.C_last, self.C_last_in))
         self.NC = model.classifier[1].out_features
         self.w_lin, self.b_lin = "classifier.1.weight", "classifier.1.bias"
@@ -182,8 +182,7 @@ class MobileNetV2Executor:
         self.dlogits = torch.zeros(B, self.NC, **f32)
         self.pd = torch.zeros(B, self.C_last, **f32)
         # ---------------- workspaces (stream-ordered reuse)
-        maxC = max([self.C_last] + [b.hidden for b in self.blocks])
-        self.ws_part = torch.zeros(max(parts) * 2 * maxC + 1024, **f32)
+        self.ws_part = torch.zeros(max(K.bn_part_floats(P, C) for P, C in parts) + 1024, **f32)
         self.ws_wgrad = torch.zeros(max(wg) + 1024, **f32)
         self.img = torch.zeros(B, img_size, img_size, 4, dtype=torch.bfloat16, device=device)
         self.labels = torch.zeros(B, dtype=torch.int64, device=device)

@@ -47,9 +47,14 @@ BF16, F32 = torch.bfloat16, torch.float32
 
 
 # --------------------------------------------------------------------------- BN
+def bn_part_floats(P, C):
+    """Workspace a BN finalize over P partial rows needs ([P][2][C] + level-1 fold scratch)."""
+    return (P + lib().colsum_rows(P)) * 2 * C
+
+
 def bn_fwd_finalize(part, P, C, count, gamma, beta, eps, momentum, rmean, rvar, nbt, mean, rstd,
                     scale, shift):
-    _chk(part, F32, P * 2 * C, "part")
+    _chk(part, F32, bn_part_floats(P, C), "part")
     for n, t in (("gamma", gamma), ("beta", beta), ("rmean", rmean), ("rvar", rvar), ("mean", mean),
                  ("rstd", rstd), ("scale", scale), ("shift", shift)):
         if t is not None and t.numel() < C:
@@ -59,7 +64,7 @@ def bn_fwd_finalize(part, P, C, count, gamma, beta, eps, momentum, rmean, rvar, 
 
 
 def bn_bwd_finalize(part, P, C, count, mean, rstd, gamma, coef, dgamma=None, dbeta=None):
-    _chk(part, F32, P * 2 * C, "part")
+    _chk(part, F32, bn_part_floats(P, C), "part")
     _chk(coef, F32, 3 * C, "coef")
     lib().bn_bwd_finalize(_p(part), P, C, float(count), _p(mean), _p(rstd), _p(gamma), _p(coef),
                           _p(dgamma), _p(dbeta), _s())
@@ -139,12 +144,17 @@ def dw_dgrad(g, yself, coef, w, yprev, ps, pt, gout, part, B, H, W, C, stride):
                    B, H, W, C, stride, _s())
 
 
+def dw_wgrad_workspace(B, H, W, C, stride):
+    P = dw_num_partials("wgrad", B, H, W, C, stride)
+    return (P + lib().colsum_rows(P)) * 9 * C
+
+
 def dw_wgrad(g, yself, coef, yprev, ps, pt, part, grad, B, H, W, C, stride):
     _dw_check(B, H, W, C, stride)
     Ho, Wo = dw_out_hw(H, W, stride)
     _chk(g, BF16, B * Ho * Wo * C, "g")
     _chk(yprev, BF16, B * H * W * C, "yprev")
-    _chk(part, F32, dw_num_partials("wgrad", B, H, W, C, stride) * 9 * C, "part")
+    _chk(part, F32, dw_wgrad_workspace(B, H, W, C, stride), "part")
     _chk(grad, F32, 9 * C, "grad")
     lib().dw_wgrad(_p(g), _p(yself), _p(coef), _p(yprev), _p(ps), _p(pt), _p(part), _p(grad),
                    B, H, W, C, stride, _s())

@@ -145,8 +145,7 @@ def test_dw_dgrad_wgrad(dev, B, H, W, C, stride):
     assert rel(st[1], (gref * yprev.float()).reshape(-1, C).sum(0)) < 2e-2
     # wgrad
     wref = torch.nn.grad.conv2d_weight(z, w.shape, dy, stride=stride, padding=1, groups=C)
-    Pw = K.dw_num_partials("wgrad", B, H, W, C, stride)
-    wpart = torch.zeros(Pw * 9 * C, device=dev)
+    wpart = torch.zeros(K.dw_wgrad_workspace(B, H, W, C, stride), device=dev)
     grad = torch.empty(C * 9, device=dev)
     K.dw_wgrad(g, yself, coef, yprev, s, t, wpart, grad, B, H, W, C, stride)
     assert rel(grad.view(C, 1, 3, 3), wref) < 1e-3
