@@ -11,9 +11,11 @@
 //    a 64-lane wave still reads >= 256 contiguous bytes per pixel row;
 //  * the 3 x (PIX*S+2) input window is streamed one kernel row at a time
 //    (rolled loop) so each input vector is loaded and BN-transformed once per
-//    row and only one row of the window is live; the 3x3 weights sit in LDS as
-//    fp32 [9][C] (three 16-B reads per row) — ~70-100 VGPRs, 4+ waves/SIMD to
-//    hide HBM latency;
+//    row and only one row of the window is live; the 3x3 weights are stored
+//    tap-major [9][C] in the flat parameter buffer (three 8-B loads per row) —
+//    ~70-100 VGPRs, 4+ waves/SIMD to hide HBM latency;
+//  * a workgroup owns a slab of <= 64 channels (blockIdx.y) over many rows, so
+//    BN / weight-gradient partial rows stay small and rows stream long;
 //  * the input operand is the *pre-BN* output of the producer: the producer's
 //    BatchNorm-apply + ReLU6 is fused into the load (zero padding is applied in
 //    the post-activation space, as in the reference graph);
@@ -29,6 +31,7 @@ constexpr int CPT = 4;        // channels per thread
 
 struct DwGeom {
   int B, H, W, C, Ho, Wo, rows_per_wg;
+  int CC;  // channels handled by one workgroup (blockIdx.y selects the chunk)
 };
 
 PG_DEVICE void unpack4(const uint2 &u, float (&f)[CPT]) {
@@ -61,40 +64,32 @@ PG_DEVICE void load_act4(const bf16_t *__restrict__ x, const DwGeom &g, int b, i
   for (int k = 0; k < CPT; ++k) v[k] = act_apply<ACT>(v[k], s[k], t[k]);
 }
 
-// stage weights w[C][9] (bf16, torch layout) -> lds fp32 [9][C]
-PG_DEVICE void stage_weights(const bf16_t *__restrict__ w, int C, float *wl) {
-  for (int i = threadIdx.x; i < 9 * C; i += blockDim.x) {
-    const int c = i / 9, q = i % 9;
-    wl[q * C + c] = bf2f(w[i]);
-  }
+// weights are stored tap-major [9][C] (bf16 shadow of the flat parameter buffer; the
+// torch-layout Parameter is a strided view of it), so one kernel row is 3 x 8-B loads
+PG_DEVICE void ldw4(const bf16_t *__restrict__ w, int C, int q, int c0, float (&o)[CPT]) {
+  unpack4(ldg8(w + (size_t)q * C + c0), o);
 }
 
-PG_DEVICE void lds_w4(const float *wl, int C, int q, int c0, float (&o)[CPT]) {
-  const float4 v = *reinterpret_cast<const float4 *>(wl + q * C + c0);
-  o[0] = v.x;
-  o[1] = v.y;
-  o[2] = v.z;
-  o[3] = v.w;
-}
-
-// Block-level reduction of per-thread [NV][CPT] channel partials into part[blockIdx][NV][C];
-// threads are laid out tid = tw * C4 + c4.  lds must hold TW*C floats (<= 1024).
+// Block-level reduction of per-thread [NV][CPT] channel partials of this workgroup's CC
+// channels into part[blockIdx.x][NV][C] (columns cbase..cbase+CC); tid = tw * C4 + c4.
+// lds must hold TW*CC floats (<= 1024).
 template <int NV>
-PG_DEVICE void block_channel_partials(float (&acc)[NV][CPT], float *__restrict__ part, int C, int C4,
-                                      int TW, float *lds) {
+PG_DEVICE void block_channel_partials(float (&acc)[NV][CPT], float *__restrict__ part, int C, int CC,
+                                      int cbase, int TW, float *lds) {
   const int tid = threadIdx.x;
+  const int C4 = CC / CPT;
   const int c4 = tid % C4, tw = tid / C4;
   const bool active = tw < TW;
   for (int v = 0; v < NV; ++v) {
     if (active) {
-      *reinterpret_cast<float4 *>(lds + tw * C + c4 * CPT) =
+      *reinterpret_cast<float4 *>(lds + tw * CC + c4 * CPT) =
           make_float4(acc[v][0], acc[v][1], acc[v][2], acc[v][3]);
     }
     __syncthreads();
-    for (int c = tid; c < C; c += blockDim.x) {
+    for (int c = tid; c < CC; c += blockDim.x) {
       float s = 0.f;
-      for (int w = 0; w < TW; ++w) s += lds[w * C + c];
-      part[((size_t)blockIdx.x * NV + v) * C + c] = s;
+      for (int w = 0; w < TW; ++w) s += lds[w * CC + c];
+      part[((size_t)blockIdx.x * NV + v) * C + cbase + c] = s;
     }
     __syncthreads();
   }
@@ -109,16 +104,15 @@ template <int S, int ACT, int PIX>
 __global__ __launch_bounds__(kMaxThreads) void dw_fwd_kernel(
     const bf16_t *__restrict__ x, const float *__restrict__ in_s, const float *__restrict__ in_t,
     const bf16_t *__restrict__ w, bf16_t *__restrict__ y, float *__restrict__ part, DwGeom g) {
-  extern __shared__ __attribute__((aligned(16))) float wl[];  // [9][C] weights, then reduction scratch
-  float *red = wl;  // reused for the final reduction (after a barrier)
-  const int C4 = g.C / CPT;
+  __shared__ __attribute__((aligned(16))) float red[1024];
+  const int C4 = g.CC / CPT;
   const int TW = blockDim.x / C4;
   const int tid = threadIdx.x;
   const int c4 = tid % C4, tw = tid / C4;
-  const int c0 = c4 * CPT;
+  const int cbase = blockIdx.y * g.CC;
+  const int c0 = cbase + c4 * CPT;
   constexpr int NCOL = (PIX - 1) * S + 3;
 
-  stage_weights(w, g.C, wl);
   float s[CPT], t[CPT], stats[2][CPT];
 #pragma unroll
   for (int k = 0; k < CPT; ++k) {
@@ -147,9 +141,9 @@ __global__ __launch_bounds__(kMaxThreads) void dw_fwd_kernel(
       for (int dh = 0; dh < 3; ++dh) {
         const int ih = oh * S - 1 + dh;
         float w0[CPT], w1[CPT], w2[CPT];
-        lds_w4(wl, g.C, dh * 3 + 0, c0, w0);
-        lds_w4(wl, g.C, dh * 3 + 1, c0, w1);
-        lds_w4(wl, g.C, dh * 3 + 2, c0, w2);
+        ldw4(w, g.C, dh * 3 + 0, c0, w0);
+        ldw4(w, g.C, dh * 3 + 1, c0, w1);
+        ldw4(w, g.C, dh * 3 + 2, c0, w2);
 #pragma unroll
         for (int j = 0; j < NCOL; ++j) {
           const int iw = ow0 * S - 1 + j;
@@ -181,7 +175,7 @@ __global__ __launch_bounds__(kMaxThreads) void dw_fwd_kernel(
     }
   }
   __syncthreads();
-  block_channel_partials<2>(stats, part, g.C, C4, TW, red);
+  block_channel_partials<2>(stats, part, g.C, g.CC, cbase, TW, red);
 }
 
 // ---------------------------------------------------------------------------
@@ -193,17 +187,16 @@ __global__ __launch_bounds__(kMaxThreads) void dw_dgrad_kernel(
     const bf16_t *__restrict__ gin, const bf16_t *__restrict__ yself, const float *__restrict__ coef,
     const bf16_t *__restrict__ w, const bf16_t *__restrict__ yprev, const float *__restrict__ ps,
     const float *__restrict__ pt, bf16_t *__restrict__ gout, float *__restrict__ part, DwGeom g) {
-  extern __shared__ __attribute__((aligned(16))) float wl[];
-  float *red = wl;
-  const int C4 = g.C / CPT;
+  __shared__ __attribute__((aligned(16))) float red[1024];
+  const int C4 = g.CC / CPT;
   const int TW = blockDim.x / C4;
   const int tid = threadIdx.x;
   const int c4 = tid % C4, tw = tid / C4;
-  const int c0 = c4 * CPT;
+  const int cbase = blockIdx.y * g.CC;
+  const int c0 = cbase + c4 * CPT;
   // PIX input pixels per item; output columns touching them:
   constexpr int NCOL = (S == 1) ? PIX + 2 : PIX / 2 + 2;
 
-  stage_weights(w, g.C, wl);
   float al[CPT], be[CPT], ga[CPT], s[CPT], t[CPT], stats[2][CPT];
 #pragma unroll
   for (int k = 0; k < CPT; ++k) {
@@ -242,9 +235,9 @@ __global__ __launch_bounds__(kMaxThreads) void dw_dgrad_kernel(
         }
         if (oh < 0 || oh >= g.Ho) continue;
         float w0[CPT], w1[CPT], w2[CPT];
-        lds_w4(wl, g.C, dh * 3 + 0, c0, w0);
-        lds_w4(wl, g.C, dh * 3 + 1, c0, w1);
-        lds_w4(wl, g.C, dh * 3 + 2, c0, w2);
+        ldw4(w, g.C, dh * 3 + 0, c0, w0);
+        ldw4(w, g.C, dh * 3 + 1, c0, w1);
+        ldw4(w, g.C, dh * 3 + 2, c0, w2);
 #pragma unroll
         for (int j = 0; j < NCOL; ++j) {
           const int ow = (S == 1) ? iw0 - 1 + j : (iw0 >> 1) - 1 + j;
@@ -288,7 +281,7 @@ __global__ __launch_bounds__(kMaxThreads) void dw_dgrad_kernel(
     }
   }
   __syncthreads();
-  block_channel_partials<2>(stats, part, g.C, C4, TW, red);
+  block_channel_partials<2>(stats, part, g.C, g.CC, cbase, TW, red);
 }
 
 // ---------------------------------------------------------------------------
@@ -300,11 +293,12 @@ __global__ __launch_bounds__(kMaxThreads) void dw_wgrad_kernel(
     const bf16_t *__restrict__ yprev, const float *__restrict__ ps, const float *__restrict__ pt,
     float *__restrict__ part, DwGeom g) {
   __shared__ __attribute__((aligned(16))) float lds[1024];
-  const int C4 = g.C / CPT;
+  const int C4 = g.CC / CPT;
   const int TW = blockDim.x / C4;
   const int tid = threadIdx.x;
   const int c4 = tid % C4, tw = tid / C4;
-  const int c0 = c4 * CPT;
+  const int cbase = blockIdx.y * g.CC;
+  const int c0 = cbase + c4 * CPT;
   constexpr int NCOL = (PIX - 1) * S + 3;
 
   float al[CPT], be[CPT], ga[CPT], s[CPT], t[CPT];
@@ -365,10 +359,10 @@ __global__ __launch_bounds__(kMaxThreads) void dw_wgrad_kernel(
       }
     }
   }
-  block_channel_partials<9>(accw, part, g.C, C4, TW, lds);
+  block_channel_partials<9>(accw, part, g.C, g.CC, cbase, TW, lds);
 }
 
-// reduce [P][9][C] -> grad [C][9] (torch layout [C,1,3,3]) fp32
+// reduce [P][9][C] -> grad [9][C] fp32
 __global__ __launch_bounds__(256) void dw_wgrad_reduce_kernel(const float *__restrict__ part, int P,
                                                              int C, float *__restrict__ grad) {
   const int idx = blockIdx.x * 64 + (threadIdx.x & 63);  // over 9*C (tap-major in part)
@@ -381,8 +375,7 @@ __global__ __launch_bounds__(256) void dw_wgrad_reduce_kernel(const float *__res
   __syncthreads();
   if (ty == 0 && idx < 9 * C) {
     s = sh[0][threadIdx.x] + sh[1][threadIdx.x] + sh[2][threadIdx.x] + sh[3][threadIdx.x];
-    const int tap = idx / C, c = idx % C;
-    grad[c * 9 + tap] = s;
+    grad[idx] = s;  // [9][C] tap-major, the layout of the flat parameter buffer
   }
 }
 
@@ -392,8 +385,17 @@ __global__ __launch_bounds__(256) void dw_wgrad_reduce_kernel(const float *__res
 namespace {
 constexpr int kPixF = 4, kPixD1 = 4, kPixD2 = 8, kPixW = 4;
 
+// channels per workgroup: the largest multiple of 4 dividing C that is <= 64, so a
+// workgroup covers many pixels of a narrow channel slab (long rows per thread group,
+// small BN/weight partial rows) instead of all channels of very few pixels
+int dw_cc(int C) {
+  for (int cc = 64; cc >= 4; cc -= 4)
+    if (C % cc == 0) return cc;
+  return 4;
+}
+
 int dw_block_threads(int C) {
-  const int C4 = C / CPT;
+  const int C4 = dw_cc(C) / CPT;
   int TW = kMaxThreads / C4;
   if (TW < 1) TW = 1;
   return C4 * TW;
@@ -408,24 +410,25 @@ int dw_rows_per_wg(int rows_total, int per_row_items, int TW, int target_items_p
 }
 
 struct DwLaunch {
-  int threads, rpw, grid;
-  size_t lds;
+  int threads, rpw, grid, chunks;
 };
 
 DwLaunch dw_launch(int kind, int B, int H, int W, int C, int stride) {
   const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
   const int threads = dw_block_threads(C);
-  const int TW = threads / (C / CPT);
-  DwLaunch l{threads, 1, 1, (size_t)(9 * C > 1024 ? 9 * C : 1024) * sizeof(float)};
+  const int TW = threads / (dw_cc(C) / CPT);
+  const int chunks = C / dw_cc(C);
+  const int min_wgs = (2048 + chunks - 1) / chunks;
+  DwLaunch l{threads, 1, 1, chunks};
   if (kind == 0) {  // fwd
-    l.rpw = dw_rows_per_wg(B * Ho, (Wo + kPixF - 1) / kPixF, TW, 2, 1024);
+    l.rpw = dw_rows_per_wg(B * Ho, (Wo + kPixF - 1) / kPixF, TW, 4, min_wgs);
     l.grid = (B * Ho + l.rpw - 1) / l.rpw;
   } else if (kind == 1) {  // dgrad (over input rows)
     const int pix = stride == 1 ? kPixD1 : kPixD2;
-    l.rpw = dw_rows_per_wg(B * H, (W + pix - 1) / pix, TW, 2, 1024);
+    l.rpw = dw_rows_per_wg(B * H, (W + pix - 1) / pix, TW, 4, min_wgs);
     l.grid = (B * H + l.rpw - 1) / l.rpw;
   } else {  // wgrad
-    l.rpw = dw_rows_per_wg(B * Ho, (Wo + kPixW - 1) / kPixW, TW, 4, 512);
+    l.rpw = dw_rows_per_wg(B * Ho, (Wo + kPixW - 1) / kPixW, TW, 8, (1024 + chunks - 1) / chunks);
     l.grid = (B * Ho + l.rpw - 1) / l.rpw;
   }
   return l;
@@ -440,17 +443,17 @@ void launch_dw_fwd(const bf16_t *x, const float *in_s, const float *in_t, int ac
                    bf16_t *y, float *part, int B, int H, int W, int C, int stride, hipStream_t st) {
   const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
   const DwLaunch l = dw_launch(0, B, H, W, C, stride);
-  DwGeom g{B, H, W, C, Ho, Wo, l.rpw};
+  DwGeom g{B, H, W, C, Ho, Wo, l.rpw, dw_cc(C)};
   if (stride == 1) {
     if (act == ACT_BN_RELU6)
-      hipLaunchKernelGGL((dw_fwd_kernel<1, ACT_BN_RELU6, kPixF>), dim3(l.grid), dim3(l.threads), l.lds, st, x, in_s, in_t, w, y, part, g);
+      hipLaunchKernelGGL((dw_fwd_kernel<1, ACT_BN_RELU6, kPixF>), dim3(l.grid, l.chunks), dim3(l.threads), 0, st, x, in_s, in_t, w, y, part, g);
     else
-      hipLaunchKernelGGL((dw_fwd_kernel<1, ACT_NONE, kPixF>), dim3(l.grid), dim3(l.threads), l.lds, st, x, in_s, in_t, w, y, part, g);
+      hipLaunchKernelGGL((dw_fwd_kernel<1, ACT_NONE, kPixF>), dim3(l.grid, l.chunks), dim3(l.threads), 0, st, x, in_s, in_t, w, y, part, g);
   } else {
     if (act == ACT_BN_RELU6)
-      hipLaunchKernelGGL((dw_fwd_kernel<2, ACT_BN_RELU6, kPixF>), dim3(l.grid), dim3(l.threads), l.lds, st, x, in_s, in_t, w, y, part, g);
+      hipLaunchKernelGGL((dw_fwd_kernel<2, ACT_BN_RELU6, kPixF>), dim3(l.grid, l.chunks), dim3(l.threads), 0, st, x, in_s, in_t, w, y, part, g);
     else
-      hipLaunchKernelGGL((dw_fwd_kernel<2, ACT_NONE, kPixF>), dim3(l.grid), dim3(l.threads), l.lds, st, x, in_s, in_t, w, y, part, g);
+      hipLaunchKernelGGL((dw_fwd_kernel<2, ACT_NONE, kPixF>), dim3(l.grid, l.chunks), dim3(l.threads), 0, st, x, in_s, in_t, w, y, part, g);
   }
 }
 
@@ -459,11 +462,11 @@ void launch_dw_dgrad(const bf16_t *gin, const bf16_t *yself, const float *coef, 
                      float *part, int B, int H, int W, int C, int stride, hipStream_t st) {
   const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
   const DwLaunch l = dw_launch(1, B, H, W, C, stride);
-  DwGeom g{B, H, W, C, Ho, Wo, l.rpw};
+  DwGeom g{B, H, W, C, Ho, Wo, l.rpw, dw_cc(C)};
   if (stride == 1)
-    hipLaunchKernelGGL((dw_dgrad_kernel<1, kPixD1>), dim3(l.grid), dim3(l.threads), l.lds, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g);
+    hipLaunchKernelGGL((dw_dgrad_kernel<1, kPixD1>), dim3(l.grid, l.chunks), dim3(l.threads), 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g);
   else
-    hipLaunchKernelGGL((dw_dgrad_kernel<2, kPixD2>), dim3(l.grid), dim3(l.threads), l.lds, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g);
+    hipLaunchKernelGGL((dw_dgrad_kernel<2, kPixD2>), dim3(l.grid, l.chunks), dim3(l.threads), 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g);
 }
 
 void launch_colsum(const float *src, int R, long long n, float *dst, int &rows_out, hipStream_t st);
@@ -473,11 +476,11 @@ void launch_dw_wgrad(const bf16_t *gin, const bf16_t *yself, const float *coef, 
                      int C, int stride, hipStream_t st) {
   const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
   const DwLaunch l = dw_launch(2, B, H, W, C, stride);
-  DwGeom g{B, H, W, C, Ho, Wo, l.rpw};
+  DwGeom g{B, H, W, C, Ho, Wo, l.rpw, dw_cc(C)};
   if (stride == 1)
-    hipLaunchKernelGGL((dw_wgrad_kernel<1, kPixW>), dim3(l.grid), dim3(l.threads), 0, st, gin, yself, coef, yprev, ps, pt, part, g);
+    hipLaunchKernelGGL((dw_wgrad_kernel<1, kPixW>), dim3(l.grid, l.chunks), dim3(l.threads), 0, st, gin, yself, coef, yprev, ps, pt, part, g);
   else
-    hipLaunchKernelGGL((dw_wgrad_kernel<2, kPixW>), dim3(l.grid), dim3(l.threads), 0, st, gin, yself, coef, yprev, ps, pt, part, g);
+    hipLaunchKernelGGL((dw_wgrad_kernel<2, kPixW>), dim3(l.grid, l.chunks), dim3(l.threads), 0, st, gin, yself, coef, yprev, ps, pt, part, g);
   // two-level deterministic reduction of the [P][9C] partials (level 1 written after them)
   int rows = l.grid;
   float *tmp = part + (size_t)l.grid * 9 * C;

@@ -11,6 +11,11 @@ classifier first, the stem last) with every tensor 64-element aligned, so the
 gradient all-reduce buckets are contiguous prefixes/ranges of the gradient
 buffer that become ready in order while backward is still running
 (reference DDP buckets: SURVEY.md §2.7 N6).
+
+Depthwise 3x3 weights ``[C,1,3,3]`` are stored *tap-major* ``[9][C]`` so the
+depthwise kernels read the 4 channels of one tap with a single 8-byte load; the
+Parameter is a strided view of that storage, so ``state_dict()`` still yields
+torchvision-layout tensors.
 """
 from typing import Dict, List, Tuple
 
@@ -21,6 +26,10 @@ ALIGN = 64
 
 def _align(n: int, a: int = ALIGN) -> int:
     return (n + a - 1) // a * a
+
+
+def is_depthwise3x3(p: torch.Tensor) -> bool:
+    return p.dim() == 4 and p.shape[1] == 1 and tuple(p.shape[2:]) == (3, 3) and p.shape[0] % 4 == 0
 
 
 class FlatParams:
@@ -43,16 +52,25 @@ class FlatParams:
         self.exp_avg_sq = torch.zeros_like(self.master)
         self.shadow = torch.zeros(self.numel, dtype=torch.bfloat16, device=device) if with_shadow else None
         self.params = {}
+        self.tap_major = {n for n, p in order if is_depthwise3x3(p)}
         with torch.no_grad():
             for name, p in order:
-                o, n = self.offsets[name]
-                self.master[o:o + n].copy_(p.detach().reshape(-1).to(device))
-                p.data = self.master[o:o + n].view(p.shape)
-                p.grad = self.grad[o:o + n].view(p.shape)
+                w_view, g_view = self.view(self.master, name, p.shape), self.view(self.grad, name, p.shape)
+                w_view.copy_(p.detach().to(device))
+                p.data = w_view
+                p.grad = g_view
                 self.params[name] = p
         self.refresh_shadow()
 
     # views ---------------------------------------------------------------
+    def view(self, buf: torch.Tensor, name: str, shape) -> torch.Tensor:
+        """Parameter-shaped view of ``name`` inside a flat buffer (strided for tap-major weights)."""
+        o, n = self.offsets[name]
+        if name in self.tap_major:
+            C = shape[0]
+            return buf[o:o + n].view(9, C).t().view(*shape)
+        return buf[o:o + n].view(shape)
+
     def w(self, name: str) -> torch.Tensor:
         o, n = self.offsets[name]
         return self.master[o:o + n]

@@ -87,7 +87,7 @@ def main(B=8, S=64, fp64=False):
               f"torch-bf16 rel {rel(acts16[bn.prefix].float(), a):.4f}")
     res = []
     for name, p in ref.named_parameters():
-        g = exe.flat.g(name).view_as(p)
+        g = exe.flat.view(exe.flat.grad, name, p.shape)
         res.append((F.cosine_similarity(g.flatten().float(), p.grad.flatten().float(), dim=0).item(),
                     rel(g, p.grad), name))
     res.sort()

@@ -40,6 +40,11 @@ def relu6(x):
     return x.clamp(0, 6)
 
 
+def tapmajor(w):
+    """[C,1,3,3] depthwise weight -> the kernels' tap-major [9][C] storage."""
+    return w.reshape(w.shape[0], 9).t().contiguous()
+
+
 def sum_parts(part, P, C, nv=2):
     return part[: P * nv * C].view(P, nv, C).sum(0)
 
@@ -109,7 +114,7 @@ def test_dw_fwd(dev, B, H, W, C, stride):
     y = torch.empty(B, Ho, Wo, C, dtype=torch.bfloat16, device=dev)
     P = K.dw_num_partials("fwd", B, H, W, C, stride)
     part = torch.zeros(P * 2 * C, device=dev)
-    K.dw_fwd(x, s, t, K.ACT_BN_RELU6, w, y, part, B, H, W, C, stride)
+    K.dw_fwd(x, s, t, K.ACT_BN_RELU6, tapmajor(w), y, part, B, H, W, C, stride)
     z = relu6(x.float() * s + t).permute(0, 3, 1, 2)
     ref = F.conv2d(z, w.float(), stride=stride, padding=1, groups=C).permute(0, 2, 3, 1)
     assert rel(y, ref) < 8e-3
@@ -138,7 +143,7 @@ def test_dw_dgrad_wgrad(dev, B, H, W, C, stride):
     gout = torch.empty(B, H, W, C, dtype=torch.bfloat16, device=dev)
     P = K.dw_num_partials("dgrad", B, H, W, C, stride)
     part = torch.zeros(P * 2 * C, device=dev)
-    K.dw_dgrad(g, yself, coef, w, yprev, s, t, gout, part, B, H, W, C, stride)
+    K.dw_dgrad(g, yself, coef, tapmajor(w), yprev, s, t, gout, part, B, H, W, C, stride)
     assert rel(gout, gref) < 8e-3
     st = sum_parts(part, P, C)
     assert rel(st[0], gref.reshape(-1, C).sum(0)) < 2e-2
@@ -148,7 +153,7 @@ def test_dw_dgrad_wgrad(dev, B, H, W, C, stride):
     wpart = torch.zeros(K.dw_wgrad_workspace(B, H, W, C, stride), device=dev)
     grad = torch.empty(C * 9, device=dev)
     K.dw_wgrad(g, yself, coef, yprev, s, t, wpart, grad, B, H, W, C, stride)
-    assert rel(grad.view(C, 1, 3, 3), wref) < 1e-3
+    assert rel(grad.view(9, C).t().reshape(C, 1, 3, 3), wref) < 1e-3
 
 
 # ----------------------------------------------------------------------------- pointwise
