@@ -108,7 +108,8 @@ class BlockPlan:
 
 class MobileNetV2Executor:
     def __init__(self, model: MobileNetV2, batch: int, img_size: int, device: torch.device,
-                 flat: Optional[FlatParams] = None, dropout_seed: int = 0):
+                 flat: Optional[FlatParams] = None, dropout_seed: int = 0,
+                 hyper: Optional[torch.Tensor] = None):
         assert device.type == "cuda", "the native executor runs on the GPU"
         self.model = model.to(device)
         self.B, self.S, self.device = batch, img_size, device
@@ -186,7 +187,7 @@ class MobileNetV2Executor:
         self.ws_wgrad = torch.zeros(max(wg) + 1024, **f32)
         self.img = torch.zeros(B, img_size, img_size, 4, dtype=torch.bfloat16, device=device)
         self.labels = torch.zeros(B, dtype=torch.int64, device=device)
-        self.hyper = torch.zeros(2, **f32)   # [lr, step]
+        self.hyper = hyper if hyper is not None else torch.zeros(2, **f32)   # [lr, step] (device)
         self.on_params_ready: Optional[Callable[[List[str]], None]] = None
 
     # ------------------------------------------------------------------ helpers

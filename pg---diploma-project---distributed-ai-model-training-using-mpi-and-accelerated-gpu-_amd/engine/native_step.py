@@ -24,7 +24,7 @@ class NativeTrainStep:
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, world_size: int = 1,
                  rank: int = 0, use_graph: bool = True, seed: int = 0, bucket_mb: float = 4.0,
                  first_bucket_mb: float = 1.0, reduce_dtype: torch.dtype = torch.float32,
-                 double_resize: bool = True, augment: bool = True):
+                 double_resize: bool = True, augment: bool = True, train_augment: bool = True):
         self.device, self.B, self.S = device, batch, img_size
         self.world, self.rank = world_size, rank
         self.exe = MobileNetV2Executor(model, batch, img_size, device, dropout_seed=(seed * 7919) ^ rank)
@@ -33,6 +33,7 @@ class NativeTrainStep:
         self.seed = seed
         self.double_resize = double_resize
         self.augment_enabled = augment
+        self.train_augment = train_augment   # False: deterministic Resize+Normalize (test transform)
         self.hyper = self.exe.hyper
         self.hyper[0] = lr
         self.metrics = torch.zeros(3, dtype=torch.float64, device=device)
@@ -73,6 +74,21 @@ class NativeTrainStep:
         st._pos = 0
         return st
 
+    def sibling(self, batch: int) -> "NativeTrainStep":
+        """A step object for another batch size sharing weights, optimizer state, lr/step
+        counter, metrics, data and gradient reducer (used for the short last batch of an
+        epoch, which the reference's DataLoader keeps).  Runs eagerly."""
+        st = NativeTrainStep.__new__(NativeTrainStep)
+        st.__dict__.update(self.__dict__)
+        st.B = batch
+        st.exe = MobileNetV2Executor(self.exe.model, batch, self.S, self.device, flat=self.flat,
+                                     dropout_seed=self.exe.dropout_seed, hyper=self.hyper)
+        st.exe.on_params_ready = self.exe.on_params_ready
+        st.idx = torch.zeros(batch, dtype=torch.int64, device=self.device)
+        st.aug_params = torch.zeros(batch, K.AUG_NPARAMS, dtype=torch.float32, device=self.device)
+        st.use_graph, st.graph, st._eager_runs = False, None, 0
+        return st
+
     def set_data(self, src_u8: torch.Tensor, labels: torch.Tensor):
         assert src_u8.is_cuda and src_u8.dtype == torch.uint8 and src_u8.shape[1:] == (32, 32, 3)
         self.src = src_u8.contiguous()
@@ -92,7 +108,8 @@ class NativeTrainStep:
         exe = self.exe
         K.step_begin(self.hyper)
         if self.augment_enabled:
-            K.augment(self.src, self.idx, self.src_labels, exe.img, exe.labels, self.aug_params, train=True,
+            K.augment(self.src, self.idx, self.src_labels, exe.img, exe.labels, self.aug_params,
+                      train=self.train_augment,
                       double_resize=self.double_resize, seed=self.seed + 17 * self.rank, hyper=self.hyper,
                       epoch_ctr=0, out_hw=self.S)
         if self.reducer is not None:

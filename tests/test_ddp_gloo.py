@@ -1,0 +1,124 @@
+"""Data-parallel layer on CPU with the gloo backend, world_size 2 (SURVEY.md §4 'Distributed (fake)').
+
+* bucketed all-reduce == all-reduce of the whole gradient
+* W ranks on shards == 1 rank on the concatenated batch (BN in eval mode, so the
+  per-rank batch statistics of training-mode BN do not enter the comparison)
+* the full Trainer (torch backend) runs 2 ranks and keeps replicas identical
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from pgdist.parallel.ddp import build_buckets
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _init(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def test_build_buckets_small_first_bucket():
+    ranges = [(f"p{i}", i * 1000, i * 1000 + 1000) for i in range(20)]   # 20 x 4 KB
+    b = build_buckets(ranges, cap_bytes=16000, first_cap_bytes=4000)
+    assert b[0][2] == ["p0"]
+    assert all(len(x[2]) == 4 for x in b[1:-1])
+    covered = [n for _, _, names in b for n in names]
+    assert covered == [f"p{i}" for i in range(20)]
+
+
+def _worker_equivalence(rank, world, port, q):
+    import pgdist  # noqa: F401
+    from pgdist.models import mobilenet_v2
+    from pgdist.engine.flat import FlatParams
+    from pgdist.parallel.ddp import BucketedGradReducer
+    _init(rank, world, port)
+    torch.manual_seed(0)
+    model = mobilenet_v2(10).eval()
+    flat = FlatParams(model, torch.device("cpu"), with_shadow=False)
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(8, 3, 32, 32, generator=g)
+    y = torch.randint(0, 10, (8,), generator=g)
+    # full-batch reference gradient on every rank
+    flat.grad.zero_()
+    torch.nn.functional.cross_entropy(model(x), y).backward()
+    ref = flat.grad.clone()
+    # sharded gradient + bucketed all-reduce (small caps -> many buckets)
+    flat.grad.zero_()
+    sl = slice(rank * 4, rank * 4 + 4)
+    torch.nn.functional.cross_entropy(model(x[sl]), y[sl]).backward()
+    red = BucketedGradReducer(flat.grad, [(n,) + flat.range_of(n) for n in flat.order],
+                              bucket_cap_mb=0.5, first_bucket_mb=0.05)
+    red.begin()
+    for n in flat.order:            # parameters become ready one by one (backward order)
+        red.mark_ready([n])
+    red.finish()
+    flat.grad.mul_(1.0 / world)
+    err = ((flat.grad - ref).norm() / ref.norm()).item()
+    q.put((rank, err, len(red.buckets)))
+    dist.destroy_process_group()
+
+
+def test_sharded_gradient_equals_full_batch():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker_equivalence, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, err, nb in res:
+        assert err < 1e-5, (rank, err)
+        assert nb > 3
+
+
+def _worker_trainer(rank, world, port, tmp, q):
+    import pgdist  # noqa: F401
+    from pgdist.config import TrainConfig
+    from pgdist.engine.trainer import Trainer
+    from pgdist.parallel.bootstrap import DistInfo
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    info = DistInfo(rank=rank, world_size=world, local_rank=rank, local_world_size=world, master_port=port)
+    cfg = TrainConfig(data="synthetic", synthetic_train_size=48, synthetic_test_size=16, batch_size=8, epochs=1,
+                      img_size=32, device="cpu", backend="torch", precision="fp32", augment="none",
+                      save_path=os.path.join(tmp, "best_mpi.pth"), log_format="ddp", seed=42)
+    tr = Trainer(cfg, info=info)
+    tr.fit()
+    w = tr.flat.master.clone()
+    allw = [torch.zeros_like(w) for _ in range(world)]
+    dist.all_gather(allw, w)
+    q.put((rank, max((a - w).abs().max().item() for a in allw), tr.history[-1]["train_images"]))
+    dist.destroy_process_group()
+
+
+def test_trainer_two_ranks_keeps_replicas_in_sync(tmp_path):
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker_trainer, args=(r, world, port, str(tmp_path), q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, diff, n in res:
+        assert diff == 0.0
+        assert n == 48
+    assert (tmp_path / "best_mpi.pth").exists()
+    sd = torch.load(tmp_path / "best_mpi.pth", weights_only=True)
+    assert not any(k.startswith("module.") for k in sd) and len(sd) == 314

@@ -96,17 +96,17 @@ def test_native_train_step_loss_decreases(dev):
     from pgdist.engine.native_step import NativeTrainStep
     torch.manual_seed(0)
     model = mobilenet_v2(10)
-    st = NativeTrainStep(model, 16, dev, img_size=64, lr=1e-3, use_graph=True)
+    st = NativeTrainStep(model, 16, dev, img_size=64, lr=1e-3, use_graph=True, train_augment=False)
     # 4 images x 4 copies each: memorisation task
     src = torch.randint(0, 256, (4, 32, 32, 3), dtype=torch.uint8, device=dev)
     labels = torch.tensor([0, 3, 5, 7], device=dev)
     st.set_data(src, labels)
     idx = torch.arange(16, device=dev) % 4
     losses = []
-    for i in range(30):
+    for i in range(40):
         st.run(idx)
         if i % 5 == 4:
             l, c, n = st.read_metrics()
             losses.append(l / n)
-    assert losses[-1] < losses[0] * 0.7, losses
+    assert losses[-1] < losses[0] * 0.5, losses
     assert st.graph is not None
