@@ -4,34 +4,37 @@
 // MobileNetV2 run through cuDNN (SURVEY.md §2.6 "Depthwise conv 3x3"); on ROCm
 // the library path (MIOpen / CK grouped-conv bwd-weight) takes ~23 ms per call
 // at bs=128 (profiles/r1_torch_miopen_baseline_kernel_stats.csv).  Depthwise is
-// pure bandwidth (1.8-4.5 FLOP/B), so these kernels are built around bytes and
-// occupancy:
+// pure bandwidth (1.8-4.5 FLOP/B), so these kernels are organised around the
+// memory system:
 //
-//  * thread = 4 channels (one 8-B vector) x a run of PIX output pixels along W;
-//    a 64-lane wave still reads >= 256 contiguous bytes per pixel row;
-//  * the 3 x (PIX*S+2) input window is streamed one kernel row at a time
-//    (rolled loop) so each input vector is loaded and BN-transformed once per
-//    row and only one row of the window is live; the 3x3 weights are stored
-//    tap-major [9][C] in the flat parameter buffer (three 8-B loads per row) —
-//    ~70-100 VGPRs, 4+ waves/SIMD to hide HBM latency;
-//  * a workgroup owns a slab of <= 64 channels (blockIdx.y) over many rows, so
-//    BN / weight-gradient partial rows stay small and rows stream long;
-//  * the input operand is the *pre-BN* output of the producer: the producer's
-//    BatchNorm-apply + ReLU6 is fused into the load (zero padding is applied in
-//    the post-activation space, as in the reference graph);
-//  * the forward epilogue emits per-workgroup BN partial sums of the output, the
-//    dgrad epilogue emits the producer-BN backward partials — no standalone BN
-//    passes over the activation.
+//  * vertical strips: a thread owns 4 channels (one 8-B vector) of ONE output
+//    column and walks R rows down the image, keeping a rolling 3-row x 3-column
+//    window in registers — every input row is loaded once per thread, and the
+//    lanes of a wave (channel-fastest, then column) read one contiguous run of
+//    pixels per load instruction (the neighbours' halo columns hit the same lines);
+//  * a workgroup = a tile of TWc columns x R rows of one image and a slab of
+//    CC <= 64 channels (blockIdx.y): small per-workgroup partial rows, long
+//    streams; ~100 VGPRs;
+//  * weights are tap-major [9][C] in the flat parameter buffer (one 8-B load per
+//    tap and 4 channels);
+//  * the producer's BatchNorm-apply + ReLU6 is fused into the input load (zero
+//    padding in the post-activation space), the forward epilogue emits this
+//    layer's BN partial sums, the dgrad epilogue the producer-BN backward
+//    partials; the weight gradient is reduced per workgroup and then by a
+//    deterministic two-level column sum.
 #include "../common.h"
 
 namespace {
 
-constexpr int kMaxThreads = 256;
 constexpr int CPT = 4;        // channels per thread
+constexpr int kRows = 8;      // output rows per strip
 
 struct DwGeom {
-  int B, H, W, C, Ho, Wo, rows_per_wg;
-  int CC;  // channels handled by one workgroup (blockIdx.y selects the chunk)
+  int B, H, W, C, Ho, Wo;
+  int CC;     // channels per workgroup (blockIdx.y selects the slab)
+  int TWc;    // columns per workgroup
+  int R;      // rows per workgroup
+  int tiles_w, tiles_h;
 };
 
 PG_DEVICE void unpack4(const uint2 &u, float (&f)[CPT]) {
@@ -49,46 +52,94 @@ PG_DEVICE uint2 pack4(const float (&f)[CPT]) {
 PG_DEVICE uint2 ldg8(const bf16_t *p) { return *reinterpret_cast<const uint2 *>(p); }
 PG_DEVICE void stg8(bf16_t *p, const uint2 &v) { *reinterpret_cast<uint2 *>(p) = v; }
 
-// 4 channels at (b, ih, iw), producer BN (+relu6) applied; out of range -> 0
-template <int ACT>
-PG_DEVICE void load_act4(const bf16_t *__restrict__ x, const DwGeom &g, int b, int ih, int iw,
-                         int c0, const float (&s)[CPT], const float (&t)[CPT], float (&v)[CPT]) {
-  if (ih < 0 || ih >= g.H || iw < 0 || iw >= g.W) {
+PG_DEVICE void zero4(float (&v)[CPT]) {
 #pragma unroll
-    for (int k = 0; k < CPT; ++k) v[k] = 0.f;
+  for (int k = 0; k < CPT; ++k) v[k] = 0.f;
+}
+
+// 4 channels at (b, ih, iw) of an [*, H, W, C] tensor, producer BN (+relu6) applied; OOB -> 0
+template <int ACT>
+PG_DEVICE void load_act4(const bf16_t *__restrict__ x, int H, int W, int C, int b, int ih, int iw,
+                         int c0, const float (&s)[CPT], const float (&t)[CPT], float (&v)[CPT]) {
+  if (ih < 0 || ih >= H || iw < 0 || iw >= W) {
+    zero4(v);
     return;
   }
-  const size_t off = (((size_t)b * g.H + ih) * g.W + iw) * g.C + c0;
-  unpack4(ldg8(x + off), v);
+  unpack4(ldg8(x + (((size_t)b * H + ih) * W + iw) * C + c0), v);
 #pragma unroll
   for (int k = 0; k < CPT; ++k) v[k] = act_apply<ACT>(v[k], s[k], t[k]);
 }
 
-// weights are stored tap-major [9][C] (bf16 shadow of the flat parameter buffer; the
-// torch-layout Parameter is a strided view of it), so one kernel row is 3 x 8-B loads
-PG_DEVICE void ldw4(const bf16_t *__restrict__ w, int C, int q, int c0, float (&o)[CPT]) {
-  unpack4(ldg8(w + (size_t)q * C + c0), o);
+// dy = a*g + b*y + c at (b, oh, ow) of [*, Ho, Wo, C]; OOB -> 0
+PG_DEVICE void load_dy4(const bf16_t *__restrict__ g, const bf16_t *__restrict__ y, int Ho, int Wo, int C,
+                        int b, int oh, int ow, int c0, const float (&al)[CPT], const float (&be)[CPT],
+                        const float (&ga)[CPT], float (&v)[CPT]) {
+  if (oh < 0 || oh >= Ho || ow < 0 || ow >= Wo) {
+    zero4(v);
+    return;
+  }
+  const size_t off = (((size_t)b * Ho + oh) * Wo + ow) * C + c0;
+  float gv[CPT], yv[CPT];
+  unpack4(ldg8(g + off), gv);
+  unpack4(ldg8(y + off), yv);
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) v[k] = fmaf(al[k], gv[k], fmaf(be[k], yv[k], ga[k]));
+}
+
+
+// Raw (untransformed) 3-column row segment, loaded one strip row ahead so the
+// loads are in flight while the current row's FMAs run (software pipelining).
+struct Raw3 {
+  uint2 v[3];
+};
+PG_DEVICE void load_raw3(Raw3 &r, const bf16_t *__restrict__ x, int H, int W, int C, int b, int ih,
+                         int iw0, int c0) {
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    const int iw = iw0 + d;
+    r.v[d] = (ih >= 0 && ih < H && iw >= 0 && iw < W) ? ldg8(x + (((size_t)b * H + ih) * W + iw) * C + c0)
+                                                      : make_uint2(0, 0);
+  }
+}
+// transform a raw row; out-of-range entries must become exactly 0 after the transform
+template <int ACT>
+PG_DEVICE void act3(const Raw3 &r, int ih, int H, int iw0, int W, const float (&s)[CPT], const float (&t)[CPT],
+                    float (&out)[3][CPT]) {
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    const bool ok = ih >= 0 && ih < H && iw0 + d >= 0 && iw0 + d < W;
+    unpack4(r.v[d], out[d]);
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) out[d][k] = ok ? act_apply<ACT>(out[d][k], s[k], t[k]) : 0.f;
+  }
+}
+
+// tile decode: blockIdx.x -> (b, row block, column block)
+struct Tile {
+  int b, r0, w0;
+};
+PG_DEVICE Tile tile_of(const DwGeom &g) {
+  const int tw = blockIdx.x % g.tiles_w;
+  const int rest = blockIdx.x / g.tiles_w;
+  const int th = rest % g.tiles_h;
+  return Tile{rest / g.tiles_h, th * g.R, tw * g.TWc};
 }
 
 // Block-level reduction of per-thread [NV][CPT] channel partials of this workgroup's CC
-// channels into part[blockIdx.x][NV][C] (columns cbase..cbase+CC); tid = tw * C4 + c4.
-// lds must hold TW*CC floats (<= 1024).
+// channels into part[blockIdx.x][NV][C] (columns cbase..cbase+CC); tid = col * C4 + c4.
 template <int NV>
 PG_DEVICE void block_channel_partials(float (&acc)[NV][CPT], float *__restrict__ part, int C, int CC,
-                                      int cbase, int TW, float *lds) {
+                                      int cbase, int ncol, float *lds) {
   const int tid = threadIdx.x;
   const int C4 = CC / CPT;
-  const int c4 = tid % C4, tw = tid / C4;
-  const bool active = tw < TW;
+  const int c4 = tid % C4, col = tid / C4;
   for (int v = 0; v < NV; ++v) {
-    if (active) {
-      *reinterpret_cast<float4 *>(lds + tw * CC + c4 * CPT) =
-          make_float4(acc[v][0], acc[v][1], acc[v][2], acc[v][3]);
-    }
+    if (col < ncol)
+      *reinterpret_cast<float4 *>(lds + col * CC + c4 * CPT) = make_float4(acc[v][0], acc[v][1], acc[v][2], acc[v][3]);
     __syncthreads();
     for (int c = tid; c < CC; c += blockDim.x) {
       float s = 0.f;
-      for (int w = 0; w < TW; ++w) s += lds[w * CC + c];
+      for (int w = 0; w < ncol; ++w) s += lds[w * CC + c];
       part[((size_t)blockIdx.x * NV + v) * C + cbase + c] = s;
     }
     __syncthreads();
@@ -100,104 +151,120 @@ PG_DEVICE void block_channel_partials(float (&acc)[NV][CPT], float *__restrict__
 // ---------------------------------------------------------------------------
 // forward: y = dwconv(act(x)), partial (sum y, sum y^2)
 // ---------------------------------------------------------------------------
-template <int S, int ACT, int PIX>
-__global__ __launch_bounds__(kMaxThreads) void dw_fwd_kernel(
+template <int S, int ACT>
+__global__ __launch_bounds__(256) void dw_fwd_kernel(
     const bf16_t *__restrict__ x, const float *__restrict__ in_s, const float *__restrict__ in_t,
     const bf16_t *__restrict__ w, bf16_t *__restrict__ y, float *__restrict__ part, DwGeom g) {
   __shared__ __attribute__((aligned(16))) float red[1024];
   const int C4 = g.CC / CPT;
-  const int TW = blockDim.x / C4;
   const int tid = threadIdx.x;
-  const int c4 = tid % C4, tw = tid / C4;
+  const int c4 = tid % C4, col = tid / C4;
   const int cbase = blockIdx.y * g.CC;
   const int c0 = cbase + c4 * CPT;
-  constexpr int NCOL = (PIX - 1) * S + 3;
+  const Tile tl = tile_of(g);
+  const int ow = tl.w0 + col;
+  const bool active = col < g.TWc && ow < g.Wo;
 
   float s[CPT], t[CPT], stats[2][CPT];
+  uint2 wt[9];   // packed bf16 taps (unpacked at use: fewer live VGPRs -> more waves)
 #pragma unroll
   for (int k = 0; k < CPT; ++k) {
     s[k] = (ACT != ACT_NONE) ? in_s[c0 + k] : 1.f;
     t[k] = (ACT != ACT_NONE) ? in_t[c0 + k] : 0.f;
     stats[0][k] = stats[1][k] = 0.f;
   }
-  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 9; ++q) wt[q] = ldg8(w + (size_t)q * g.C + c0);
 
-  const int nch = (g.Wo + PIX - 1) / PIX;
-  const int rows_total = g.B * g.Ho;
-  const int r0 = blockIdx.x * g.rows_per_wg;
-  const int nrows = min(g.rows_per_wg, rows_total - r0);
-  const int items = nrows * nch;
-  if (tw < TW) {
-    for (int it = tw; it < items; it += TW) {
-      const int r = r0 + it / nch;
-      const int ow0 = (it % nch) * PIX;
-      const int b = r / g.Ho, oh = r % g.Ho;
-      float acc[PIX][CPT];
+  if (active) {
+    const int oh_end = min(tl.r0 + g.R, g.Ho);
+    const int iw0 = ow * S - 1;
+    // rolling window win[r][dw][k] = input rows oh*S-1+r; next rows prefetched raw
+    float win[3][3][CPT];
+    Raw3 n1, n2;
+    {
+      const int ih0 = tl.r0 * S - 1;
+      Raw3 r0, r1, r2;
+      load_raw3(r0, x, g.H, g.W, g.C, tl.b, ih0, iw0, c0);
+      load_raw3(r1, x, g.H, g.W, g.C, tl.b, ih0 + 1, iw0, c0);
+      load_raw3(r2, x, g.H, g.W, g.C, tl.b, ih0 + 2, iw0, c0);
+      act3<ACT>(r0, ih0, g.H, iw0, g.W, s, t, win[0]);
+      act3<ACT>(r1, ih0 + 1, g.H, iw0, g.W, s, t, win[1]);
+      act3<ACT>(r2, ih0 + 2, g.H, iw0, g.W, s, t, win[2]);
+    }
+    for (int oh = tl.r0; oh < oh_end; ++oh) {
+      const int ihb = oh * S - 1;
+      if (oh > tl.r0) {
+        if constexpr (S == 1) {
 #pragma unroll
-      for (int o = 0; o < PIX; ++o)
+          for (int dw = 0; dw < 3; ++dw)
 #pragma unroll
-        for (int k = 0; k < CPT; ++k) acc[o][k] = 0.f;
-#pragma unroll 1
-      for (int dh = 0; dh < 3; ++dh) {
-        const int ih = oh * S - 1 + dh;
-        float w0[CPT], w1[CPT], w2[CPT];
-        ldw4(w, g.C, dh * 3 + 0, c0, w0);
-        ldw4(w, g.C, dh * 3 + 1, c0, w1);
-        ldw4(w, g.C, dh * 3 + 2, c0, w2);
-#pragma unroll
-        for (int j = 0; j < NCOL; ++j) {
-          const int iw = ow0 * S - 1 + j;
-          float v[CPT];
-          load_act4<ACT>(x, g, b, ih, iw, c0, s, t, v);
-#pragma unroll
-          for (int o = 0; o < PIX; ++o) {
-            const int dw = j - o * S;
-            if (dw >= 0 && dw <= 2) {
-#pragma unroll
-              for (int k = 0; k < CPT; ++k)
-                acc[o][k] = fmaf(v[k], dw == 0 ? w0[k] : (dw == 1 ? w1[k] : w2[k]), acc[o][k]);
+            for (int k = 0; k < CPT; ++k) {
+              win[0][dw][k] = win[1][dw][k];
+              win[1][dw][k] = win[2][dw][k];
             }
-          }
+          act3<ACT>(n1, ihb + 2, g.H, iw0, g.W, s, t, win[2]);
+        } else {
+#pragma unroll
+          for (int dw = 0; dw < 3; ++dw)
+#pragma unroll
+            for (int k = 0; k < CPT; ++k) win[0][dw][k] = win[2][dw][k];
+          act3<ACT>(n1, ihb + 1, g.H, iw0, g.W, s, t, win[1]);
+          act3<ACT>(n2, ihb + 2, g.H, iw0, g.W, s, t, win[2]);
         }
       }
-#pragma unroll
-      for (int o = 0; o < PIX; ++o) {
-        if (ow0 + o < g.Wo) {
-          const size_t off = (((size_t)b * g.Ho + oh) * g.Wo + ow0 + o) * g.C + c0;
-          stg8(y + off, pack4(acc[o]));
-#pragma unroll
-          for (int k = 0; k < CPT; ++k) {
-            stats[0][k] += acc[o][k];
-            stats[1][k] = fmaf(acc[o][k], acc[o][k], stats[1][k]);
-          }
+      if (oh + 1 < oh_end) {   // prefetch the rows the next output row adds
+        const int nb = (oh + 1) * S - 1;
+        if constexpr (S == 1) {
+          load_raw3(n1, x, g.H, g.W, g.C, tl.b, nb + 2, iw0, c0);
+        } else {
+          load_raw3(n1, x, g.H, g.W, g.C, tl.b, nb + 1, iw0, c0);
+          load_raw3(n2, x, g.H, g.W, g.C, tl.b, nb + 2, iw0, c0);
         }
+      }
+      float acc[CPT];
+      zero4(acc);
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int dw = 0; dw < 3; ++dw) {
+          float wv[CPT];
+          unpack4(wt[r * 3 + dw], wv);
+#pragma unroll
+          for (int k = 0; k < CPT; ++k) acc[k] = fmaf(win[r][dw][k], wv[k], acc[k]);
+        }
+      stg8(y + (((size_t)tl.b * g.Ho + oh) * g.Wo + ow) * g.C + c0, pack4(acc));
+#pragma unroll
+      for (int k = 0; k < CPT; ++k) {
+        stats[0][k] += acc[k];
+        stats[1][k] = fmaf(acc[k], acc[k], stats[1][k]);
       }
     }
   }
-  __syncthreads();
-  block_channel_partials<2>(stats, part, g.C, g.CC, cbase, TW, red);
+  block_channel_partials<2>(stats, part, g.C, g.CC, cbase, g.TWc, red);
 }
 
 // ---------------------------------------------------------------------------
 // dgrad: gout = mask_prev * dwconv^T(dy),  dy = a*g + b*y + c (this layer's BN backward)
-// partial (sum gout, sum gout*yprev) for the producer BN
+// thread = one INPUT column, strip of input rows; partial (sum gout, sum gout*yprev)
 // ---------------------------------------------------------------------------
-template <int S, int PIX>
-__global__ __launch_bounds__(kMaxThreads) void dw_dgrad_kernel(
+template <int S>
+__global__ __launch_bounds__(256) void dw_dgrad_kernel(
     const bf16_t *__restrict__ gin, const bf16_t *__restrict__ yself, const float *__restrict__ coef,
     const bf16_t *__restrict__ w, const bf16_t *__restrict__ yprev, const float *__restrict__ ps,
     const float *__restrict__ pt, bf16_t *__restrict__ gout, float *__restrict__ part, DwGeom g) {
   __shared__ __attribute__((aligned(16))) float red[1024];
   const int C4 = g.CC / CPT;
-  const int TW = blockDim.x / C4;
   const int tid = threadIdx.x;
-  const int c4 = tid % C4, tw = tid / C4;
+  const int c4 = tid % C4, col = tid / C4;
   const int cbase = blockIdx.y * g.CC;
   const int c0 = cbase + c4 * CPT;
-  // PIX input pixels per item; output columns touching them:
-  constexpr int NCOL = (S == 1) ? PIX + 2 : PIX / 2 + 2;
+  const Tile tl = tile_of(g);        // tiles over the INPUT grid (H x W)
+  const int iw = tl.w0 + col;
+  const bool active = col < g.TWc && iw < g.W;
 
   float al[CPT], be[CPT], ga[CPT], s[CPT], t[CPT], stats[2][CPT];
+  float wt[9][CPT];
 #pragma unroll
   for (int k = 0; k < CPT; ++k) {
     al[k] = coef[c0 + k];
@@ -207,69 +274,119 @@ __global__ __launch_bounds__(kMaxThreads) void dw_dgrad_kernel(
     t[k] = pt[c0 + k];
     stats[0][k] = stats[1][k] = 0.f;
   }
-  __syncthreads();
-  const int nch = (g.W + PIX - 1) / PIX;
-  const int rows_total = g.B * g.H;
-  const int r0 = blockIdx.x * g.rows_per_wg;
-  const int nrows = min(g.rows_per_wg, rows_total - r0);
-  const int items = nrows * nch;
-  if (tw < TW) {
-    for (int it = tw; it < items; it += TW) {
-      const int r = r0 + it / nch;
-      const int iw0 = (it % nch) * PIX;
-      const int b = r / g.H, ih = r % g.H;
-      float acc[PIX][CPT];
 #pragma unroll
-      for (int o = 0; o < PIX; ++o)
+  for (int q = 0; q < 9; ++q) unpack4(ldg8(w + (size_t)q * g.C + c0), wt[q]);
+
+  if (active) {
+    const int ih_end = min(tl.r0 + g.R, g.H);
+    if constexpr (S == 1) {
+      // dx[ih][iw] = sum_{dh,dw} dy[ih+1-dh][iw+1-dw] * w[dh][dw];  window rows ih-1..ih+1 (as dy rows)
+      float win[3][3][CPT];   // win[r][c]: dy row ih-1+r, col iw-1+c
 #pragma unroll
-        for (int k = 0; k < CPT; ++k) acc[o][k] = 0.f;
-#pragma unroll 1
-      for (int dh = 0; dh < 3; ++dh) {
-        int oh;
-        if constexpr (S == 1) {
-          oh = ih + 1 - dh;
-        } else {
-          const int num = ih + 1 - dh;
-          if (num & 1) continue;
-          oh = num >> 1;
-        }
-        if (oh < 0 || oh >= g.Ho) continue;
-        float w0[CPT], w1[CPT], w2[CPT];
-        ldw4(w, g.C, dh * 3 + 0, c0, w0);
-        ldw4(w, g.C, dh * 3 + 1, c0, w1);
-        ldw4(w, g.C, dh * 3 + 2, c0, w2);
+      for (int r = 0; r < 3; ++r)
 #pragma unroll
-        for (int j = 0; j < NCOL; ++j) {
-          const int ow = (S == 1) ? iw0 - 1 + j : (iw0 >> 1) - 1 + j;
-          if (ow < 0 || ow >= g.Wo) continue;
-          const size_t off = (((size_t)b * g.Ho + oh) * g.Wo + ow) * g.C + c0;
-          float gv[CPT], yv[CPT];
-          unpack4(ldg8(gin + off), gv);
-          unpack4(ldg8(yself + off), yv);
+        for (int c = 0; c < 3; ++c)
+          load_dy4(gin, yself, g.Ho, g.Wo, g.C, tl.b, tl.r0 - 1 + r, iw - 1 + c, c0, al, be, ga, win[r][c]);
+      Raw3 ng, ny;   // next dy row (raw g and y), prefetched one row ahead
+      for (int ih = tl.r0; ih < ih_end; ++ih) {
+        if (ih > tl.r0) {
 #pragma unroll
-          for (int k = 0; k < CPT; ++k) gv[k] = fmaf(al[k], gv[k], fmaf(be[k], yv[k], ga[k]));
+          for (int c = 0; c < 3; ++c)
 #pragma unroll
-          for (int i = 0; i < PIX; ++i) {
-            const int dw = (S == 1) ? (i - j + 2) : (i + 3 - 2 * j);
-            if (dw >= 0 && dw <= 2) {
-#pragma unroll
-              for (int k = 0; k < CPT; ++k)
-                acc[i][k] = fmaf(gv[k], dw == 0 ? w0[k] : (dw == 1 ? w1[k] : w2[k]), acc[i][k]);
+            for (int k = 0; k < CPT; ++k) {
+              win[0][c][k] = win[1][c][k];
+              win[1][c][k] = win[2][c][k];
             }
+          const int oh = ih + 1;
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            const bool ok = oh >= 0 && oh < g.Ho && iw - 1 + c >= 0 && iw - 1 + c < g.Wo;
+            float gv[CPT], yv[CPT];
+            unpack4(ng.v[c], gv);
+            unpack4(ny.v[c], yv);
+#pragma unroll
+            for (int k = 0; k < CPT; ++k) win[2][c][k] = ok ? fmaf(al[k], gv[k], fmaf(be[k], yv[k], ga[k])) : 0.f;
           }
         }
-      }
+        if (ih + 1 < ih_end) {
+          load_raw3(ng, gin, g.Ho, g.Wo, g.C, tl.b, ih + 2, iw - 1, c0);
+          load_raw3(ny, yself, g.Ho, g.Wo, g.C, tl.b, ih + 2, iw - 1, c0);
+        }
+        float acc[CPT];
+        zero4(acc);
+        // dy row ih+1-dh = win[2-dh], col iw+1-dw = win[..][2-dw]
 #pragma unroll
-      for (int i = 0; i < PIX; ++i) {
-        if (iw0 + i < g.W) {
-          const size_t off = (((size_t)b * g.H + ih) * g.W + iw0 + i) * g.C + c0;
+        for (int dh = 0; dh < 3; ++dh)
+#pragma unroll
+          for (int dw = 0; dw < 3; ++dw)
+#pragma unroll
+            for (int k = 0; k < CPT; ++k) acc[k] = fmaf(win[2 - dh][2 - dw][k], wt[dh * 3 + dw][k], acc[k]);
+        const size_t off = (((size_t)tl.b * g.H + ih) * g.W + iw) * g.C + c0;
+        float yp[CPT];
+        unpack4(ldg8(yprev + off), yp);
+#pragma unroll
+        for (int k = 0; k < CPT; ++k) acc[k] *= relu6_mask(yp[k], s[k], t[k]);
+        const uint2 packed = pack4(acc);
+        float gr[CPT];
+        unpack4(packed, gr);
+#pragma unroll
+        for (int k = 0; k < CPT; ++k) {
+          stats[0][k] += gr[k];
+          stats[1][k] = fmaf(gr[k], yp[k], stats[1][k]);
+        }
+        stg8(gout + off, packed);
+      }
+    } else {
+      // stride 2.  Column: even iw -> ow = iw/2 (dw=1); odd iw -> ow = (iw+1)/2 (dw=0), (iw-1)/2 (dw=2)
+      // Row: even ih = 2o -> dy row o (dh=1); odd ih = 2o+1 -> dy rows o (dh=2), o+1 (dh=0)
+      const bool odd_w = iw & 1;
+      const int owA = odd_w ? (iw + 1) >> 1 : iw >> 1;   // dw = 0 (odd) or 1 (even)
+      const int owB = (iw - 1) >> 1;                      // dw = 2 (odd only)
+      // per-thread tap weights (selected with static indices: no runtime-indexed arrays)
+      float wA[3][CPT], wB[3][CPT];   // [dh] for column A (dw = 0 if odd else 1) and B (dw = 2)
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int k = 0; k < CPT; ++k) {
+          wA[r][k] = odd_w ? wt[r * 3 + 0][k] : wt[r * 3 + 1][k];
+          wB[r][k] = odd_w ? wt[r * 3 + 2][k] : 0.f;
+        }
+      // tiles start at even rows (R even)
+      float cur[2][CPT], nxt[2][CPT];   // dy row o / o+1 at columns A, B
+      int o = tl.r0 >> 1;
+      load_dy4(gin, yself, g.Ho, g.Wo, g.C, tl.b, o, owA, c0, al, be, ga, cur[0]);
+      if (odd_w) load_dy4(gin, yself, g.Ho, g.Wo, g.C, tl.b, o, owB, c0, al, be, ga, cur[1]);
+      else zero4(cur[1]);
+      for (int ih = tl.r0; ih < ih_end; ih += 2) {
+        o = ih >> 1;
+        load_dy4(gin, yself, g.Ho, g.Wo, g.C, tl.b, o + 1, owA, c0, al, be, ga, nxt[0]);
+        if (odd_w) load_dy4(gin, yself, g.Ho, g.Wo, g.C, tl.b, o + 1, owB, c0, al, be, ga, nxt[1]);
+        else zero4(nxt[1]);
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          const int r = ih + half;
+          if (r >= ih_end) break;
+          float acc[CPT];
+          zero4(acc);
+          if (half == 0) {          // even row: dh = 1, dy row o
+#pragma unroll
+            for (int k = 0; k < CPT; ++k)
+              acc[k] = fmaf(cur[0][k], wA[1][k], fmaf(cur[1][k], wB[1][k], acc[k]));
+          } else {                  // odd row: dh = 2 (row o), dh = 0 (row o+1)
+#pragma unroll
+            for (int k = 0; k < CPT; ++k) {
+              acc[k] = fmaf(cur[0][k], wA[2][k], fmaf(cur[1][k], wB[2][k], acc[k]));
+              acc[k] = fmaf(nxt[0][k], wA[0][k], fmaf(nxt[1][k], wB[0][k], acc[k]));
+            }
+          }
+          const size_t off = (((size_t)tl.b * g.H + r) * g.W + iw) * g.C + c0;
           float yp[CPT];
           unpack4(ldg8(yprev + off), yp);
 #pragma unroll
-          for (int k = 0; k < CPT; ++k) acc[i][k] *= relu6_mask(yp[k], s[k], t[k]);
-          const uint2 packed = pack4(acc[i]);
+          for (int k = 0; k < CPT; ++k) acc[k] *= relu6_mask(yp[k], s[k], t[k]);
+          const uint2 packed = pack4(acc);
           float gr[CPT];
-          unpack4(packed, gr);  // statistics of the stored (bf16) gradient
+          unpack4(packed, gr);
 #pragma unroll
           for (int k = 0; k < CPT; ++k) {
             stats[0][k] += gr[k];
@@ -277,29 +394,35 @@ __global__ __launch_bounds__(kMaxThreads) void dw_dgrad_kernel(
           }
           stg8(gout + off, packed);
         }
+#pragma unroll
+        for (int k = 0; k < CPT; ++k) {
+          cur[0][k] = nxt[0][k];
+          cur[1][k] = nxt[1][k];
+        }
       }
     }
   }
-  __syncthreads();
-  block_channel_partials<2>(stats, part, g.C, g.CC, cbase, TW, red);
+  block_channel_partials<2>(stats, part, g.C, g.CC, cbase, g.TWc, red);
 }
 
 // ---------------------------------------------------------------------------
-// wgrad: dW[c][tap] partials per workgroup  [P][9][C]
+// wgrad: dW[tap][c] partials per workgroup  [P][9][C]
+// thread = one output column, strip of output rows, rolling z window
 // ---------------------------------------------------------------------------
-template <int S, int PIX>
-__global__ __launch_bounds__(kMaxThreads) void dw_wgrad_kernel(
+template <int S>
+__global__ __launch_bounds__(256) void dw_wgrad_kernel(
     const bf16_t *__restrict__ gin, const bf16_t *__restrict__ yself, const float *__restrict__ coef,
     const bf16_t *__restrict__ yprev, const float *__restrict__ ps, const float *__restrict__ pt,
     float *__restrict__ part, DwGeom g) {
   __shared__ __attribute__((aligned(16))) float lds[1024];
   const int C4 = g.CC / CPT;
-  const int TW = blockDim.x / C4;
   const int tid = threadIdx.x;
-  const int c4 = tid % C4, tw = tid / C4;
+  const int c4 = tid % C4, col = tid / C4;
   const int cbase = blockIdx.y * g.CC;
   const int c0 = cbase + c4 * CPT;
-  constexpr int NCOL = (PIX - 1) * S + 3;
+  const Tile tl = tile_of(g);
+  const int ow = tl.w0 + col;
+  const bool active = col < g.TWc && ow < g.Wo;
 
   float al[CPT], be[CPT], ga[CPT], s[CPT], t[CPT];
   float accw[9][CPT];
@@ -313,59 +436,81 @@ __global__ __launch_bounds__(kMaxThreads) void dw_wgrad_kernel(
 #pragma unroll
     for (int q = 0; q < 9; ++q) accw[q][k] = 0.f;
   }
-  const int nch = (g.Wo + PIX - 1) / PIX;
-  const int rows_total = g.B * g.Ho;
-  const int r0 = blockIdx.x * g.rows_per_wg;
-  const int nrows = min(g.rows_per_wg, rows_total - r0);
-  const int items = nrows * nch;
-  if (tw < TW) {
-    for (int it = tw; it < items; it += TW) {
-      const int r = r0 + it / nch;
-      const int ow0 = (it % nch) * PIX;
-      const int b = r / g.Ho, oh = r % g.Ho;
-      float dy[PIX][CPT];
+  if (active) {
+    const int oh_end = min(tl.r0 + g.R, g.Ho);
+    const int iw0 = ow * S - 1;
+    float win[3][3][CPT];
+    Raw3 n1, n2;
+    uint2 gnext = make_uint2(0, 0), ynext = make_uint2(0, 0);
+    {
+      const int ih0 = tl.r0 * S - 1;
+      Raw3 r0, r1, r2;
+      load_raw3(r0, yprev, g.H, g.W, g.C, tl.b, ih0, iw0, c0);
+      load_raw3(r1, yprev, g.H, g.W, g.C, tl.b, ih0 + 1, iw0, c0);
+      load_raw3(r2, yprev, g.H, g.W, g.C, tl.b, ih0 + 2, iw0, c0);
+      const size_t off = (((size_t)tl.b * g.Ho + tl.r0) * g.Wo + ow) * g.C + c0;
+      gnext = ldg8(gin + off);
+      ynext = ldg8(yself + off);
+      act3<ACT_BN_RELU6>(r0, ih0, g.H, iw0, g.W, s, t, win[0]);
+      act3<ACT_BN_RELU6>(r1, ih0 + 1, g.H, iw0, g.W, s, t, win[1]);
+      act3<ACT_BN_RELU6>(r2, ih0 + 2, g.H, iw0, g.W, s, t, win[2]);
+    }
+    for (int oh = tl.r0; oh < oh_end; ++oh) {
+      const int ihb = oh * S - 1;
+      if (oh > tl.r0) {
+        if constexpr (S == 1) {
 #pragma unroll
-      for (int o = 0; o < PIX; ++o) {
-        if (ow0 + o < g.Wo) {
-          const size_t off = (((size_t)b * g.Ho + oh) * g.Wo + ow0 + o) * g.C + c0;
-          float gv[CPT], yv[CPT];
-          unpack4(ldg8(gin + off), gv);
-          unpack4(ldg8(yself + off), yv);
+          for (int dw = 0; dw < 3; ++dw)
 #pragma unroll
-          for (int k = 0; k < CPT; ++k) dy[o][k] = fmaf(al[k], gv[k], fmaf(be[k], yv[k], ga[k]));
+            for (int k = 0; k < CPT; ++k) {
+              win[0][dw][k] = win[1][dw][k];
+              win[1][dw][k] = win[2][dw][k];
+            }
+          act3<ACT_BN_RELU6>(n1, ihb + 2, g.H, iw0, g.W, s, t, win[2]);
         } else {
 #pragma unroll
-          for (int k = 0; k < CPT; ++k) dy[o][k] = 0.f;
+          for (int dw = 0; dw < 3; ++dw)
+#pragma unroll
+            for (int k = 0; k < CPT; ++k) win[0][dw][k] = win[2][dw][k];
+          act3<ACT_BN_RELU6>(n1, ihb + 1, g.H, iw0, g.W, s, t, win[1]);
+          act3<ACT_BN_RELU6>(n2, ihb + 2, g.H, iw0, g.W, s, t, win[2]);
         }
       }
+      float dy[CPT];
+      {
+        float gv[CPT], yv[CPT];
+        unpack4(gnext, gv);
+        unpack4(ynext, yv);
 #pragma unroll
-      for (int dh = 0; dh < 3; ++dh) {
-        const int ih = oh * S - 1 + dh;
-#pragma unroll
-        for (int j = 0; j < NCOL; ++j) {
-          const int iw = ow0 * S - 1 + j;
-          float v[CPT];
-          load_act4<ACT_BN_RELU6>(yprev, g, b, ih, iw, c0, s, t, v);
-#pragma unroll
-          for (int o = 0; o < PIX; ++o) {
-            const int dw = j - o * S;
-            if (dw >= 0 && dw <= 2) {
-#pragma unroll
-              for (int k = 0; k < CPT; ++k) accw[dh * 3 + dw][k] = fmaf(dy[o][k], v[k], accw[dh * 3 + dw][k]);
-            }
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);  // keep one window row live
+        for (int k = 0; k < CPT; ++k) dy[k] = fmaf(al[k], gv[k], fmaf(be[k], yv[k], ga[k]));
       }
+      if (oh + 1 < oh_end) {   // prefetch next row: z rows and dy
+        const int nb = (oh + 1) * S - 1;
+        if constexpr (S == 1) {
+          load_raw3(n1, yprev, g.H, g.W, g.C, tl.b, nb + 2, iw0, c0);
+        } else {
+          load_raw3(n1, yprev, g.H, g.W, g.C, tl.b, nb + 1, iw0, c0);
+          load_raw3(n2, yprev, g.H, g.W, g.C, tl.b, nb + 2, iw0, c0);
+        }
+        const size_t off = (((size_t)tl.b * g.Ho + oh + 1) * g.Wo + ow) * g.C + c0;
+        gnext = ldg8(gin + off);
+        ynext = ldg8(yself + off);
+      }
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int dw = 0; dw < 3; ++dw)
+#pragma unroll
+          for (int k = 0; k < CPT; ++k) accw[r * 3 + dw][k] = fmaf(dy[k], win[r][dw][k], accw[r * 3 + dw][k]);
     }
   }
-  block_channel_partials<9>(accw, part, g.C, g.CC, cbase, TW, lds);
+  block_channel_partials<9>(accw, part, g.C, g.CC, cbase, g.TWc, lds);
 }
 
-// reduce [P][9][C] -> grad [9][C] fp32
+// reduce [P][9][C] -> grad [9][C] fp32 (tap-major, the flat-buffer layout)
 __global__ __launch_bounds__(256) void dw_wgrad_reduce_kernel(const float *__restrict__ part, int P,
                                                              int C, float *__restrict__ grad) {
-  const int idx = blockIdx.x * 64 + (threadIdx.x & 63);  // over 9*C (tap-major in part)
+  const int idx = blockIdx.x * 64 + (threadIdx.x & 63);
   const int ty = threadIdx.x >> 6;
   __shared__ float sh[4][64];
   float s = 0.f;
@@ -373,100 +518,76 @@ __global__ __launch_bounds__(256) void dw_wgrad_reduce_kernel(const float *__res
     for (int p = ty; p < P; p += 4) s += part[(size_t)p * 9 * C + idx];
   sh[ty][threadIdx.x & 63] = s;
   __syncthreads();
-  if (ty == 0 && idx < 9 * C) {
-    s = sh[0][threadIdx.x] + sh[1][threadIdx.x] + sh[2][threadIdx.x] + sh[3][threadIdx.x];
-    grad[idx] = s;  // [9][C] tap-major, the layout of the flat parameter buffer
-  }
+  if (ty == 0 && idx < 9 * C)
+    grad[idx] = sh[0][threadIdx.x] + sh[1][threadIdx.x] + sh[2][threadIdx.x] + sh[3][threadIdx.x];
 }
 
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int kPixF = 4, kPixD1 = 4, kPixD2 = 8, kPixW = 4;
-
-// channels per workgroup: the largest multiple of 4 dividing C that is <= 64, so a
-// workgroup covers many pixels of a narrow channel slab (long rows per thread group,
-// small BN/weight partial rows) instead of all channels of very few pixels
+// channels per workgroup: the largest multiple of 4 dividing C that is <= 64
 int dw_cc(int C) {
   for (int cc = 64; cc >= 4; cc -= 4)
     if (C % cc == 0) return cc;
   return 4;
 }
 
-int dw_block_threads(int C) {
-  const int C4 = dw_cc(C) / CPT;
-  int TW = kMaxThreads / C4;
-  if (TW < 1) TW = 1;
-  return C4 * TW;
+// kind 0 = fwd (tiles over the output grid), 1 = dgrad (input grid), 2 = wgrad (output grid)
+DwGeom dw_geom(int kind, int B, int H, int W, int C, int stride) {
+  DwGeom g;
+  g.B = B;
+  g.H = H;
+  g.W = W;
+  g.C = C;
+  g.Ho = (H - 1) / stride + 1;
+  g.Wo = (W - 1) / stride + 1;
+  g.CC = dw_cc(C);
+  const int C4 = g.CC / CPT;
+  const int gw = kind == 1 ? W : g.Wo, gh = kind == 1 ? H : g.Ho;
+  int twc = 256 / C4;
+  if (twc > gw) twc = gw;
+  g.TWc = twc;
+  int R = kRows;
+  if (kind == 2) R = 2 * kRows;                 // weight gradient: longer strips, fewer partial rows
+  if (kind == 1 && stride == 2 && (R & 1)) ++R;  // dgrad s2 tiles start on even input rows
+  if (R > gh) R = (kind == 1 && stride == 2) ? ((gh + 1) & ~1) : gh;
+  g.R = R;
+  g.tiles_w = (gw + g.TWc - 1) / g.TWc;
+  g.tiles_h = (gh + g.R - 1) / g.R;
+  return g;
 }
 
-int dw_rows_per_wg(int rows_total, int per_row_items, int TW, int target_items_per_thread,
-                   int min_wgs) {
-  int rpw = (TW * target_items_per_thread + per_row_items - 1) / per_row_items;
-  if (rpw < 1) rpw = 1;
-  while (rpw > 1 && (rows_total + rpw - 1) / rpw < min_wgs) rpw >>= 1;
-  return rpw;
-}
-
-struct DwLaunch {
-  int threads, rpw, grid, chunks;
-};
-
-DwLaunch dw_launch(int kind, int B, int H, int W, int C, int stride) {
-  const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
-  const int threads = dw_block_threads(C);
-  const int TW = threads / (dw_cc(C) / CPT);
-  const int chunks = C / dw_cc(C);
-  const int min_wgs = (2048 + chunks - 1) / chunks;
-  DwLaunch l{threads, 1, 1, chunks};
-  if (kind == 0) {  // fwd
-    l.rpw = dw_rows_per_wg(B * Ho, (Wo + kPixF - 1) / kPixF, TW, 4, min_wgs);
-    l.grid = (B * Ho + l.rpw - 1) / l.rpw;
-  } else if (kind == 1) {  // dgrad (over input rows)
-    const int pix = stride == 1 ? kPixD1 : kPixD2;
-    l.rpw = dw_rows_per_wg(B * H, (W + pix - 1) / pix, TW, 4, min_wgs);
-    l.grid = (B * H + l.rpw - 1) / l.rpw;
-  } else {  // wgrad
-    l.rpw = dw_rows_per_wg(B * Ho, (Wo + kPixW - 1) / kPixW, TW, 8, (1024 + chunks - 1) / chunks);
-    l.grid = (B * Ho + l.rpw - 1) / l.rpw;
-  }
-  return l;
-}
+int dw_grid_x(const DwGeom &g) { return g.B * g.tiles_h * g.tiles_w; }
+int dw_threads(const DwGeom &g) { return (g.CC / CPT) * g.TWc; }
 }  // namespace
 
-int dw_fwd_num_partials(int B, int H, int W, int C, int stride) { return dw_launch(0, B, H, W, C, stride).grid; }
-int dw_dgrad_num_partials(int B, int H, int W, int C, int stride) { return dw_launch(1, B, H, W, C, stride).grid; }
-int dw_wgrad_num_partials(int B, int H, int W, int C, int stride) { return dw_launch(2, B, H, W, C, stride).grid; }
+int dw_fwd_num_partials(int B, int H, int W, int C, int stride) { return dw_grid_x(dw_geom(0, B, H, W, C, stride)); }
+int dw_dgrad_num_partials(int B, int H, int W, int C, int stride) { return dw_grid_x(dw_geom(1, B, H, W, C, stride)); }
+int dw_wgrad_num_partials(int B, int H, int W, int C, int stride) { return dw_grid_x(dw_geom(2, B, H, W, C, stride)); }
 
 void launch_dw_fwd(const bf16_t *x, const float *in_s, const float *in_t, int act, const bf16_t *w,
                    bf16_t *y, float *part, int B, int H, int W, int C, int stride, hipStream_t st) {
-  const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
-  const DwLaunch l = dw_launch(0, B, H, W, C, stride);
-  DwGeom g{B, H, W, C, Ho, Wo, l.rpw, dw_cc(C)};
+  const DwGeom g = dw_geom(0, B, H, W, C, stride);
+  dim3 grid(dw_grid_x(g), C / g.CC), block(dw_threads(g));
   if (stride == 1) {
-    if (act == ACT_BN_RELU6)
-      hipLaunchKernelGGL((dw_fwd_kernel<1, ACT_BN_RELU6, kPixF>), dim3(l.grid, l.chunks), dim3(l.threads), 0, st, x, in_s, in_t, w, y, part, g);
-    else
-      hipLaunchKernelGGL((dw_fwd_kernel<1, ACT_NONE, kPixF>), dim3(l.grid, l.chunks), dim3(l.threads), 0, st, x, in_s, in_t, w, y, part, g);
+    if (act == ACT_BN_RELU6) hipLaunchKernelGGL((dw_fwd_kernel<1, ACT_BN_RELU6>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
+    else hipLaunchKernelGGL((dw_fwd_kernel<1, ACT_NONE>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
   } else {
-    if (act == ACT_BN_RELU6)
-      hipLaunchKernelGGL((dw_fwd_kernel<2, ACT_BN_RELU6, kPixF>), dim3(l.grid, l.chunks), dim3(l.threads), 0, st, x, in_s, in_t, w, y, part, g);
-    else
-      hipLaunchKernelGGL((dw_fwd_kernel<2, ACT_NONE, kPixF>), dim3(l.grid, l.chunks), dim3(l.threads), 0, st, x, in_s, in_t, w, y, part, g);
+    if (act == ACT_BN_RELU6) hipLaunchKernelGGL((dw_fwd_kernel<2, ACT_BN_RELU6>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
+    else hipLaunchKernelGGL((dw_fwd_kernel<2, ACT_NONE>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
   }
 }
 
 void launch_dw_dgrad(const bf16_t *gin, const bf16_t *yself, const float *coef, const bf16_t *w,
                      const bf16_t *yprev, const float *ps, const float *pt, bf16_t *gout,
                      float *part, int B, int H, int W, int C, int stride, hipStream_t st) {
-  const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
-  const DwLaunch l = dw_launch(1, B, H, W, C, stride);
-  DwGeom g{B, H, W, C, Ho, Wo, l.rpw, dw_cc(C)};
+  const DwGeom g = dw_geom(1, B, H, W, C, stride);
+  dim3 grid(dw_grid_x(g), C / g.CC), block(dw_threads(g));
   if (stride == 1)
-    hipLaunchKernelGGL((dw_dgrad_kernel<1, kPixD1>), dim3(l.grid, l.chunks), dim3(l.threads), 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g);
+    hipLaunchKernelGGL((dw_dgrad_kernel<1>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g);
   else
-    hipLaunchKernelGGL((dw_dgrad_kernel<2, kPixD2>), dim3(l.grid, l.chunks), dim3(l.threads), 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g);
+    hipLaunchKernelGGL((dw_dgrad_kernel<2>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g);
 }
 
 void launch_colsum(const float *src, int R, long long n, float *dst, int &rows_out, hipStream_t st);
@@ -474,17 +595,17 @@ void launch_colsum(const float *src, int R, long long n, float *dst, int &rows_o
 void launch_dw_wgrad(const bf16_t *gin, const bf16_t *yself, const float *coef, const bf16_t *yprev,
                      const float *ps, const float *pt, float *part, float *grad, int B, int H, int W,
                      int C, int stride, hipStream_t st) {
-  const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
-  const DwLaunch l = dw_launch(2, B, H, W, C, stride);
-  DwGeom g{B, H, W, C, Ho, Wo, l.rpw, dw_cc(C)};
+  const DwGeom g = dw_geom(2, B, H, W, C, stride);
+  const int P = dw_grid_x(g);
+  dim3 grid(P, C / g.CC), block(dw_threads(g));
   if (stride == 1)
-    hipLaunchKernelGGL((dw_wgrad_kernel<1, kPixW>), dim3(l.grid, l.chunks), dim3(l.threads), 0, st, gin, yself, coef, yprev, ps, pt, part, g);
+    hipLaunchKernelGGL((dw_wgrad_kernel<1>), grid, block, 0, st, gin, yself, coef, yprev, ps, pt, part, g);
   else
-    hipLaunchKernelGGL((dw_wgrad_kernel<2, kPixW>), dim3(l.grid, l.chunks), dim3(l.threads), 0, st, gin, yself, coef, yprev, ps, pt, part, g);
-  // two-level deterministic reduction of the [P][9C] partials (level 1 written after them)
-  int rows = l.grid;
-  float *tmp = part + (size_t)l.grid * 9 * C;
-  launch_colsum(part, l.grid, 9LL * C, tmp, rows, st);
+    hipLaunchKernelGGL((dw_wgrad_kernel<2>), grid, block, 0, st, gin, yself, coef, yprev, ps, pt, part, g);
+  // deterministic two-level reduction of the [P][9C] partials (level 1 written after them)
+  int rows = P;
+  float *tmp = part + (size_t)P * 9 * C;
+  launch_colsum(part, P, 9LL * C, tmp, rows, st);
   hipLaunchKernelGGL(dw_wgrad_reduce_kernel, dim3((9 * C + 63) / 64), dim3(256), 0, st,
-                     rows == l.grid ? part : tmp, rows, C, grad);
+                     rows == P ? part : tmp, rows, C, grad);
 }
