@@ -40,7 +40,8 @@ void launch_dw_dgrad(const bf16_t *, const bf16_t *, const float *, const bf16_t
                      hipStream_t);
 void launch_dw_wgrad(const bf16_t *, const bf16_t *, const float *, const bf16_t *, const float *,
                      const float *, float *, float *, int, int, int, int, int, hipStream_t);
-int pw_gemm_num_partials(int, int);
+int pw_gemm_num_partials(int, int, int);
+void launch_wt_transpose(const bf16_t *, bf16_t *, const int *, int, hipStream_t);
 void launch_pw_gemm(int, int, const bf16_t *, const bf16_t *, const float *, const float *,
                     const float *, const bf16_t *, bf16_t *, const bf16_t *, const float *,
                     const float *, const bf16_t *, float *, int, int, int, hipStream_t);
@@ -137,6 +138,9 @@ PYBIND11_MODULE(_pgdist_C, m) {
     launch_pw_gemm(pro, epi, ptr<bf16_t>(A), ptr<bf16_t>(A2), ptr<float>(pa), ptr<float>(pb),
                    ptr<float>(pc), ptr<bf16_t>(W), ptr<bf16_t>(out), ptr<bf16_t>(Yt), ptr<float>(es),
                    ptr<float>(et), ptr<bf16_t>(R), ptr<float>(part), M, N, K, S(s));
+  });
+  m.def("wt_transpose", [](P src, P dst, P tab, int n, P s) {
+    launch_wt_transpose(ptr<bf16_t>(src), ptr<bf16_t>(dst), ptr<int>(tab), n, S(s));
   });
   m.def("pw_wgrad_workspace_floats", &pw_wgrad_workspace_floats);
   m.def("pw_wgrad", [](P G, P Y, P ga, P gb, P gc, P X, P xs, P xt, int xact, P part, P grad, int M,

@@ -6,18 +6,24 @@
 // These shapes are memory-bound on MI355X (K and N are tiny next to M), so the
 // kernel is organised as a row stream:
 //
-//  * 256-thread workgroup = 4 waves x 32 rows = 128-row M tile, N tile BN in
-//    {32,64,128}; each wave owns 2 x (BN/16) v_mfma_f32_16x16x32_bf16 tiles;
+//  * 256-thread workgroup = 4 waves x 32 rows; each wave owns 2 x (BN/16)
+//    v_mfma_f32_16x16x32_bf16 tiles, N tile BN in {32,64};
 //  * the A fragment (lane: row l&15, k = 8*(l>>4)..+7) is one 16-B global load
-//    per lane, transformed in registers by the fused prologue:
+//    per lane, issued one 64-k step AHEAD (also across M tiles of the
+//    grid-stride sweep) and transformed in registers by the fused prologue
+//    (per-k parameters staged in LDS):
 //      ACT_NONE      A as stored (materialised block output)
 //      ACT_BN_RELU6  relu6(A*s[k]+t[k])      -- producer BN + ReLU6 (forward)
-//      PRO_BNBWD     a[k]*G + b[k]*Y + c[k]   -- this layer's BN backward (dgrad;
-//                    the weight is then read as [K][N] and transposed while staged)
-//  * the weight tile [BN][K-chunk] is staged once per workgroup in LDS (padded
-//    rows -> conflict-free ds_read_b128) and reused across the workgroup's
-//    M tiles (grid-stride over M with gridDim.x a multiple of 8, so the N
-//    tiles of one M tile share an XCD L2);
+//      PRO_BNBWD     a[k]*G + b[k]*Y + c[k]   -- this layer's BN backward (dgrad,
+//                    with the transposed weight produced by wt_transpose_kernel)
+//  * large M / small K (K <= 192): the whole weight tile [BN][K] is resident in
+//    LDS (padded rows -> conflict-free ds_read_b128) for the grid-stride sweep
+//    over M tiles (gridDim.x a multiple of 8, so the N tiles of one M tile share
+//    an XCD L2);
+//  * small M (14x14 / 7x7 layers) or large K: weight fragments are prefetched
+//    straight from L2 like A, and K is split over the 4 waves (KS = 2 or 4,
+//    M tile 64 or 32 rows) so the grid keeps >= ~1.5k workgroups; the KS fp32
+//    partial tiles are summed in a fixed order in LDS (deterministic);
 //  * the epilogue goes through an LDS tile so every global load/store is a
 //    coalesced 16-B row chunk:
 //      EPI_FWD       store y, partial (sum y, sum y^2) for this layer's BN
@@ -33,8 +39,6 @@ enum { PRO_BNBWD = 3, IM2COL_STEM = 4 };
 enum { EPI_FWD = 0, EPI_BWD_RELU6 = 1, EPI_BWD_LIN = 2 };
 
 namespace {
-constexpr int kBM = 128;       // rows per M tile
-constexpr int kKC = 160;       // max K chunk staged in LDS (multiple of 32)
 constexpr int kBPad = 8;       // bf16 pad per staged weight row (16 B)
 constexpr int kCPad = 8;       // bf16 pad per staged C row
 
@@ -55,59 +59,97 @@ struct PwArgs {
 };
 }  // namespace
 
+// transform one raw 16-B A fragment (8 consecutive k of one row) by the fused prologue;
+// per-k parameters come from LDS (zero for k >= K, so padded k stay exactly 0)
 template <int PRO>
-PG_DEVICE s16x8_t load_a_frag(const PwArgs &p, int row, int k) {
-  s16x8_t r = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (row >= p.M || k >= p.K) return r;
-  const size_t off = (size_t)row * p.K + k;
-  uint4 u = ldg16(p.A + off);
+PG_DEVICE s16x8_t a_transform(const uint4 &raw, const uint4 &raw2, const float *Ps, int Kp, int kl) {
   if constexpr (PRO == ACT_NONE) {
-    return __builtin_bit_cast(s16x8_t, u);
+    return __builtin_bit_cast(s16x8_t, raw);
   } else {
     float v[8];
-    unpack8(u, v);
+    unpack8(raw, v);
+    const float4 a0 = *reinterpret_cast<const float4 *>(Ps + kl), a1 = *reinterpret_cast<const float4 *>(Ps + kl + 4);
+    const float4 b0 = *reinterpret_cast<const float4 *>(Ps + Kp + kl), b1 = *reinterpret_cast<const float4 *>(Ps + Kp + kl + 4);
+    const float aa[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
     if constexpr (PRO == PRO_BNBWD) {
       float y[8];
-      unpack8(ldg16(p.A2 + off), y);
-      const float4 a0 = *reinterpret_cast<const float4 *>(p.pa + k), a1 = *reinterpret_cast<const float4 *>(p.pa + k + 4);
-      const float4 b0 = *reinterpret_cast<const float4 *>(p.pb + k), b1 = *reinterpret_cast<const float4 *>(p.pb + k + 4);
-      const float4 c0 = *reinterpret_cast<const float4 *>(p.pc + k), c1 = *reinterpret_cast<const float4 *>(p.pc + k + 4);
-      const float aa[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-      const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+      unpack8(raw2, y);
+      const float4 c0 = *reinterpret_cast<const float4 *>(Ps + 2 * Kp + kl), c1 = *reinterpret_cast<const float4 *>(Ps + 2 * Kp + kl + 4);
       const float cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = fmaf(aa[j], v[j], fmaf(bb[j], y[j], cc[j]));
     } else {
-      const float4 s0 = *reinterpret_cast<const float4 *>(p.pa + k), s1 = *reinterpret_cast<const float4 *>(p.pa + k + 4);
-      const float4 t0 = *reinterpret_cast<const float4 *>(p.pb + k), t1 = *reinterpret_cast<const float4 *>(p.pb + k + 4);
-      const float ss[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-      const float tt[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = act_apply<PRO>(v[j], ss[j], tt[j]);
+      for (int j = 0; j < 8; ++j) v[j] = act_apply<PRO>(v[j], aa[j], bb[j]);
     }
     return __builtin_bit_cast(s16x8_t, pack8(v));
   }
 }
 
-template <int PRO, int EPI, int BN>
+// Registers of one pipeline step (64 k) of a wave: A fragments for 2 sub-steps x 2
+// row fragments (+ the Y operand of the BN backward), and with BDIRECT the weight
+// fragments 2 sub-steps x CT column tiles.
+template <int PRO, int SUBS, int CTB>
+struct PwRaw {
+  uint4 a[SUBS][2];
+  uint4 y[PRO == PRO_BNBWD ? SUBS : 1][2];
+  uint4 b[SUBS][CTB > 0 ? CTB : 1];
+};
+
+template <int PRO, int EPI, int BN, int KS, bool BDIRECT>
 __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
   constexpr int CT = BN / 16;               // col tiles per wave
-  constexpr int LDB = kKC + kBPad;          // staged weight row pitch (elements)
-  constexpr int LDC = BN + kCPad;           // staged C row pitch (elements)
+  constexpr int RG = 4 / KS;                // wave row groups (each 32 rows)
+  constexpr int BM = 32 * RG;               // rows per M tile
   constexpr int CH = BN / 8;                // 16-B chunks per C row
   constexpr int RSTEP = 256 / CH;           // rows covered per epilogue pass
+  constexpr int NP = (BM + RSTEP - 1) / RSTEP;
+  constexpr int NPAR = PRO == ACT_NONE ? 0 : (PRO == PRO_BNBWD ? 3 : 2);
+  constexpr int SUBS = BDIRECT ? 1 : 2;     // 32-k MFMA sub-steps per pipeline step
+  constexpr int KSTEP = 32 * SUBS;
+  constexpr int EB = NP < 4 ? NP : 4;       // epilogue rows whose operands are loaded together
+  constexpr int LDC = BN + kCPad;           // bf16 C tile pitch (KS == 1)
+  constexpr int LDF = BN + 4;               // fp32 C partial pitch (KS > 1)
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16_t *Bs = reinterpret_cast<bf16_t *>(smem);                       // [BN][LDB]
-  bf16_t *Cs = reinterpret_cast<bf16_t *>(smem + BN * LDB * 2);        // [kBM][LDC]
-  float *Red = reinterpret_cast<float *>(smem + BN * LDB * 2);         // aliases Cs at the end
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int rg = wave % RG, kp = wave / RG;
   const int n0 = blockIdx.y * BN;
-  const int Kp = (p.K + 31) & ~31;
-  const int nmt = (p.M + kBM - 1) / kBM;
+  const int Kp = (p.K + KSTEP - 1) / KSTEP * KSTEP;
+  const int nsteps = Kp / KSTEP;
+  const int LDB = Kp + kBPad;
+  const int nmt = (p.M + BM - 1) / BM;
+  bf16_t *Bs = reinterpret_cast<bf16_t *>(smem);                                      // [BN][LDB]
+  float *Ps = reinterpret_cast<float *>(smem + (BDIRECT ? 0 : BN * LDB * 2));           // [NPAR][Kp]
+  char *cbase = smem + (BDIRECT ? 0 : BN * LDB * 2) + NPAR * Kp * 4;
+  bf16_t *Cs = reinterpret_cast<bf16_t *>(cbase);                                      // [BM][LDC]
+  float *Cf = reinterpret_cast<float *>(cbase);                                        // [KS][BM][LDF]
+  float *Red = reinterpret_cast<float *>(cbase);                                       // [RSTEP][BN] (end)
+
+  // ---- stage the weight tile (once per workgroup) and the per-k prologue parameters
+  if constexpr (!BDIRECT) {
+    const int per_row = Kp / 8;
+    for (int i = tid; i < BN * per_row; i += 256) {
+      const int r = i / per_row, c8 = (i % per_row) * 8;
+      const int n = n0 + r;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (n < p.N && c8 < p.K) v = ldg16(p.W + (size_t)n * p.K + c8);
+      *reinterpret_cast<uint4 *>(Bs + r * LDB + c8) = v;
+    }
+  }
+  if constexpr (NPAR > 0) {
+    for (int i = tid; i < Kp; i += 256) {
+      const bool ok = i < p.K;
+      Ps[i] = ok ? p.pa[i] : 0.f;
+      Ps[Kp + i] = ok ? p.pb[i] : 0.f;
+      if constexpr (NPAR == 3) Ps[2 * Kp + i] = ok ? p.pc[i] : 0.f;
+    }
+  }
+  __syncthreads();
+
   const int my_chunk = tid % CH;            // fixed epilogue column chunk
   const int ncol0 = n0 + my_chunk * 8;
-
   float st0[8], st1[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) st0[j] = st1[j] = 0.f;
@@ -120,88 +162,113 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
     }
   }
 
-  const bool single_chunk = Kp <= kKC;
-  auto stage_b = [&](int kc0, int kcl) {
-    // weight rows n0..n0+BN, k in [kc0, kc0+kcl) -> Bs (zero padded)
-    const int per_row = kcl / 8;
-    for (int i = tid; i < BN * per_row; i += 256) {
-      const int r = i / per_row, c8 = (i % per_row) * 8;
-      const int n = n0 + r, k = kc0 + c8;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (n < p.N && k < p.K) v = ldg16(p.W + (size_t)n * p.K + k);
-      *reinterpret_cast<uint4 *>(Bs + r * LDB + c8) = v;
-    }
-  };
-  // dgrad: the weight is stored [K][N] (conv weight [Cout][Cin] with GEMM K = Cout):
-  // read 8 consecutive n for one k and scatter them transposed into Bs[n][k]
-  auto stage_b_t = [&](int kc0, int kcl) {
-    const int per_k = BN / 8;
-    for (int i = tid; i < kcl * per_k; i += 256) {
-      const int kk = i / per_k, n8 = (i % per_k) * 8;
-      const int k = kc0 + kk, n = n0 + n8;
-      float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (k < p.K && n < p.N) unpack8(ldg16(p.W + (size_t)k * p.N + n), v);
+  using Raw = PwRaw<PRO, SUBS, BDIRECT ? CT : 0>;
+  auto load = [&](Raw &r, int m0, int s) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) Bs[(n8 + j) * LDB + kk] = f2bf(v[j]);
-    }
-  };
-  auto stage = [&](int kc0, int kcl) {
-    if constexpr (PRO == PRO_BNBWD) stage_b_t(kc0, kcl);
-    else stage_b(kc0, kcl);
-  };
-  if (single_chunk) {
-    stage(0, Kp);
-    __syncthreads();
-  }
-
-  for (int mt = blockIdx.x; mt < nmt; mt += gridDim.x) {
-    const int m0 = mt * kBM;
-    f32x4_t acc[2][CT];
+    for (int ss = 0; ss < SUBS; ++ss) {
+      const int k = s * KSTEP + ss * 32 + 8 * (lane >> 4);
 #pragma unroll
-    for (int r = 0; r < 2; ++r)
-#pragma unroll
-      for (int c = 0; c < CT; ++c) acc[r][c] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-    for (int kc0 = 0; kc0 < Kp; kc0 += kKC) {
-      const int kcl = min(kKC, Kp - kc0);
-      if (!single_chunk) {
-        __syncthreads();
-        stage(kc0, kcl);
-        __syncthreads();
+      for (int f = 0; f < 2; ++f) {
+        const int row = m0 + rg * 32 + f * 16 + (lane & 15);
+        const bool ok = row < p.M && k < p.K;
+        const size_t off = (size_t)row * p.K + k;
+        r.a[ss][f] = ok ? ldg16(p.A + off) : make_uint4(0, 0, 0, 0);
+        if constexpr (PRO == PRO_BNBWD) r.y[ss][f] = ok ? ldg16(p.A2 + off) : make_uint4(0, 0, 0, 0);
       }
-      for (int ks = 0; ks < kcl; ks += 32) {
-        const int kg = kc0 + ks + 8 * (lane >> 4);
-        s16x8_t af[2];
-#pragma unroll
-        for (int r = 0; r < 2; ++r)
-          af[r] = load_a_frag<PRO>(p, m0 + wave * 32 + r * 16 + (lane & 15), kg);
+      if constexpr (BDIRECT) {
 #pragma unroll
         for (int c = 0; c < CT; ++c) {
-          const s16x8_t bf = *reinterpret_cast<const s16x8_t *>(
-              Bs + (c * 16 + (lane & 15)) * LDB + ks + 8 * (lane >> 4));
-#pragma unroll
-          for (int r = 0; r < 2; ++r)
-            acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                __builtin_bit_cast(bf16x8_t, af[r]), __builtin_bit_cast(bf16x8_t, bf), acc[r][c], 0, 0, 0);
+          const int n = n0 + c * 16 + (lane & 15);
+          r.b[ss][c] = (n < p.N && k < p.K) ? ldg16(p.W + (size_t)n * p.K + k) : make_uint4(0, 0, 0, 0);
         }
       }
     }
-    // ---- stage C tile (bf16) in LDS: acc[r][c][j] = C[wave*32 + r*16 + 4*(lane>>4) + j][c*16 + (lane&15)]
+  };
+
+  f32x4_t acc[2][CT];
+  auto compute = [&](const Raw &r, int s) {
 #pragma unroll
-    for (int r = 0; r < 2; ++r)
+    for (int ss = 0; ss < SUBS; ++ss) {
+      const int kl = s * KSTEP + ss * 32 + 8 * (lane >> 4);
+      s16x8_t af[2];
+#pragma unroll
+      for (int f = 0; f < 2; ++f) af[f] = a_transform<PRO>(r.a[ss][f], r.y[PRO == PRO_BNBWD ? ss : 0][f], Ps, Kp, kl);
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        s16x8_t bf;
+        if constexpr (BDIRECT) bf = __builtin_bit_cast(s16x8_t, r.b[ss][BDIRECT ? c : 0]);
+        else bf = *reinterpret_cast<const s16x8_t *>(Bs + (c * 16 + (lane & 15)) * LDB + kl);
+#pragma unroll
+        for (int f = 0; f < 2; ++f)
+          acc[f][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8_t, af[f]), __builtin_bit_cast(bf16x8_t, bf), acc[f][c], 0, 0, 0);
+      }
+    }
+  };
+
+  // ---- flattened (M tile, k step) stream, prefetching one step ahead (across tiles too)
+  Raw cur, nxt;
+  if (blockIdx.x < nmt) load(cur, blockIdx.x * BM, kp);
+  for (int mt = blockIdx.x; mt < nmt; mt += gridDim.x) {
+    const int m0 = mt * BM;
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int c = 0; c < CT; ++c) acc[f][c] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int s = kp; s < nsteps; s += KS) {
+      int ns = s + KS, nm = mt;
+      if (ns >= nsteps) { ns = kp; nm = mt + gridDim.x; }
+      if (nm < nmt) load(nxt, nm * BM, ns);
+      compute(cur, s);
+      cur = nxt;
+    }
+    // ---- C tile to LDS: acc[f][c][j] = C[rg*32 + f*16 + 4*(lane>>4) + j][c*16 + (lane&15)]
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
 #pragma unroll
       for (int c = 0; c < CT; ++c)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          Cs[(wave * 32 + r * 16 + 4 * (lane >> 4) + j) * LDC + c * 16 + (lane & 15)] = f2bf(acc[r][c][j]);
+        for (int j = 0; j < 4; ++j) {
+          const int r = rg * 32 + f * 16 + 4 * (lane >> 4) + j, col = c * 16 + (lane & 15);
+          if constexpr (KS == 1) Cs[r * LDC + col] = f2bf(acc[f][c][j]);
+          else Cf[(kp * BM + r) * LDF + col] = acc[f][c][j];
+        }
     __syncthreads();
-    // ---- row-chunked epilogue
-    if (ncol0 < p.N) {
-      for (int rr = tid / CH; rr < kBM; rr += RSTEP) {
-        const int row = m0 + rr;
-        if (row >= p.M) break;
+#pragma unroll
+    for (int i0 = 0; i0 < NP; i0 += EB) {
+      // bwd epilogue operands of EB rows are loaded together (one latency per batch)
+      uint4 ytr[EB], rsr[EB];
+      if constexpr (EPI != EPI_FWD) {
+#pragma unroll
+        for (int e = 0; e < EB; ++e) {
+          const int rr = tid / CH + (i0 + e) * RSTEP, row = m0 + rr;
+          const bool ok = i0 + e < NP && rr < BM && row < p.M && ncol0 < p.N;
+          const size_t off = (size_t)row * p.N + ncol0;
+          ytr[e] = ok ? ldg16(p.Yt + off) : make_uint4(0, 0, 0, 0);
+          if constexpr (EPI == EPI_BWD_LIN) rsr[e] = (ok && p.R) ? ldg16(p.R + off) : make_uint4(0, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < EB; ++e) {
+      const int i = i0 + e;
+      const int rr = tid / CH + i * RSTEP, row = m0 + rr;
+      if (i < NP && rr < BM && row < p.M && ncol0 < p.N) {
         float v[8];
-        unpack8(*reinterpret_cast<const uint4 *>(Cs + rr * LDC + my_chunk * 8), v);
+        if constexpr (KS == 1) {
+          unpack8(*reinterpret_cast<const uint4 *>(Cs + rr * LDC + my_chunk * 8), v);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = 0.f;
+#pragma unroll
+          for (int q = 0; q < KS; ++q) {
+            const float4 u0 = *reinterpret_cast<const float4 *>(Cf + (q * BM + rr) * LDF + my_chunk * 8);
+            const float4 u1 = *reinterpret_cast<const float4 *>(Cf + (q * BM + rr) * LDF + my_chunk * 8 + 4);
+            v[0] += u0.x; v[1] += u0.y; v[2] += u0.z; v[3] += u0.w;
+            v[4] += u1.x; v[5] += u1.y; v[6] += u1.z; v[7] += u1.w;
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = bf2f(f2bf(v[j]));
+        }
         const size_t off = (size_t)row * p.N + ncol0;
         if constexpr (EPI == EPI_FWD) {
 #pragma unroll
@@ -211,17 +278,15 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
           }
         } else {
           float yt[8];
-          unpack8(ldg16(p.Yt + off), yt);
+          unpack8(ytr[e], yt);
           if constexpr (EPI == EPI_BWD_RELU6) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) v[j] *= relu6_mask(yt[j], es[j], et[j]);
           } else {
-            if (p.R) {
-              float rv[8];
-              unpack8(ldg16(p.R + off), rv);
+            float rv[8];
+            unpack8(rsr[e], rv);
 #pragma unroll
-              for (int j = 0; j < 8; ++j) v[j] += rv[j];
-            }
+            for (int j = 0; j < 8; ++j) v[j] += rv[j];
           }
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
@@ -231,11 +296,11 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
         }
         stg16(p.out + off, pack8(v));
       }
+      }
     }
     __syncthreads();
   }
   // ---- per-workgroup BN partials: reduce the RSTEP threads sharing a column chunk
-  // Red: [RSTEP][BN] floats (RSTEP*BN = 2048 floats) per statistic
   for (int s = 0; s < 2; ++s) {
     const int rgrp = tid / CH;
 #pragma unroll
@@ -245,6 +310,34 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
       float a = 0.f;
       for (int g = 0; g < RSTEP; ++g) a += Red[g * BN + c];
       if (n0 + c < p.N) p.part[((size_t)blockIdx.x * 2 + s) * p.N + n0 + c] = a;
+    }
+    __syncthreads();
+  }
+}
+
+// dgrad weights: W^T of every 1x1 conv, batched (one table entry per layer):
+// dst[off + c*R + r] = src[off + r*C + c]   (R = Cout, C = Cin), 32x32 tiles via LDS
+__global__ __launch_bounds__(256) void wt_transpose_kernel(const bf16_t *__restrict__ src,
+                                                           bf16_t *__restrict__ dst,
+                                                           const int *__restrict__ tab) {
+  __shared__ bf16_t T[32][33];
+  const int *e = tab + blockIdx.y * 3;
+  const long long off = e[0];
+  const int R = e[1], C = e[2];
+  const int tr = (R + 31) / 32, tc = (C + 31) / 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8
+  for (int t = blockIdx.x; t < tr * tc; t += gridDim.x) {
+    const int r0 = (t / tc) * 32, c0 = (t % tc) * 32;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = r0 + ty + 8 * i, c = c0 + tx;
+      T[ty + 8 * i][tx] = (r < R && c < C) ? src[off + (long long)r * C + c] : bf16_t(0);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = c0 + ty + 8 * i, r = r0 + tx;
+      if (r < R && c < C) dst[off + (long long)c * R + r] = T[tx][ty + 8 * i];
     }
     __syncthreads();
   }
@@ -471,49 +564,86 @@ __global__ __launch_bounds__(256) void split_reduce_kernel(const float *__restri
 // ===========================================================================
 // host launchers
 // ===========================================================================
-static int pw_bn_for(int N) { return N <= 32 ? 32 : (N <= 64 ? 64 : 128); }
-
-int pw_gemm_num_partials(int M, int N) {
-  const int BN = pw_bn_for(N);
-  const int nt = (N + BN - 1) / BN;
-  const int nmt = (M + kBM - 1) / kBM;
-  int gx = 1024 / nt;
-  gx = (gx + 7) & ~7;
+// geometry of one pointwise GEMM launch (also sizes the BN partial workspace: P = gx)
+//  * large M, K <= 192: weight tile resident in LDS for the whole grid-stride sweep;
+//  * small M or large K: weight fragments read straight from L2 alongside A, and the
+//    K dimension split over the 4 waves (KS) so the grid still has >= ~1.5k workgroups.
+struct PwGeom {
+  int BN, KS, bdirect, nt, nmt, gx;
+  size_t lds;
+};
+static PwGeom pw_geom(int M, int N, int K, int pro) {
+  PwGeom g;
+  const int Kp64 = (K + 63) / 64 * 64;
+  g.bdirect = (Kp64 > 192) || (M < 65536);
+  const int kstep = g.bdirect ? 32 : 64;
+  const int Kp = (K + kstep - 1) / kstep * kstep;
+  const int nsteps = Kp / kstep;
+  if (!g.bdirect) {
+    g.BN = N <= 32 ? 32 : 64;     // BN = 128 costs occupancy (1-2 waves/SIMD) for no bandwidth gain
+    g.KS = 1;
+  } else {
+    g.BN = (N % 64 == 0) ? 64 : 32;
+    g.KS = 1;
+    const int nt = (N + g.BN - 1) / g.BN;
+    while (g.KS < 4 && g.KS * 2 <= nsteps && (long long)nt * ((M + 128 / g.KS - 1) / (128 / g.KS)) < 1536) g.KS *= 2;
+  }
+  g.nt = (N + g.BN - 1) / g.BN;
+  const int BM = 128 / g.KS;
+  g.nmt = (M + BM - 1) / BM;
+  int gx = (g.bdirect ? 2048 : 1024) / g.nt;
+  if (gx > g.nmt) gx = g.nmt;
+  gx = (gx + 7) & ~7;                  // multiple of 8: the N tiles of one M tile share an XCD L2
   if (gx < 8) gx = 8;
-  if (gx > nmt) gx = nmt;
-  return gx;
+  g.gx = gx;
+  const int npar = pro == ACT_NONE ? 0 : (pro == PRO_BNBWD ? 3 : 2);
+  const size_t cbuf = g.KS == 1 ? (size_t)BM * (g.BN + kCPad) * 2 : (size_t)g.KS * BM * (g.BN + 4) * 4;
+  const size_t red = (size_t)(256 / (g.BN / 8)) * g.BN * 4;
+  g.lds = (g.bdirect ? 0 : (size_t)g.BN * (Kp + kBPad) * 2) + (size_t)npar * Kp * 4 + (cbuf > red ? cbuf : red);
+  return g;
 }
 
-template <int PRO, int EPI, int BN>
-static void launch_pw_t(const PwArgs &a, hipStream_t st) {
-  const int nt = (a.N + BN - 1) / BN;
-  const int gx = pw_gemm_num_partials(a.M, a.N);
-  const size_t lds = (size_t)BN * (kKC + kBPad) * 2 + (size_t)kBM * (BN + kCPad) * 2;
-  hipLaunchKernelGGL((pw_gemm_kernel<PRO, EPI, BN>), dim3(gx, nt), dim3(256), lds, st, a);
+int pw_gemm_num_partials(int M, int N, int K) { return pw_geom(M, N, K, ACT_NONE).gx; }
+
+template <int PRO, int EPI, int BN, int KS, bool BD>
+static void launch_pw_t(const PwArgs &a, const PwGeom &g, hipStream_t st) {
+  hipLaunchKernelGGL((pw_gemm_kernel<PRO, EPI, BN, KS, BD>), dim3(g.gx, g.nt), dim3(256), g.lds, st, a);
 }
 
 template <int PRO, int EPI>
-static void launch_pw_bn(const PwArgs &a, hipStream_t st) {
-  switch (pw_bn_for(a.N)) {
-    case 32: launch_pw_t<PRO, EPI, 32>(a, st); break;
-    case 64: launch_pw_t<PRO, EPI, 64>(a, st); break;
-    default: launch_pw_t<PRO, EPI, 128>(a, st); break;
+static void launch_pw_geom(const PwArgs &a, const PwGeom &g, hipStream_t st) {
+  if (!g.bdirect) {
+    if (g.BN == 32) launch_pw_t<PRO, EPI, 32, 1, false>(a, g, st);
+    else launch_pw_t<PRO, EPI, 64, 1, false>(a, g, st);
+    return;
   }
+#define PW_BD(B_, K_) \
+  if (g.BN == B_ && g.KS == K_) { launch_pw_t<PRO, EPI, B_, K_, true>(a, g, st); return; }
+  PW_BD(32, 1) PW_BD(32, 2) PW_BD(32, 4) PW_BD(64, 1) PW_BD(64, 2) PW_BD(64, 4)
+#undef PW_BD
 }
 
-// pro: 0 none, 1 bn+relu6, 3 bnbwd ; epi: 0 fwd, 1 bwd relu6, 2 bwd lin
+// pro: 0 none, 1 bn+relu6, 3 bnbwd ; epi: 0 fwd, 1 bwd relu6, 2 bwd lin.
+// W is [N][K] in GEMM terms for every mode (dgrad passes the transposed conv weight).
 void launch_pw_gemm(int pro, int epi, const bf16_t *A, const bf16_t *A2, const float *pa,
                     const float *pb, const float *pc, const bf16_t *W, bf16_t *out,
                     const bf16_t *Yt, const float *es, const float *et, const bf16_t *R, float *part,
                     int M, int N, int K, hipStream_t st) {
   PwArgs a{A, A2, pa, pb, pc, W, out, Yt, es, et, R, part, M, N, K};
+  const PwGeom g = pw_geom(M, N, K, pro);
 #define PW_CASE(P, E) \
-  if (pro == P && epi == E) { launch_pw_bn<P, E>(a, st); return; }
+  if (pro == P && epi == E) { launch_pw_geom<P, E>(a, g, st); return; }
   PW_CASE(ACT_NONE, EPI_FWD)
   PW_CASE(ACT_BN_RELU6, EPI_FWD)
   PW_CASE(PRO_BNBWD, EPI_BWD_RELU6)
   PW_CASE(PRO_BNBWD, EPI_BWD_LIN)
 #undef PW_CASE
+}
+
+// tab: int32 [n][3] = (element offset, rows R = Cout, cols C = Cin) into src/dst
+void launch_wt_transpose(const bf16_t *src, bf16_t *dst, const int *tab, int n, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(wt_transpose_kernel, dim3(64, n), dim3(256), 0, st, src, dst, tab);
 }
 
 void launch_colsum(const float *src, int R, long long n, float *dst, int &rows_out, hipStream_t st);

@@ -152,14 +152,14 @@ class MobileNetV2Executor:
             bp.G = torch.empty(Mout, blk.oup, dtype=torch.bfloat16, device=device)
             self.blocks.append(bp)
             if expand:
-                parts.append((K.pw_num_partials(Min, blk.hidden), blk.hidden))        # fwd expand
-                parts.append((K.pw_num_partials(Min, blk.inp), blk.inp))               # bwd expand dgrad
+                parts.append((K.pw_num_partials(Min, blk.hidden, blk.inp), blk.hidden))        # fwd expand
+                parts.append((K.pw_num_partials(Min, blk.inp, blk.hidden), blk.inp))               # bwd expand dgrad
                 wg.append(K.pw_wgrad_workspace(Min, blk.hidden, blk.inp))
             parts.append((K.dw_num_partials("fwd", B, Hin, Hin, blk.hidden, blk.stride), blk.hidden))
             parts.append((K.dw_num_partials("dgrad", B, Hin, Hin, blk.hidden, blk.stride), blk.hidden))
             wg.append(K.dw_wgrad_workspace(B, Hin, Hin, blk.hidden, blk.stride))
-            parts.append((K.pw_num_partials(Mout, blk.oup), blk.oup))                 # fwd project
-            parts.append((K.pw_num_partials(Mout, blk.hidden), blk.hidden))           # bwd project dgrad
+            parts.append((K.pw_num_partials(Mout, blk.oup, blk.hidden), blk.oup))                 # fwd project
+            parts.append((K.pw_num_partials(Mout, blk.hidden, blk.oup), blk.hidden))           # bwd project dgrad
             wg.append(K.pw_wgrad_workspace(Mout, blk.oup, blk.hidden))
             cur_h = Ho
         # ---------------- final 1x1 conv + head
@@ -170,8 +170,8 @@ class MobileNetV2Executor:
         self.C_last = last[0].out_channels
         self.w_last = f"features.{len(feats) - 1}.0.weight"
         self.bn_last = BNState(self.flat, last[1], f"features.{len(feats) - 1}.1", Mf, self.C_last, device)
-        parts.append((K.pw_num_partials(Mf, self.C_last), self.C_last))
-        parts.append((K.pw_num_partials(Mf, self.C_last_in), self.C_last_in))
+        parts.append((K.pw_num_partials(Mf, self.C_last, self.C_last_in), self.C_last))
+        parts.append((K.pw_num_partials(Mf, self.C_last_in, self.C_last), self.C_last_in))
         parts.append((B, self.C_last))
         wg.append(K.pw_wgrad_workspace(Mf, self.C_last, self.C_last_in))
         self.NC = model.classifier[1].out_features
@@ -189,6 +189,15 @@ class MobileNetV2Executor:
         self.labels = torch.zeros(B, dtype=torch.int64, device=device)
         self.hyper = hyper if hyper is not None else torch.zeros(2, **f32)   # [lr, step] (device)
         self.on_params_ready: Optional[Callable[[List[str]], None]] = None
+        # 1x1 weights transposed for dgrad: table rows (offset, Cout, Cin)
+        tab = []
+        for bp in self.blocks:
+            if bp.expand:
+                tab.append((self.flat.offsets[bp.w_e][0], bp.hidden, bp.cin))
+            tab.append((self.flat.offsets[bp.w_p][0], bp.cout, bp.hidden))
+        tab.append((self.flat.offsets[self.w_last][0], self.C_last, self.C_last_in))
+        self.wt_tab = torch.tensor(tab, dtype=torch.int32, device=device).contiguous()
+        self.wt_n = len(tab)
 
     # ------------------------------------------------------------------ helpers
     def _ready(self, names):
@@ -217,7 +226,7 @@ class MobileNetV2Executor:
                               bp.cin, pa=inp_bn.scale, pb=inp_bn.shift)
                 else:
                     K.pw_gemm(K.ACT_NONE, K.EPI_FWD, inp_t, f.b(bp.w_e), bp.bn_e.y, ws, Min, bp.hidden, bp.cin)
-                self._fin_fwd(bp.bn_e, K.pw_num_partials(Min, bp.hidden), train)
+                self._fin_fwd(bp.bn_e, K.pw_num_partials(Min, bp.hidden, bp.cin), train)
                 dw_in = bp.bn_e
             else:
                 assert inp_t is None, "t=1 block expects the (virtual) stem output"
@@ -228,7 +237,7 @@ class MobileNetV2Executor:
             Mout = B * bp.Ho * bp.Wo
             K.pw_gemm(K.ACT_BN_RELU6, K.EPI_FWD, bp.bn_d.y, f.b(bp.w_p), bp.bn_p.y, ws, Mout, bp.cout, bp.hidden,
                       pa=bp.bn_d.scale, pb=bp.bn_d.shift)
-            self._fin_fwd(bp.bn_p, K.pw_num_partials(Mout, bp.cout), train)
+            self._fin_fwd(bp.bn_p, K.pw_num_partials(Mout, bp.cout, bp.hidden), train)
             K.bn_apply(bp.bn_p.y, bp.bn_p.scale, bp.bn_p.shift, bp.o, relu6=False,
                        res=inp_t if bp.residual else None)
             inp_bn, inp_t = bp.bn_p, bp.o
@@ -236,7 +245,7 @@ class MobileNetV2Executor:
         Mf = B * self.Hf * self.Hf
         K.pw_gemm(K.ACT_NONE, K.EPI_FWD, inp_t, f.b(self.w_last), self.bn_last.y, ws, Mf, self.C_last,
                   self.C_last_in)
-        self._fin_fwd(self.bn_last, K.pw_num_partials(Mf, self.C_last), train)
+        self._fin_fwd(self.bn_last, K.pw_num_partials(Mf, self.C_last, self.C_last_in), train)
         # head (+ its backward when training)
         K.head(self.bn_last.y, self.bn_last.scale, self.bn_last.shift, f.w(self.w_lin), f.w(self.b_lin),
                self.labels, B, self.Hf * self.Hf, self.C_last, self.NC, self.drop_p, self.dropout_seed,
@@ -249,6 +258,8 @@ class MobileNetV2Executor:
     def backward(self):
         f, B, S = self.flat, self.B, self.S
         ws, wg = self.ws_part, self.ws_wgrad
+        # transposed 1x1 weights for the dgrad GEMMs (one batched launch)
+        K.wt_transpose(f.shadow, f.shadow_t, self.wt_tab, self.wt_n)
         self._ready([self.w_lin, self.b_lin])
         # BN of the final conv (g produced by the head kernel)
         bnl = self.bn_last
@@ -257,9 +268,9 @@ class MobileNetV2Executor:
         Mf = B * self.Hf * self.Hf
         last_blk = self.blocks[-1]
         # dgrad of the final conv -> gradient w.r.t. o_17 (feeds BN_p of block 17, linear)
-        K.pw_gemm(K.PRO_BNBWD, K.EPI_BWD_LIN, bnl.g, f.b(self.w_last), last_blk.G, ws, Mf, self.C_last_in,
+        K.pw_gemm(K.PRO_BNBWD, K.EPI_BWD_LIN, bnl.g, f.bt(self.w_last), last_blk.G, ws, Mf, self.C_last_in,
                   self.C_last, A2=bnl.y, pa=bnl.a, pb=bnl.b, pc=bnl.c, Yt=last_blk.bn_p.y, R=None)
-        P_g = K.pw_num_partials(Mf, self.C_last_in)
+        P_g = K.pw_num_partials(Mf, self.C_last_in, self.C_last)
         last_blk.bn_p.finalize_bwd(ws, P_g)
         K.pw_wgrad(bnl.g, bnl.y, bnl.a, bnl.b, bnl.c, last_blk.o, None, None, K.ACT_NONE, wg,
                    f.g(self.w_last), Mf, self.C_last, self.C_last_in)
@@ -273,9 +284,9 @@ class MobileNetV2Executor:
             bnp, bnd = bp.bn_p, bp.bn_d
             # bn_p backward coefficients were finalised by whoever produced bp.G
             # project dgrad -> g_d (relu6 mask of BN_d) + BN_d partials
-            K.pw_gemm(K.PRO_BNBWD, K.EPI_BWD_RELU6, bp.G, f.b(bp.w_p), bnd.g, ws, Mout, bp.hidden, bp.cout,
+            K.pw_gemm(K.PRO_BNBWD, K.EPI_BWD_RELU6, bp.G, f.bt(bp.w_p), bnd.g, ws, Mout, bp.hidden, bp.cout,
                       A2=bnp.y, pa=bnp.a, pb=bnp.b, pc=bnp.c, Yt=bnd.y, es=bnd.scale, et=bnd.shift)
-            bnd.finalize_bwd(ws, K.pw_num_partials(Mout, bp.hidden))
+            bnd.finalize_bwd(ws, K.pw_num_partials(Mout, bp.hidden, bp.cout))
             # project wgrad
             K.pw_wgrad(bp.G, bnp.y, bnp.a, bnp.b, bnp.c, bnd.y, bnd.scale, bnd.shift, K.ACT_BN_RELU6, wg,
                        f.g(bp.w_p), Mout, bp.cout, bp.hidden)
@@ -292,10 +303,10 @@ class MobileNetV2Executor:
                 bne = bp.bn_e
                 assert prev is not None
                 # expand dgrad -> gradient w.r.t. the block input o_prev (+ skip gradient)
-                K.pw_gemm(K.PRO_BNBWD, K.EPI_BWD_LIN, bne.g, f.b(bp.w_e), prev.G, ws, Min, bp.cin, bp.hidden,
+                K.pw_gemm(K.PRO_BNBWD, K.EPI_BWD_LIN, bne.g, f.bt(bp.w_e), prev.G, ws, Min, bp.cin, bp.hidden,
                           A2=bne.y, pa=bne.a, pb=bne.b, pc=bne.c, Yt=prev.bn_p.y,
                           R=bp.G if bp.residual else None)
-                prev.bn_p.finalize_bwd(ws, K.pw_num_partials(Min, bp.cin))
+                prev.bn_p.finalize_bwd(ws, K.pw_num_partials(Min, bp.cin, bp.hidden))
                 K.pw_wgrad(bne.g, bne.y, bne.a, bne.b, bne.c, prev.o, None, None, K.ACT_NONE, wg,
                            f.g(bp.w_e), Min, bp.hidden, bp.cin)
                 self._ready([bp.w_e] + prev.bn_p.param_names)

@@ -51,6 +51,8 @@ class FlatParams:
         self.exp_avg = torch.zeros_like(self.master)
         self.exp_avg_sq = torch.zeros_like(self.master)
         self.shadow = torch.zeros(self.numel, dtype=torch.bfloat16, device=device) if with_shadow else None
+        # transposed bf16 copies of the 1x1 conv weights (same offsets; filled by the executor)
+        self.shadow_t = torch.zeros_like(self.shadow) if with_shadow else None
         self.params = {}
         self.tap_major = {n for n, p in order if is_depthwise3x3(p)}
         with torch.no_grad():
@@ -82,6 +84,10 @@ class FlatParams:
     def b(self, name: str) -> torch.Tensor:
         o, n = self.offsets[name]
         return self.shadow[o:o + n]
+
+    def bt(self, name: str) -> torch.Tensor:
+        o, n = self.offsets[name]
+        return self.shadow_t[o:o + n]
 
     def range_of(self, name: str) -> Tuple[int, int]:
         o, n = self.offsets[name]

@@ -161,13 +161,16 @@ def dw_wgrad(g, yself, coef, yprev, ps, pt, part, grad, B, H, W, C, stride):
 
 
 # --------------------------------------------------------------------------- pointwise
-def pw_num_partials(M, N):
-    return lib().pw_gemm_num_partials(M, N)
+def pw_num_partials(M, N, K):
+    return lib().pw_gemm_num_partials(M, N, K)
 
 
 def pw_gemm(pro, epi, A, W, out, part, M, N, K, A2=None, pa=None, pb=None, pc=None, Yt=None,
             es=None, et=None, R=None):
-    """out[M,N] = prologue(A)[M,K] @ W^T, W [N,K] (fwd) or W [K,N] (pro == PRO_BNBWD)."""
+    """out[M,N] = prologue(A)[M,K] @ W^T with W [N,K] in GEMM terms for every mode.
+
+    For the dgrad (pro == PRO_BNBWD) W is the TRANSPOSED conv weight ([Cin][Cout],
+    see :func:`wt_transpose`)."""
     if K % 8 or N % 8:
         raise ValueError(f"pw_gemm: K={K}, N={N} must be multiples of 8")
     _chk(A, BF16, M * K, "A")
@@ -176,7 +179,7 @@ def pw_gemm(pro, epi, A, W, out, part, M, N, K, A2=None, pa=None, pb=None, pc=No
     _chk(out, BF16, M * N, "out")
     _chk(Yt, BF16, M * N, "Yt")
     _chk(R, BF16, M * N, "R")
-    _chk(part, F32, pw_num_partials(M, N) * 2 * N, "part")
+    _chk(part, F32, pw_num_partials(M, N, K) * 2 * N, "part")
     if pro in (ACT_BN_RELU6, PRO_BNBWD):
         assert pa is not None and pb is not None and pa.numel() >= K
     if pro == PRO_BNBWD:
@@ -187,6 +190,15 @@ def pw_gemm(pro, epi, A, W, out, part, M, N, K, A2=None, pa=None, pb=None, pc=No
         assert es is not None and et is not None
     lib().pw_gemm(int(pro), int(epi), _p(A), _p(A2), _p(pa), _p(pb), _p(pc), _p(W), _p(out), _p(Yt),
                   _p(es), _p(et), _p(R), _p(part), M, N, K, _s())
+
+
+def wt_transpose(src, dst, tab, n):
+    """Batched bf16 transpose of 1x1 conv weights: for each row (off, R, C) of the int32
+    table ``tab`` [n,3], dst[off + c*R + r] = src[off + r*C + c]."""
+    _chk(src, BF16, 1, "src")
+    _chk(dst, BF16, src.numel(), "dst")
+    assert tab.dtype == torch.int32 and tab.is_contiguous() and tab.numel() >= 3 * n
+    lib().wt_transpose(_p(src), _p(dst), _p(tab), int(n), _s())
 
 
 def pw_wgrad_workspace(M, N, K):

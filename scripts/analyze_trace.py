@@ -55,6 +55,32 @@ def main(path, B=128, S=224):
         for (nm, d), b in zip(ds, order):
             gb = byt(b) / 1e9
             print(f"  C={b['hid']:4d} H={b['H']:3d} s={b['s']}  {d:7.1f} us  {gb * 1e3:7.1f} MB  {gb / d * 1e6 / 1e3:6.2f} TB/s")
+    # pointwise: forward (expand, project per block, then final 1x1), backward in reverse
+    fwd, bwd = [], []
+    for b in bl:
+        if b["t"] != 1:
+            fwd.append(("exp", b["Min"], b["cin"], b["hid"]))
+        fwd.append(("prj", b["Mout"], b["hid"], b["cout"]))
+    Mf = B * Hf * Hf
+    fwd.append(("last", Mf, bl[-1]["cout"], 1280))
+    bwd = fwd[::-1]
+    pw = by.get("pw_gemm_kernel", [])
+    wg = by.get("pw_wgrad_kernel", [])
+    n = len(fwd)
+    print(f"\npw layers (M, K->N): fwd / dgrad / wgrad  us @ TB/s")
+    tf = td = tw = 0.0
+    for i, (kind, M, K, N) in enumerate(fwd):
+        j = n - 1 - i
+        bf = M * (K + N) * 2
+        bd = M * (2 * N + 2 * K) * 2      # G, Y in; out (+ Yt / residual) -- approx
+        bw = M * (2 * N + K) * 2
+        f_ = pw[i][1] if i < len(pw) else 0
+        d_ = pw[n + j][1] if n + j < len(pw) else 0
+        w_ = wg[j][1] if j < len(wg) else 0
+        tf, td, tw = tf + f_, td + d_, tw + w_
+        print(f"  {kind:4s} M={M:8d} {K:4d}->{N:4d}  fwd {f_:6.1f} {bf / f_ / 1e6 if f_ else 0:5.2f}  "
+              f"dgrad {d_:6.1f} {bd / d_ / 1e6 if d_ else 0:5.2f}  wgrad {w_:6.1f} {bw / w_ / 1e6 if w_ else 0:5.2f}")
+    print(f"  totals: fwd {tf:.0f} us  dgrad {td:.0f} us  wgrad {tw:.0f} us (+ stem wgrad {wg[-1][1] if wg else 0:.0f})")
     for fam in ("pw_gemm_kernel", "pw_wgrad_kernel", "colsum_kernel", "bn_fwd_finalize_kernel", "split_reduce_kernel"):
         ds = by.get(fam, [])
         print(f"\n{fam}: {len(ds)} dispatches {sum(d for _, d in ds):.1f} us total; per dispatch: " +

@@ -157,8 +157,10 @@ def test_dw_dgrad_wgrad(dev, B, H, W, C, stride):
 
 
 # ----------------------------------------------------------------------------- pointwise
+# small M -> L2-direct weights with the K split over waves (KS 1/2/4); M >= 65536 -> LDS-resident weights
 PW_CASES = [(1000, 16, 96), (4096, 24, 144), (777, 96, 24), (3000, 320, 1280), (2048, 160, 960),
-            (513, 32, 32), (6272, 960, 160), (256, 64, 384)]
+            (513, 32, 32), (6272, 960, 160), (256, 64, 384), (70001, 16, 96), (65600, 144, 24),
+            (66000, 192, 64), (68000, 24, 160)]
 
 
 @pytest.mark.parametrize("M,K_,N", PW_CASES)
@@ -168,7 +170,7 @@ def test_pw_fwd(dev, M, K_, N, pro):
     s, t = bn_params(K_, dev)
     W = bf(rnd(N, K_, dev=dev, seed=5) / math.sqrt(K_))
     out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
-    P = K.pw_num_partials(M, N)
+    P = K.pw_num_partials(M, N, K_)
     part = torch.zeros(P * 2 * N, device=dev)
     K.pw_gemm(pro, K.EPI_FWD, A, W, out, part, M, N, K_, pa=s, pb=t)
     x = relu6(A.float() * s + t) if pro == K.ACT_BN_RELU6 else A.float()
@@ -192,9 +194,13 @@ def test_pw_dgrad(dev, M, Kf, Nf, epi):
     es, et = bn_params(Kf, dev, 7)
     R = bf(rnd(M, Kf, dev=dev, seed=8)) if epi == K.EPI_BWD_LIN else None
     out = torch.empty(M, Kf, dtype=torch.bfloat16, device=dev)
-    P = K.pw_num_partials(M, Kf)
+    P = K.pw_num_partials(M, Kf, Nf)
     part = torch.zeros(P * 2 * Kf, device=dev)
-    K.pw_gemm(K.PRO_BNBWD, epi, G, W, out, part, M, Kf, Nf, A2=Y, pa=coef[0], pb=coef[1], pc=coef[2],
+    Wt = torch.empty_like(W)
+    tab = torch.tensor([[0, Nf, Kf]], dtype=torch.int32, device=dev)
+    K.wt_transpose(W, Wt, tab, 1)
+    assert torch.equal(Wt.view(Kf, Nf), W.t())
+    K.pw_gemm(K.PRO_BNBWD, epi, G, Wt, out, part, M, Kf, Nf, A2=Y, pa=coef[0], pb=coef[1], pc=coef[2],
               Yt=Yt, es=es, et=et, R=R)
     dy = coef[0] * G.float() + coef[1] * Y.float() + coef[2]
     ref = dy @ W.float()
