@@ -41,6 +41,12 @@ void launch_dw_dgrad(const bf16_t *, const bf16_t *, const float *, const bf16_t
 void launch_dw_wgrad(const bf16_t *, const bf16_t *, const float *, const bf16_t *, const float *,
                      const float *, float *, float *, int, int, int, int, int, hipStream_t);
 int pw_gemm_num_partials(int, int, int);
+bool pw_bwd_supported(int, int, int);
+int pw_bwd_num_partials(int, int, int);
+long long pw_bwd_wgrad_workspace_floats(int, int, int);
+void launch_pw_bwd(int, const bf16_t *, const bf16_t *, const float *, const float *, const float *,
+                   const bf16_t *, bf16_t *, const bf16_t *, const float *, const float *, const bf16_t *,
+                   const bf16_t *, float *, float *, float *, int, int, int, hipStream_t);
 void launch_wt_transpose(const bf16_t *, bf16_t *, const int *, int, hipStream_t);
 void launch_pw_gemm(int, int, const bf16_t *, const bf16_t *, const float *, const float *,
                     const float *, const bf16_t *, bf16_t *, const bf16_t *, const float *,
@@ -141,6 +147,16 @@ PYBIND11_MODULE(_pgdist_C, m) {
   });
   m.def("wt_transpose", [](P src, P dst, P tab, int n, P s) {
     launch_wt_transpose(ptr<bf16_t>(src), ptr<bf16_t>(dst), ptr<int>(tab), n, S(s));
+  });
+  m.def("pw_bwd_supported", &pw_bwd_supported);
+  m.def("pw_bwd_num_partials", &pw_bwd_num_partials);
+  m.def("pw_bwd_wgrad_workspace_floats", &pw_bwd_wgrad_workspace_floats);
+  m.def("pw_bwd", [](int epi, P G, P Y, P ca, P cb, P cc, P WT, P out, P Yt, P es, P et, P R, P X,
+                     P part, P wpart, P grad, int M, int Kg, int Ng, P s) {
+    launch_pw_bwd(epi, ptr<bf16_t>(G), ptr<bf16_t>(Y), ptr<float>(ca), ptr<float>(cb), ptr<float>(cc),
+                  ptr<bf16_t>(WT), ptr<bf16_t>(out), ptr<bf16_t>(Yt), ptr<float>(es), ptr<float>(et),
+                  ptr<bf16_t>(R), ptr<bf16_t>(X), ptr<float>(part), ptr<float>(wpart), ptr<float>(grad),
+                  M, Kg, Ng, S(s));
   });
   m.def("pw_wgrad_workspace_floats", &pw_wgrad_workspace_floats);
   m.def("pw_wgrad", [](P G, P Y, P ga, P gb, P gc, P X, P xs, P xt, int xact, P part, P grad, int M,

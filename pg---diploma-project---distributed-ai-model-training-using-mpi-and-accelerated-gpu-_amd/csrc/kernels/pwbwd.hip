@@ -1,0 +1,421 @@
+// Fused pointwise-conv backward for the large-M layers (112x112 .. 28x28):
+// dgrad AND wgrad from ONE read of this layer's (G, Y).
+//
+// Reference ops: the backward of the 1x1 convs of torchvision MobileNetV2
+// (SURVEY.md §2.6), i.e. what cuDNN runs as two separate kernels (data grad,
+// filter grad) each re-reading the output gradient.  In the fused NHWC pipeline
+// the output gradient of a 1x1 conv is  dy = a[n]*G + b[n]*Y + c[n]  (the
+// layer's own BN backward), so a separate wgrad would re-read two [M][N_l]
+// bf16 tensors — for the 112x112 expand conv that is 616 MB per step.
+//
+// Per 64-row tile (4 waves, grid-stride over M, ALL loads of a tile — G, Y and the
+// epilogue operands — prefetched one tile ahead; one N tile spans the whole Ng
+// of the project convs so G, Y are read exactly once):
+//   * dy is computed once from (G, Y) and written to LDS twice: row-major
+//     dyN[m][kg] (A operand of the dgrad MFMA) and transposed dyT[kg][m]
+//     (A operand of the wgrad MFMA, reduction over m);
+//   * the wgrad's second operand x (this conv's input) is staged transposed:
+//       EPI_BWD_RELU6 (project conv): x = relu6(Yt*s + t) — Yt is the tensor the
+//         dgrad epilogue reads anyway for the ReLU6 mask, so x costs no HBM bytes;
+//       EPI_BWD_LIN   (expand conv):  x = X, the materialised block input;
+//   * dgrad:  out[m][ng] = sum_kg dy[m][kg] W^T[ng][kg]  (W^T resident in LDS),
+//     epilogue identical to pw_gemm_kernel (mask / residual, BN partials);
+//   * wgrad:  dW[kg][ng] += sum_m dyT[kg][m] xT[ng][m], accumulated in registers
+//     across the workgroup's tiles and written once as a split-M partial
+//     [gridDim.x][Kg][Ng] (deterministic fixed-order reduction afterwards).
+#include "../common.h"
+
+enum { EPI_BWD_RELU6_ = 1, EPI_BWD_LIN_ = 2 };   // same values as pwconv.hip
+
+namespace {
+struct PwBwdArgs {
+  const bf16_t *G, *Y;          // [M][Kg]
+  const float *ca, *cb, *cc;    // [Kg] BN backward coefficients of this layer
+  const bf16_t *WT;             // [Ng][Kg] transposed conv weight
+  bf16_t *out;                  // [M][Ng]
+  const bf16_t *Yt;             // [M][Ng] producer BN input
+  const float *es, *et;         // [Ng] producer BN scale / shift (RELU6 mode)
+  const bf16_t *R;              // [M][Ng] residual gradient (LIN mode, optional)
+  const bf16_t *X;              // [M][Ng] conv input (LIN mode)
+  float *part;                  // [gx][2][Ng]
+  float *wpart;                 // [gx][Kg][Ng]
+  int M, Kg, Ng;
+};
+template <int KP, int BN, int BM>
+struct BwdLds {
+  static constexpr int LDA = KP + 8, LDM = BM + 8, LDC = BN + 8;
+  static constexpr int WT = 0;                              // [BN][LDA] W^T tile (resident)
+  static constexpr int STG = WT + BN * LDA * 2;             // per-tile staging:
+  static constexpr int DYN = STG;                           //   dyN [BM][LDA]
+  static constexpr int DYT = DYN + BM * LDA * 2;            //   dyT [KP][LDM]
+  static constexpr int XT = DYT + KP * LDM * 2;             //   xT  [BN][LDM]
+  static constexpr int STG_END = XT + BN * LDM * 2;
+  static constexpr int CS = STG;                            // C tile [BM][LDC] aliases the staging
+  static constexpr int RED = STG;                           // [BM/4][BN] floats at the very end
+  static constexpr int CS_END = CS + BM * LDC * 2;
+  static constexpr int RED_END = RED + (BM / 4) * BN * 4;
+  static constexpr int M1 = STG_END > CS_END ? STG_END : CS_END;
+  static constexpr int PS = M1 > RED_END ? M1 : RED_END;     // a | b | c [KP], s | t [BN]
+  static constexpr int BYTES = PS + (3 * KP + 2 * BN) * 4;
+};
+}  // namespace
+
+// BM = 64 rows per tile (4 waves x 16 rows for the dgrad MFMA) or 32 (2 row groups x
+// 2 column halves; used when KP is large so the prefetched tile fits in registers)
+template <int EPI, int KP, int BN, int BM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void pw_bwd_fused_kernel(PwBwdArgs p) {
+  using L = BwdLds<KP, BN, BM>;
+  constexpr int LDA = L::LDA, LDM = L::LDM, LDC = L::LDC;
+  constexpr int CT = BN / 16;
+  constexpr int RGS = BM / 16;                   // dgrad row groups of 16
+  constexpr int RPW = RGS >= 4 ? RGS / 4 : 1;    // row groups per wave
+  constexpr int CSPLIT = RGS >= 4 ? 1 : 4 / RGS; // waves sharing a row group (column split)
+  constexpr int CTW = CT / CSPLIT;               // dgrad column tiles per wave
+  static_assert(CTW * CSPLIT == CT, "column tiles must split evenly over the waves");
+  constexpr int DYC = KP / 8;                    // 16-B chunks per dy row
+  constexpr int NDY = (BM / 4) * DYC;            // dy items (4 rows x 8 cols)
+  constexpr int IDY = (NDY + 255) / 256;
+  constexpr int XC = BN / 8;
+  constexpr int NX = (BM / 4) * XC;              // x / epilogue items (4 rows x 8 cols)
+  constexpr int IX = (NX + 255) / 256;
+  constexpr int WTILES = (KP / 16) * (BN / 16);
+  constexpr int WPW = (WTILES + 3) / 4;          // wgrad output tiles per wave
+  constexpr bool LIN = EPI == EPI_BWD_LIN_;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t *WTs = reinterpret_cast<bf16_t *>(smem + L::WT);
+  bf16_t *dyN = reinterpret_cast<bf16_t *>(smem + L::DYN);
+  bf16_t *dyT = reinterpret_cast<bf16_t *>(smem + L::DYT);
+  bf16_t *xT = reinterpret_cast<bf16_t *>(smem + L::XT);
+  bf16_t *Cs = reinterpret_cast<bf16_t *>(smem + L::CS);
+  float *Red = reinterpret_cast<float *>(smem + L::RED);
+  float *Ps = reinterpret_cast<float *>(smem + L::PS);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int rw = RGS >= 4 ? wave : wave % RGS, cw = RGS >= 4 ? 0 : wave / RGS;   // rows rw + 4*r
+  const int n0 = blockIdx.y * BN;
+  const int nmt = (p.M + BM - 1) / BM;
+
+  // ---- resident operands: W^T tile, BN-backward coefficients, producer BN scale/shift
+  for (int i = tid; i < BN * DYC; i += 256) {
+    const int r = i / DYC, c8 = (i % DYC) * 8, n = n0 + r;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (n < p.Ng && c8 < p.Kg) v = ldg16(p.WT + (size_t)n * p.Kg + c8);
+    *reinterpret_cast<uint4 *>(WTs + r * LDA + c8) = v;
+  }
+  for (int i = tid; i < KP; i += 256) {
+    const bool ok = i < p.Kg;
+    Ps[i] = ok ? p.ca[i] : 0.f;
+    Ps[KP + i] = ok ? p.cb[i] : 0.f;
+    Ps[2 * KP + i] = ok ? p.cc[i] : 0.f;
+  }
+  for (int i = tid; i < BN; i += 256) {
+    const bool ok = !LIN && n0 + i < p.Ng;
+    Ps[3 * KP + i] = ok ? p.es[n0 + i] : 0.f;
+    Ps[3 * KP + BN + i] = ok ? p.et[n0 + i] : 0.f;
+  }
+  __syncthreads();
+
+  float st0[IX][8], st1[IX][8];
+#pragma unroll
+  for (int i = 0; i < IX; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) st0[i][j] = st1[i][j] = 0.f;
+  f32x4_t accW[WPW];
+#pragma unroll
+  for (int u = 0; u < WPW; ++u) accW[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // ---- staging registers (one tile ahead): G, Y; Yt (both modes); X and R (LIN)
+  uint4 gq[IDY][4], yq[IDY][4], tq[IX][4], xq[LIN ? IX : 1][4], rq[LIN ? IX : 1][4];
+  auto load_tile = [&](int m0) {
+#pragma unroll
+    for (int i = 0; i < IDY; ++i) {
+      const int it = tid + i * 256;
+      const int c8 = (it % DYC) * 8, m4 = it / DYC;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = m0 + m4 * 4 + q;
+        const bool ok = it < NDY && row < p.M && c8 < p.Kg;
+        const size_t off = (size_t)row * p.Kg + c8;
+        gq[i][q] = ok ? ldg16(p.G + off) : make_uint4(0, 0, 0, 0);
+        yq[i][q] = ok ? ldg16(p.Y + off) : make_uint4(0, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < IX; ++i) {
+      const int it = tid + i * 256;
+      const int c8 = (it % XC) * 8, m4 = it / XC;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = m0 + m4 * 4 + q;
+        const bool ok = it < NX && row < p.M && n0 + c8 < p.Ng;
+        const size_t off = (size_t)row * p.Ng + n0 + c8;
+        tq[i][q] = ok ? ldg16(p.Yt + off) : make_uint4(0, 0, 0, 0);
+        if constexpr (LIN) {
+          xq[i][q] = ok ? ldg16(p.X + off) : make_uint4(0, 0, 0, 0);
+          rq[i][q] = (ok && p.R) ? ldg16(p.R + off) : make_uint4(0, 0, 0, 0);
+        }
+      }
+    }
+  };
+
+  if (blockIdx.x < nmt) load_tile(blockIdx.x * BM);
+  for (int mt = blockIdx.x; mt < nmt; mt += gridDim.x) {
+    const int m0 = mt * BM;
+    __syncthreads();                 // previous tile's epilogue is done with Cs (aliases the staging)
+    // ---- stage dy (row-major + transposed) and x (transposed) for this tile
+#pragma unroll
+    for (int i = 0; i < IDY; ++i) {
+      const int it = tid + i * 256;
+      if (it < NDY) {
+        const int c8 = (it % DYC) * 8, m4 = it / DYC;
+        float a[8], b[8], c[8], v[4][8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          a[j] = Ps[c8 + j];
+          b[j] = Ps[KP + c8 + j];
+          c[j] = Ps[2 * KP + c8 + j];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float g[8], y[8];
+          unpack8(gq[i][q], g);
+          unpack8(yq[i][q], y);
+          const bool valid = m0 + m4 * 4 + q < p.M;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[q][j] = valid ? bf2f(f2bf(fmaf(a[j], g[j], fmaf(b[j], y[j], c[j])))) : 0.f;
+          *reinterpret_cast<uint4 *>(dyN + (m4 * 4 + q) * LDA + c8) = pack8(v[q]);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          uint2 w;
+          w.x = pack2(v[0][j], v[1][j]);
+          w.y = pack2(v[2][j], v[3][j]);
+          *reinterpret_cast<uint2 *>(dyT + (c8 + j) * LDM + m4 * 4) = w;
+        }
+      }
+    }
+    uint4 ct[IX][4], cr[LIN ? IX : 1][4];   // this tile's epilogue operands (raw Yt, R)
+#pragma unroll
+    for (int i = 0; i < IX; ++i) {
+      const int it = tid + i * 256;
+      const int c8 = (it % XC) * 8, m4 = it / XC;
+      float v[4][8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        ct[i][q] = tq[i][q];
+        if constexpr (LIN) {
+          cr[i][q] = rq[i][q];
+          unpack8(xq[i][q], v[q]);
+        } else {
+          const bool valid = m0 + m4 * 4 + q < p.M;
+          unpack8(tq[i][q], v[q]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            v[q][j] = valid ? relu6f(fmaf(v[q][j], Ps[3 * KP + c8 + j], Ps[3 * KP + BN + c8 + j])) : 0.f;
+        }
+      }
+      if (it < NX) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          uint2 w;
+          w.x = pack2(v[0][j], v[1][j]);
+          w.y = pack2(v[2][j], v[3][j]);
+          *reinterpret_cast<uint2 *>(xT + (c8 + j) * LDM + m4 * 4) = w;
+        }
+      }
+    }
+    __syncthreads();
+    if (mt + gridDim.x < nmt) load_tile((mt + gridDim.x) * BM);   // next tile in flight from here on
+    // ---- dgrad MFMA: wave -> rows rw*16 .. +16, column tiles cw*CTW .. +CTW
+    f32x4_t acc[RPW][CTW];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r)
+#pragma unroll
+      for (int c = 0; c < CTW; ++c) acc[r][c] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KP / 32; ++ks) {
+      s16x8_t af[RPW];
+#pragma unroll
+      for (int r = 0; r < RPW; ++r)
+        af[r] = *reinterpret_cast<const s16x8_t *>(dyN + ((rw + 4 * r) * 16 + (lane & 15)) * LDA + ks * 32 + 8 * (lane >> 4));
+#pragma unroll
+      for (int c = 0; c < CTW; ++c) {
+        const s16x8_t bf = *reinterpret_cast<const s16x8_t *>(WTs + ((cw * CTW + c) * 16 + (lane & 15)) * LDA + ks * 32 + 8 * (lane >> 4));
+#pragma unroll
+        for (int r = 0; r < RPW; ++r)
+          acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[r]),
+                                                              __builtin_bit_cast(bf16x8_t, bf), acc[r][c], 0, 0, 0);
+      }
+    }
+    // ---- wgrad MFMA: dW[kg][ng] over this tile's 64 rows
+#pragma unroll
+    for (int u = 0; u < WPW; ++u) {
+      const int t = wave + 4 * u;
+      if (t < WTILES) {
+        const int ti = t / (BN / 16), tj = t % (BN / 16);
+#pragma unroll
+        for (int ms = 0; ms < BM / 32; ++ms) {
+          const s16x8_t af = *reinterpret_cast<const s16x8_t *>(dyT + (ti * 16 + (lane & 15)) * LDM + ms * 32 + 8 * (lane >> 4));
+          const s16x8_t bf = *reinterpret_cast<const s16x8_t *>(xT + (tj * 16 + (lane & 15)) * LDM + ms * 32 + 8 * (lane >> 4));
+          accW[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af),
+                                                            __builtin_bit_cast(bf16x8_t, bf), accW[u], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();                 // staging reads done: Cs may overwrite it
+    // acc[r][c][j] = C[(rw + 4r)*16 + 4*(lane>>4) + j][(cw*CTW + c)*16 + (lane&15)]
+#pragma unroll
+    for (int r = 0; r < RPW; ++r)
+#pragma unroll
+      for (int c = 0; c < CTW; ++c)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          Cs[((rw + 4 * r) * 16 + 4 * (lane >> 4) + j) * LDC + (cw * CTW + c) * 16 + (lane & 15)] = f2bf(acc[r][c][j]);
+    __syncthreads();
+    // ---- epilogue, item mapping (4 rows x 8 cols, operands already in registers)
+#pragma unroll
+    for (int i = 0; i < IX; ++i) {
+      const int it = tid + i * 256;
+      if (it < NX) {
+        const int c8 = (it % XC) * 8, m4 = it / XC;
+        float es[8], et[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          es[j] = Ps[3 * KP + c8 + j];
+          et[j] = Ps[3 * KP + BN + c8 + j];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int row = m0 + m4 * 4 + q;
+          if (row < p.M && n0 + c8 < p.Ng) {
+            float v[8], yt[8];
+            unpack8(*reinterpret_cast<const uint4 *>(Cs + (m4 * 4 + q) * LDC + c8), v);
+            unpack8(ct[i][q], yt);
+            if constexpr (!LIN) {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) v[j] *= relu6_mask(yt[j], es[j], et[j]);
+            } else {
+              float rv[8];
+              unpack8(cr[i][q], rv);
+#pragma unroll
+              for (int j = 0; j < 8; ++j) v[j] += rv[j];
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              st0[i][j] += v[j];
+              st1[i][j] = fmaf(v[j], yt[j], st1[i][j]);
+            }
+            stg16(p.out + (size_t)row * p.Ng + n0 + c8, pack8(v));
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // ---- wgrad partial of this workgroup: accW[u][j] = dW[ti*16 + 4*(lane>>4) + j][n0 + tj*16 + (lane&15)]
+  float *wdst = p.wpart + (size_t)blockIdx.x * p.Kg * p.Ng;
+#pragma unroll
+  for (int u = 0; u < WPW; ++u) {
+    const int t = wave + 4 * u;
+    if (t < WTILES) {
+      const int ti = t / (BN / 16), tj = t % (BN / 16);
+      const int ng = n0 + tj * 16 + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int kg = ti * 16 + 4 * (lane >> 4) + j;
+        if (kg < p.Kg && ng < p.Ng) wdst[(size_t)kg * p.Ng + ng] = accW[u][j];
+      }
+    }
+  }
+  // ---- BN partials of the produced gradient (sum g, sum g*yt): Red[m4][col], 16 row groups
+  for (int s = 0; s < 2; ++s) {
+#pragma unroll
+    for (int i = 0; i < IX; ++i) {
+      const int it = tid + i * 256;
+      if (it < NX) {
+        const int c8 = (it % XC) * 8, m4 = it / XC;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) Red[m4 * BN + c8 + j] = s == 0 ? st0[i][j] : st1[i][j];
+      }
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += 256) {
+      float a = 0.f;
+#pragma unroll
+      for (int g = 0; g < BM / 4; ++g) a += Red[g * BN + c];
+      if (n0 + c < p.Ng) p.part[((size_t)blockIdx.x * 2 + s) * p.Ng + n0 + c] = a;
+    }
+    __syncthreads();
+  }
+}
+
+// ===========================================================================
+// host side
+// ===========================================================================
+void launch_wgrad_reduce(float *part, int S, long long n, float *grad, hipStream_t st);
+int colsum_rows(int R);
+
+namespace {
+struct BwdGeom {
+  int KP, BN, BM, nt, gx;
+  bool ok;
+};
+BwdGeom bwd_geom(int M, int Kg, int Ng) {
+  BwdGeom g{};
+  g.KP = (Kg + 31) / 32 * 32;
+  // one N tile covering all of Ng where it is small enough (no re-read of G, Y per tile)
+  if (Ng <= 32) g.BN = 32;
+  else if (Ng % 64 == 0 || Ng % 48 != 0 || g.KP >= 160) g.BN = 64;
+  else g.BN = 48;
+  // rows per tile: enough 4x8 staging items for all 256 threads, while the prefetched
+  // (G, Y) tile stays within 2 waves/SIMD of registers
+  const int chunks = (g.KP > g.BN ? g.KP : g.BN) / 8;
+  g.BM = g.KP >= 160 ? 32 : (chunks <= 4 ? 256 : (chunks <= 8 ? 128 : 64));
+  g.ok = M >= 65536 && g.KP <= 192 && Kg % 8 == 0 && Ng % 8 == 0 && Kg > 0 && Ng > 0;
+  g.nt = (Ng + g.BN - 1) / g.BN;
+  const int nmt = (M + g.BM - 1) / g.BM;
+  int gx = 512 / g.nt;
+  if (gx > nmt) gx = nmt;
+  gx = (gx + 7) & ~7;
+  if (gx < 8) gx = 8;
+  g.gx = gx;
+  return g;
+}
+
+template <int EPI, int KP, int BN, int BM>
+void launch_bwd_t(const PwBwdArgs &a, const BwdGeom &g, hipStream_t st) {
+  hipLaunchKernelGGL((pw_bwd_fused_kernel<EPI, KP, BN, BM>), dim3(g.gx, g.nt), dim3(256),
+                     (BwdLds<KP, BN, BM>::BYTES), st, a);
+}
+
+template <int EPI>
+void launch_bwd_epi(const PwBwdArgs &a, const BwdGeom &g, hipStream_t st) {
+#define BWD_CASE(KQ, BQ, MQ) \
+  if (g.KP == KQ && g.BN == BQ && g.BM == MQ) { launch_bwd_t<EPI, KQ, BQ, MQ>(a, g, st); return; }
+  BWD_CASE(32, 32, 256) BWD_CASE(64, 32, 128) BWD_CASE(96, 32, 64) BWD_CASE(128, 32, 64)
+  BWD_CASE(32, 48, 128) BWD_CASE(64, 48, 128) BWD_CASE(96, 48, 64) BWD_CASE(128, 48, 64)
+  BWD_CASE(32, 64, 128) BWD_CASE(64, 64, 128) BWD_CASE(96, 64, 64) BWD_CASE(128, 64, 64)
+  BWD_CASE(160, 32, 32) BWD_CASE(192, 32, 32) BWD_CASE(160, 64, 32) BWD_CASE(192, 64, 32)
+#undef BWD_CASE
+}
+}  // namespace
+
+bool pw_bwd_supported(int M, int Kg, int Ng) { return bwd_geom(M, Kg, Ng).ok; }
+int pw_bwd_num_partials(int M, int Kg, int Ng) { return bwd_geom(M, Kg, Ng).gx; }
+long long pw_bwd_wgrad_workspace_floats(int M, int Kg, int Ng) {
+  const int S = bwd_geom(M, Kg, Ng).gx;
+  return (long long)(S + colsum_rows(S)) * Kg * Ng;
+}
+
+// epi: 1 = EPI_BWD_RELU6 (project conv; wgrad x = relu6(Yt*es+et)), 2 = EPI_BWD_LIN (x = X)
+void launch_pw_bwd(int epi, const bf16_t *G, const bf16_t *Y, const float *ca, const float *cb,
+                   const float *cc, const bf16_t *WT, bf16_t *out, const bf16_t *Yt, const float *es,
+                   const float *et, const bf16_t *R, const bf16_t *X, float *part, float *wpart,
+                   float *grad, int M, int Kg, int Ng, hipStream_t st) {
+  const BwdGeom g = bwd_geom(M, Kg, Ng);
+  if (!g.ok) return;
+  PwBwdArgs a{G, Y, ca, cb, cc, WT, out, Yt, es, et, R, X, part, wpart, M, Kg, Ng};
+  if (epi == EPI_BWD_RELU6_) launch_bwd_epi<EPI_BWD_RELU6_>(a, g, st);
+  else launch_bwd_epi<EPI_BWD_LIN_>(a, g, st);
+  launch_wgrad_reduce(wpart, g.gx, (long long)Kg * Ng, grad, st);
+}

@@ -718,6 +718,8 @@ void launch_stem_wgrad(const bf16_t *G, const bf16_t *Y, const float *ga, const 
   hipLaunchKernelGGL(stem_wgrad_permute_kernel, dim3((O * 27 + 255) / 256), dim3(256), 0, st, tmp, grad, O);
 }
 
+void launch_wgrad_reduce(float *part, int S, long long n, float *grad, hipStream_t st);
+
 void launch_pw_wgrad(const bf16_t *G, const bf16_t *Y, const float *ga, const float *gb,
                      const float *gc, const bf16_t *X, const float *xs, const float *xt, int xact,
                      float *part, float *grad, int M, int N, int K, hipStream_t st) {
@@ -726,7 +728,11 @@ void launch_pw_wgrad(const bf16_t *G, const bf16_t *Y, const float *ga, const fl
   PwWgArgs a{G, Y, ga, gb, gc, X, xs, xt, part, M, N, K, rps, 0, 0, 0, 0};
   if (xact == ACT_BN_RELU6) launch_wg_x<ACT_BN_RELU6>(a, TN, TK, S, st);
   else launch_wg_x<ACT_NONE>(a, TN, TK, S, st);
-  const long long n = (long long)N * K;
+  launch_wgrad_reduce(part, S, (long long)N * K, grad, st);
+}
+
+// grad[n] = sum over S split rows of part[S][n] (fixed order; part needs S + colsum_rows(S) rows)
+void launch_wgrad_reduce(float *part, int S, long long n, float *grad, hipStream_t st) {
   int rows = S;
   float *lvl1 = part + (size_t)S * n;
   launch_colsum(part, S, n, lvl1, rows, st);

@@ -155,12 +155,18 @@ class MobileNetV2Executor:
                 parts.append((K.pw_num_partials(Min, blk.hidden, blk.inp), blk.hidden))        # fwd expand
                 parts.append((K.pw_num_partials(Min, blk.inp, blk.hidden), blk.inp))               # bwd expand dgrad
                 wg.append(K.pw_wgrad_workspace(Min, blk.hidden, blk.inp))
+                if K.pw_bwd_supported(Min, blk.hidden, blk.inp):
+                    parts.append((K.pw_bwd_num_partials(Min, blk.hidden, blk.inp), blk.inp))
+                    wg.append(K.pw_bwd_wgrad_workspace(Min, blk.hidden, blk.inp))
             parts.append((K.dw_num_partials("fwd", B, Hin, Hin, blk.hidden, blk.stride), blk.hidden))
             parts.append((K.dw_num_partials("dgrad", B, Hin, Hin, blk.hidden, blk.stride), blk.hidden))
             wg.append(K.dw_wgrad_workspace(B, Hin, Hin, blk.hidden, blk.stride))
             parts.append((K.pw_num_partials(Mout, blk.oup, blk.hidden), blk.oup))                 # fwd project
             parts.append((K.pw_num_partials(Mout, blk.hidden, blk.oup), blk.hidden))           # bwd project dgrad
             wg.append(K.pw_wgrad_workspace(Mout, blk.oup, blk.hidden))
+            if K.pw_bwd_supported(Mout, blk.oup, blk.hidden):
+                parts.append((K.pw_bwd_num_partials(Mout, blk.oup, blk.hidden), blk.hidden))
+                wg.append(K.pw_bwd_wgrad_workspace(Mout, blk.oup, blk.hidden))
             cur_h = Ho
         # ---------------- final 1x1 conv + head
         last = feats[-1]
@@ -284,12 +290,18 @@ class MobileNetV2Executor:
             bnp, bnd = bp.bn_p, bp.bn_d
             # bn_p backward coefficients were finalised by whoever produced bp.G
             # project dgrad -> g_d (relu6 mask of BN_d) + BN_d partials
-            K.pw_gemm(K.PRO_BNBWD, K.EPI_BWD_RELU6, bp.G, f.bt(bp.w_p), bnd.g, ws, Mout, bp.hidden, bp.cout,
-                      A2=bnp.y, pa=bnp.a, pb=bnp.b, pc=bnp.c, Yt=bnd.y, es=bnd.scale, et=bnd.shift)
-            bnd.finalize_bwd(ws, K.pw_num_partials(Mout, bp.hidden, bp.cout))
-            # project wgrad
-            K.pw_wgrad(bp.G, bnp.y, bnp.a, bnp.b, bnp.c, bnd.y, bnd.scale, bnd.shift, K.ACT_BN_RELU6, wg,
-                       f.g(bp.w_p), Mout, bp.cout, bp.hidden)
+            if K.pw_bwd_supported(Mout, bp.cout, bp.hidden):
+                # fused dgrad + wgrad (x = relu6(BN_d(y_d)) rebuilt from the mask operand)
+                K.pw_bwd(K.EPI_BWD_RELU6, bp.G, bnp.y, bnp.a, bnp.b, bnp.c, f.bt(bp.w_p), bnd.g, bnd.y, ws, wg,
+                         f.g(bp.w_p), Mout, bp.cout, bp.hidden, es=bnd.scale, et=bnd.shift)
+                bnd.finalize_bwd(ws, K.pw_bwd_num_partials(Mout, bp.cout, bp.hidden))
+            else:
+                K.pw_gemm(K.PRO_BNBWD, K.EPI_BWD_RELU6, bp.G, f.bt(bp.w_p), bnd.g, ws, Mout, bp.hidden, bp.cout,
+                          A2=bnp.y, pa=bnp.a, pb=bnp.b, pc=bnp.c, Yt=bnd.y, es=bnd.scale, et=bnd.shift)
+                bnd.finalize_bwd(ws, K.pw_num_partials(Mout, bp.hidden, bp.cout))
+                # project wgrad
+                K.pw_wgrad(bp.G, bnp.y, bnp.a, bnp.b, bnp.c, bnd.y, bnd.scale, bnd.shift, K.ACT_BN_RELU6, wg,
+                           f.g(bp.w_p), Mout, bp.cout, bp.hidden)
             self._ready([bp.w_p] + bnd.param_names)
             # depthwise: input BN is BN_e (expand) or the stem BN0 (t=1 block)
             dw_in = bp.bn_e if bp.expand else self.bn0
@@ -303,12 +315,18 @@ class MobileNetV2Executor:
                 bne = bp.bn_e
                 assert prev is not None
                 # expand dgrad -> gradient w.r.t. the block input o_prev (+ skip gradient)
-                K.pw_gemm(K.PRO_BNBWD, K.EPI_BWD_LIN, bne.g, f.bt(bp.w_e), prev.G, ws, Min, bp.cin, bp.hidden,
-                          A2=bne.y, pa=bne.a, pb=bne.b, pc=bne.c, Yt=prev.bn_p.y,
-                          R=bp.G if bp.residual else None)
-                prev.bn_p.finalize_bwd(ws, K.pw_num_partials(Min, bp.cin, bp.hidden))
-                K.pw_wgrad(bne.g, bne.y, bne.a, bne.b, bne.c, prev.o, None, None, K.ACT_NONE, wg,
-                           f.g(bp.w_e), Min, bp.hidden, bp.cin)
+                if K.pw_bwd_supported(Min, bp.hidden, bp.cin):
+                    K.pw_bwd(K.EPI_BWD_LIN, bne.g, bne.y, bne.a, bne.b, bne.c, f.bt(bp.w_e), prev.G, prev.bn_p.y,
+                             ws, wg, f.g(bp.w_e), Min, bp.hidden, bp.cin, R=bp.G if bp.residual else None,
+                             X=prev.o)
+                    prev.bn_p.finalize_bwd(ws, K.pw_bwd_num_partials(Min, bp.hidden, bp.cin))
+                else:
+                    K.pw_gemm(K.PRO_BNBWD, K.EPI_BWD_LIN, bne.g, f.bt(bp.w_e), prev.G, ws, Min, bp.cin, bp.hidden,
+                              A2=bne.y, pa=bne.a, pb=bne.b, pc=bne.c, Yt=prev.bn_p.y,
+                              R=bp.G if bp.residual else None)
+                    prev.bn_p.finalize_bwd(ws, K.pw_num_partials(Min, bp.cin, bp.hidden))
+                    K.pw_wgrad(bne.g, bne.y, bne.a, bne.b, bne.c, prev.o, None, None, K.ACT_NONE, wg,
+                               f.g(bp.w_e), Min, bp.hidden, bp.cin)
                 self._ready([bp.w_e] + prev.bn_p.param_names)
             else:
                 # t=1 block: its input is relu6(BN0(stem)) -> stem weight gradient

@@ -201,6 +201,53 @@ def wt_transpose(src, dst, tab, n):
     lib().wt_transpose(_p(src), _p(dst), _p(tab), int(n), _s())
 
 
+def pw_bwd_supported(M, Kg, Ng):
+    """True when the fused dgrad+wgrad kernel handles this 1x1 conv backward (large M)."""
+    return bool(lib().pw_bwd_supported(M, Kg, Ng))
+
+
+def pw_bwd_num_partials(M, Kg, Ng):
+    return lib().pw_bwd_num_partials(M, Kg, Ng)
+
+
+def pw_bwd_wgrad_workspace(M, Kg, Ng):
+    return lib().pw_bwd_wgrad_workspace_floats(M, Kg, Ng)
+
+
+def pw_bwd(epi, G, Y, ca, cb, cc, WT, out, Yt, part, wpart, grad, M, Kg, Ng, es=None, et=None, R=None,
+           X=None):
+    """Fused 1x1-conv backward (one read of G, Y):
+
+    dy = ca*G + cb*Y + cc                      [M, Kg]   (this conv's BN backward)
+    out = epi(dy @ WT^T)                       [M, Ng]   WT = transposed conv weight [Ng, Kg]
+      EPI_BWD_RELU6: out *= 1[0 < Yt*es+et < 6];  EPI_BWD_LIN: out += R
+    grad[Kg, Ng] = dy^T @ x,  x = relu6(Yt*es+et) (RELU6) or X (LIN)
+    part <- BN partials (sum out, sum out*Yt) per workgroup.
+    """
+    if not pw_bwd_supported(M, Kg, Ng):
+        raise ValueError(f"pw_bwd: unsupported shape M={M} Kg={Kg} Ng={Ng}")
+    _chk(G, BF16, M * Kg, "G")
+    _chk(Y, BF16, M * Kg, "Y")
+    _chk(WT, BF16, Ng * Kg, "WT")
+    _chk(out, BF16, M * Ng, "out")
+    _chk(Yt, BF16, M * Ng, "Yt")
+    _chk(R, BF16, M * Ng, "R")
+    _chk(X, BF16, M * Ng, "X")
+    _chk(part, F32, pw_bwd_num_partials(M, Kg, Ng) * 2 * Ng, "part")
+    _chk(wpart, F32, pw_bwd_wgrad_workspace(M, Kg, Ng), "wpart")
+    _chk(grad, F32, Kg * Ng, "grad")
+    for t, nm in ((ca, "ca"), (cb, "cb"), (cc, "cc")):
+        _chk(t, F32, Kg, nm)
+    if epi == EPI_BWD_RELU6:
+        assert es is not None and et is not None
+    elif epi == EPI_BWD_LIN:
+        assert X is not None
+    else:
+        raise ValueError(f"pw_bwd: bad epilogue {epi}")
+    lib().pw_bwd(int(epi), _p(G), _p(Y), _p(ca), _p(cb), _p(cc), _p(WT), _p(out), _p(Yt), _p(es), _p(et),
+                 _p(R), _p(X), _p(part), _p(wpart), _p(grad), M, Kg, Ng, _s())
+
+
 def pw_wgrad_workspace(M, N, K):
     return lib().pw_wgrad_workspace_floats(M, N, K)
 

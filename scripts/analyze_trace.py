@@ -81,7 +81,7 @@ def main(path, B=128, S=224):
         print(f"  {kind:4s} M={M:8d} {K:4d}->{N:4d}  fwd {f_:6.1f} {bf / f_ / 1e6 if f_ else 0:5.2f}  "
               f"dgrad {d_:6.1f} {bd / d_ / 1e6 if d_ else 0:5.2f}  wgrad {w_:6.1f} {bw / w_ / 1e6 if w_ else 0:5.2f}")
     print(f"  totals: fwd {tf:.0f} us  dgrad {td:.0f} us  wgrad {tw:.0f} us (+ stem wgrad {wg[-1][1] if wg else 0:.0f})")
-    for fam in ("pw_gemm_kernel", "pw_wgrad_kernel", "colsum_kernel", "bn_fwd_finalize_kernel", "split_reduce_kernel"):
+    for fam in ("pw_bwd_fused_kernel", "pw_gemm_kernel", "pw_wgrad_kernel", "colsum_kernel", "bn_fwd_finalize_kernel", "split_reduce_kernel"):
         ds = by.get(fam, [])
         print(f"\n{fam}: {len(ds)} dispatches {sum(d for _, d in ds):.1f} us total; per dispatch: " +
               " ".join(f"{d:.0f}" for _, d in ds[:80]))

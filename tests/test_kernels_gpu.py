@@ -234,6 +234,49 @@ def test_pw_wgrad(dev, M, Kf, Nf, xact):
     assert rel(grad.view(Nf, Kf), ref) < 2e-3
 
 
+# fused dgrad + wgrad of a 1x1 conv (large M): (M, Kg = conv Cout, Ng = conv Cin, epilogue, residual)
+PW_BWD_CASES = [(70001, 96, 16, "lin", True), (66000, 24, 144, "relu6", False), (65600, 192, 32, "lin", False),
+                (70000, 32, 192, "relu6", False), (65613, 144, 24, "lin", True), (65540, 16, 32, "relu6", False)]
+
+
+@pytest.mark.parametrize("M,Kg,Ng,mode,res", PW_BWD_CASES)
+def test_pw_bwd_fused(dev, M, Kg, Ng, mode, res):
+    assert K.pw_bwd_supported(M, Kg, Ng)
+    G = bf(rnd(M, Kg, dev=dev, seed=1))
+    Y = bf(rnd(M, Kg, dev=dev, seed=2))
+    coef = torch.stack([torch.rand(Kg, device=dev) + 0.5, torch.rand(Kg, device=dev) - 0.5,
+                        torch.rand(Kg, device=dev) - 0.5]).contiguous()
+    W = bf(rnd(Kg, Ng, dev=dev, seed=5) / math.sqrt(Kg))        # conv weight [Cout=Kg][Cin=Ng]
+    WT = W.t().contiguous()
+    Yt = bf(rnd(M, Ng, dev=dev, seed=6))
+    es, et = bn_params(Ng, dev, 7)
+    R = bf(rnd(M, Ng, dev=dev, seed=8)) if res else None
+    X = bf(rnd(M, Ng, dev=dev, seed=9)) if mode == "lin" else None
+    out = torch.empty(M, Ng, dtype=torch.bfloat16, device=dev)
+    P = K.pw_bwd_num_partials(M, Kg, Ng)
+    part = torch.zeros(P * 2 * Ng, device=dev)
+    wpart = torch.zeros(K.pw_bwd_wgrad_workspace(M, Kg, Ng), device=dev)
+    grad = torch.empty(Kg * Ng, device=dev)
+    epi = K.EPI_BWD_RELU6 if mode == "relu6" else K.EPI_BWD_LIN
+    K.pw_bwd(epi, G, Y, coef[0], coef[1], coef[2], WT, out, Yt, part, wpart, grad, M, Kg, Ng,
+             es=es, et=et, R=R, X=X)
+    dy = bf(coef[0] * G.float() + coef[1] * Y.float() + coef[2]).float()
+    ref = dy @ W.float()
+    if mode == "relu6":
+        a = Yt.float() * es + et
+        ref = ref * ((a > 0) & (a < 6)).float()
+        x = bf(relu6(a)).float()
+    else:
+        if res:
+            ref = ref + R.float()
+        x = X.float()
+    assert rel(out, ref) < 8e-3
+    st = sum_parts(part, P, Ng)
+    assert rel(st[0], ref.sum(0)) < 2e-2
+    assert rel(st[1], (ref * Yt.float()).sum(0)) < 2e-2
+    assert rel(grad.view(Kg, Ng), dy.t() @ x) < 2e-3
+
+
 # ----------------------------------------------------------------------------- stem
 @pytest.mark.parametrize("B,S", [(2, 32), (3, 64), (2, 224)])
 def test_stem(dev, B, S):
