@@ -69,6 +69,8 @@ void launch_augment(const unsigned char *, const long long *, const long long *,
                     long long *, float *, hipStream_t);
 void launch_step_begin(float *, hipStream_t);
 int colsum_rows(int);
+long long bn_part_floats(int, int);
+void register_side_stream(hipStream_t);
 void launch_reduce_metrics(const float *, const float *, int, double *, hipStream_t);
 
 template <typename T>
@@ -84,7 +86,10 @@ PYBIND11_MODULE(_pgdist_C, m) {
   m.doc() = "pgdist native library: gfx950 HIP kernels + C++ runtime";
   m.attr("arch") = "gfx950";
   m.def("last_error", &last_error);
-  m.def("colsum_rows", &colsum_rows, "rows of level-1 scratch a reduction over R partial rows needs");
+  m.def("colsum_rows", &colsum_rows, "rows of level-1 scratch a wgrad reduction over R partial rows needs");
+  m.def("register_side_stream", [](P s) { register_side_stream(S(s)); },
+        "give reductions launched on this stream their own arrival counters");
+  m.def("bn_part_floats", &bn_part_floats, "floats of workspace a BN finalize over P partial rows needs");
 
   // ---- BatchNorm ----
   m.def("bn_fwd_finalize", [](P part, int Pn, int C, float count, P gamma, P beta, float eps,

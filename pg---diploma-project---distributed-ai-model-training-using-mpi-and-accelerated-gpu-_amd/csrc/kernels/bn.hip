@@ -8,37 +8,81 @@
 // materialisation of block outputs (BN + residual) — reference semantics:
 // torchvision BatchNorm2d(eps=1e-5, momentum=0.1) inside MobileNetV2
 // (SURVEY.md §2.6 "BatchNorm2d (train)", §2.8).
-#include "../common.h"
+#include "../reduce.h"
 
 // ---------------------------------------------------------------------------
-// forward finalize: partial (sum, sumsq) -> mean, rstd, scale, shift (+ running stats)
-// grid: ceil(C/64) blocks of 256 threads (64 channels x 4 partial stripes)
+// Reduction of the [P][2][C] partials (one launch, reduce.h): grid (ceil(C/16) channel
+// blocks, nch row chunks), 256 threads = 32 columns ({sum, sumsq} x 16 channels) x 8
+// row stripes, fp64 accumulation.  The last workgroup of each channel block gets the
+// totals in fin[0..15] (stat 0) / fin[16..31] (stat 1) and runs the finalize.
 // ---------------------------------------------------------------------------
+namespace {
+constexpr int kBnMinRows = 16;
+
+PG_DEVICE bool bn_reduce(const float *__restrict__ part, int P, int C, int rch, int nch, double *lvl1,
+                         int *ctr, double (&sh)[8][32], double (&fin)[32], int &flag) {
+  const int tid = threadIdx.x, col = tid & 31, stripe = tid >> 5;
+  const int c = blockIdx.x * 16 + (col & 15), stat = col >> 4;
+  const int r0 = blockIdx.y * rch, r1 = min(P, r0 + rch);
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;   // 4 loads in flight per thread, fixed order
+  if (c < C) {
+    const float *src = part + stat * C + c;
+    const size_t ld = (size_t)2 * C;
+    int r = r0 + stripe;
+    for (; r + 24 < r1; r += 32) {
+      a0 += (double)src[r * ld];
+      a1 += (double)src[(r + 8) * ld];
+      a2 += (double)src[(r + 16) * ld];
+      a3 += (double)src[(r + 24) * ld];
+    }
+    for (; r < r1; r += 8) a0 += (double)src[r * ld];
+  }
+  sh[stripe][col] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  const size_t row = (size_t)gridDim.x * 32;
+  if (tid < 32) {
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += sh[k][tid];
+    if (nch == 1) fin[tid] = s;
+    else st_sc1(lvl1 + blockIdx.y * row + blockIdx.x * 32 + tid, s);
+  }
+  if (nch == 1) {
+    __syncthreads();
+    return true;
+  }
+  if (!arrive_last(ctr, nch, &flag)) return false;
+  double b = 0.0;
+  for (int k = stripe; k < nch; k += 8) b += ld_sc1(lvl1 + k * row + blockIdx.x * 32 + col);
+  sh[stripe][col] = b;
+  __syncthreads();
+  if (tid < 32) {
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += sh[k][tid];
+    fin[tid] = s;
+  }
+  __syncthreads();
+  return true;
+}
+}  // namespace
+
+// forward: partial (sum, sumsq) -> mean, rstd, scale, shift (+ running stats, unbiased var)
 __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(
-    const float *__restrict__ part, int P, int C, float count,
+    const float *__restrict__ part, int P, int C, int rch, int nch, double *lvl1, int *ctr, float count,
     const float *__restrict__ gamma, const float *__restrict__ beta, float eps, float momentum,
     float *__restrict__ running_mean, float *__restrict__ running_var, long long *__restrict__ nbt,
     float *__restrict__ mean_out, float *__restrict__ rstd_out, float *__restrict__ scale_out,
     float *__restrict__ shift_out) {
-  __shared__ double sh[2][4][64];
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + tx;
-  double s = 0.0, q = 0.0;
-  if (c < C) {
-    for (int p = ty; p < P; p += 4) {
-      s += (double)part[(size_t)p * 2 * C + c];
-      q += (double)part[(size_t)p * 2 * C + C + c];
-    }
-  }
-  sh[0][ty][tx] = s;
-  sh[1][ty][tx] = q;
-  __syncthreads();
-  if (ty == 0 && c < C) {
-    s = sh[0][0][tx] + sh[0][1][tx] + sh[0][2][tx] + sh[0][3][tx];
-    q = sh[1][0][tx] + sh[1][1][tx] + sh[1][2][tx] + sh[1][3][tx];
+  __shared__ double sh[8][32];
+  __shared__ double fin[32];
+  __shared__ int flag;
+  if (!bn_reduce(part, P, C, rch, nch, lvl1, ctr, sh, fin, flag)) return;
+  const int tid = threadIdx.x, c = blockIdx.x * 16 + tid;
+  if (tid < 16 && c < C) {
     const double n = (double)count;
-    const double mean = s / n;
-    double var = q / n - mean * mean;
+    const double mean = fin[tid] / n;
+    double var = fin[16 + tid] / n - mean * mean;
     if (var < 0.0) var = 0.0;
     const float rstd = (float)(1.0 / sqrt(var + (double)eps));
     const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
@@ -52,33 +96,21 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(
       running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unbiased;
     }
   }
-  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
+  if (nbt && blockIdx.x == 0 && tid == 0) nbt[0] += 1;
 }
 
-// ---------------------------------------------------------------------------
-// backward finalize: partial (sum g, sum g*y) -> dy = alpha*g + beta*y + gamma_c
-// coef layout [3][C] = alpha, beta, gamma_c ; writes dgamma/dbeta (fp32 grads)
-// ---------------------------------------------------------------------------
+// backward: partial (sum g, sum g*y) -> dy = alpha*g + beta*y + gamma_c ; coef [3][C], dgamma/dbeta
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(
-    const float *__restrict__ part, int P, int C, float count, const float *__restrict__ mean,
-    const float *__restrict__ rstd, const float *__restrict__ gamma, float *__restrict__ coef,
-    float *__restrict__ dgamma, float *__restrict__ dbeta) {
-  __shared__ double sh[2][4][64];
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + tx;
-  double sg = 0.0, sgy = 0.0;
-  if (c < C) {
-    for (int p = ty; p < P; p += 4) {
-      sg += (double)part[(size_t)p * 2 * C + c];
-      sgy += (double)part[(size_t)p * 2 * C + C + c];
-    }
-  }
-  sh[0][ty][tx] = sg;
-  sh[1][ty][tx] = sgy;
-  __syncthreads();
-  if (ty == 0 && c < C) {
-    sg = sh[0][0][tx] + sh[0][1][tx] + sh[0][2][tx] + sh[0][3][tx];
-    sgy = sh[1][0][tx] + sh[1][1][tx] + sh[1][2][tx] + sh[1][3][tx];
+    const float *__restrict__ part, int P, int C, int rch, int nch, double *lvl1, int *ctr, float count,
+    const float *__restrict__ mean, const float *__restrict__ rstd, const float *__restrict__ gamma,
+    float *__restrict__ coef, float *__restrict__ dgamma, float *__restrict__ dbeta) {
+  __shared__ double sh[8][32];
+  __shared__ double fin[32];
+  __shared__ int flag;
+  if (!bn_reduce(part, P, C, rch, nch, lvl1, ctr, sh, fin, flag)) return;
+  const int tid = threadIdx.x, c = blockIdx.x * 16 + tid;
+  if (tid < 16 && c < C) {
+    const double sg = fin[tid], sgy = fin[16 + tid];
     const double n = (double)count, mu = mean[c], rs = rstd[c];
     const double g = gamma ? gamma[c] : 1.0;
     const double sgx = (sgy - mu * sg) * rs;  // sum g * xhat
@@ -120,30 +152,40 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t *__restrict_
 // ---------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------
-void launch_colsum(const float *src, int R, long long n, float *dst, int &rows_out, hipStream_t st);
+// part: [P][2][C] followed by the level-1 scratch (bn_part_floats(P, C) floats in total)
+long long bn_part_floats(int P, int C) {
+  const int nch = red_nch(P, kBnMinRows);
+  const long long lvl1 = nch > 1 ? (long long)nch * ((C + 15) / 16) * 32 * 2 : 0;   // doubles -> floats
+  return (long long)P * 2 * C + lvl1 + 4;
+}
 
-// part: [P][2][C] followed by scratch for the level-1 fold (colsum_rows(P) * 2C floats)
+namespace {
+double *bn_lvl1(const float *part, int P, int C) {
+  // 8-B aligned scratch right after the partials (P * 2C floats, C even)
+  return reinterpret_cast<double *>(const_cast<float *>(part) + (size_t)P * 2 * C);
+}
+}  // namespace
+
 void launch_bn_fwd_finalize(const float *part, int P, int C, float count, const float *gamma,
                             const float *beta, float eps, float momentum, float *rmean,
                             float *rvar, long long *nbt, float *mean, float *rstd, float *scale,
                             float *shift, hipStream_t st) {
-  int rows = P;
-  float *tmp = const_cast<float *>(part) + (size_t)P * 2 * C;
-  launch_colsum(part, P, 2LL * C, tmp, rows, st);
-  if (rows != P) { part = tmp; P = rows; }
-  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, st, part, P, C,
-                     count, gamma, beta, eps, momentum, rmean, rvar, nbt, mean, rstd, scale, shift);
+  const int rch = red_rch(P, kBnMinRows), nch = red_nch(P, kBnMinRows);
+  const int nb = (C + 15) / 16;
+  int *ctr = nch > 1 ? reduce_counters(nb, st) : nullptr;
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(nb, nch), dim3(256), 0, st, part, P, C, rch, nch,
+                     bn_lvl1(part, P, C), ctr, count, gamma, beta, eps, momentum, rmean, rvar, nbt, mean,
+                     rstd, scale, shift);
 }
 
 void launch_bn_bwd_finalize(const float *part, int P, int C, float count, const float *mean,
                             const float *rstd, const float *gamma, float *coef, float *dgamma,
                             float *dbeta, hipStream_t st) {
-  int rows = P;
-  float *tmp = const_cast<float *>(part) + (size_t)P * 2 * C;
-  launch_colsum(part, P, 2LL * C, tmp, rows, st);
-  if (rows != P) { part = tmp; P = rows; }
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, st, part, P, C,
-                     count, mean, rstd, gamma, coef, dgamma, dbeta);
+  const int rch = red_rch(P, kBnMinRows), nch = red_nch(P, kBnMinRows);
+  const int nb = (C + 15) / 16;
+  int *ctr = nch > 1 ? reduce_counters(nb, st) : nullptr;
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(nb, nch), dim3(256), 0, st, part, P, C, rch, nch,
+                     bn_lvl1(part, P, C), ctr, count, mean, rstd, gamma, coef, dgamma, dbeta);
 }
 
 void launch_bn_apply(const bf16_t *y, const bf16_t *res, const float *scale, const float *shift,

@@ -507,21 +507,6 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(
   block_channel_partials<9>(accw, part, g.C, g.CC, cbase, g.TWc, lds);
 }
 
-// reduce [P][9][C] -> grad [9][C] fp32 (tap-major, the flat-buffer layout)
-__global__ __launch_bounds__(256) void dw_wgrad_reduce_kernel(const float *__restrict__ part, int P,
-                                                             int C, float *__restrict__ grad) {
-  const int idx = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int ty = threadIdx.x >> 6;
-  __shared__ float sh[4][64];
-  float s = 0.f;
-  if (idx < 9 * C)
-    for (int p = ty; p < P; p += 4) s += part[(size_t)p * 9 * C + idx];
-  sh[ty][threadIdx.x & 63] = s;
-  __syncthreads();
-  if (ty == 0 && idx < 9 * C)
-    grad[idx] = sh[0][threadIdx.x] + sh[1][threadIdx.x] + sh[2][threadIdx.x] + sh[3][threadIdx.x];
-}
-
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
@@ -590,7 +575,7 @@ void launch_dw_dgrad(const bf16_t *gin, const bf16_t *yself, const float *coef, 
     hipLaunchKernelGGL((dw_dgrad_kernel<2>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g);
 }
 
-void launch_colsum(const float *src, int R, long long n, float *dst, int &rows_out, hipStream_t st);
+void launch_wgrad_reduce(float *part, int S, long long n, float *grad, hipStream_t st);
 
 void launch_dw_wgrad(const bf16_t *gin, const bf16_t *yself, const float *coef, const bf16_t *yprev,
                      const float *ps, const float *pt, float *part, float *grad, int B, int H, int W,
@@ -602,10 +587,6 @@ void launch_dw_wgrad(const bf16_t *gin, const bf16_t *yself, const float *coef, 
     hipLaunchKernelGGL((dw_wgrad_kernel<1>), grid, block, 0, st, gin, yself, coef, yprev, ps, pt, part, g);
   else
     hipLaunchKernelGGL((dw_wgrad_kernel<2>), grid, block, 0, st, gin, yself, coef, yprev, ps, pt, part, g);
-  // deterministic two-level reduction of the [P][9C] partials (level 1 written after them)
-  int rows = P;
-  float *tmp = part + (size_t)P * 9 * C;
-  launch_colsum(part, P, 9LL * C, tmp, rows, st);
-  hipLaunchKernelGGL(dw_wgrad_reduce_kernel, dim3((9 * C + 63) / 64), dim3(256), 0, st,
-                     rows == P ? part : tmp, rows, C, grad);
+  // deterministic two-level reduction of the [P][9C] partials -> grad [9][C] (tap-major)
+  launch_wgrad_reduce(part, P, 9LL * C, grad, st);
 }

@@ -46,45 +46,3 @@ void launch_reduce_metrics(const float *loss, const float *correct, int B, doubl
                            hipStream_t st) {
   hipLaunchKernelGGL(reduce_metrics_kernel, dim3(1), dim3(256), 0, st, loss, correct, B, acc);
 }
-
-// ---------------------------------------------------------------------------
-// Deterministic column reduction, level 1:  dst[q][i] = sum_{r in chunk q} src[r][i].
-// Producers emit per-workgroup partial rows (BN statistics, weight-gradient
-// split-K slabs); a sequential per-thread loop over thousands of rows is
-// latency-bound (tens of us), so rows are first folded in chunks by a 2-D grid
-// (columns x row-chunks) and consumers read <= 32 rows.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void colsum_kernel(const float *__restrict__ src, int R, long long n,
-                                                    int rch, float *__restrict__ dst) {
-  const long long i = blockIdx.x * 256ll + threadIdx.x;
-  if (i >= n) return;
-  const int r0 = blockIdx.y * rch, r1 = min(R, r0 + rch);
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-  int r = r0;
-  for (; r + 3 < r1; r += 4) {
-    a0 += src[(size_t)r * n + i];
-    a1 += src[(size_t)(r + 1) * n + i];
-    a2 += src[(size_t)(r + 2) * n + i];
-    a3 += src[(size_t)(r + 3) * n + i];
-  }
-  for (; r < r1; ++r) a0 += src[(size_t)r * n + i];
-  dst[(size_t)blockIdx.y * n + i] = (a0 + a1) + (a2 + a3);
-}
-
-// rows_out = number of rows the consumer must read: R (no-op) or ceil(R / rch) in dst
-void launch_colsum(const float *src, int R, long long n, float *dst, int &rows_out, hipStream_t st) {
-  if (R <= 32) {
-    rows_out = R;
-    return;
-  }
-  const int rch = (R + 31) / 32;
-  rows_out = (R + rch - 1) / rch;
-  dim3 grid((unsigned)((n + 255) / 256), rows_out);
-  hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, st, src, R, n, rch, dst);
-}
-
-int colsum_rows(int R) {
-  if (R <= 32) return 0;
-  const int rch = (R + 31) / 32;
-  return (R + rch - 1) / rch;
-}

@@ -551,16 +551,6 @@ __global__ __launch_bounds__(256) void pw_wgrad_kernel(PwWgArgs p) {
       }
 }
 
-__global__ __launch_bounds__(256) void split_reduce_kernel(const float *__restrict__ part, int S,
-                                                          long long n, float *__restrict__ out) {
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
-       i += (long long)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int k = 0; k < S; ++k) s += part[(size_t)k * n + i];
-    out[i] = s;
-  }
-}
-
 // ===========================================================================
 // host launchers
 // ===========================================================================
@@ -646,8 +636,8 @@ void launch_wt_transpose(const bf16_t *src, bf16_t *dst, const int *tab, int n, 
   hipLaunchKernelGGL(wt_transpose_kernel, dim3(64, n), dim3(256), 0, st, src, dst, tab);
 }
 
-void launch_colsum(const float *src, int R, long long n, float *dst, int &rows_out, hipStream_t st);
 int colsum_rows(int R);
+void launch_wgrad_reduce(float *part, int S, long long n, float *grad, hipStream_t st);
 
 // split-M geometry: tiles of TN x TK outputs, S splits of >= kMinRowsPerSplit rows each
 static constexpr int kMinRowsPerSplit = 512;
@@ -710,15 +700,10 @@ void launch_stem_wgrad(const bf16_t *G, const bf16_t *Y, const float *ga, const 
   PwWgArgs a{G, Y, ga, gb, gc, img, nullptr, nullptr, part, M, O, 36, rps, H, W, Ho, Wo};
   launch_wg_x<IM2COL_STEM>(a, TN, TK, S, st);
   const long long n = (long long)O * 36;
-  int rows = S;
-  float *lvl1 = part + (size_t)S * n;
-  launch_colsum(part, S, n, lvl1, rows, st);
-  float *tmp = lvl1 + (size_t)colsum_rows(S) * n;
-  hipLaunchKernelGGL(split_reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, st, rows == S ? part : lvl1, rows, n, tmp);
+  float *tmp = part + (size_t)(S + colsum_rows(S)) * n;
+  launch_wgrad_reduce(part, S, n, tmp, st);
   hipLaunchKernelGGL(stem_wgrad_permute_kernel, dim3((O * 27 + 255) / 256), dim3(256), 0, st, tmp, grad, O);
 }
-
-void launch_wgrad_reduce(float *part, int S, long long n, float *grad, hipStream_t st);
 
 void launch_pw_wgrad(const bf16_t *G, const bf16_t *Y, const float *ga, const float *gb,
                      const float *gc, const bf16_t *X, const float *xs, const float *xt, int xact,
@@ -731,12 +716,3 @@ void launch_pw_wgrad(const bf16_t *G, const bf16_t *Y, const float *ga, const fl
   launch_wgrad_reduce(part, S, (long long)N * K, grad, st);
 }
 
-// grad[n] = sum over S split rows of part[S][n] (fixed order; part needs S + colsum_rows(S) rows)
-void launch_wgrad_reduce(float *part, int S, long long n, float *grad, hipStream_t st) {
-  int rows = S;
-  float *lvl1 = part + (size_t)S * n;
-  launch_colsum(part, S, n, lvl1, rows, st);
-  int grid = (int)((n + 255) / 256);
-  if (grid > 2048) grid = 2048;
-  hipLaunchKernelGGL(split_reduce_kernel, dim3(grid), dim3(256), 0, st, rows == S ? part : lvl1, rows, n, grad);
-}

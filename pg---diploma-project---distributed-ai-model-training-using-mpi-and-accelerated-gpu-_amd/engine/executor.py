@@ -109,7 +109,7 @@ class BlockPlan:
 class MobileNetV2Executor:
     def __init__(self, model: MobileNetV2, batch: int, img_size: int, device: torch.device,
                  flat: Optional[FlatParams] = None, dropout_seed: int = 0,
-                 hyper: Optional[torch.Tensor] = None):
+                 hyper: Optional[torch.Tensor] = None, side_stream: bool = True):
         assert device.type == "cuda", "the native executor runs on the GPU"
         self.model = model.to(device)
         self.B, self.S, self.device = batch, img_size, device
@@ -124,7 +124,8 @@ class MobileNetV2Executor:
         self.stem_w = "features.0.0.weight"
         self.bn0 = BNState(self.flat, feats[0][1], "features.0.1", B * H * H, feats[0][0].out_channels, device)
         parts = [(K.stem_num_partials(B, img_size, img_size), 32)]   # (partial rows, channels)
-        wg = [K.stem_wgrad_workspace(B, img_size, img_size, 32)]
+        wg = [K.stem_wgrad_workspace(B, img_size, img_size, 32)]   # side-stream weight gradients
+        wgm = [0]                                                    # fused dgrad+wgrad (main stream)
         # ---------------- blocks
         self.blocks: List[BlockPlan] = []
         cur_h = H
@@ -157,7 +158,7 @@ class MobileNetV2Executor:
                 wg.append(K.pw_wgrad_workspace(Min, blk.hidden, blk.inp))
                 if K.pw_bwd_supported(Min, blk.hidden, blk.inp):
                     parts.append((K.pw_bwd_num_partials(Min, blk.hidden, blk.inp), blk.inp))
-                    wg.append(K.pw_bwd_wgrad_workspace(Min, blk.hidden, blk.inp))
+                    wgm.append(K.pw_bwd_wgrad_workspace(Min, blk.hidden, blk.inp))
             parts.append((K.dw_num_partials("fwd", B, Hin, Hin, blk.hidden, blk.stride), blk.hidden))
             parts.append((K.dw_num_partials("dgrad", B, Hin, Hin, blk.hidden, blk.stride), blk.hidden))
             wg.append(K.dw_wgrad_workspace(B, Hin, Hin, blk.hidden, blk.stride))
@@ -166,7 +167,7 @@ class MobileNetV2Executor:
             wg.append(K.pw_wgrad_workspace(Mout, blk.oup, blk.hidden))
             if K.pw_bwd_supported(Mout, blk.oup, blk.hidden):
                 parts.append((K.pw_bwd_num_partials(Mout, blk.oup, blk.hidden), blk.hidden))
-                wg.append(K.pw_bwd_wgrad_workspace(Mout, blk.oup, blk.hidden))
+                wgm.append(K.pw_bwd_wgrad_workspace(Mout, blk.oup, blk.hidden))
             cur_h = Ho
         # ---------------- final 1x1 conv + head
         last = feats[-1]
@@ -191,6 +192,13 @@ class MobileNetV2Executor:
         # ---------------- workspaces (stream-ordered reuse)
         self.ws_part = torch.zeros(max(K.bn_part_floats(P, C) for P, C in parts) + 1024, **f32)
         self.ws_wgrad = torch.zeros(max(wg) + 1024, **f32)
+        self.ws_wgrad_main = torch.zeros(max(wgm) + 1024, **f32)
+        # weight gradients that are not fused into a dgrad run on a side stream, overlapping
+        # the dgrad -> BN-finalize chain (the backward's critical path)
+        self.side = None
+        if device.type == "cuda" and side_stream:
+            self.side = torch.cuda.Stream(device)
+            K.register_side_stream(self.side)
         self.img = torch.zeros(B, img_size, img_size, 4, dtype=torch.bfloat16, device=device)
         self.labels = torch.zeros(B, dtype=torch.int64, device=device)
         self.hyper = hyper if hyper is not None else torch.zeros(2, **f32)   # [lr, step] (device)
@@ -207,8 +215,27 @@ class MobileNetV2Executor:
 
     # ------------------------------------------------------------------ helpers
     def _ready(self, names):
-        if self.on_params_ready is not None:
+        """Gradients of ``names`` are final once the work enqueued so far completes.  With a
+        side stream the callback (DDP bucket launch) runs on it after it has joined the main
+        stream, so the collective is ordered after both streams' producers."""
+        if self.on_params_ready is None:
+            return
+        if self.side is None:
             self.on_params_ready(names)
+            return
+        self.side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.side):
+            self.on_params_ready(names)
+
+    def _wgrad(self, fn):
+        """Enqueue a weight-gradient launch on the side stream (after the main stream's
+        work so far, which produced its inputs)."""
+        if self.side is None:
+            fn()
+            return
+        self.side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.side):
+            fn()
 
     def _fin_fwd(self, bn: BNState, P: int, train: bool):
         if train:
@@ -263,7 +290,7 @@ class MobileNetV2Executor:
     # ------------------------------------------------------------------ backward
     def backward(self):
         f, B, S = self.flat, self.B, self.S
-        ws, wg = self.ws_part, self.ws_wgrad
+        ws, wg, wgm = self.ws_part, self.ws_wgrad, self.ws_wgrad_main
         # transposed 1x1 weights for the dgrad GEMMs (one batched launch)
         K.wt_transpose(f.shadow, f.shadow_t, self.wt_tab, self.wt_n)
         self._ready([self.w_lin, self.b_lin])
@@ -278,8 +305,8 @@ class MobileNetV2Executor:
                   self.C_last, A2=bnl.y, pa=bnl.a, pb=bnl.b, pc=bnl.c, Yt=last_blk.bn_p.y, R=None)
         P_g = K.pw_num_partials(Mf, self.C_last_in, self.C_last)
         last_blk.bn_p.finalize_bwd(ws, P_g)
-        K.pw_wgrad(bnl.g, bnl.y, bnl.a, bnl.b, bnl.c, last_blk.o, None, None, K.ACT_NONE, wg,
-                   f.g(self.w_last), Mf, self.C_last, self.C_last_in)
+        self._wgrad(lambda: K.pw_wgrad(bnl.g, bnl.y, bnl.a, bnl.b, bnl.c, last_blk.o, None, None, K.ACT_NONE,
+                                       wg, f.g(self.w_last), Mf, self.C_last, self.C_last_in))
         self._ready([self.w_last] + last_blk.bn_p.param_names)
 
         for bi in range(len(self.blocks) - 1, -1, -1):
@@ -292,7 +319,7 @@ class MobileNetV2Executor:
             # project dgrad -> g_d (relu6 mask of BN_d) + BN_d partials
             if K.pw_bwd_supported(Mout, bp.cout, bp.hidden):
                 # fused dgrad + wgrad (x = relu6(BN_d(y_d)) rebuilt from the mask operand)
-                K.pw_bwd(K.EPI_BWD_RELU6, bp.G, bnp.y, bnp.a, bnp.b, bnp.c, f.bt(bp.w_p), bnd.g, bnd.y, ws, wg,
+                K.pw_bwd(K.EPI_BWD_RELU6, bp.G, bnp.y, bnp.a, bnp.b, bnp.c, f.bt(bp.w_p), bnd.g, bnd.y, ws, wgm,
                          f.g(bp.w_p), Mout, bp.cout, bp.hidden, es=bnd.scale, et=bnd.shift)
                 bnd.finalize_bwd(ws, K.pw_bwd_num_partials(Mout, bp.cout, bp.hidden))
             else:
@@ -300,16 +327,16 @@ class MobileNetV2Executor:
                           A2=bnp.y, pa=bnp.a, pb=bnp.b, pc=bnp.c, Yt=bnd.y, es=bnd.scale, et=bnd.shift)
                 bnd.finalize_bwd(ws, K.pw_num_partials(Mout, bp.hidden, bp.cout))
                 # project wgrad
-                K.pw_wgrad(bp.G, bnp.y, bnp.a, bnp.b, bnp.c, bnd.y, bnd.scale, bnd.shift, K.ACT_BN_RELU6, wg,
-                           f.g(bp.w_p), Mout, bp.cout, bp.hidden)
+                self._wgrad(lambda: K.pw_wgrad(bp.G, bnp.y, bnp.a, bnp.b, bnp.c, bnd.y, bnd.scale, bnd.shift,
+                                               K.ACT_BN_RELU6, wg, f.g(bp.w_p), Mout, bp.cout, bp.hidden))
             self._ready([bp.w_p] + bnd.param_names)
             # depthwise: input BN is BN_e (expand) or the stem BN0 (t=1 block)
             dw_in = bp.bn_e if bp.expand else self.bn0
             K.dw_dgrad(bnd.g, bnd.y, bnd.coef, f.b(bp.w_d), dw_in.y, dw_in.scale, dw_in.shift, dw_in.g, ws,
                        B, Hin, Hin, bp.hidden, bp.stride)
             dw_in.finalize_bwd(ws, K.dw_num_partials("dgrad", B, Hin, Hin, bp.hidden, bp.stride))
-            K.dw_wgrad(bnd.g, bnd.y, bnd.coef, dw_in.y, dw_in.scale, dw_in.shift, wg, f.g(bp.w_d),
-                       B, Hin, Hin, bp.hidden, bp.stride)
+            self._wgrad(lambda: K.dw_wgrad(bnd.g, bnd.y, bnd.coef, dw_in.y, dw_in.scale, dw_in.shift, wg,
+                                           f.g(bp.w_d), B, Hin, Hin, bp.hidden, bp.stride))
             self._ready([bp.w_d] + dw_in.param_names)
             if bp.expand:
                 bne = bp.bn_e
@@ -317,7 +344,7 @@ class MobileNetV2Executor:
                 # expand dgrad -> gradient w.r.t. the block input o_prev (+ skip gradient)
                 if K.pw_bwd_supported(Min, bp.hidden, bp.cin):
                     K.pw_bwd(K.EPI_BWD_LIN, bne.g, bne.y, bne.a, bne.b, bne.c, f.bt(bp.w_e), prev.G, prev.bn_p.y,
-                             ws, wg, f.g(bp.w_e), Min, bp.hidden, bp.cin, R=bp.G if bp.residual else None,
+                             ws, wgm, f.g(bp.w_e), Min, bp.hidden, bp.cin, R=bp.G if bp.residual else None,
                              X=prev.o)
                     prev.bn_p.finalize_bwd(ws, K.pw_bwd_num_partials(Min, bp.hidden, bp.cin))
                 else:
@@ -325,14 +352,17 @@ class MobileNetV2Executor:
                               A2=bne.y, pa=bne.a, pb=bne.b, pc=bne.c, Yt=prev.bn_p.y,
                               R=bp.G if bp.residual else None)
                     prev.bn_p.finalize_bwd(ws, K.pw_num_partials(Min, bp.cin, bp.hidden))
-                    K.pw_wgrad(bne.g, bne.y, bne.a, bne.b, bne.c, prev.o, None, None, K.ACT_NONE, wg,
-                               f.g(bp.w_e), Min, bp.hidden, bp.cin)
+                    self._wgrad(lambda: K.pw_wgrad(bne.g, bne.y, bne.a, bne.b, bne.c, prev.o, None, None,
+                                                   K.ACT_NONE, wg, f.g(bp.w_e), Min, bp.hidden, bp.cin))
                 self._ready([bp.w_e] + prev.bn_p.param_names)
             else:
                 # t=1 block: its input is relu6(BN0(stem)) -> stem weight gradient
                 bn0 = self.bn0
-                K.stem_wgrad(bn0.g, bn0.y, bn0.a, bn0.b, bn0.c, self.img, wg, f.g(self.stem_w), B, S, S, 32)
+                self._wgrad(lambda: K.stem_wgrad(bn0.g, bn0.y, bn0.a, bn0.b, bn0.c, self.img, wg,
+                                                 f.g(self.stem_w), B, S, S, 32))
                 self._ready([self.stem_w])
+        if self.side is not None:   # join: the optimizer (main stream) needs every gradient
+            torch.cuda.current_stream(self.device).wait_stream(self.side)
 
     # ------------------------------------------------------------------ eval
     def eval_prepare(self):

@@ -47,9 +47,15 @@ BF16, F32 = torch.bfloat16, torch.float32
 
 
 # --------------------------------------------------------------------------- BN
+def register_side_stream(stream):
+    """Reductions launched on ``stream`` get their own arrival counters (they may run
+    concurrently with reductions on the main stream)."""
+    lib().register_side_stream(stream.cuda_stream)
+
+
 def bn_part_floats(P, C):
     """Workspace a BN finalize over P partial rows needs ([P][2][C] + level-1 fold scratch)."""
-    return (P + lib().colsum_rows(P)) * 2 * C
+    return lib().bn_part_floats(P, C)
 
 
 def bn_fwd_finalize(part, P, C, count, gamma, beta, eps, momentum, rmean, rvar, nbt, mean, rstd,

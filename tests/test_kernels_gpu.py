@@ -45,11 +45,40 @@ def tapmajor(w):
     return w.reshape(w.shape[0], 9).t().contiguous()
 
 
+def bn_ws(part, P, C):
+    """[P][2][C] partials padded to the workspace a BN finalize needs (level-1 scratch)."""
+    flat = part.reshape(-1)
+    extra = K.bn_part_floats(P, C) - flat.numel()
+    return torch.cat([flat, torch.zeros(max(extra, 0), device=flat.device)]).contiguous()
+
+
 def sum_parts(part, P, C, nv=2):
     return part[: P * nv * C].view(P, nv, C).sum(0)
 
 
 # ----------------------------------------------------------------------------- BN
+@pytest.mark.parametrize("P,C", [(40, 24), (700, 96), (10752, 32), (3001, 1280)])
+def test_bn_reduce_two_level(dev, P, C):
+    """Single-launch two-level reduction (last-workgroup hand-off), repeated launches with
+    different data and uneven row counts: every launch must match an fp64 reference exactly
+    enough and re-arm its counters."""
+    gamma, beta = bn_params(C, dev, 3)
+    for it in range(6):
+        part = rnd(P, 2, C, dev=dev, seed=100 + it) + 1.0
+        part[:, 1] = part[:, 1].abs() * 3 + 5
+        ws = bn_ws(part, P, C)
+        mean, rstd, scale, shift = [torch.empty(C, device=dev) for _ in range(4)]
+        K.bn_fwd_finalize(ws, P, C, 1e6, gamma, beta, 1e-5, 0.1, None, None, None, mean, rstd, scale, shift)
+        s = part.double().sum(0)
+        m_ref = s[0] / 1e6
+        assert torch.allclose(mean.double(), m_ref, rtol=1e-5, atol=1e-7)
+        coef = torch.empty(3, C, device=dev)
+        dg, db = torch.empty(C, device=dev), torch.empty(C, device=dev)
+        K.bn_bwd_finalize(ws, P, C, 1e6, mean, rstd, gamma, coef, dg, db)
+        assert torch.allclose(db.double(), s[0], rtol=1e-5, atol=1e-3)
+    torch.cuda.synchronize()
+
+
 def test_bn_finalize_and_apply(dev):
     M, C = 5000, 96
     y = bf(rnd(M, C, dev=dev) * 2 + 0.3)
@@ -60,7 +89,7 @@ def test_bn_finalize_and_apply(dev):
     rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
     nbt = torch.zeros(1, dtype=torch.int64, device=dev)
     mean, rstd, scale, shift = [torch.empty(C, device=dev) for _ in range(4)]
-    K.bn_fwd_finalize(part, P, C, M, gamma, beta, 1e-5, 0.1, rm, rv, nbt, mean, rstd, scale, shift)
+    K.bn_fwd_finalize(bn_ws(part, P, C), P, C, M, gamma, beta, 1e-5, 0.1, rm, rv, nbt, mean, rstd, scale, shift)
     ref = torch.nn.BatchNorm2d(C).to(dev)
     with torch.no_grad():
         ref.weight.copy_(gamma)
@@ -93,7 +122,7 @@ def test_bn_bwd_finalize_matches_autograd(dev):
     part = torch.stack([g.sum(0), (g * y).sum(0)]).unsqueeze(0).contiguous()
     coef = torch.empty(3, C, device=dev)
     dgam, dbet = torch.empty(C, device=dev), torch.empty(C, device=dev)
-    K.bn_bwd_finalize(part, 1, C, M, mean.contiguous(), rstd.contiguous(), gamma, coef, dgam, dbet)
+    K.bn_bwd_finalize(bn_ws(part, 1, C), 1, C, M, mean.contiguous(), rstd.contiguous(), gamma, coef, dgam, dbet)
     dy = coef[0] * g + coef[1] * y + coef[2]
     assert rel(dy, yy.grad) < 1e-4
     assert rel(dgam, ga.grad) < 1e-4
