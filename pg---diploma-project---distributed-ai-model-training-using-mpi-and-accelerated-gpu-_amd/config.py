@@ -60,7 +60,9 @@ class TrainConfig:
     log_format: str = "serial"                # serial | ddp (reference line formats)
     max_steps_per_epoch: Optional[int] = None
     eval_every: int = 1
-    profile: bool = False
+    profile: bool = False                     # roctx ranges + per-step HIP-event timing summary per epoch
+    watchdog_s: float = 0.0                   # >0: abort a rank that makes no progress for this long (s)
+    dist_timeout_s: float = 1800.0            # collective timeout (init_process_group)
 
     def replace(self, **kw) -> "TrainConfig":
         return dataclasses.replace(self, **kw)

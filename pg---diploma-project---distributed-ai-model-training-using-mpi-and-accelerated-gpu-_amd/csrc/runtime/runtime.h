@@ -1,10 +1,16 @@
 // Host-side native runtime pieces of pgdist (C++17, no torch dependency).
+//
+// core.h holds the plain C++ implementations (also built standalone, with
+// AddressSanitizer / ThreadSanitizer, by tests/test_native_sanitizers.py);
+// this header adds the Python (pybind11) entry points.
 #pragma once
 #include <pybind11/pybind11.h>
 #include <pybind11/numpy.h>
 #include <pybind11/stl.h>
 #include <string>
 #include <vector>
+
+#include "core.h"
 
 namespace pgdist_rt {
 namespace py = pybind11;

@@ -34,7 +34,9 @@ from ..models import build_model
 from ..parallel.bootstrap import init_distributed, barrier
 from ..parallel.ddp import BucketedGradReducer, broadcast_parameters, all_reduce_scalars
 from ..parallel.sampler import ShardSampler
+from ..parallel.watchdog import Watchdog
 from ..utils import logging as L
+from ..utils.profiling import StepTimer, trace_range
 from . import checkpoint as ckpt
 from .flat import FlatParams
 
@@ -47,8 +49,19 @@ def step_lr(base_lr: float, epoch: int, step_size: int, gamma: float) -> float:
 class Trainer:
     def __init__(self, cfg: TrainConfig, info=None):
         self.cfg = cfg
-        self.info, self.device, self.dist_backend = init_distributed(cfg.dist_backend, cfg.device, info=info)
+        self.info, self.device, self.dist_backend = init_distributed(cfg.dist_backend, cfg.device, info=info,
+                                                                     timeout_s=cfg.dist_timeout_s)
         self.rank, self.world = self.info.rank, self.info.world_size
+        self.watchdog = None
+        if cfg.watchdog_s and cfg.watchdog_s > 0:
+            store = None
+            try:
+                from torch.distributed import distributed_c10d as c10d
+                store = c10d._get_default_store() if self.world > 1 else None
+            except Exception:
+                store = None
+            self.watchdog = Watchdog(cfg.watchdog_s, self.rank, self.world, store=store).start()
+        self.timer = None
         backend = cfg.backend
         if backend == "auto":
             backend = "hip" if self.device.type == "cuda" else "torch"
@@ -170,14 +183,25 @@ class Trainer:
         nb = math.ceil(len(idx) / bs)
         if self.cfg.max_steps_per_epoch:
             nb = min(nb, self.cfg.max_steps_per_epoch)
+        prof = self.cfg.profile
+        self.timer = StepTimer(bs * self.world, warmup=2 if epoch == self.start_epoch else 0,
+                               device=self.device) if prof else None
         if self.backend == "hip":
             didx = torch.from_numpy(idx).to(self.device)
             self.step.metrics.zero_()
-            for b in range(nb):
-                sl = didx[b * bs:(b + 1) * bs]
-                st = self.step if sl.numel() == bs else self._tail(sl.numel())
-                st.run(sl)
-            return self.step.read_metrics()
+            with trace_range(f"train_epoch_{epoch}", prof):
+                for b in range(nb):
+                    sl = didx[b * bs:(b + 1) * bs]
+                    st = self.step if sl.numel() == bs else self._tail(sl.numel())
+                    if self.timer is not None and sl.numel() == bs:
+                        self.timer.start()
+                        st.run(sl)
+                        self.timer.stop()
+                    else:
+                        st.run(sl)
+                    if self.watchdog is not None:
+                        self.watchdog.kick(phase=f"train epoch {epoch} batch {b}")
+                return self.step.read_metrics()
         self.model.train()
         loss_sum, correct, count = 0.0, 0, 0
         for b in range(nb):
@@ -194,6 +218,8 @@ class Trainer:
                 self.reducer.finish()
                 self.flat.grad.mul_(1.0 / self.world)
             self.opt.step()
+            if self.watchdog is not None:
+                self.watchdog.kick(phase=f"train epoch {epoch} batch {b}")
             loss_sum += loss.item() * y.numel()
             correct += int((out.argmax(1) == y).sum().item())
             count += y.numel()
@@ -267,6 +293,13 @@ class Trainer:
             else:
                 L.emit(L.serial_epoch_line(epoch + 1, cfg.epochs, dt, train_loss, train_acc_local, test_loss,
                                            test_acc_local), self.rank)
+            if self.timer is not None:
+                t = self.timer.summary()
+                if t.get("steps"):
+                    L.emit(f"[pgdist] epoch {epoch + 1} step {t['mean_ms']:.2f} ms (p50 {t['p50_ms']:.2f}, "
+                           f"p90 {t['p90_ms']:.2f}) -> {t['img_per_s']:.0f} img/s (train steps only)", self.rank)
+            if self.watchdog is not None:
+                self.watchdog.kick(phase=f"epoch {epoch + 1} done")
             if cfg.global_accuracy and self.world > 1:
                 L.emit(f"[pgdist] epoch {epoch + 1} global test acc {test_acc_global:.4f} "
                        f"train img/s {g_tn / dt:.1f}", self.rank)
@@ -289,6 +322,8 @@ class Trainer:
             ckpt.save_best(self.best_state, save_path)
             L.emit(L.saved_line(save_path), self.rank)
         self.history = history
+        if self.watchdog is not None:
+            self.watchdog.stop()
         return history
 
     # ------------------------------------------------------------------ checkpoint/resume
