@@ -47,7 +47,10 @@ def main():
     ap.add_argument("--batch-size", type=int, default=128)
     ap.add_argument("--model", default="mobilenet_v2")
     ap.add_argument("--backend", default="auto", help="hip (native kernels) | torch (MIOpen/PyTorch ops)")
-    ap.add_argument("--graph", type=int, default=1)
+    ap.add_argument("--graph", type=int, default=0,
+                    help="capture the step in a hipGraph (1) or launch eagerly (0, default: measured faster "
+                         "with the weight-gradient side stream, whose branches the graph replay serialises)")
+    ap.add_argument("--side-stream", type=int, default=1, help="weight gradients on a second HIP stream")
     ap.add_argument("--img-size", type=int, default=224)
     args = ap.parse_args()
 
@@ -58,7 +61,7 @@ def main():
 
     from pgdist.engine.bench_step import build_bench_step
     step_fn, meta = build_bench_step(args.model, args.batch_size, device, backend=args.backend,
-                                     img_size=args.img_size, use_graph=bool(args.graph),
+                                     img_size=args.img_size, use_graph=bool(args.graph), side_stream=bool(args.side_stream),
                                      world_size=world, rank=info.rank)
 
     def sync():
@@ -101,7 +104,7 @@ def main():
             "config": {"model": args.model, "global_batch": args.batch_size * world,
                        "per_gpu_batch": args.batch_size, "seq_len": None, "img_size": args.img_size,
                        "parallelism": f"dp{world}", "backend": meta.get("backend"),
-                       "hip_graph": meta.get("graph")},
+                       "hip_graph": meta.get("graph"), "side_stream": meta.get("side_stream")},
         }
         print(json.dumps(out), flush=True)
     cleanup()

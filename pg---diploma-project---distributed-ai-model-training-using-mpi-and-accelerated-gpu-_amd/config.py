@@ -44,7 +44,7 @@ class TrainConfig:
     backend: str = "auto"                     # auto (hip on GPU, torch on CPU) | hip | torch
     precision: str = "bf16"                   # bf16 | fp32 (torch backend only)
     seed: Optional[int] = 42
-    graph: bool = True                        # capture the train step in a hipGraph (hip backend)
+    graph: bool = False                       # hipGraph capture of the step (hip backend; eager + side stream measured faster)
     deterministic: bool = False
     # distributed
     dist_backend: str = "auto"                # auto (nccl on GPU = RCCL, gloo on CPU)

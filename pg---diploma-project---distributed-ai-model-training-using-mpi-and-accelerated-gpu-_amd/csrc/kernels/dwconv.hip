@@ -288,6 +288,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(
         for (int c = 0; c < 3; ++c)
           load_dy4(gin, yself, g.Ho, g.Wo, g.C, tl.b, tl.r0 - 1 + r, iw - 1 + c, c0, al, be, ga, win[r][c]);
       Raw3 ng, ny;   // next dy row (raw g and y), prefetched one row ahead
+      uint2 ypn = ldg8(yprev + (((size_t)tl.b * g.H + tl.r0) * g.W + iw) * g.C + c0);   // yprev, one row ahead
       for (int ih = tl.r0; ih < ih_end; ++ih) {
         if (ih > tl.r0) {
 #pragma unroll
@@ -308,9 +309,11 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(
             for (int k = 0; k < CPT; ++k) win[2][c][k] = ok ? fmaf(al[k], gv[k], fmaf(be[k], yv[k], ga[k])) : 0.f;
           }
         }
+        const uint2 ypc = ypn;
         if (ih + 1 < ih_end) {
           load_raw3(ng, gin, g.Ho, g.Wo, g.C, tl.b, ih + 2, iw - 1, c0);
           load_raw3(ny, yself, g.Ho, g.Wo, g.C, tl.b, ih + 2, iw - 1, c0);
+          ypn = ldg8(yprev + (((size_t)tl.b * g.H + ih + 1) * g.W + iw) * g.C + c0);
         }
         float acc[CPT];
         zero4(acc);
@@ -323,7 +326,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(
             for (int k = 0; k < CPT; ++k) acc[k] = fmaf(win[2 - dh][2 - dw][k], wt[dh * 3 + dw][k], acc[k]);
         const size_t off = (((size_t)tl.b * g.H + ih) * g.W + iw) * g.C + c0;
         float yp[CPT];
-        unpack4(ldg8(yprev + off), yp);
+        unpack4(ypc, yp);
 #pragma unroll
         for (int k = 0; k < CPT; ++k) acc[k] *= relu6_mask(yp[k], s[k], t[k]);
         const uint2 packed = pack4(acc);
@@ -351,17 +354,52 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(
           wA[r][k] = odd_w ? wt[r * 3 + 0][k] : wt[r * 3 + 1][k];
           wB[r][k] = odd_w ? wt[r * 3 + 2][k] : 0.f;
         }
-      // tiles start at even rows (R even)
+      // tiles start at even rows (R even).  Everything one iteration (2 input rows) ahead:
+      // raw dy (g, y) of the next dy row and the yprev rows of the next iteration.
+      auto ld_raw = [&](uint2 &dst, const bf16_t *src, int H_, int W_, int r, int c) {
+        dst = (r >= 0 && r < H_ && c >= 0 && c < W_) ? ldg8(src + (((size_t)tl.b * H_ + r) * W_ + c) * g.C + c0)
+                                                     : make_uint2(0, 0);
+      };
+      auto dy_of = [&](const uint2 &gg, const uint2 &yy, int r, int c, float (&v)[CPT]) {
+        const bool ok = r >= 0 && r < g.Ho && c >= 0 && c < g.Wo;
+        float gv[CPT], yv[CPT];
+        unpack4(gg, gv);
+        unpack4(yy, yv);
+#pragma unroll
+        for (int k = 0; k < CPT; ++k) v[k] = ok ? fmaf(al[k], gv[k], fmaf(be[k], yv[k], ga[k])) : 0.f;
+      };
       float cur[2][CPT], nxt[2][CPT];   // dy row o / o+1 at columns A, B
+      uint2 rgA, ryA, rgB, ryB;         // raw dy row o+1 (columns A, B)
+      uint2 yp0r, yp1r;                 // raw yprev rows of the current iteration
       int o = tl.r0 >> 1;
-      load_dy4(gin, yself, g.Ho, g.Wo, g.C, tl.b, o, owA, c0, al, be, ga, cur[0]);
-      if (odd_w) load_dy4(gin, yself, g.Ho, g.Wo, g.C, tl.b, o, owB, c0, al, be, ga, cur[1]);
-      else zero4(cur[1]);
+      {
+        uint2 gA, yA, gB, yB;
+        ld_raw(gA, gin, g.Ho, g.Wo, o, owA);
+        ld_raw(yA, yself, g.Ho, g.Wo, o, owA);
+        ld_raw(gB, gin, g.Ho, g.Wo, o, odd_w ? owB : -1);
+        ld_raw(yB, yself, g.Ho, g.Wo, o, odd_w ? owB : -1);
+        dy_of(gA, yA, o, owA, cur[0]);
+        dy_of(gB, yB, o, odd_w ? owB : -1, cur[1]);
+      }
+      ld_raw(rgA, gin, g.Ho, g.Wo, o + 1, owA);
+      ld_raw(ryA, yself, g.Ho, g.Wo, o + 1, owA);
+      ld_raw(rgB, gin, g.Ho, g.Wo, o + 1, odd_w ? owB : -1);
+      ld_raw(ryB, yself, g.Ho, g.Wo, o + 1, odd_w ? owB : -1);
+      ld_raw(yp0r, yprev, g.H, g.W, tl.r0, iw);
+      ld_raw(yp1r, yprev, g.H, g.W, tl.r0 + 1 < ih_end ? tl.r0 + 1 : -1, iw);
       for (int ih = tl.r0; ih < ih_end; ih += 2) {
         o = ih >> 1;
-        load_dy4(gin, yself, g.Ho, g.Wo, g.C, tl.b, o + 1, owA, c0, al, be, ga, nxt[0]);
-        if (odd_w) load_dy4(gin, yself, g.Ho, g.Wo, g.C, tl.b, o + 1, owB, c0, al, be, ga, nxt[1]);
-        else zero4(nxt[1]);
+        dy_of(rgA, ryA, o + 1, owA, nxt[0]);
+        dy_of(rgB, ryB, o + 1, odd_w ? owB : -1, nxt[1]);
+        const uint2 ypc[2] = {yp0r, yp1r};
+        if (ih + 2 < ih_end) {   // next iteration's operands, in flight during this one's FMAs
+          ld_raw(rgA, gin, g.Ho, g.Wo, o + 2, owA);
+          ld_raw(ryA, yself, g.Ho, g.Wo, o + 2, owA);
+          ld_raw(rgB, gin, g.Ho, g.Wo, o + 2, odd_w ? owB : -1);
+          ld_raw(ryB, yself, g.Ho, g.Wo, o + 2, odd_w ? owB : -1);
+          ld_raw(yp0r, yprev, g.H, g.W, ih + 2, iw);
+          ld_raw(yp1r, yprev, g.H, g.W, ih + 3 < ih_end ? ih + 3 : -1, iw);
+        }
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
           const int r = ih + half;
@@ -381,7 +419,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(
           }
           const size_t off = (((size_t)tl.b * g.H + r) * g.W + iw) * g.C + c0;
           float yp[CPT];
-          unpack4(ldg8(yprev + off), yp);
+          unpack4(ypc[half], yp);
 #pragma unroll
           for (int k = 0; k < CPT; ++k) acc[k] *= relu6_mask(yp[k], s[k], t[k]);
           const uint2 packed = pack4(acc);
