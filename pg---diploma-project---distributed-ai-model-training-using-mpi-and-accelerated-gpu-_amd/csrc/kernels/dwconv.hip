@@ -13,7 +13,7 @@
 //    lanes of a wave (channel-fastest, then column) read one contiguous run of
 //    pixels per load instruction (the neighbours' halo columns hit the same lines);
 //  * a workgroup = a tile of TWc columns x R rows of one image and a slab of
-//    CC <= 64 channels (blockIdx.y): small per-workgroup partial rows, long
+//    CC <= 64 channels (one slab per workgroup): small per-workgroup partial rows, long
 //    streams; ~100 VGPRs;
 //  * weights are tap-major [9][C] in the flat parameter buffer (one 8-B load per
 //    tap and 4 channels);
@@ -31,7 +31,7 @@ constexpr int kRows = 8;      // output rows per strip
 
 struct DwGeom {
   int B, H, W, C, Ho, Wo;
-  int CC;     // channels per workgroup (blockIdx.y selects the slab)
+  int CC;     // channels per workgroup (tile_of() decodes the slab)
   int TWc;    // columns per workgroup
   int R;      // rows per workgroup
   int tiles_w, tiles_h;
@@ -114,22 +114,40 @@ PG_DEVICE void act3(const Raw3 &r, int ih, int H, int iw0, int W, const float (&
   }
 }
 
-// tile decode: blockIdx.x -> (b, row block, column block)
+// Workgroup decode.  The 1-D grid enumerates (tile, channel slab) pairs so that the slabs
+// of one spatial tile are 8 workgroup ids apart: same XCD (ids are dealt to the 8 XCDs
+// round-robin) and dispatched together, so the 128-B lines shared by neighbouring slabs
+// (a pixel's C channels are contiguous in NHWC) are fetched from HBM once into that L2.
 struct Tile {
   int b, r0, w0;
+  int idx;     // tile index (partial row)
+  int slab;    // channel slab
 };
 PG_DEVICE Tile tile_of(const DwGeom &g) {
-  const int tw = blockIdx.x % g.tiles_w;
-  const int rest = blockIdx.x / g.tiles_w;
+  const int L = blockIdx.x;
+  const int nslab = g.C / g.CC;
+  const int ntiles = g.B * g.tiles_h * g.tiles_w;
+  const int full = (ntiles / 8) * 8 * nslab;
+  int t, sl;
+  if (L < full) {
+    t = (L / (8 * nslab)) * 8 + L % 8;
+    sl = (L / 8) % nslab;
+  } else {
+    const int rem = ntiles % 8, Lr = L - full;
+    t = (ntiles / 8) * 8 + Lr % rem;
+    sl = Lr / rem;
+  }
+  const int tw = t % g.tiles_w;
+  const int rest = t / g.tiles_w;
   const int th = rest % g.tiles_h;
-  return Tile{rest / g.tiles_h, th * g.R, tw * g.TWc};
+  return Tile{rest / g.tiles_h, th * g.R, tw * g.TWc, t, sl};
 }
 
 // Block-level reduction of per-thread [NV][CPT] channel partials of this workgroup's CC
-// channels into part[blockIdx.x][NV][C] (columns cbase..cbase+CC); tid = col * C4 + c4.
+// channels into part[prow][NV][C] (columns cbase..cbase+CC); tid = col * C4 + c4.
 template <int NV>
 PG_DEVICE void block_channel_partials(float (&acc)[NV][CPT], float *__restrict__ part, int C, int CC,
-                                      int cbase, int ncol, float *lds) {
+                                      int cbase, int ncol, float *lds, int prow) {
   const int tid = threadIdx.x;
   const int C4 = CC / CPT;
   const int c4 = tid % C4, col = tid / C4;
@@ -140,7 +158,7 @@ PG_DEVICE void block_channel_partials(float (&acc)[NV][CPT], float *__restrict__
     for (int c = tid; c < CC; c += blockDim.x) {
       float s = 0.f;
       for (int w = 0; w < ncol; ++w) s += lds[w * CC + c];
-      part[((size_t)blockIdx.x * NV + v) * C + cbase + c] = s;
+      part[((size_t)prow * NV + v) * C + cbase + c] = s;
     }
     __syncthreads();
   }
@@ -159,9 +177,9 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(
   const int C4 = g.CC / CPT;
   const int tid = threadIdx.x;
   const int c4 = tid % C4, col = tid / C4;
-  const int cbase = blockIdx.y * g.CC;
-  const int c0 = cbase + c4 * CPT;
   const Tile tl = tile_of(g);
+  const int cbase = tl.slab * g.CC;
+  const int c0 = cbase + c4 * CPT;
   const int ow = tl.w0 + col;
   const bool active = col < g.TWc && ow < g.Wo;
 
@@ -241,7 +259,7 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(
       }
     }
   }
-  block_channel_partials<2>(stats, part, g.C, g.CC, cbase, g.TWc, red);
+  block_channel_partials<2>(stats, part, g.C, g.CC, cbase, g.TWc, red, tl.idx);
 }
 
 // ---------------------------------------------------------------------------
@@ -257,9 +275,10 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(
   const int C4 = g.CC / CPT;
   const int tid = threadIdx.x;
   const int c4 = tid % C4, col = tid / C4;
-  const int cbase = blockIdx.y * g.CC;
+  const Tile tl = tile_of(g);
+  const int cbase = tl.slab * g.CC;
   const int c0 = cbase + c4 * CPT;
-  const Tile tl = tile_of(g);        // tiles over the INPUT grid (H x W)
+  // tiles over the INPUT grid (H x W)
   const int iw = tl.w0 + col;
   const bool active = col < g.TWc && iw < g.W;
 
@@ -440,7 +459,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(
       }
     }
   }
-  block_channel_partials<2>(stats, part, g.C, g.CC, cbase, g.TWc, red);
+  block_channel_partials<2>(stats, part, g.C, g.CC, cbase, g.TWc, red, tl.idx);
 }
 
 // ---------------------------------------------------------------------------
@@ -456,9 +475,9 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(
   const int C4 = g.CC / CPT;
   const int tid = threadIdx.x;
   const int c4 = tid % C4, col = tid / C4;
-  const int cbase = blockIdx.y * g.CC;
-  const int c0 = cbase + c4 * CPT;
   const Tile tl = tile_of(g);
+  const int cbase = tl.slab * g.CC;
+  const int c0 = cbase + c4 * CPT;
   const int ow = tl.w0 + col;
   const bool active = col < g.TWc && ow < g.Wo;
 
@@ -542,7 +561,7 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(
           for (int k = 0; k < CPT; ++k) accw[r * 3 + dw][k] = fmaf(dy[k], win[r][dw][k], accw[r * 3 + dw][k]);
     }
   }
-  block_channel_partials<9>(accw, part, g.C, g.CC, cbase, g.TWc, lds);
+  block_channel_partials<9>(accw, part, g.C, g.CC, cbase, g.TWc, lds, tl.idx);
 }
 
 // ---------------------------------------------------------------------------
@@ -592,7 +611,7 @@ int dw_wgrad_num_partials(int B, int H, int W, int C, int stride) { return dw_gr
 void launch_dw_fwd(const bf16_t *x, const float *in_s, const float *in_t, int act, const bf16_t *w,
                    bf16_t *y, float *part, int B, int H, int W, int C, int stride, hipStream_t st) {
   const DwGeom g = dw_geom(0, B, H, W, C, stride);
-  dim3 grid(dw_grid_x(g), C / g.CC), block(dw_threads(g));
+  dim3 grid(dw_grid_x(g) * (C / g.CC)), block(dw_threads(g));
   if (stride == 1) {
     if (act == ACT_BN_RELU6) hipLaunchKernelGGL((dw_fwd_kernel<1, ACT_BN_RELU6>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
     else hipLaunchKernelGGL((dw_fwd_kernel<1, ACT_NONE>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
@@ -606,7 +625,7 @@ void launch_dw_dgrad(const bf16_t *gin, const bf16_t *yself, const float *coef, 
                      const bf16_t *yprev, const float *ps, const float *pt, bf16_t *gout,
                      float *part, int B, int H, int W, int C, int stride, hipStream_t st) {
   const DwGeom g = dw_geom(1, B, H, W, C, stride);
-  dim3 grid(dw_grid_x(g), C / g.CC), block(dw_threads(g));
+  dim3 grid(dw_grid_x(g) * (C / g.CC)), block(dw_threads(g));
   if (stride == 1)
     hipLaunchKernelGGL((dw_dgrad_kernel<1>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g);
   else
@@ -620,7 +639,7 @@ void launch_dw_wgrad(const bf16_t *gin, const bf16_t *yself, const float *coef, 
                      int C, int stride, hipStream_t st) {
   const DwGeom g = dw_geom(2, B, H, W, C, stride);
   const int P = dw_grid_x(g);
-  dim3 grid(P, C / g.CC), block(dw_threads(g));
+  dim3 grid(P * (C / g.CC)), block(dw_threads(g));
   if (stride == 1)
     hipLaunchKernelGGL((dw_wgrad_kernel<1>), grid, block, 0, st, gin, yself, coef, yprev, ps, pt, part, g);
   else
