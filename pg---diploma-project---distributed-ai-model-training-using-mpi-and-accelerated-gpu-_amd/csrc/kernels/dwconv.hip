@@ -24,10 +24,12 @@
 //    deterministic two-level column sum.
 #include "../common.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int CPT = 4;        // channels per thread
-constexpr int kRows = 8;      // output rows per strip
+constexpr int kRows = 28;     // rows per strip (swept 4..112 on MI355X: 28 fastest end to end)
 
 struct DwGeom {
   int B, H, W, C, Ho, Wo;
@@ -590,8 +592,17 @@ DwGeom dw_geom(int kind, int B, int H, int W, int C, int stride) {
   int twc = 256 / C4;
   if (twc > gw) twc = gw;
   g.TWc = twc;
-  int R = kRows;
-  if (kind == 2) R = 2 * kRows;                 // weight gradient: longer strips, fewer partial rows
+  static const int env_rows = [] {
+    const char *e = getenv("PGDIST_DW_ROWS");
+    return e ? atoi(e) : 0;
+  }();
+  static const int env_wrows = [] {
+    const char *e = getenv("PGDIST_DW_WROWS");
+    return e ? atoi(e) : 0;
+  }();
+  int R = env_rows > 0 ? env_rows : kRows;
+  if (kind == 2) R = env_wrows > 0 ? env_wrows : kRows;
+  // (PGDIST_DW_ROWS / PGDIST_DW_WROWS override the strip length for tuning experiments)
   if (kind == 1 && stride == 2 && (R & 1)) ++R;  // dgrad s2 tiles start on even input rows
   if (R > gh) R = (kind == 1 && stride == 2) ? ((gh + 1) & ~1) : gh;
   g.R = R;

@@ -25,6 +25,8 @@
 //     [gridDim.x][Kg][Ng] (deterministic fixed-order reduction afterwards).
 #include "../common.h"
 
+#include <cstdlib>
+
 enum { EPI_BWD_RELU6_ = 1, EPI_BWD_LIN_ = 2 };   // same values as pwconv.hip
 
 namespace {
@@ -374,7 +376,8 @@ BwdGeom bwd_geom(int M, int Kg, int Ng) {
   g.ok = M >= 65536 && g.KP <= 192 && Kg % 8 == 0 && Ng % 8 == 0 && Kg > 0 && Ng > 0;
   g.nt = (Ng + g.BN - 1) / g.BN;
   const int nmt = (M + g.BM - 1) / g.BM;
-  int gx = 512 / g.nt;
+  static const int env_wgs = [] { const char *e = getenv("PGDIST_PWB_WGS"); return e ? atoi(e) : 0; }();
+  int gx = (env_wgs > 0 ? env_wgs : 512) / g.nt;
   if (gx > nmt) gx = nmt;
   gx = (gx + 7) & ~7;
   if (gx < 8) gx = 8;

@@ -35,6 +35,8 @@
 // m packed per ds_write_b64) so both fragments are plain ds_read_b128.
 #include "../common.h"
 
+#include <cstdlib>
+
 enum { PRO_BNBWD = 3, IM2COL_STEM = 4 };
 enum { EPI_FWD = 0, EPI_BWD_RELU6 = 1, EPI_BWD_LIN = 2 };
 
@@ -581,7 +583,9 @@ static PwGeom pw_geom(int M, int N, int K, int pro) {
   g.nt = (N + g.BN - 1) / g.BN;
   const int BM = 128 / g.KS;
   g.nmt = (M + BM - 1) / BM;
-  int gx = (g.bdirect ? 2048 : 1024) / g.nt;
+  static const int env_lds = [] { const char *e = getenv("PGDIST_PW_WGS"); return e ? atoi(e) : 0; }();
+  static const int env_bd = [] { const char *e = getenv("PGDIST_PW_WGS_BD"); return e ? atoi(e) : 0; }();
+  int gx = (g.bdirect ? (env_bd > 0 ? env_bd : 1024) : (env_lds > 0 ? env_lds : 1024)) / g.nt;
   if (gx > g.nmt) gx = g.nmt;
   gx = (gx + 7) & ~7;                  // multiple of 8: the N tiles of one M tile share an XCD L2
   if (gx < 8) gx = 8;
