@@ -597,7 +597,16 @@ static PwGeom pw_geom(int M, int N, int K, int pro) {
   return g;
 }
 
-int pw_gemm_num_partials(int M, int N, int K) { return pw_geom(M, N, K, ACT_NONE).gx; }
+int pw_tile_num_partials(int M, int N, int K);
+void launch_pw_tile(int pro, int epi, const bf16_t *A, const bf16_t *A2, const float *pa, const float *pb,
+                    const float *pc, const bf16_t *W, bf16_t *out, const bf16_t *Yt, const float *es,
+                    const float *et, const bf16_t *R, float *part, int M, int N, int K, hipStream_t st);
+
+// small M or large K -> the two-operand LDS-tiled kernel (pwtile.hip)
+int pw_gemm_num_partials(int M, int N, int K) {
+  const PwGeom g = pw_geom(M, N, K, ACT_NONE);
+  return g.bdirect ? pw_tile_num_partials(M, N, K) : g.gx;
+}
 
 template <int PRO, int EPI, int BN, int KS, bool BD>
 static void launch_pw_t(const PwArgs &a, const PwGeom &g, hipStream_t st) {
@@ -611,10 +620,6 @@ static void launch_pw_geom(const PwArgs &a, const PwGeom &g, hipStream_t st) {
     else launch_pw_t<PRO, EPI, 64, 1, false>(a, g, st);
     return;
   }
-#define PW_BD(B_, K_) \
-  if (g.BN == B_ && g.KS == K_) { launch_pw_t<PRO, EPI, B_, K_, true>(a, g, st); return; }
-  PW_BD(32, 1) PW_BD(32, 2) PW_BD(32, 4) PW_BD(64, 1) PW_BD(64, 2) PW_BD(64, 4)
-#undef PW_BD
 }
 
 // pro: 0 none, 1 bn+relu6, 3 bnbwd ; epi: 0 fwd, 1 bwd relu6, 2 bwd lin.
@@ -625,6 +630,10 @@ void launch_pw_gemm(int pro, int epi, const bf16_t *A, const bf16_t *A2, const f
                     int M, int N, int K, hipStream_t st) {
   PwArgs a{A, A2, pa, pb, pc, W, out, Yt, es, et, R, part, M, N, K};
   const PwGeom g = pw_geom(M, N, K, pro);
+  if (g.bdirect) {
+    launch_pw_tile(pro, epi, A, A2, pa, pb, pc, W, out, Yt, es, et, R, part, M, N, K, st);
+    return;
+  }
 #define PW_CASE(P, E) \
   if (pro == P && epi == E) { launch_pw_geom<P, E>(a, g, st); return; }
   PW_CASE(ACT_NONE, EPI_FWD)

@@ -1,0 +1,303 @@
+// Pointwise (1x1) conv GEMM for the small-M layers (14x14 and 7x7 feature maps,
+// M = 25,088 / 6,272 at batch 128) — forward and dgrad, same fused BN prologue /
+// epilogue contract as pw_gemm_kernel (pwconv.hip).
+//
+// At these shapes K and N (64 .. 1280) are no longer tiny next to M, so the
+// operands are re-read by many workgroups and a classic two-operand LDS tiling
+// wins over the row-stream kernel: BM x BN output tile per workgroup (4 waves in
+// a 2 x 2 arrangement, each (BM/2) x (BN/2) of v_mfma_f32_16x16x32_bf16 tiles),
+// k-steps of 32 with both operand tiles double-buffered in LDS and the next
+// step's global loads in flight during the current step's MFMAs.  The BN
+// prologue (ReLU6(BN) of the producer, or this layer's BN backward
+// a*G + b*Y + c) is applied once per element while staging A.  Workgroup ids
+// put the N tiles of an M tile 8 ids apart (same XCD, dispatched together) so
+// the A tile is fetched from HBM once into that XCD's L2.
+#include "../common.h"
+
+enum { PRO_BNBWD_T = 3 };
+enum { EPI_FWD_T = 0, EPI_BWD_RELU6_T = 1, EPI_BWD_LIN_T = 2 };
+
+namespace {
+struct PwTArgs {
+  const bf16_t *A;      // [M][K]
+  const bf16_t *A2;     // [M][K] (Y for the BN backward prologue)
+  const float *pa, *pb, *pc;
+  const bf16_t *W;      // [N][K]
+  bf16_t *out;          // [M][N]
+  const bf16_t *Yt;     // [M][N]
+  const float *es, *et;
+  const bf16_t *R;      // [M][N]
+  float *part;          // [nmt][2][N]
+  int M, N, K;
+};
+constexpr int kLDK = 32 + 8;   // staged operand row pitch (bf16): 80 B
+}  // namespace
+
+template <int PRO, int EPI, int BM, int BN>
+__global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
+  constexpr int NPAR = PRO == ACT_NONE ? 0 : (PRO == PRO_BNBWD_T ? 3 : 2);
+  constexpr int RT = BM / 32, CTW = BN / 32;          // per-wave 16x16 tiles (rows, cols)
+  constexpr int ACH = BM * 4 / 256, BCH = BN * 4 / 256;
+  constexpr int LDC = BN + 8;
+  constexpr int CH = BN / 8, RSTEP = 256 / CH, NP = BM / RSTEP;
+  constexpr int EB = NP < 4 ? NP : 4;
+  static_assert(ACH >= 1 && BCH >= 1 && NP >= 1, "tile too small for 256 threads");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t *As = reinterpret_cast<bf16_t *>(smem);                         // [2][BM][kLDK]
+  bf16_t *Bs = As + 2 * BM * kLDK;                                       // [2][BN][kLDK]
+  float *Ps = reinterpret_cast<float *>(Bs + 2 * BN * kLDK);             // [NPAR][Kp]
+  bf16_t *Cs = reinterpret_cast<bf16_t *>(smem);                         // [BM][LDC] (after the K loop)
+  float *Red = reinterpret_cast<float *>(smem);                          // [RSTEP][BN] (at the end)
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int NT = (p.N + BN - 1) / BN;
+  const int nmt = (p.M + BM - 1) / BM;
+  // workgroup -> (mt, nt): the NT tiles of one M tile are 8 ids apart (same XCD)
+  int mt, nt;
+  {
+    const int L = blockIdx.x, full = (nmt / 8) * 8 * NT;
+    if (L < full) {
+      mt = (L / (8 * NT)) * 8 + L % 8;
+      nt = (L / 8) % NT;
+    } else {
+      const int rem = nmt % 8, Lr = L - full;
+      mt = (nmt / 8) * 8 + Lr % rem;
+      nt = Lr / rem;
+    }
+  }
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int Kp = (p.K + 31) & ~31;
+  const int nk = Kp / 32;
+
+  if constexpr (NPAR > 0) {
+    for (int i = tid; i < Kp; i += 256) {
+      const bool ok = i < p.K;
+      Ps[i] = ok ? p.pa[i] : 0.f;
+      Ps[Kp + i] = ok ? p.pb[i] : 0.f;
+      if constexpr (NPAR == 3) Ps[2 * Kp + i] = ok ? p.pc[i] : 0.f;
+    }
+  }
+
+  uint4 ra[ACH], ry[PRO == PRO_BNBWD_T ? ACH : 1], rb[BCH];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int c = tid + i * 256, row = c >> 2, kk = (c & 3) * 8;
+      const int gr = m0 + row, k = k0 + kk;
+      const bool ok = gr < p.M && k < p.K;
+      const size_t off = (size_t)gr * p.K + k;
+      ra[i] = ok ? ldg16(p.A + off) : make_uint4(0, 0, 0, 0);
+      if constexpr (PRO == PRO_BNBWD_T) ry[i] = ok ? ldg16(p.A2 + off) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int c = tid + i * 256, n = c >> 2, kk = (c & 3) * 8;
+      const int gn = n0 + n, k = k0 + kk;
+      rb[i] = (gn < p.N && k < p.K) ? ldg16(p.W + (size_t)gn * p.K + k) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto write = [&](int buf, int k0) {
+    bf16_t *Ab = As + buf * BM * kLDK;
+    bf16_t *Bb = Bs + buf * BN * kLDK;
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int c = tid + i * 256, row = c >> 2, kk = (c & 3) * 8;
+      uint4 v = ra[i];
+      if constexpr (PRO != ACT_NONE) {
+        const int k = k0 + kk;
+        float x[8];
+        unpack8(ra[i], x);
+        if constexpr (PRO == PRO_BNBWD_T) {
+          float y[8];
+          unpack8(ry[i], y);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) x[j] = fmaf(Ps[k + j], x[j], fmaf(Ps[Kp + k + j], y[j], Ps[2 * Kp + k + j]));
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) x[j] = act_apply<PRO>(x[j], Ps[k + j], Ps[Kp + k + j]);
+        }
+        v = pack8(x);
+      }
+      *reinterpret_cast<uint4 *>(Ab + row * kLDK + kk) = v;
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int c = tid + i * 256, n = c >> 2, kk = (c & 3) * 8;
+      *reinterpret_cast<uint4 *>(Bb + n * kLDK + kk) = rb[i];
+    }
+  };
+
+  f32x4_t acc[RT][CTW];
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int c = 0; c < CTW; ++c) acc[r][c] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  load(0);
+  __syncthreads();   // Ps staged
+  write(0, 0);
+  __syncthreads();
+  for (int ks = 0; ks < nk; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nk) load((ks + 1) * 32);
+    const bf16_t *Ab = As + buf * BM * kLDK;
+    const bf16_t *Bb = Bs + buf * BN * kLDK;
+    s16x8_t af[RT];
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+      af[r] = *reinterpret_cast<const s16x8_t *>(Ab + (wm * (BM / 2) + r * 16 + (lane & 15)) * kLDK + 8 * (lane >> 4));
+#pragma unroll
+    for (int c = 0; c < CTW; ++c) {
+      const s16x8_t bf = *reinterpret_cast<const s16x8_t *>(Bb + (wn * (BN / 2) + c * 16 + (lane & 15)) * kLDK + 8 * (lane >> 4));
+#pragma unroll
+      for (int r = 0; r < RT; ++r)
+        acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[r]),
+                                                            __builtin_bit_cast(bf16x8_t, bf), acc[r][c], 0, 0, 0);
+    }
+    if (ks + 1 < nk) write(buf ^ 1, (ks + 1) * 32);
+    __syncthreads();
+  }
+
+  // ---- epilogue: bf16 C tile in LDS, then 16-B row chunks (same contract as pw_gemm_kernel)
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int c = 0; c < CTW; ++c)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        Cs[(wm * (BM / 2) + r * 16 + 4 * (lane >> 4) + j) * LDC + wn * (BN / 2) + c * 16 + (lane & 15)] =
+            f2bf(acc[r][c][j]);
+  __syncthreads();
+  const int my_chunk = tid % CH, ncol0 = n0 + my_chunk * 8;
+  float st0[8], st1[8], es[8], et[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    st0[j] = st1[j] = 0.f;
+    es[j] = (EPI == EPI_BWD_RELU6_T && ncol0 + j < p.N) ? p.es[ncol0 + j] : 0.f;
+    et[j] = (EPI == EPI_BWD_RELU6_T && ncol0 + j < p.N) ? p.et[ncol0 + j] : 0.f;
+  }
+#pragma unroll
+  for (int i0 = 0; i0 < NP; i0 += EB) {
+    uint4 ytr[EB], rsr[EB];
+    if constexpr (EPI != EPI_FWD_T) {
+#pragma unroll
+      for (int e = 0; e < EB; ++e) {
+        const int rr = tid / CH + (i0 + e) * RSTEP, row = m0 + rr;
+        const bool ok = row < p.M && ncol0 < p.N;
+        const size_t off = (size_t)row * p.N + ncol0;
+        ytr[e] = ok ? ldg16(p.Yt + off) : make_uint4(0, 0, 0, 0);
+        if constexpr (EPI == EPI_BWD_LIN_T) rsr[e] = (ok && p.R) ? ldg16(p.R + off) : make_uint4(0, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < EB; ++e) {
+      const int rr = tid / CH + (i0 + e) * RSTEP, row = m0 + rr;
+      if (row < p.M && ncol0 < p.N) {
+        float v[8];
+        unpack8(*reinterpret_cast<const uint4 *>(Cs + rr * LDC + my_chunk * 8), v);
+        if constexpr (EPI == EPI_FWD_T) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            st0[j] += v[j];
+            st1[j] = fmaf(v[j], v[j], st1[j]);
+          }
+        } else {
+          float yt[8];
+          unpack8(ytr[e], yt);
+          if constexpr (EPI == EPI_BWD_RELU6_T) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] *= relu6_mask(yt[j], es[j], et[j]);
+          } else {
+            float rv[8];
+            unpack8(rsr[e], rv);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] += rv[j];
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            st0[j] += v[j];
+            st1[j] = fmaf(v[j], yt[j], st1[j]);
+          }
+        }
+        stg16(p.out + (size_t)row * p.N + ncol0, pack8(v));
+      }
+    }
+  }
+  __syncthreads();
+  // ---- BN partials of this tile's columns -> part[mt][2][N]
+  for (int s = 0; s < 2; ++s) {
+    const int rgrp = tid / CH;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Red[rgrp * BN + my_chunk * 8 + j] = s == 0 ? st0[j] : st1[j];
+    __syncthreads();
+    for (int c = tid; c < BN; c += 256) {
+      float a = 0.f;
+      for (int g = 0; g < RSTEP; ++g) a += Red[g * BN + c];
+      if (n0 + c < p.N) p.part[((size_t)mt * 2 + s) * p.N + n0 + c] = a;
+    }
+    __syncthreads();
+  }
+}
+
+// ===========================================================================
+// host side
+// ===========================================================================
+namespace {
+struct TileGeom {
+  int BM, BN, nmt, nt;
+  size_t lds;
+};
+TileGeom tile_geom(int M, int N, int K, int pro) {
+  TileGeom g{};
+  // largest tile that still gives >= 384 workgroups (~1.5 per CU), else the smallest
+  const int cand[4][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}};
+  int pick = 3;
+  for (int i = 0; i < 4; ++i) {
+    const long long wgs = (long long)((M + cand[i][0] - 1) / cand[i][0]) * ((N + cand[i][1] - 1) / cand[i][1]);
+    if (wgs >= 384) { pick = i; break; }
+  }
+  g.BM = cand[pick][0];
+  g.BN = cand[pick][1];
+  g.nmt = (M + g.BM - 1) / g.BM;
+  g.nt = (N + g.BN - 1) / g.BN;
+  const int npar = pro == ACT_NONE ? 0 : (pro == PRO_BNBWD_T ? 3 : 2);
+  const size_t kp = (size_t)((K + 31) & ~31);
+  const size_t ops = (size_t)2 * (g.BM + g.BN) * kLDK * 2;
+  const size_t ctile = (size_t)g.BM * (g.BN + 8) * 2;
+  const size_t red = (size_t)(256 / (g.BN / 8)) * g.BN * 4;
+  size_t body = ops > ctile ? ops : ctile;
+  if (red > body) body = red;
+  g.lds = body + npar * kp * 4;
+  return g;
+}
+
+template <int PRO, int EPI, int BM, int BN>
+void launch_tile_t(const PwTArgs &a, const TileGeom &g, hipStream_t st) {
+  hipLaunchKernelGGL((pw_tile_kernel<PRO, EPI, BM, BN>), dim3(g.nmt * g.nt), dim3(256), g.lds, st, a);
+}
+
+template <int PRO, int EPI>
+void launch_tile_pe(const PwTArgs &a, const TileGeom &g, hipStream_t st) {
+  if (g.BM == 128 && g.BN == 128) launch_tile_t<PRO, EPI, 128, 128>(a, g, st);
+  else if (g.BM == 64 && g.BN == 128) launch_tile_t<PRO, EPI, 64, 128>(a, g, st);
+  else if (g.BM == 128 && g.BN == 64) launch_tile_t<PRO, EPI, 128, 64>(a, g, st);
+  else launch_tile_t<PRO, EPI, 64, 64>(a, g, st);
+}
+}  // namespace
+
+int pw_tile_num_partials(int M, int N, int K) { return tile_geom(M, N, K, ACT_NONE).nmt; }
+
+void launch_pw_tile(int pro, int epi, const bf16_t *A, const bf16_t *A2, const float *pa, const float *pb,
+                    const float *pc, const bf16_t *W, bf16_t *out, const bf16_t *Yt, const float *es,
+                    const float *et, const bf16_t *R, float *part, int M, int N, int K, hipStream_t st) {
+  PwTArgs a{A, A2, pa, pb, pc, W, out, Yt, es, et, R, part, M, N, K};
+  const TileGeom g = tile_geom(M, N, K, pro);
+#define PT_CASE(P, E) \
+  if (pro == P && epi == E) { launch_tile_pe<P, E>(a, g, st); return; }
+  PT_CASE(ACT_NONE, EPI_FWD_T)
+  PT_CASE(ACT_BN_RELU6, EPI_FWD_T)
+  PT_CASE(PRO_BNBWD_T, EPI_BWD_RELU6_T)
+  PT_CASE(PRO_BNBWD_T, EPI_BWD_LIN_T)
+#undef PT_CASE
+}

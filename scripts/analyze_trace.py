@@ -64,19 +64,37 @@ def main(path, B=128, S=224):
     Mf = B * Hf * Hf
     fwd.append(("last", Mf, bl[-1]["cout"], 1280))
     bwd = fwd[::-1]
-    pw = by.get("pw_gemm_kernel", [])
+    # forward + dgrad GEMMs in dispatch order (row-stream kernel for large M, tiled for small M)
+    pw = [(r["Kernel_Name"], (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3) for r in step
+          if r["Kernel_Name"].split("(")[0].replace("void ", "").split("<")[0] in ("pw_gemm_kernel", "pw_tile_kernel")]
+    fused = [d for n, d in by.get("pw_bwd_fused_kernel", [])]
     wg = by.get("pw_wgrad_kernel", [])
     n = len(fwd)
     print(f"\npw layers (M, K->N): fwd / dgrad / wgrad  us @ TB/s")
     tf = td = tw = 0.0
+    # the large-M backward layers are fused (dgrad + wgrad in one kernel): they are missing from
+    # the dgrad/wgrad lists, so map dgrad/wgrad dispatches onto the unfused layers only
+    unfused = [i for i, (kind, M, K, N) in enumerate(fwd) if M < 65536 or kind == "last"]
+    nf = len(fwd) - len(unfused) if fused else 0
+    dg = {}
+    wg_ = {}
+    if fused:
+        for k, i in enumerate(sorted(unfused, reverse=True)):
+            if len(fwd) + k < len(pw):
+                dg[i] = pw[len(fwd) + k][1]
+            if k < len(wg):
+                wg_[i] = wg[k][1]
     for i, (kind, M, K, N) in enumerate(fwd):
         j = n - 1 - i
         bf = M * (K + N) * 2
         bd = M * (2 * N + 2 * K) * 2      # G, Y in; out (+ Yt / residual) -- approx
         bw = M * (2 * N + K) * 2
         f_ = pw[i][1] if i < len(pw) else 0
-        d_ = pw[n + j][1] if n + j < len(pw) else 0
-        w_ = wg[j][1] if j < len(wg) else 0
+        if fused:
+            d_, w_ = dg.get(i, 0.0), wg_.get(i, 0.0)
+        else:
+            d_ = pw[n + j][1] if n + j < len(pw) else 0
+            w_ = wg[j][1] if j < len(wg) else 0
         tf, td, tw = tf + f_, td + d_, tw + w_
         print(f"  {kind:4s} M={M:8d} {K:4d}->{N:4d}  fwd {f_:6.1f} {bf / f_ / 1e6 if f_ else 0:5.2f}  "
               f"dgrad {d_:6.1f} {bd / d_ / 1e6 if d_ else 0:5.2f}  wgrad {w_:6.1f} {bw / w_ / 1e6 if w_ else 0:5.2f}")
