@@ -45,7 +45,8 @@ def _pybind_includes():
 def _flags():
     common = ["-O3", "-std=c++17", "-fPIC", "-I" + CSRC, "-Wno-unused-result"]
     hip = common + [f"--offload-arch={ARCH}", "-x", "hip", "-munsafe-fp-atomics"]
-    host = common + ["-fvisibility=hidden"] + ["-I" + p for p in _pybind_includes()]
+    # host translation units (bindings, runtime) contain no kernels; target gfx950 only as well
+    host = common + [f"--offload-arch={ARCH}", "-fvisibility=hidden"] + ["-I" + p for p in _pybind_includes()]
     return hip, host
 
 

@@ -69,6 +69,7 @@ void launch_augment(const unsigned char *, const long long *, const long long *,
                     long long *, float *, hipStream_t);
 void launch_step_begin(float *, hipStream_t);
 int colsum_rows(int);
+void launch_wgrad_reduce(float *, int, long long, float *, hipStream_t);
 long long bn_part_floats(int, int);
 void register_side_stream(hipStream_t);
 void launch_reduce_metrics(const float *, const float *, int, double *, hipStream_t);
@@ -163,6 +164,9 @@ PYBIND11_MODULE(_pgdist_C, m) {
                   ptr<bf16_t>(R), ptr<bf16_t>(X), ptr<float>(part), ptr<float>(wpart), ptr<float>(grad),
                   M, Kg, Ng, S(s));
   });
+  m.def("wgrad_reduce", [](P part, int nsplit, long long n, P grad, P s) {
+    launch_wgrad_reduce(ptr<float>(part), nsplit, n, ptr<float>(grad), S(s));
+  }, "grad[n] = sum of the S split rows of part[S][n] (deterministic, one launch)");
   m.def("pw_wgrad_workspace_floats", &pw_wgrad_workspace_floats);
   m.def("pw_wgrad", [](P G, P Y, P ga, P gb, P gc, P X, P xs, P xt, int xact, P part, P grad, int M,
                        int N, int K, P s) {

@@ -420,5 +420,6 @@ void launch_pw_bwd(int epi, const bf16_t *G, const bf16_t *Y, const float *ca, c
   PwBwdArgs a{G, Y, ca, cb, cc, WT, out, Yt, es, et, R, X, part, wpart, M, Kg, Ng};
   if (epi == EPI_BWD_RELU6_) launch_bwd_epi<EPI_BWD_RELU6_>(a, g, st);
   else launch_bwd_epi<EPI_BWD_LIN_>(a, g, st);
-  launch_wgrad_reduce(wpart, g.gx, (long long)Kg * Ng, grad, st);
+  // grad == nullptr: the caller reduces wpart itself (e.g. on its weight-gradient stream)
+  if (grad) launch_wgrad_reduce(wpart, g.gx, (long long)Kg * Ng, grad, st);
 }

@@ -125,7 +125,7 @@ class MobileNetV2Executor:
         self.bn0 = BNState(self.flat, feats[0][1], "features.0.1", B * H * H, feats[0][0].out_channels, device)
         parts = [(K.stem_num_partials(B, img_size, img_size), 32)]   # (partial rows, channels)
         wg = [K.stem_wgrad_workspace(B, img_size, img_size, 32)]   # side-stream weight gradients
-        wgm = [0]                                                    # fused dgrad+wgrad (main stream)
+        wparts = {}   # fused dgrad+wgrad: one split-M partial buffer per layer, reduced on the side stream
         # ---------------- blocks
         self.blocks: List[BlockPlan] = []
         cur_h = H
@@ -158,7 +158,7 @@ class MobileNetV2Executor:
                 wg.append(K.pw_wgrad_workspace(Min, blk.hidden, blk.inp))
                 if K.pw_bwd_supported(Min, blk.hidden, blk.inp):
                     parts.append((K.pw_bwd_num_partials(Min, blk.hidden, blk.inp), blk.inp))
-                    wgm.append(K.pw_bwd_wgrad_workspace(Min, blk.hidden, blk.inp))
+                    wparts[(i, "e")] = K.pw_bwd_wgrad_workspace(Min, blk.hidden, blk.inp)
             parts.append((K.dw_num_partials("fwd", B, Hin, Hin, blk.hidden, blk.stride), blk.hidden))
             parts.append((K.dw_num_partials("dgrad", B, Hin, Hin, blk.hidden, blk.stride), blk.hidden))
             wg.append(K.dw_wgrad_workspace(B, Hin, Hin, blk.hidden, blk.stride))
@@ -167,7 +167,7 @@ class MobileNetV2Executor:
             wg.append(K.pw_wgrad_workspace(Mout, blk.oup, blk.hidden))
             if K.pw_bwd_supported(Mout, blk.oup, blk.hidden):
                 parts.append((K.pw_bwd_num_partials(Mout, blk.oup, blk.hidden), blk.hidden))
-                wgm.append(K.pw_bwd_wgrad_workspace(Mout, blk.oup, blk.hidden))
+                wparts[(i, "p")] = K.pw_bwd_wgrad_workspace(Mout, blk.oup, blk.hidden)
             cur_h = Ho
         # ---------------- final 1x1 conv + head
         last = feats[-1]
@@ -192,7 +192,7 @@ class MobileNetV2Executor:
         # ---------------- workspaces (stream-ordered reuse)
         self.ws_part = torch.zeros(max(K.bn_part_floats(P, C) for P, C in parts) + 1024, **f32)
         self.ws_wgrad = torch.zeros(max(wg) + 1024, **f32)
-        self.ws_wgrad_main = torch.zeros(max(wgm) + 1024, **f32)
+        self._wpart = {k: torch.zeros(v + 1024, **f32) for k, v in wparts.items()}
         # weight gradients that are not fused into a dgrad run on a side stream, overlapping
         # the dgrad -> BN-finalize chain (the backward's critical path)
         self.side = None
@@ -290,7 +290,7 @@ class MobileNetV2Executor:
     # ------------------------------------------------------------------ backward
     def backward(self):
         f, B, S = self.flat, self.B, self.S
-        ws, wg, wgm = self.ws_part, self.ws_wgrad, self.ws_wgrad_main
+        ws, wg = self.ws_part, self.ws_wgrad
         # transposed 1x1 weights for the dgrad GEMMs (one batched launch)
         K.wt_transpose(f.shadow, f.shadow_t, self.wt_tab, self.wt_n)
         self._ready([self.w_lin, self.b_lin])
@@ -319,8 +319,11 @@ class MobileNetV2Executor:
             # project dgrad -> g_d (relu6 mask of BN_d) + BN_d partials
             if K.pw_bwd_supported(Mout, bp.cout, bp.hidden):
                 # fused dgrad + wgrad (x = relu6(BN_d(y_d)) rebuilt from the mask operand)
-                K.pw_bwd(K.EPI_BWD_RELU6, bp.G, bnp.y, bnp.a, bnp.b, bnp.c, f.bt(bp.w_p), bnd.g, bnd.y, ws, wgm,
-                         f.g(bp.w_p), Mout, bp.cout, bp.hidden, es=bnd.scale, et=bnd.shift)
+                wpm = self._wpart[(bp.idx, "p")]
+                K.pw_bwd(K.EPI_BWD_RELU6, bp.G, bnp.y, bnp.a, bnp.b, bnp.c, f.bt(bp.w_p), bnd.g, bnd.y, ws, wpm,
+                         None, Mout, bp.cout, bp.hidden, es=bnd.scale, et=bnd.shift)
+                self._wgrad(lambda: K.wgrad_reduce(wpm, K.pw_bwd_num_partials(Mout, bp.cout, bp.hidden),
+                                                   bp.cout * bp.hidden, f.g(bp.w_p)))
                 bnd.finalize_bwd(ws, K.pw_bwd_num_partials(Mout, bp.cout, bp.hidden))
             else:
                 K.pw_gemm(K.PRO_BNBWD, K.EPI_BWD_RELU6, bp.G, f.bt(bp.w_p), bnd.g, ws, Mout, bp.hidden, bp.cout,
@@ -343,9 +346,12 @@ class MobileNetV2Executor:
                 assert prev is not None
                 # expand dgrad -> gradient w.r.t. the block input o_prev (+ skip gradient)
                 if K.pw_bwd_supported(Min, bp.hidden, bp.cin):
+                    wpe = self._wpart[(bp.idx, "e")]
                     K.pw_bwd(K.EPI_BWD_LIN, bne.g, bne.y, bne.a, bne.b, bne.c, f.bt(bp.w_e), prev.G, prev.bn_p.y,
-                             ws, wgm, f.g(bp.w_e), Min, bp.hidden, bp.cin, R=bp.G if bp.residual else None,
+                             ws, wpe, None, Min, bp.hidden, bp.cin, R=bp.G if bp.residual else None,
                              X=prev.o)
+                    self._wgrad(lambda: K.wgrad_reduce(wpe, K.pw_bwd_num_partials(Min, bp.hidden, bp.cin),
+                                                       bp.hidden * bp.cin, f.g(bp.w_e)))
                     prev.bn_p.finalize_bwd(ws, K.pw_bwd_num_partials(Min, bp.hidden, bp.cin))
                 else:
                     K.pw_gemm(K.PRO_BNBWD, K.EPI_BWD_LIN, bne.g, f.bt(bp.w_e), prev.G, ws, Min, bp.cin, bp.hidden,

@@ -241,7 +241,7 @@ def pw_bwd(epi, G, Y, ca, cb, cc, WT, out, Yt, part, wpart, grad, M, Kg, Ng, es=
     _chk(X, BF16, M * Ng, "X")
     _chk(part, F32, pw_bwd_num_partials(M, Kg, Ng) * 2 * Ng, "part")
     _chk(wpart, F32, pw_bwd_wgrad_workspace(M, Kg, Ng), "wpart")
-    _chk(grad, F32, Kg * Ng, "grad")
+    _chk(grad, F32, Kg * Ng, "grad")   # grad=None: reduce wpart later with wgrad_reduce()
     for t, nm in ((ca, "ca"), (cb, "cb"), (cc, "cc")):
         _chk(t, F32, Kg, nm)
     if epi == EPI_BWD_RELU6:
@@ -252,6 +252,13 @@ def pw_bwd(epi, G, Y, ca, cb, cc, WT, out, Yt, part, wpart, grad, M, Kg, Ng, es=
         raise ValueError(f"pw_bwd: bad epilogue {epi}")
     lib().pw_bwd(int(epi), _p(G), _p(Y), _p(ca), _p(cb), _p(cc), _p(WT), _p(out), _p(Yt), _p(es), _p(et),
                  _p(R), _p(X), _p(part), _p(wpart), _p(grad), M, Kg, Ng, _s())
+
+
+def wgrad_reduce(part, S, n, grad):
+    """grad[n] = sum of the S split rows of part (part holds S + colsum_rows(S) rows of n)."""
+    _chk(part, F32, (S + lib().colsum_rows(S)) * n, "part")
+    _chk(grad, F32, n, "grad")
+    lib().wgrad_reduce(_p(part), int(S), int(n), _p(grad), _s())
 
 
 def pw_wgrad_workspace(M, N, K):
