@@ -19,13 +19,35 @@ from ..parallel.ddp import BucketedGradReducer, broadcast_parameters
 from .executor import MobileNetV2Executor
 
 
+def coalesce_bn_buffers(model: torch.nn.Module):
+    """Re-home every BatchNorm running_mean / running_var into one flat fp32 tensor and every
+    num_batches_tracked into one int64 tensor (module buffers become views), so the per-step
+    buffer broadcast of the reference's DDP is two collectives instead of 156."""
+    mods = [m for m in model.modules() if isinstance(m, torch.nn.BatchNorm2d)]
+    dev = mods[0].running_mean.device
+    n = sum(m.running_mean.numel() + m.running_var.numel() for m in mods)
+    flat = torch.empty(n, dtype=torch.float32, device=dev)
+    nbt = torch.empty(len(mods), dtype=torch.int64, device=dev)
+    o = 0
+    for i, m in enumerate(mods):
+        for name in ("running_mean", "running_var"):
+            b = getattr(m, name)
+            v = flat[o:o + b.numel()]
+            v.copy_(b)
+            setattr(m, name, v)
+            o += b.numel()
+        nbt[i:i + 1].copy_(m.num_batches_tracked.view(1))
+        m.num_batches_tracked = nbt[i]
+    return flat, nbt
+
+
 class NativeTrainStep:
     def __init__(self, model, batch: int, device: torch.device, img_size: int = 224, lr: float = 1e-4,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, world_size: int = 1,
                  rank: int = 0, use_graph: bool = True, seed: int = 0, bucket_mb: float = 4.0,
                  first_bucket_mb: float = 1.0, reduce_dtype: torch.dtype = torch.float32,
                  double_resize: bool = True, augment: bool = True, train_augment: bool = True,
-                 side_stream: bool = True):
+                 side_stream: bool = True, bn_broadcast: bool = False):
         self.device, self.B, self.S = device, batch, img_size
         self.world, self.rank = world_size, rank
         self.exe = MobileNetV2Executor(model, batch, img_size, device, dropout_seed=(seed * 7919) ^ rank,
@@ -51,6 +73,12 @@ class NativeTrainStep:
             self.reducer = BucketedGradReducer(self.flat.grad, ranges, bucket_mb, first_bucket_mb, reduce_dtype)
             self.exe.on_params_ready = self.reducer.mark_ready
             self.sync_from_rank0()
+        # reference DDP default (broadcast_buffers=True): rank 0's BN running statistics are
+        # broadcast before every training forward; the buffers are coalesced into one flat
+        # fp32 tensor (+ one int64 tensor of num_batches_tracked) so that is two collectives
+        self.bn_broadcast = bn_broadcast and world_size > 1
+        if self.bn_broadcast:
+            self.bn_flat, self.bn_nbt = coalesce_bn_buffers(self.exe.model)
         # RCCL collectives are issued eagerly between graph segments; a single-graph
         # capture is used on one GPU
         self.use_graph = use_graph and world_size == 1
@@ -116,6 +144,8 @@ class NativeTrainStep:
                       epoch_ctr=0, out_hw=self.S)
         if self.reducer is not None:
             self.reducer.begin()
+        if self.bn_broadcast:
+            broadcast_parameters([self.bn_flat, self.bn_nbt])
         exe.forward(train=True)
         exe.backward()
         if self.reducer is not None:

@@ -117,7 +117,8 @@ class Trainer:
                                     use_graph=cfg.graph, seed=cfg.seed or 0, bucket_mb=cfg.bucket_mb,
                                     first_bucket_mb=cfg.first_bucket_mb,
                                     reduce_dtype=torch.bfloat16 if cfg.grad_reduce_dtype == "bf16" else torch.float32,
-                                    augment=True, train_augment=cfg.augment != "none")
+                                    augment=True, train_augment=cfg.augment != "none",
+                                    bn_broadcast=cfg.bn_sync == "broadcast")
         self.flat = self.step.flat
         self.train_src = torch.from_numpy(self.train_data.images).to(self.device)
         self.train_labels = torch.from_numpy(self.train_data.labels).to(self.device)
@@ -207,6 +208,8 @@ class Trainer:
         for b in range(nb):
             sel = idx[b * bs:(b + 1) * bs]
             x, y = self._torch_batch(self.train_data, sel, True)
+            if self.world > 1 and self.cfg.bn_sync == "broadcast":   # DDP broadcast_buffers=True
+                broadcast_parameters(self._bn_buffers())
             self.flat.grad.zero_()
             with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.amp):
                 out = self.model(x)
@@ -224,6 +227,10 @@ class Trainer:
             correct += int((out.argmax(1) == y).sum().item())
             count += y.numel()
         return loss_sum, correct, count
+
+    def _bn_buffers(self):
+        mods = [m for m in self.model.modules() if isinstance(m, torch.nn.BatchNorm2d)]
+        return [b for m in mods for b in (m.running_mean, m.running_var, m.num_batches_tracked)]
 
     @torch.no_grad()
     def evaluate(self):

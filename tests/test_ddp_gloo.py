@@ -86,7 +86,7 @@ def test_sharded_gradient_equals_full_batch():
         assert nb > 3
 
 
-def _worker_trainer(rank, world, port, tmp, q):
+def _worker_trainer(rank, world, port, tmp, q, bn_sync="eval"):
     import pgdist  # noqa: F401
     from pgdist.config import TrainConfig
     from pgdist.engine.trainer import Trainer
@@ -96,29 +96,39 @@ def _worker_trainer(rank, world, port, tmp, q):
     info = DistInfo(rank=rank, world_size=world, local_rank=rank, local_world_size=world, master_port=port)
     cfg = TrainConfig(data="synthetic", synthetic_train_size=48, synthetic_test_size=16, batch_size=8, epochs=1,
                       img_size=32, device="cpu", backend="torch", precision="fp32", augment="none",
-                      save_path=os.path.join(tmp, "best_mpi.pth"), log_format="ddp", seed=42)
+                      save_path=os.path.join(tmp, "best_mpi.pth"), log_format="ddp", seed=42, bn_sync=bn_sync)
     tr = Trainer(cfg, info=info)
     tr.fit()
     w = tr.flat.master.clone()
     allw = [torch.zeros_like(w) for _ in range(world)]
     dist.all_gather(allw, w)
-    q.put((rank, max((a - w).abs().max().item() for a in allw), tr.history[-1]["train_images"]))
+    rs = torch.cat([b.float().reshape(-1) for b in tr._bn_buffers()])
+    allrs = [torch.zeros_like(rs) for _ in range(world)]
+    dist.all_gather(allrs, rs)
+    q.put((rank, max((a - w).abs().max().item() for a in allw), tr.history[-1]["train_images"],
+           max((a - rs).abs().max().item() for a in allrs)))
     dist.destroy_process_group()
 
 
-def test_trainer_two_ranks_keeps_replicas_in_sync(tmp_path):
+@pytest.mark.parametrize("bn_sync", ["eval", "broadcast", "none"])
+def test_trainer_two_ranks_keeps_replicas_in_sync(tmp_path, bn_sync):
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker_trainer, args=(r, world, port, str(tmp_path), q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker_trainer, args=(r, world, port, str(tmp_path), q, bn_sync))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
-    for rank, diff, n in res:
+    for rank, diff, n, bn_diff in res:
         assert diff == 0.0
         assert n == 48
+        if bn_sync == "none":       # rank-local running statistics (different shards)
+            assert bn_diff > 0.0
+        else:                       # rank-0 statistics broadcast (reference DDP broadcast_buffers)
+            assert bn_diff == 0.0
     assert (tmp_path / "best_mpi.pth").exists()
     sd = torch.load(tmp_path / "best_mpi.pth", weights_only=True)
     assert not any(k.startswith("module.") for k in sd) and len(sd) == 314

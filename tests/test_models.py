@@ -48,3 +48,25 @@ def test_pretrained_head_swap(tmp_path):
 def test_resnet50_param_count():
     assert sum(p.numel() for p in resnet50(1000).parameters()) == 25557032
     assert build_model("resnet50", 10).fc.out_features == 10
+
+
+def test_coalesce_bn_buffers_views_and_values():
+    from pgdist.engine.native_step import coalesce_bn_buffers
+    torch.manual_seed(0)
+    m = mobilenet_v2(10)
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            mod.running_mean.uniform_()
+            mod.running_var.uniform_(1, 2)
+            mod.num_batches_tracked.fill_(3)
+    before = {k: v.clone() for k, v in m.state_dict().items()}
+    flat, nbt = coalesce_bn_buffers(m)
+    after = m.state_dict()
+    assert set(before) == set(after)
+    for k in before:
+        assert torch.equal(before[k], after[k]), k
+    assert flat.numel() == 2 * 17056 and nbt.numel() == 52
+    flat.zero_()
+    nbt.zero_()
+    bn = m.features[0][1]
+    assert float(bn.running_mean.abs().sum()) == 0.0 and int(bn.num_batches_tracked) == 0
