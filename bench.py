@@ -89,7 +89,9 @@ def main():
     imgs_per_s = args.batch_size * world * args.steps / elapsed
     if info.rank == 0:
         out = {
-            "metric": "images/sec (whole node) MobileNetV2/CIFAR-10 224² bs128 at 1/2/4/8 MI355X; val acc",
+            "metric": ("images/sec (whole node) MobileNetV2/CIFAR-10 224² bs128 at 1/2/4/8 MI355X; val acc"
+                       if args.model == "mobilenet_v2" else
+                       f"images/sec (whole node) {args.model} 224² synthetic bs{args.batch_size}/GPU"),
             "value": round(imgs_per_s, 2),
             "unit": "images/s",
             "n_gpus": world,
@@ -98,7 +100,7 @@ def main():
             "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(imgs_per_s / ref_for(world), 3),
+            "vs_baseline": round(imgs_per_s / ref_for(world), 3) if args.model == "mobilenet_v2" else None,
             "dtype": "bf16",
             "data": "synthetic (device-resident uint8 32x32x3 CIFAR-shaped images, GPU-augmented to 224x224; random-init weights)",
             "config": {"model": args.model, "global_batch": args.batch_size * world,
