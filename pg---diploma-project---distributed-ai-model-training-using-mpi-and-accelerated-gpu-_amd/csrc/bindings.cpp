@@ -37,7 +37,8 @@ void launch_dw_fwd(const bf16_t *, const float *, const float *, int, const bf16
                    float *, int, int, int, int, int, hipStream_t);
 void launch_dw_dgrad(const bf16_t *, const bf16_t *, const float *, const bf16_t *, const bf16_t *,
                      const float *, const float *, bf16_t *, float *, int, int, int, int, int,
-                     hipStream_t);
+                     float *, hipStream_t);
+long long dw_dgrad_wgrad_workspace_floats(int, int, int, int, int);
 void launch_dw_wgrad(const bf16_t *, const bf16_t *, const float *, const bf16_t *, const float *,
                      const float *, float *, float *, int, int, int, int, int, hipStream_t);
 int pw_gemm_num_partials(int, int, int);
@@ -132,11 +133,12 @@ PYBIND11_MODULE(_pgdist_C, m) {
                   ptr<float>(part), B, H, W, C, stride, S(s));
   });
   m.def("dw_dgrad", [](P g, P ys, P coef, P w, P yp, P ps, P pt, P gout, P part, int B, int H,
-                       int W, int C, int stride, P s) {
+                       int W, int C, int stride, P wpart, P s) {
     launch_dw_dgrad(ptr<bf16_t>(g), ptr<bf16_t>(ys), ptr<float>(coef), ptr<bf16_t>(w),
                     ptr<bf16_t>(yp), ptr<float>(ps), ptr<float>(pt), ptr<bf16_t>(gout),
-                    ptr<float>(part), B, H, W, C, stride, S(s));
+                    ptr<float>(part), B, H, W, C, stride, ptr<float>(wpart), S(s));
   });
+  m.def("dw_dgrad_wgrad_workspace_floats", &dw_dgrad_wgrad_workspace_floats);
   m.def("dw_wgrad", [](P g, P ys, P coef, P yp, P ps, P pt, P part, P grad, int B, int H, int W,
                        int C, int stride, P s) {
     launch_dw_wgrad(ptr<bf16_t>(g), ptr<bf16_t>(ys), ptr<float>(coef), ptr<bf16_t>(yp),

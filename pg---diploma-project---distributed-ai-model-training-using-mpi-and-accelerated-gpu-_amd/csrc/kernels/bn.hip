@@ -18,10 +18,13 @@
 // ---------------------------------------------------------------------------
 namespace {
 constexpr int kBnMinRows = 16;
+constexpr int kBnOneMax = 1024;   // single-phase (no hand-off) up to this many partial rows
 
+// blockDim.x = 32 * NS threads: 32 columns x NS row stripes (NS = 8 for the two-level
+// launch, 32 for the single-workgroup-per-channel-block launch used when P <= 1024)
 PG_DEVICE bool bn_reduce(const float *__restrict__ part, int P, int C, int rch, int nch, double *lvl1,
-                         int *ctr, double (&sh)[8][32], double (&fin)[32], int &flag) {
-  const int tid = threadIdx.x, col = tid & 31, stripe = tid >> 5;
+                         int *ctr, double (&sh)[32][32], double (&fin)[32], int &flag) {
+  const int tid = threadIdx.x, col = tid & 31, stripe = tid >> 5, NS = blockDim.x >> 5;
   const int c = blockIdx.x * 16 + (col & 15), stat = col >> 4;
   const int r0 = blockIdx.y * rch, r1 = min(P, r0 + rch);
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;   // 4 loads in flight per thread, fixed order
@@ -29,21 +32,20 @@ PG_DEVICE bool bn_reduce(const float *__restrict__ part, int P, int C, int rch, 
     const float *src = part + stat * C + c;
     const size_t ld = (size_t)2 * C;
     int r = r0 + stripe;
-    for (; r + 24 < r1; r += 32) {
+    for (; r + 3 * NS < r1; r += 4 * NS) {
       a0 += (double)src[r * ld];
-      a1 += (double)src[(r + 8) * ld];
-      a2 += (double)src[(r + 16) * ld];
-      a3 += (double)src[(r + 24) * ld];
+      a1 += (double)src[(r + NS) * ld];
+      a2 += (double)src[(r + 2 * NS) * ld];
+      a3 += (double)src[(r + 3 * NS) * ld];
     }
-    for (; r < r1; r += 8) a0 += (double)src[r * ld];
+    for (; r < r1; r += NS) a0 += (double)src[r * ld];
   }
   sh[stripe][col] = (a0 + a1) + (a2 + a3);
   __syncthreads();
   const size_t row = (size_t)gridDim.x * 32;
   if (tid < 32) {
     double s = 0.0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) s += sh[k][tid];
+    for (int k = 0; k < NS; ++k) s += sh[k][tid];
     if (nch == 1) fin[tid] = s;
     else st_sc1(lvl1 + blockIdx.y * row + blockIdx.x * 32 + tid, s);
   }
@@ -53,13 +55,12 @@ PG_DEVICE bool bn_reduce(const float *__restrict__ part, int P, int C, int rch, 
   }
   if (!arrive_last(ctr, nch, &flag)) return false;
   double b = 0.0;
-  for (int k = stripe; k < nch; k += 8) b += ld_sc1(lvl1 + k * row + blockIdx.x * 32 + col);
+  for (int k = stripe; k < nch; k += NS) b += ld_sc1(lvl1 + k * row + blockIdx.x * 32 + col);
   sh[stripe][col] = b;
   __syncthreads();
   if (tid < 32) {
     double s = 0.0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) s += sh[k][tid];
+    for (int k = 0; k < NS; ++k) s += sh[k][tid];
     fin[tid] = s;
   }
   __syncthreads();
@@ -68,13 +69,13 @@ PG_DEVICE bool bn_reduce(const float *__restrict__ part, int P, int C, int rch, 
 }  // namespace
 
 // forward: partial (sum, sumsq) -> mean, rstd, scale, shift (+ running stats, unbiased var)
-__global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(
+__global__ __launch_bounds__(1024) void bn_fwd_finalize_kernel(
     const float *__restrict__ part, int P, int C, int rch, int nch, double *lvl1, int *ctr, float count,
     const float *__restrict__ gamma, const float *__restrict__ beta, float eps, float momentum,
     float *__restrict__ running_mean, float *__restrict__ running_var, long long *__restrict__ nbt,
     float *__restrict__ mean_out, float *__restrict__ rstd_out, float *__restrict__ scale_out,
     float *__restrict__ shift_out) {
-  __shared__ double sh[8][32];
+  __shared__ double sh[32][32];
   __shared__ double fin[32];
   __shared__ int flag;
   if (!bn_reduce(part, P, C, rch, nch, lvl1, ctr, sh, fin, flag)) return;
@@ -100,11 +101,11 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(
 }
 
 // backward: partial (sum g, sum g*y) -> dy = alpha*g + beta*y + gamma_c ; coef [3][C], dgamma/dbeta
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(
+__global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
     const float *__restrict__ part, int P, int C, int rch, int nch, double *lvl1, int *ctr, float count,
     const float *__restrict__ mean, const float *__restrict__ rstd, const float *__restrict__ gamma,
     float *__restrict__ coef, float *__restrict__ dgamma, float *__restrict__ dbeta) {
-  __shared__ double sh[8][32];
+  __shared__ double sh[32][32];
   __shared__ double fin[32];
   __shared__ int flag;
   if (!bn_reduce(part, P, C, rch, nch, lvl1, ctr, sh, fin, flag)) return;
@@ -170,10 +171,12 @@ void launch_bn_fwd_finalize(const float *part, int P, int C, float count, const 
                             const float *beta, float eps, float momentum, float *rmean,
                             float *rvar, long long *nbt, float *mean, float *rstd, float *scale,
                             float *shift, hipStream_t st) {
-  const int rch = red_rch(P, kBnMinRows), nch = red_nch(P, kBnMinRows);
+  // P <= 1024: one 1024-thread workgroup per 16 channels reads all rows (no hand-off)
+  const bool one = P <= kBnOneMax;
+  const int rch = one ? P : red_rch(P, kBnMinRows), nch = one ? 1 : red_nch(P, kBnMinRows);
   const int nb = (C + 15) / 16;
   int *ctr = nch > 1 ? reduce_counters(nb, st) : nullptr;
-  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(nb, nch), dim3(256), 0, st, part, P, C, rch, nch,
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(nb, nch), dim3(one ? 1024 : 256), 0, st, part, P, C, rch, nch,
                      bn_lvl1(part, P, C), ctr, count, gamma, beta, eps, momentum, rmean, rvar, nbt, mean,
                      rstd, scale, shift);
 }
@@ -181,10 +184,11 @@ void launch_bn_fwd_finalize(const float *part, int P, int C, float count, const 
 void launch_bn_bwd_finalize(const float *part, int P, int C, float count, const float *mean,
                             const float *rstd, const float *gamma, float *coef, float *dgamma,
                             float *dbeta, hipStream_t st) {
-  const int rch = red_rch(P, kBnMinRows), nch = red_nch(P, kBnMinRows);
+  const bool one = P <= kBnOneMax;
+  const int rch = one ? P : red_rch(P, kBnMinRows), nch = one ? 1 : red_nch(P, kBnMinRows);
   const int nb = (C + 15) / 16;
   int *ctr = nch > 1 ? reduce_counters(nb, st) : nullptr;
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(nb, nch), dim3(256), 0, st, part, P, C, rch, nch,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(nb, nch), dim3(one ? 1024 : 256), 0, st, part, P, C, rch, nch,
                      bn_lvl1(part, P, C), ctr, count, mean, rstd, gamma, coef, dgamma, dbeta);
 }
 

@@ -268,11 +268,16 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(
 // dgrad: gout = mask_prev * dwconv^T(dy),  dy = a*g + b*y + c (this layer's BN backward)
 // thread = one INPUT column, strip of input rows; partial (sum gout, sum gout*yprev)
 // ---------------------------------------------------------------------------
-template <int S>
+// WG = true: the weight gradient of the same layer is accumulated on the way (fused dgrad +
+// wgrad): every input pixel's z = relu6(BN(yprev)) meets exactly the dy taps the dgrad already
+// holds in registers, so dW costs 9 FMAs per pixel and no second read of (g, y, yprev);
+// per-workgroup wgrad partials go to wpart[tile][9][C] (reduced like dw_wgrad's).
+template <int S, bool WG>
 __global__ __launch_bounds__(256) void dw_dgrad_kernel(
     const bf16_t *__restrict__ gin, const bf16_t *__restrict__ yself, const float *__restrict__ coef,
     const bf16_t *__restrict__ w, const bf16_t *__restrict__ yprev, const float *__restrict__ ps,
-    const float *__restrict__ pt, bf16_t *__restrict__ gout, float *__restrict__ part, DwGeom g) {
+    const float *__restrict__ pt, bf16_t *__restrict__ gout, float *__restrict__ part, DwGeom g,
+    float *__restrict__ wpart) {
   __shared__ __attribute__((aligned(16))) float red[1024];
   const int C4 = g.CC / CPT;
   const int tid = threadIdx.x;
@@ -285,7 +290,8 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(
   const bool active = col < g.TWc && iw < g.W;
 
   float al[CPT], be[CPT], ga[CPT], s[CPT], t[CPT], stats[2][CPT];
-  float wt[9][CPT];
+  uint2 wtp[9];   // packed bf16 taps (unpacked at use: fewer live VGPRs -> more waves)
+  float accw[WG ? 9 : 1][CPT];   // fused weight-gradient partials (tap-major)
 #pragma unroll
   for (int k = 0; k < CPT; ++k) {
     al[k] = coef[c0 + k];
@@ -296,7 +302,11 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(
     stats[0][k] = stats[1][k] = 0.f;
   }
 #pragma unroll
-  for (int q = 0; q < 9; ++q) unpack4(ldg8(w + (size_t)q * g.C + c0), wt[q]);
+  for (int q = 0; q < (WG ? 9 : 1); ++q)
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) accw[q][k] = 0.f;
+#pragma unroll
+  for (int q = 0; q < 9; ++q) wtp[q] = ldg8(w + (size_t)q * g.C + c0);
 
   if (active) {
     const int ih_end = min(tl.r0 + g.R, g.H);
@@ -342,12 +352,27 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(
 #pragma unroll
         for (int dh = 0; dh < 3; ++dh)
 #pragma unroll
-          for (int dw = 0; dw < 3; ++dw)
+          for (int dw = 0; dw < 3; ++dw) {
+            float wv[CPT];
+            unpack4(wtp[dh * 3 + dw], wv);
 #pragma unroll
-            for (int k = 0; k < CPT; ++k) acc[k] = fmaf(win[2 - dh][2 - dw][k], wt[dh * 3 + dw][k], acc[k]);
+            for (int k = 0; k < CPT; ++k) acc[k] = fmaf(win[2 - dh][2 - dw][k], wv[k], acc[k]);
+          }
         const size_t off = (((size_t)tl.b * g.H + ih) * g.W + iw) * g.C + c0;
         float yp[CPT];
         unpack4(ypc, yp);
+        if constexpr (WG) {   // dW[dh][dw] += z[ih][iw] * dy[ih+1-dh][iw+1-dw]
+          float z[CPT];
+#pragma unroll
+          for (int k = 0; k < CPT; ++k) z[k] = relu6f(fmaf(yp[k], s[k], t[k]));
+#pragma unroll
+          for (int dh = 0; dh < 3; ++dh)
+#pragma unroll
+            for (int dw = 0; dw < 3; ++dw)
+#pragma unroll
+              for (int k = 0; k < CPT; ++k)
+                accw[WG ? dh * 3 + dw : 0][k] = fmaf(z[k], win[2 - dh][2 - dw][k], accw[WG ? dh * 3 + dw : 0][k]);
+        }
 #pragma unroll
         for (int k = 0; k < CPT; ++k) acc[k] *= relu6_mask(yp[k], s[k], t[k]);
         const uint2 packed = pack4(acc);
@@ -369,12 +394,17 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(
       // per-thread tap weights (selected with static indices: no runtime-indexed arrays)
       float wA[3][CPT], wB[3][CPT];   // [dh] for column A (dw = 0 if odd else 1) and B (dw = 2)
 #pragma unroll
-      for (int r = 0; r < 3; ++r)
+      for (int r = 0; r < 3; ++r) {
+        float w0[CPT], w1[CPT], w2[CPT];
+        unpack4(wtp[r * 3 + 0], w0);
+        unpack4(wtp[r * 3 + 1], w1);
+        unpack4(wtp[r * 3 + 2], w2);
 #pragma unroll
         for (int k = 0; k < CPT; ++k) {
-          wA[r][k] = odd_w ? wt[r * 3 + 0][k] : wt[r * 3 + 1][k];
-          wB[r][k] = odd_w ? wt[r * 3 + 2][k] : 0.f;
+          wA[r][k] = odd_w ? w0[k] : w1[k];
+          wB[r][k] = odd_w ? w2[k] : 0.f;
         }
+      }
       // tiles start at even rows (R even).  Everything one iteration (2 input rows) ahead:
       // raw dy (g, y) of the next dy row and the yprev rows of the next iteration.
       auto ld_raw = [&](uint2 &dst, const bf16_t *src, int H_, int W_, int r, int c) {
@@ -390,6 +420,11 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(
         for (int k = 0; k < CPT; ++k) v[k] = ok ? fmaf(al[k], gv[k], fmaf(be[k], yv[k], ga[k])) : 0.f;
       };
       float cur[2][CPT], nxt[2][CPT];   // dy row o / o+1 at columns A, B
+      float accA[WG ? 3 : 1][CPT], accB[WG ? 3 : 1][CPT];   // fused dW[dh][dwA] / dW[dh][2]
+#pragma unroll
+      for (int r = 0; r < (WG ? 3 : 1); ++r)
+#pragma unroll
+        for (int k = 0; k < CPT; ++k) accA[r][k] = accB[r][k] = 0.f;
       uint2 rgA, ryA, rgB, ryB;         // raw dy row o+1 (columns A, B)
       uint2 yp0r, yp1r;                 // raw yprev rows of the current iteration
       int o = tl.r0 >> 1;
@@ -441,6 +476,26 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(
           const size_t off = (((size_t)tl.b * g.H + r) * g.W + iw) * g.C + c0;
           float yp[CPT];
           unpack4(ypc[half], yp);
+          if constexpr (WG) {
+            float z[CPT];
+#pragma unroll
+            for (int k = 0; k < CPT; ++k) z[k] = relu6f(fmaf(yp[k], s[k], t[k]));
+            if (half == 0) {          // dh = 1 with dy row o
+#pragma unroll
+              for (int k = 0; k < CPT; ++k) {
+                accA[WG ? 1 : 0][k] = fmaf(z[k], cur[0][k], accA[WG ? 1 : 0][k]);
+                accB[WG ? 1 : 0][k] = fmaf(z[k], cur[1][k], accB[WG ? 1 : 0][k]);
+              }
+            } else {                  // dh = 2 with row o, dh = 0 with row o+1
+#pragma unroll
+              for (int k = 0; k < CPT; ++k) {
+                accA[WG ? 2 : 0][k] = fmaf(z[k], cur[0][k], accA[WG ? 2 : 0][k]);
+                accB[WG ? 2 : 0][k] = fmaf(z[k], cur[1][k], accB[WG ? 2 : 0][k]);
+                accA[0][k] = fmaf(z[k], nxt[0][k], accA[0][k]);
+                accB[0][k] = fmaf(z[k], nxt[1][k], accB[0][k]);
+              }
+            }
+          }
 #pragma unroll
           for (int k = 0; k < CPT; ++k) acc[k] *= relu6_mask(yp[k], s[k], t[k]);
           const uint2 packed = pack4(acc);
@@ -459,9 +514,20 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(
           cur[1][k] = nxt[1][k];
         }
       }
+      if constexpr (WG) {   // column A is tap dw = 0 (odd iw) or 1 (even iw); column B is dw = 2
+#pragma unroll
+        for (int dh = 0; dh < 3; ++dh)
+#pragma unroll
+          for (int k = 0; k < CPT; ++k) {
+            accw[WG ? dh * 3 + 0 : 0][k] = odd_w ? accA[WG ? dh : 0][k] : 0.f;
+            accw[WG ? dh * 3 + 1 : 0][k] = odd_w ? 0.f : accA[WG ? dh : 0][k];
+            accw[WG ? dh * 3 + 2 : 0][k] = accB[WG ? dh : 0][k];
+          }
+      }
     }
   }
   block_channel_partials<2>(stats, part, g.C, g.CC, cbase, g.TWc, red, tl.idx);
+  if constexpr (WG) block_channel_partials<9>(accw, wpart, g.C, g.CC, cbase, g.TWc, red, tl.idx);
 }
 
 // ---------------------------------------------------------------------------
@@ -632,15 +698,30 @@ void launch_dw_fwd(const bf16_t *x, const float *in_s, const float *in_t, int ac
   }
 }
 
+int colsum_rows(int R);
+
 void launch_dw_dgrad(const bf16_t *gin, const bf16_t *yself, const float *coef, const bf16_t *w,
                      const bf16_t *yprev, const float *ps, const float *pt, bf16_t *gout,
-                     float *part, int B, int H, int W, int C, int stride, hipStream_t st) {
+                     float *part, int B, int H, int W, int C, int stride, float *wpart, hipStream_t st) {
   const DwGeom g = dw_geom(1, B, H, W, C, stride);
   dim3 grid(dw_grid_x(g) * (C / g.CC)), block(dw_threads(g));
-  if (stride == 1)
-    hipLaunchKernelGGL((dw_dgrad_kernel<1>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g);
-  else
-    hipLaunchKernelGGL((dw_dgrad_kernel<2>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g);
+  if (wpart) {
+    if (stride == 1)
+      hipLaunchKernelGGL((dw_dgrad_kernel<1, true>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g, wpart);
+    else
+      hipLaunchKernelGGL((dw_dgrad_kernel<2, true>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g, wpart);
+  } else {
+    if (stride == 1)
+      hipLaunchKernelGGL((dw_dgrad_kernel<1, false>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g, wpart);
+    else
+      hipLaunchKernelGGL((dw_dgrad_kernel<2, false>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g, wpart);
+  }
+}
+
+// wpart of the fused dgrad + wgrad: [P][9][C] with P = dgrad tiles, + level-1 rows of the reduction
+long long dw_dgrad_wgrad_workspace_floats(int B, int H, int W, int C, int stride) {
+  const int P = dw_grid_x(dw_geom(1, B, H, W, C, stride));
+  return (long long)(P + colsum_rows(P)) * 9 * C;
 }
 
 void launch_wgrad_reduce(float *part, int S, long long n, float *grad, hipStream_t st);

@@ -107,6 +107,8 @@ class BlockPlan:
 
 
 class MobileNetV2Executor:
+    DW_FUSE_MIN_H = 56   # depthwise dgrad+wgrad fused on maps >= this size (measured on MI355X)
+
     def __init__(self, model: MobileNetV2, batch: int, img_size: int, device: torch.device,
                  flat: Optional[FlatParams] = None, dropout_seed: int = 0,
                  hyper: Optional[torch.Tensor] = None, side_stream: bool = True):
@@ -161,7 +163,10 @@ class MobileNetV2Executor:
                     wparts[(i, "e")] = K.pw_bwd_wgrad_workspace(Min, blk.hidden, blk.inp)
             parts.append((K.dw_num_partials("fwd", B, Hin, Hin, blk.hidden, blk.stride), blk.hidden))
             parts.append((K.dw_num_partials("dgrad", B, Hin, Hin, blk.hidden, blk.stride), blk.hidden))
-            wg.append(K.dw_wgrad_workspace(B, Hin, Hin, blk.hidden, blk.stride))
+            if Hin >= self.DW_FUSE_MIN_H:
+                wparts[(i, "d")] = K.dw_dgrad_wgrad_workspace(B, Hin, Hin, blk.hidden, blk.stride)
+            else:
+                wg.append(K.dw_wgrad_workspace(B, Hin, Hin, blk.hidden, blk.stride))
             parts.append((K.pw_num_partials(Mout, blk.oup, blk.hidden), blk.oup))                 # fwd project
             parts.append((K.pw_num_partials(Mout, blk.hidden, blk.oup), blk.hidden))           # bwd project dgrad
             wg.append(K.pw_wgrad_workspace(Mout, blk.oup, blk.hidden))
@@ -335,11 +340,22 @@ class MobileNetV2Executor:
             self._ready([bp.w_p] + bnd.param_names)
             # depthwise: input BN is BN_e (expand) or the stem BN0 (t=1 block)
             dw_in = bp.bn_e if bp.expand else self.bn0
-            K.dw_dgrad(bnd.g, bnd.y, bnd.coef, f.b(bp.w_d), dw_in.y, dw_in.scale, dw_in.shift, dw_in.g, ws,
-                       B, Hin, Hin, bp.hidden, bp.stride)
-            dw_in.finalize_bwd(ws, K.dw_num_partials("dgrad", B, Hin, Hin, bp.hidden, bp.stride))
-            self._wgrad(lambda: K.dw_wgrad(bnd.g, bnd.y, bnd.coef, dw_in.y, dw_in.scale, dw_in.shift, wg,
-                                           f.g(bp.w_d), B, Hin, Hin, bp.hidden, bp.stride))
+            Pd = K.dw_num_partials("dgrad", B, Hin, Hin, bp.hidden, bp.stride)
+            wpd = self._wpart.get((bp.idx, "d"))
+            if wpd is not None:
+                # large maps (bandwidth-bound): fused dgrad + wgrad, one pass over (g, y, yprev);
+                # the wgrad partials are reduced on the side stream
+                K.dw_dgrad(bnd.g, bnd.y, bnd.coef, f.b(bp.w_d), dw_in.y, dw_in.scale, dw_in.shift, dw_in.g, ws,
+                           B, Hin, Hin, bp.hidden, bp.stride, wpart=wpd)
+                dw_in.finalize_bwd(ws, Pd)
+                self._wgrad(lambda: K.wgrad_reduce(wpd, Pd, 9 * bp.hidden, f.g(bp.w_d)))
+            else:
+                # small maps (latency-bound): lean dgrad on the critical path, wgrad on the side stream
+                K.dw_dgrad(bnd.g, bnd.y, bnd.coef, f.b(bp.w_d), dw_in.y, dw_in.scale, dw_in.shift, dw_in.g, ws,
+                           B, Hin, Hin, bp.hidden, bp.stride)
+                dw_in.finalize_bwd(ws, Pd)
+                self._wgrad(lambda: K.dw_wgrad(bnd.g, bnd.y, bnd.coef, dw_in.y, dw_in.scale, dw_in.shift, wg,
+                                               f.g(bp.w_d), B, Hin, Hin, bp.hidden, bp.stride))
             self._ready([bp.w_d] + dw_in.param_names)
             if bp.expand:
                 bne = bp.bn_e

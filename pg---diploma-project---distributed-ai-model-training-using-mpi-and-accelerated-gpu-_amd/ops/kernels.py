@@ -138,7 +138,15 @@ def dw_fwd(x, in_s, in_t, act, w, y, part, B, H, W, C, stride):
     lib().dw_fwd(_p(x), _p(in_s), _p(in_t), int(act), _p(w), _p(y), _p(part), B, H, W, C, stride, _s())
 
 
-def dw_dgrad(g, yself, coef, w, yprev, ps, pt, gout, part, B, H, W, C, stride):
+def dw_dgrad_wgrad_workspace(B, H, W, C, stride):
+    """Floats of wpart a fused depthwise dgrad + wgrad needs ([P][9][C] + reduction rows)."""
+    return lib().dw_dgrad_wgrad_workspace_floats(B, H, W, C, stride)
+
+
+def dw_dgrad(g, yself, coef, w, yprev, ps, pt, gout, part, B, H, W, C, stride, wpart=None):
+    """Depthwise dgrad (+ BN partials of gout).  With ``wpart`` the layer's weight gradient is
+    accumulated in the same pass into split partials wpart[P][9][C] (P = dw_num_partials
+    ("dgrad", ...)); reduce them with ``wgrad_reduce(wpart, P, 9 * C, grad)``."""
     _dw_check(B, H, W, C, stride)
     Ho, Wo = dw_out_hw(H, W, stride)
     _chk(g, BF16, B * Ho * Wo * C, "g")
@@ -146,8 +154,9 @@ def dw_dgrad(g, yself, coef, w, yprev, ps, pt, gout, part, B, H, W, C, stride):
     _chk(yprev, BF16, B * H * W * C, "yprev")
     _chk(gout, BF16, B * H * W * C, "gout")
     _chk(part, F32, dw_num_partials("dgrad", B, H, W, C, stride) * 2 * C, "part")
+    _chk(wpart, F32, dw_dgrad_wgrad_workspace(B, H, W, C, stride), "wpart")
     lib().dw_dgrad(_p(g), _p(yself), _p(coef), _p(w), _p(yprev), _p(ps), _p(pt), _p(gout), _p(part),
-                   B, H, W, C, stride, _s())
+                   B, H, W, C, stride, _p(wpart), _s())
 
 
 def dw_wgrad_workspace(B, H, W, C, stride):
