@@ -6,13 +6,15 @@
 // operands are re-read by many workgroups and a classic two-operand LDS tiling
 // wins over the row-stream kernel: BM x BN output tile per workgroup (4 waves in
 // a 2 x 2 arrangement, each (BM/2) x (BN/2) of v_mfma_f32_16x16x32_bf16 tiles),
-// k-steps of 32 with both operand tiles double-buffered in LDS and the next
+// k-steps of 32 or 64 with both operand tiles double-buffered in LDS and the next
 // step's global loads in flight during the current step's MFMAs.  The BN
 // prologue (ReLU6(BN) of the producer, or this layer's BN backward
 // a*G + b*Y + c) is applied once per element while staging A.  Workgroup ids
 // put the N tiles of an M tile 8 ids apart (same XCD, dispatched together) so
 // the A tile is fetched from HBM once into that XCD's L2.
 #include "../common.h"
+
+#include <cstdlib>
 
 enum { PRO_BNBWD_T = 3 };
 enum { EPI_FWD_T = 0, EPI_BWD_RELU6_T = 1, EPI_BWD_LIN_T = 2 };
@@ -30,14 +32,17 @@ struct PwTArgs {
   float *part;          // [nmt][2][N]
   int M, N, K;
 };
-constexpr int kLDK = 32 + 8;   // staged operand row pitch (bf16): 80 B
 }  // namespace
 
-template <int PRO, int EPI, int BM, int BN>
+// KSTEP: k per pipeline step (32, or 64 for long K: half the steps / barriers, twice the
+// bytes in flight per step)
+template <int PRO, int EPI, int BM, int BN, int KSTEP>
 __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
+  constexpr int kLDK = KSTEP + 8;                      // staged operand row pitch (bf16)
+  constexpr int KCH = KSTEP / 8;                       // 16-B chunks per staged row
   constexpr int NPAR = PRO == ACT_NONE ? 0 : (PRO == PRO_BNBWD_T ? 3 : 2);
   constexpr int RT = BM / 32, CTW = BN / 32;          // per-wave 16x16 tiles (rows, cols)
-  constexpr int ACH = BM * 4 / 256, BCH = BN * 4 / 256;
+  constexpr int ACH = BM * KCH / 256, BCH = BN * KCH / 256;
   constexpr int LDC = BN + 8;
   constexpr int CH = BN / 8, RSTEP = 256 / CH, NP = BM / RSTEP;
   constexpr int EB = NP < 4 ? NP : 4;
@@ -67,8 +72,8 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
     }
   }
   const int m0 = mt * BM, n0 = nt * BN;
-  const int Kp = (p.K + 31) & ~31;
-  const int nk = Kp / 32;
+  const int Kp = (p.K + KSTEP - 1) / KSTEP * KSTEP;
+  const int nk = Kp / KSTEP;
 
   if constexpr (NPAR > 0) {
     for (int i = tid; i < Kp; i += 256) {
@@ -83,7 +88,7 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
   auto load = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
-      const int c = tid + i * 256, row = c >> 2, kk = (c & 3) * 8;
+      const int c = tid + i * 256, row = c / KCH, kk = (c % KCH) * 8;
       const int gr = m0 + row, k = k0 + kk;
       const bool ok = gr < p.M && k < p.K;
       const size_t off = (size_t)gr * p.K + k;
@@ -92,7 +97,7 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
     }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
-      const int c = tid + i * 256, n = c >> 2, kk = (c & 3) * 8;
+      const int c = tid + i * 256, n = c / KCH, kk = (c % KCH) * 8;
       const int gn = n0 + n, k = k0 + kk;
       rb[i] = (gn < p.N && k < p.K) ? ldg16(p.W + (size_t)gn * p.K + k) : make_uint4(0, 0, 0, 0);
     }
@@ -102,7 +107,7 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
     bf16_t *Bb = Bs + buf * BN * kLDK;
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
-      const int c = tid + i * 256, row = c >> 2, kk = (c & 3) * 8;
+      const int c = tid + i * 256, row = c / KCH, kk = (c % KCH) * 8;
       uint4 v = ra[i];
       if constexpr (PRO != ACT_NONE) {
         const int k = k0 + kk;
@@ -123,7 +128,7 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
     }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
-      const int c = tid + i * 256, n = c >> 2, kk = (c & 3) * 8;
+      const int c = tid + i * 256, n = c / KCH, kk = (c % KCH) * 8;
       *reinterpret_cast<uint4 *>(Bb + n * kLDK + kk) = rb[i];
     }
   };
@@ -140,22 +145,27 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
   __syncthreads();
   for (int ks = 0; ks < nk; ++ks) {
     const int buf = ks & 1;
-    if (ks + 1 < nk) load((ks + 1) * 32);
+    if (ks + 1 < nk) load((ks + 1) * KSTEP);
     const bf16_t *Ab = As + buf * BM * kLDK;
     const bf16_t *Bb = Bs + buf * BN * kLDK;
-    s16x8_t af[RT];
 #pragma unroll
-    for (int r = 0; r < RT; ++r)
-      af[r] = *reinterpret_cast<const s16x8_t *>(Ab + (wm * (BM / 2) + r * 16 + (lane & 15)) * kLDK + 8 * (lane >> 4));
-#pragma unroll
-    for (int c = 0; c < CTW; ++c) {
-      const s16x8_t bf = *reinterpret_cast<const s16x8_t *>(Bb + (wn * (BN / 2) + c * 16 + (lane & 15)) * kLDK + 8 * (lane >> 4));
+    for (int sub = 0; sub < KSTEP / 32; ++sub) {
+      s16x8_t af[RT];
 #pragma unroll
       for (int r = 0; r < RT; ++r)
-        acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[r]),
-                                                            __builtin_bit_cast(bf16x8_t, bf), acc[r][c], 0, 0, 0);
+        af[r] = *reinterpret_cast<const s16x8_t *>(Ab + (wm * (BM / 2) + r * 16 + (lane & 15)) * kLDK + sub * 32 +
+                                                   8 * (lane >> 4));
+#pragma unroll
+      for (int c = 0; c < CTW; ++c) {
+        const s16x8_t bf = *reinterpret_cast<const s16x8_t *>(Bb + (wn * (BN / 2) + c * 16 + (lane & 15)) * kLDK +
+                                                              sub * 32 + 8 * (lane >> 4));
+#pragma unroll
+        for (int r = 0; r < RT; ++r)
+          acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[r]),
+                                                              __builtin_bit_cast(bf16x8_t, bf), acc[r][c], 0, 0, 0);
+      }
     }
-    if (ks + 1 < nk) write(buf ^ 1, (ks + 1) * 32);
+    if (ks + 1 < nk) write(buf ^ 1, (ks + 1) * KSTEP);
     __syncthreads();
   }
 
@@ -245,7 +255,7 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
 // ===========================================================================
 namespace {
 struct TileGeom {
-  int BM, BN, nmt, nt;
+  int BM, BN, KS, nmt, nt;
   size_t lds;
 };
 TileGeom tile_geom(int M, int N, int K, int pro) {
@@ -261,9 +271,11 @@ TileGeom tile_geom(int M, int N, int K, int pro) {
   g.BN = cand[pick][1];
   g.nmt = (M + g.BM - 1) / g.BM;
   g.nt = (N + g.BN - 1) / g.BN;
+  static const int k64 = [] { const char *e = getenv("PGDIST_TILE_K64"); return e ? atoi(e) : 256; }();
+  g.KS = K >= k64 ? 64 : 32;
   const int npar = pro == ACT_NONE ? 0 : (pro == PRO_BNBWD_T ? 3 : 2);
-  const size_t kp = (size_t)((K + 31) & ~31);
-  const size_t ops = (size_t)2 * (g.BM + g.BN) * kLDK * 2;
+  const size_t kp = (size_t)((K + g.KS - 1) / g.KS * g.KS);
+  const size_t ops = (size_t)2 * (g.BM + g.BN) * (g.KS + 8) * 2;
   const size_t ctile = (size_t)g.BM * (g.BN + 8) * 2;
   const size_t red = (size_t)(256 / (g.BN / 8)) * g.BN * 4;
   size_t body = ops > ctile ? ops : ctile;
@@ -274,7 +286,8 @@ TileGeom tile_geom(int M, int N, int K, int pro) {
 
 template <int PRO, int EPI, int BM, int BN>
 void launch_tile_t(const PwTArgs &a, const TileGeom &g, hipStream_t st) {
-  hipLaunchKernelGGL((pw_tile_kernel<PRO, EPI, BM, BN>), dim3(g.nmt * g.nt), dim3(256), g.lds, st, a);
+  if (g.KS == 64) hipLaunchKernelGGL((pw_tile_kernel<PRO, EPI, BM, BN, 64>), dim3(g.nmt * g.nt), dim3(256), g.lds, st, a);
+  else hipLaunchKernelGGL((pw_tile_kernel<PRO, EPI, BM, BN, 32>), dim3(g.nmt * g.nt), dim3(256), g.lds, st, a);
 }
 
 template <int PRO, int EPI>
