@@ -51,7 +51,7 @@ void launch_pw_bwd(int, const bf16_t *, const bf16_t *, const float *, const flo
 void launch_wt_transpose(const bf16_t *, bf16_t *, const int *, int, hipStream_t);
 void launch_pw_gemm(int, int, const bf16_t *, const bf16_t *, const float *, const float *,
                     const float *, const bf16_t *, bf16_t *, const bf16_t *, const float *,
-                    const float *, const bf16_t *, float *, int, int, int, hipStream_t);
+                    const float *, const bf16_t *, float *, int, int, int, bf16_t *, hipStream_t);
 long long pw_wgrad_workspace_floats(int, int, int);
 void launch_pw_wgrad(const bf16_t *, const bf16_t *, const float *, const float *, const float *,
                      const bf16_t *, const float *, const float *, int, float *, float *, int, int,
@@ -148,10 +148,10 @@ PYBIND11_MODULE(_pgdist_C, m) {
   // ---- pointwise ----
   m.def("pw_gemm_num_partials", &pw_gemm_num_partials);
   m.def("pw_gemm", [](int pro, int epi, P A, P A2, P pa, P pb, P pc, P W, P out, P Yt, P es, P et,
-                      P R, P part, int M, int N, int K, P s) {
+                      P R, P part, int M, int N, int K, P Aout, P s) {
     launch_pw_gemm(pro, epi, ptr<bf16_t>(A), ptr<bf16_t>(A2), ptr<float>(pa), ptr<float>(pb),
                    ptr<float>(pc), ptr<bf16_t>(W), ptr<bf16_t>(out), ptr<bf16_t>(Yt), ptr<float>(es),
-                   ptr<float>(et), ptr<bf16_t>(R), ptr<float>(part), M, N, K, S(s));
+                   ptr<float>(et), ptr<bf16_t>(R), ptr<float>(part), M, N, K, ptr<bf16_t>(Aout), S(s));
   });
   m.def("wt_transpose", [](P src, P dst, P tab, int n, P s) {
     launch_wt_transpose(ptr<bf16_t>(src), ptr<bf16_t>(dst), ptr<int>(tab), n, S(s));

@@ -37,7 +37,9 @@
 
 #include <cstdlib>
 
-enum { PRO_BNBWD = 3, IM2COL_STEM = 4 };
+enum { PRO_BNBWD = 3, IM2COL_STEM = 4, PRO_BNRES = 5 };
+// PRO_BNRES: A = A*s + t + A2 (the linear BN of a block output plus its residual): the block
+// output is materialised by its consumer GEMM (Aout) instead of a separate BN-apply pass
 enum { EPI_FWD = 0, EPI_BWD_RELU6 = 1, EPI_BWD_LIN = 2 };
 
 namespace {
@@ -58,6 +60,7 @@ struct PwArgs {
   const bf16_t *R;      // [M][N] residual gradient (EPI_BWD_LIN, optional)
   float *part;          // [gridDim.x][2][N]
   int M, N, K;
+  bf16_t *Aout;         // optional [M][K]: the transformed A (block output), written by N-tile 0
 };
 }  // namespace
 
@@ -81,6 +84,11 @@ PG_DEVICE s16x8_t a_transform(const uint4 &raw, const uint4 &raw2, const float *
       const float cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = fmaf(aa[j], v[j], fmaf(bb[j], y[j], cc[j]));
+    } else if constexpr (PRO == PRO_BNRES) {
+      float r[8];
+      unpack8(raw2, r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = fmaf(v[j], aa[j], bb[j]) + r[j];
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = act_apply<PRO>(v[j], aa[j], bb[j]);
@@ -95,7 +103,7 @@ PG_DEVICE s16x8_t a_transform(const uint4 &raw, const uint4 &raw2, const float *
 template <int PRO, int SUBS, int CTB>
 struct PwRaw {
   uint4 a[SUBS][2];
-  uint4 y[PRO == PRO_BNBWD ? SUBS : 1][2];
+  uint4 y[(PRO == PRO_BNBWD || PRO == PRO_BNRES) ? SUBS : 1][2];
   uint4 b[SUBS][CTB > 0 ? CTB : 1];
 };
 
@@ -108,6 +116,7 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
   constexpr int RSTEP = 256 / CH;           // rows covered per epilogue pass
   constexpr int NP = (BM + RSTEP - 1) / RSTEP;
   constexpr int NPAR = PRO == ACT_NONE ? 0 : (PRO == PRO_BNBWD ? 3 : 2);
+  constexpr bool HAS_A2 = PRO == PRO_BNBWD || PRO == PRO_BNRES;
   constexpr int SUBS = BDIRECT ? 1 : 2;     // 32-k MFMA sub-steps per pipeline step
   constexpr int KSTEP = 32 * SUBS;
   constexpr int EB = NP < 4 ? NP : 4;       // epilogue rows whose operands are loaded together
@@ -175,7 +184,7 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
         const bool ok = row < p.M && k < p.K;
         const size_t off = (size_t)row * p.K + k;
         r.a[ss][f] = ok ? ldg16(p.A + off) : make_uint4(0, 0, 0, 0);
-        if constexpr (PRO == PRO_BNBWD) r.y[ss][f] = ok ? ldg16(p.A2 + off) : make_uint4(0, 0, 0, 0);
+        if constexpr (HAS_A2) r.y[ss][f] = ok ? ldg16(p.A2 + off) : make_uint4(0, 0, 0, 0);
       }
       if constexpr (BDIRECT) {
 #pragma unroll
@@ -188,13 +197,21 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
   };
 
   f32x4_t acc[2][CT];
+  int cur_m0 = 0;
   auto compute = [&](const Raw &r, int s) {
 #pragma unroll
     for (int ss = 0; ss < SUBS; ++ss) {
       const int kl = s * KSTEP + ss * 32 + 8 * (lane >> 4);
       s16x8_t af[2];
 #pragma unroll
-      for (int f = 0; f < 2; ++f) af[f] = a_transform<PRO>(r.a[ss][f], r.y[PRO == PRO_BNBWD ? ss : 0][f], Ps, Kp, kl);
+      for (int f = 0; f < 2; ++f) af[f] = a_transform<PRO>(r.a[ss][f], r.y[HAS_A2 ? ss : 0][f], Ps, Kp, kl);
+      if (p.Aout && blockIdx.y == 0) {   // materialise the transformed A (block output) once
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          const int row = cur_m0 + rg * 32 + f * 16 + (lane & 15);
+          if (row < p.M && kl < p.K) stg16(p.Aout + (size_t)row * p.K + kl, __builtin_bit_cast(uint4, af[f]));
+        }
+      }
 #pragma unroll
       for (int c = 0; c < CT; ++c) {
         s16x8_t bf;
@@ -213,6 +230,7 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
   if (blockIdx.x < nmt) load(cur, blockIdx.x * BM, kp);
   for (int mt = blockIdx.x; mt < nmt; mt += gridDim.x) {
     const int m0 = mt * BM;
+    cur_m0 = m0;
 #pragma unroll
     for (int f = 0; f < 2; ++f)
 #pragma unroll
@@ -590,7 +608,7 @@ static PwGeom pw_geom(int M, int N, int K, int pro) {
   gx = (gx + 7) & ~7;                  // multiple of 8: the N tiles of one M tile share an XCD L2
   if (gx < 8) gx = 8;
   g.gx = gx;
-  const int npar = pro == ACT_NONE ? 0 : (pro == PRO_BNBWD ? 3 : 2);
+  const int npar = pro == ACT_NONE ? 0 : (pro == PRO_BNBWD ? 3 : 2);   // PRO_BNRES: s, t (+ A2)
   const size_t cbuf = g.KS == 1 ? (size_t)BM * (g.BN + kCPad) * 2 : (size_t)g.KS * BM * (g.BN + 4) * 4;
   const size_t red = (size_t)(256 / (g.BN / 8)) * g.BN * 4;
   g.lds = (g.bdirect ? 0 : (size_t)g.BN * (Kp + kBPad) * 2) + (size_t)npar * Kp * 4 + (cbuf > red ? cbuf : red);
@@ -600,7 +618,8 @@ static PwGeom pw_geom(int M, int N, int K, int pro) {
 int pw_tile_num_partials(int M, int N, int K);
 void launch_pw_tile(int pro, int epi, const bf16_t *A, const bf16_t *A2, const float *pa, const float *pb,
                     const float *pc, const bf16_t *W, bf16_t *out, const bf16_t *Yt, const float *es,
-                    const float *et, const bf16_t *R, float *part, int M, int N, int K, hipStream_t st);
+                    const float *et, const bf16_t *R, float *part, int M, int N, int K, bf16_t *Aout,
+                    hipStream_t st);
 
 // small M or large K -> the two-operand LDS-tiled kernel (pwtile.hip)
 int pw_gemm_num_partials(int M, int N, int K) {
@@ -627,17 +646,19 @@ static void launch_pw_geom(const PwArgs &a, const PwGeom &g, hipStream_t st) {
 void launch_pw_gemm(int pro, int epi, const bf16_t *A, const bf16_t *A2, const float *pa,
                     const float *pb, const float *pc, const bf16_t *W, bf16_t *out,
                     const bf16_t *Yt, const float *es, const float *et, const bf16_t *R, float *part,
-                    int M, int N, int K, hipStream_t st) {
-  PwArgs a{A, A2, pa, pb, pc, W, out, Yt, es, et, R, part, M, N, K};
+                    int M, int N, int K, bf16_t *Aout, hipStream_t st) {
+  PwArgs a{A, A2, pa, pb, pc, W, out, Yt, es, et, R, part, M, N, K, Aout};
   const PwGeom g = pw_geom(M, N, K, pro);
   if (g.bdirect) {
-    launch_pw_tile(pro, epi, A, A2, pa, pb, pc, W, out, Yt, es, et, R, part, M, N, K, st);
+    launch_pw_tile(pro, epi, A, A2, pa, pb, pc, W, out, Yt, es, et, R, part, M, N, K, Aout, st);
     return;
   }
 #define PW_CASE(P, E) \
   if (pro == P && epi == E) { launch_pw_geom<P, E>(a, g, st); return; }
   PW_CASE(ACT_NONE, EPI_FWD)
   PW_CASE(ACT_BN_RELU6, EPI_FWD)
+  PW_CASE(ACT_BN, EPI_FWD)
+  PW_CASE(PRO_BNRES, EPI_FWD)
   PW_CASE(PRO_BNBWD, EPI_BWD_RELU6)
   PW_CASE(PRO_BNBWD, EPI_BWD_LIN)
 #undef PW_CASE

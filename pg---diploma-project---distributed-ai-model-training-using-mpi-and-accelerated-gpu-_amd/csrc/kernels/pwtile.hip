@@ -16,7 +16,7 @@
 
 #include <cstdlib>
 
-enum { PRO_BNBWD_T = 3 };
+enum { PRO_BNBWD_T = 3, PRO_BNRES_T = 5 };
 enum { EPI_FWD_T = 0, EPI_BWD_RELU6_T = 1, EPI_BWD_LIN_T = 2 };
 
 namespace {
@@ -31,6 +31,7 @@ struct PwTArgs {
   const bf16_t *R;      // [M][N]
   float *part;          // [nmt][2][N]
   int M, N, K;
+  bf16_t *Aout;         // optional [M][K]: transformed A (block output), written by N-tile 0
 };
 }  // namespace
 
@@ -84,7 +85,8 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
     }
   }
 
-  uint4 ra[ACH], ry[PRO == PRO_BNBWD_T ? ACH : 1], rb[BCH];
+  constexpr bool HAS_A2 = PRO == PRO_BNBWD_T || PRO == PRO_BNRES_T;
+  uint4 ra[ACH], ry[HAS_A2 ? ACH : 1], rb[BCH];
   auto load = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
@@ -93,7 +95,7 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
       const bool ok = gr < p.M && k < p.K;
       const size_t off = (size_t)gr * p.K + k;
       ra[i] = ok ? ldg16(p.A + off) : make_uint4(0, 0, 0, 0);
-      if constexpr (PRO == PRO_BNBWD_T) ry[i] = ok ? ldg16(p.A2 + off) : make_uint4(0, 0, 0, 0);
+      if constexpr (HAS_A2) ry[i] = ok ? ldg16(p.A2 + off) : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
@@ -118,11 +120,20 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
           unpack8(ry[i], y);
 #pragma unroll
           for (int j = 0; j < 8; ++j) x[j] = fmaf(Ps[k + j], x[j], fmaf(Ps[Kp + k + j], y[j], Ps[2 * Kp + k + j]));
+        } else if constexpr (PRO == PRO_BNRES_T) {
+          float r[8];
+          unpack8(ry[i], r);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) x[j] = fmaf(x[j], Ps[k + j], Ps[Kp + k + j]) + r[j];
         } else {
 #pragma unroll
           for (int j = 0; j < 8; ++j) x[j] = act_apply<PRO>(x[j], Ps[k + j], Ps[Kp + k + j]);
         }
         v = pack8(x);
+        if (p.Aout && nt == 0) {   // materialise the block output once (N-tile 0)
+          const int gr = m0 + row;
+          if (gr < p.M && k < p.K) stg16(p.Aout + (size_t)gr * p.K + k, v);
+        }
       }
       *reinterpret_cast<uint4 *>(Ab + row * kLDK + kk) = v;
     }
@@ -303,13 +314,16 @@ int pw_tile_num_partials(int M, int N, int K) { return tile_geom(M, N, K, ACT_NO
 
 void launch_pw_tile(int pro, int epi, const bf16_t *A, const bf16_t *A2, const float *pa, const float *pb,
                     const float *pc, const bf16_t *W, bf16_t *out, const bf16_t *Yt, const float *es,
-                    const float *et, const bf16_t *R, float *part, int M, int N, int K, hipStream_t st) {
-  PwTArgs a{A, A2, pa, pb, pc, W, out, Yt, es, et, R, part, M, N, K};
+                    const float *et, const bf16_t *R, float *part, int M, int N, int K, bf16_t *Aout,
+                    hipStream_t st) {
+  PwTArgs a{A, A2, pa, pb, pc, W, out, Yt, es, et, R, part, M, N, K, Aout};
   const TileGeom g = tile_geom(M, N, K, pro);
 #define PT_CASE(P, E) \
   if (pro == P && epi == E) { launch_tile_pe<P, E>(a, g, st); return; }
   PT_CASE(ACT_NONE, EPI_FWD_T)
   PT_CASE(ACT_BN_RELU6, EPI_FWD_T)
+  PT_CASE(ACT_BN, EPI_FWD_T)
+  PT_CASE(PRO_BNRES_T, EPI_FWD_T)
   PT_CASE(PRO_BNBWD_T, EPI_BWD_RELU6_T)
   PT_CASE(PRO_BNBWD_T, EPI_BWD_LIN_T)
 #undef PT_CASE

@@ -24,6 +24,7 @@ complete bucket starts while backward continues.
 
 Every buffer is allocated once, so the whole step can be captured in a hipGraph.
 """
+import os
 from dataclasses import dataclass, field
 from typing import Callable, List, Optional
 
@@ -108,6 +109,9 @@ class BlockPlan:
 
 class MobileNetV2Executor:
     DW_FUSE_MIN_H = 56   # depthwise dgrad+wgrad fused on maps >= this size (measured on MI355X)
+    # block outputs materialised by the consumer GEMM instead of a BN-apply pass: measured neutral
+    # on MI355X (the consumer reads y_p and the residual per N tile), so off by default
+    FUSE_BLOCK_OUTPUT = os.environ.get("PGDIST_FUSE_BLOCK_OUT", "0") == "1"
 
     def __init__(self, model: MobileNetV2, batch: int, img_size: int, device: torch.device,
                  flat: Optional[FlatParams] = None, dropout_seed: int = 0,
@@ -242,6 +246,15 @@ class MobileNetV2Executor:
         with torch.cuda.stream(self.side):
             fn()
 
+    def _consume_output(self, pend, W, out, ws, M, N, K_):
+        """Forward 1x1 conv whose input is a pending block output: prologue BN_p (+ residual),
+        side-writes the block output o."""
+        bn, res, o = pend
+        if res is not None:
+            K.pw_gemm(K.PRO_BNRES, K.EPI_FWD, bn.y, W, out, ws, M, N, K_, A2=res, pa=bn.scale, pb=bn.shift, Aout=o)
+        else:
+            K.pw_gemm(K.ACT_BN, K.EPI_FWD, bn.y, W, out, ws, M, N, K_, pa=bn.scale, pb=bn.shift, Aout=o)
+
     def _fin_fwd(self, bn: BNState, P: int, train: bool):
         if train:
             bn.finalize_fwd(self.ws_part, P)
@@ -255,11 +268,17 @@ class MobileNetV2Executor:
         K.stem_fwd(self.img, f.b(self.stem_w), self.bn0.y, ws, B, S, S)
         self._fin_fwd(self.bn0, K.stem_num_partials(B, S, S), train)
         inp_bn, inp_t = self.bn0, None   # block input: virtual relu6(bn0(y0))
+        # A block output o = BN_p(y_p) (+ residual) is not materialised by a separate pass: its
+        # consumer GEMM (next expand conv, or the final 1x1 conv) applies BN_p (+ residual) in
+        # its prologue and writes o (needed for the next residual and the backward) on the way.
+        pend = None      # (bn_p, residual tensor or None, o) of the previous block
         for bp in self.blocks:
             Hin = bp.H
             Min = B * Hin * Hin
             if bp.expand:
-                if inp_t is None:
+                if pend is not None:
+                    self._consume_output(pend, f.b(bp.w_e), bp.bn_e.y, ws, Min, bp.hidden, bp.cin)
+                elif inp_t is None:
                     K.pw_gemm(K.ACT_BN_RELU6, K.EPI_FWD, inp_bn.y, f.b(bp.w_e), bp.bn_e.y, ws, Min, bp.hidden,
                               bp.cin, pa=inp_bn.scale, pb=inp_bn.shift)
                 else:
@@ -267,7 +286,7 @@ class MobileNetV2Executor:
                 self._fin_fwd(bp.bn_e, K.pw_num_partials(Min, bp.hidden, bp.cin), train)
                 dw_in = bp.bn_e
             else:
-                assert inp_t is None, "t=1 block expects the (virtual) stem output"
+                assert inp_t is None and pend is None, "t=1 block expects the (virtual) stem output"
                 dw_in = inp_bn
             K.dw_fwd(dw_in.y, dw_in.scale, dw_in.shift, K.ACT_BN_RELU6, f.b(bp.w_d), bp.bn_d.y, ws, B, Hin, Hin,
                      bp.hidden, bp.stride)
@@ -276,13 +295,19 @@ class MobileNetV2Executor:
             K.pw_gemm(K.ACT_BN_RELU6, K.EPI_FWD, bp.bn_d.y, f.b(bp.w_p), bp.bn_p.y, ws, Mout, bp.cout, bp.hidden,
                       pa=bp.bn_d.scale, pb=bp.bn_d.shift)
             self._fin_fwd(bp.bn_p, K.pw_num_partials(Mout, bp.cout, bp.hidden), train)
-            K.bn_apply(bp.bn_p.y, bp.bn_p.scale, bp.bn_p.shift, bp.o, relu6=False,
-                       res=inp_t if bp.residual else None)
+            if self.FUSE_BLOCK_OUTPUT:
+                pend = (bp.bn_p, inp_t if bp.residual else None, bp.o)
+            else:
+                K.bn_apply(bp.bn_p.y, bp.bn_p.scale, bp.bn_p.shift, bp.o, relu6=False,
+                           res=inp_t if bp.residual else None)
             inp_bn, inp_t = bp.bn_p, bp.o
-        # final 1x1 conv
+        # final 1x1 conv (materialises the last block output o_17)
         Mf = B * self.Hf * self.Hf
-        K.pw_gemm(K.ACT_NONE, K.EPI_FWD, inp_t, f.b(self.w_last), self.bn_last.y, ws, Mf, self.C_last,
-                  self.C_last_in)
+        if pend is not None:
+            self._consume_output(pend, f.b(self.w_last), self.bn_last.y, ws, Mf, self.C_last, self.C_last_in)
+        else:
+            K.pw_gemm(K.ACT_NONE, K.EPI_FWD, inp_t, f.b(self.w_last), self.bn_last.y, ws, Mf, self.C_last,
+                      self.C_last_in)
         self._fin_fwd(self.bn_last, K.pw_num_partials(Mf, self.C_last, self.C_last_in), train)
         # head (+ its backward when training)
         K.head(self.bn_last.y, self.bn_last.scale, self.bn_last.shift, f.w(self.w_lin), f.w(self.b_lin),

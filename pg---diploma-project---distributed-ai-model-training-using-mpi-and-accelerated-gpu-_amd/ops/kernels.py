@@ -15,7 +15,7 @@ import torch
 
 from ._lib import lib
 
-ACT_NONE, ACT_BN_RELU6, ACT_BN, PRO_BNBWD = 0, 1, 2, 3
+ACT_NONE, ACT_BN_RELU6, ACT_BN, PRO_BNBWD, PRO_BNRES = 0, 1, 2, 3, 5   # PRO_BNRES: A*s + t + A2
 EPI_FWD, EPI_BWD_RELU6, EPI_BWD_LIN = 0, 1, 2
 AUG_NPARAMS = 16
 
@@ -181,7 +181,7 @@ def pw_num_partials(M, N, K):
 
 
 def pw_gemm(pro, epi, A, W, out, part, M, N, K, A2=None, pa=None, pb=None, pc=None, Yt=None,
-            es=None, et=None, R=None):
+            es=None, et=None, R=None, Aout=None):
     """out[M,N] = prologue(A)[M,K] @ W^T with W [N,K] in GEMM terms for every mode.
 
     For the dgrad (pro == PRO_BNBWD) W is the TRANSPOSED conv weight ([Cin][Cout],
@@ -195,16 +195,21 @@ def pw_gemm(pro, epi, A, W, out, part, M, N, K, A2=None, pa=None, pb=None, pc=No
     _chk(Yt, BF16, M * N, "Yt")
     _chk(R, BF16, M * N, "R")
     _chk(part, F32, pw_num_partials(M, N, K) * 2 * N, "part")
-    if pro in (ACT_BN_RELU6, PRO_BNBWD):
+    if pro in (ACT_BN_RELU6, ACT_BN, PRO_BNBWD, PRO_BNRES):
         assert pa is not None and pb is not None and pa.numel() >= K
     if pro == PRO_BNBWD:
         assert A2 is not None and pc is not None
+    if pro == PRO_BNRES:
+        assert A2 is not None and epi == EPI_FWD
+    if Aout is not None and pro not in (ACT_BN_RELU6, ACT_BN, PRO_BNRES):
+        raise ValueError("pw_gemm: Aout needs a transforming prologue")
     if epi in (EPI_BWD_RELU6, EPI_BWD_LIN):
         assert Yt is not None
     if epi == EPI_BWD_RELU6:
         assert es is not None and et is not None
+    _chk(Aout, BF16, M * K, "Aout")
     lib().pw_gemm(int(pro), int(epi), _p(A), _p(A2), _p(pa), _p(pb), _p(pc), _p(W), _p(out), _p(Yt),
-                  _p(es), _p(et), _p(R), _p(part), M, N, K, _s())
+                  _p(es), _p(et), _p(R), _p(part), M, N, K, _p(Aout), _s())
 
 
 def wt_transpose(src, dst, tab, n):

@@ -219,6 +219,27 @@ def test_pw_fwd(dev, M, K_, N, pro):
     assert rel(st[1], (ref * ref).sum(0)) < 1e-2
 
 
+@pytest.mark.parametrize("M,K_,N", [(70001, 24, 144), (25088, 64, 384), (6272, 320, 1280), (100352, 32, 192)])
+@pytest.mark.parametrize("res", [False, True])
+def test_pw_fwd_block_output(dev, M, K_, N, res):
+    """Consumer GEMM of a block output: prologue BN (+ residual) and the block output o written
+    on the way (replaces a separate BN-apply pass)."""
+    A = bf(rnd(M, K_, dev=dev, seed=M))
+    Rz = bf(rnd(M, K_, dev=dev, seed=M + 1)) if res else None
+    s, t = bn_params(K_, dev)
+    W = bf(rnd(N, K_, dev=dev, seed=5) / math.sqrt(K_))
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    o = torch.full((M, K_), 7.0, dtype=torch.bfloat16, device=dev)
+    P = K.pw_num_partials(M, N, K_)
+    part = torch.zeros(P * 2 * N, device=dev)
+    pro = K.PRO_BNRES if res else K.ACT_BN
+    K.pw_gemm(pro, K.EPI_FWD, A, W, out, part, M, N, K_, A2=Rz, pa=s, pb=t, Aout=o)
+    x = A.float() * s + t + (Rz.float() if res else 0.0)
+    assert rel(o, x) < 4e-3
+    ref = bf(x).float() @ W.float().t()
+    assert rel(out, ref) < 8e-3
+
+
 @pytest.mark.parametrize("M,Kf,Nf", PW_CASES)
 @pytest.mark.parametrize("epi", [K.EPI_BWD_RELU6, K.EPI_BWD_LIN])
 def test_pw_dgrad(dev, M, Kf, Nf, epi):
