@@ -30,6 +30,10 @@ namespace {
 
 constexpr int CPT = 4;        // channels per thread
 constexpr int kRows = 28;     // rows per strip (swept 4..112 on MI355X: 28 fastest end to end)
+#ifndef PGDIST_DGRAD_PF
+#define PGDIST_DGRAD_PF 2
+#endif
+constexpr int kDgradPrefetch = PGDIST_DGRAD_PF;   // rows of loads in flight ahead (stride-1 dgrad)
 
 struct DwGeom {
   int B, H, W, C, Ho, Wo;
@@ -318,72 +322,90 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(
 #pragma unroll
         for (int c = 0; c < 3; ++c)
           load_dy4(gin, yself, g.Ho, g.Wo, g.C, tl.b, tl.r0 - 1 + r, iw - 1 + c, c0, al, be, ga, win[r][c]);
-      Raw3 ng, ny;   // next dy row (raw g and y), prefetched one row ahead
-      uint2 ypn = ldg8(yprev + (((size_t)tl.b * g.H + tl.r0) * g.W + iw) * g.C + c0);   // yprev, one row ahead
-      for (int ih = tl.r0; ih < ih_end; ++ih) {
-        if (ih > tl.r0) {
+      // kPf-deep ring of raw loads (statically indexed: the row loop is unrolled by kPf):
+      // dy row (r0 + 1 + i) sits in slot (i - 1) % kPf, yprev row (r0 + i) in slot i % kPf
+      constexpr int kPf = kDgradPrefetch;
+      Raw3 rg[kPf], ry[kPf];
+      uint2 ypr[kPf];
 #pragma unroll
-          for (int c = 0; c < 3; ++c)
+      for (int q = 0; q < kPf; ++q) {
+        load_raw3(rg[q], gin, g.Ho, g.Wo, g.C, tl.b, tl.r0 + 2 + q, iw - 1, c0);
+        load_raw3(ry[q], yself, g.Ho, g.Wo, g.C, tl.b, tl.r0 + 2 + q, iw - 1, c0);
+        const int r = tl.r0 + q;
+        ypr[q] = r < ih_end ? ldg8(yprev + (((size_t)tl.b * g.H + r) * g.W + iw) * g.C + c0) : make_uint2(0, 0);
+      }
+      for (int base = 0; tl.r0 + base < ih_end; base += kPf) {
 #pragma unroll
-            for (int k = 0; k < CPT; ++k) {
-              win[0][c][k] = win[1][c][k];
-              win[1][c][k] = win[2][c][k];
+        for (int j = 0; j < kPf; ++j) {
+          const int i = base + j, ih = tl.r0 + i;
+          if (ih >= ih_end) break;
+          if (i > 0) {
+            const int sl = (j + kPf - 1) % kPf;   // slot of dy row ih + 1 (static after unrolling)
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+#pragma unroll
+              for (int k = 0; k < CPT; ++k) {
+                win[0][c][k] = win[1][c][k];
+                win[1][c][k] = win[2][c][k];
+              }
+            const int oh = ih + 1;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+              const bool ok = oh >= 0 && oh < g.Ho && iw - 1 + c >= 0 && iw - 1 + c < g.Wo;
+              float gv[CPT], yv[CPT];
+              unpack4(rg[sl].v[c], gv);
+              unpack4(ry[sl].v[c], yv);
+#pragma unroll
+              for (int k = 0; k < CPT; ++k) win[2][c][k] = ok ? fmaf(al[k], gv[k], fmaf(be[k], yv[k], ga[k])) : 0.f;
             }
-          const int oh = ih + 1;
-#pragma unroll
-          for (int c = 0; c < 3; ++c) {
-            const bool ok = oh >= 0 && oh < g.Ho && iw - 1 + c >= 0 && iw - 1 + c < g.Wo;
-            float gv[CPT], yv[CPT];
-            unpack4(ng.v[c], gv);
-            unpack4(ny.v[c], yv);
-#pragma unroll
-            for (int k = 0; k < CPT; ++k) win[2][c][k] = ok ? fmaf(al[k], gv[k], fmaf(be[k], yv[k], ga[k])) : 0.f;
+            // refill the slot with dy row ih + 1 + kPf
+            load_raw3(rg[sl], gin, g.Ho, g.Wo, g.C, tl.b, ih + 1 + kPf, iw - 1, c0);
+            load_raw3(ry[sl], yself, g.Ho, g.Wo, g.C, tl.b, ih + 1 + kPf, iw - 1, c0);
           }
-        }
-        const uint2 ypc = ypn;
-        if (ih + 1 < ih_end) {
-          load_raw3(ng, gin, g.Ho, g.Wo, g.C, tl.b, ih + 2, iw - 1, c0);
-          load_raw3(ny, yself, g.Ho, g.Wo, g.C, tl.b, ih + 2, iw - 1, c0);
-          ypn = ldg8(yprev + (((size_t)tl.b * g.H + ih + 1) * g.W + iw) * g.C + c0);
-        }
-        float acc[CPT];
-        zero4(acc);
-        // dy row ih+1-dh = win[2-dh], col iw+1-dw = win[..][2-dw]
-#pragma unroll
-        for (int dh = 0; dh < 3; ++dh)
-#pragma unroll
-          for (int dw = 0; dw < 3; ++dw) {
-            float wv[CPT];
-            unpack4(wtp[dh * 3 + dw], wv);
-#pragma unroll
-            for (int k = 0; k < CPT; ++k) acc[k] = fmaf(win[2 - dh][2 - dw][k], wv[k], acc[k]);
+          const uint2 ypc = ypr[j];
+          {
+            const int r = ih + kPf;
+            ypr[j] = r < ih_end ? ldg8(yprev + (((size_t)tl.b * g.H + r) * g.W + iw) * g.C + c0) : make_uint2(0, 0);
           }
-        const size_t off = (((size_t)tl.b * g.H + ih) * g.W + iw) * g.C + c0;
-        float yp[CPT];
-        unpack4(ypc, yp);
-        if constexpr (WG) {   // dW[dh][dw] += z[ih][iw] * dy[ih+1-dh][iw+1-dw]
-          float z[CPT];
-#pragma unroll
-          for (int k = 0; k < CPT; ++k) z[k] = relu6f(fmaf(yp[k], s[k], t[k]));
+          float acc[CPT];
+          zero4(acc);
+          // dy row ih+1-dh = win[2-dh], col iw+1-dw = win[..][2-dw]
 #pragma unroll
           for (int dh = 0; dh < 3; ++dh)
 #pragma unroll
-            for (int dw = 0; dw < 3; ++dw)
+            for (int dw = 0; dw < 3; ++dw) {
+              float wv[CPT];
+              unpack4(wtp[dh * 3 + dw], wv);
 #pragma unroll
-              for (int k = 0; k < CPT; ++k)
-                accw[WG ? dh * 3 + dw : 0][k] = fmaf(z[k], win[2 - dh][2 - dw][k], accw[WG ? dh * 3 + dw : 0][k]);
+              for (int k = 0; k < CPT; ++k) acc[k] = fmaf(win[2 - dh][2 - dw][k], wv[k], acc[k]);
+            }
+          const size_t off = (((size_t)tl.b * g.H + ih) * g.W + iw) * g.C + c0;
+          float yp[CPT];
+          unpack4(ypc, yp);
+          if constexpr (WG) {   // dW[dh][dw] += z[ih][iw] * dy[ih+1-dh][iw+1-dw]
+            float z[CPT];
+#pragma unroll
+            for (int k = 0; k < CPT; ++k) z[k] = relu6f(fmaf(yp[k], s[k], t[k]));
+#pragma unroll
+            for (int dh = 0; dh < 3; ++dh)
+#pragma unroll
+              for (int dw = 0; dw < 3; ++dw)
+#pragma unroll
+                for (int k = 0; k < CPT; ++k)
+                  accw[WG ? dh * 3 + dw : 0][k] = fmaf(z[k], win[2 - dh][2 - dw][k], accw[WG ? dh * 3 + dw : 0][k]);
+          }
+#pragma unroll
+          for (int k = 0; k < CPT; ++k) acc[k] *= relu6_mask(yp[k], s[k], t[k]);
+          const uint2 packed = pack4(acc);
+          float gr[CPT];
+          unpack4(packed, gr);
+#pragma unroll
+          for (int k = 0; k < CPT; ++k) {
+            stats[0][k] += gr[k];
+            stats[1][k] = fmaf(gr[k], yp[k], stats[1][k]);
+          }
+          stg8(gout + off, packed);
         }
-#pragma unroll
-        for (int k = 0; k < CPT; ++k) acc[k] *= relu6_mask(yp[k], s[k], t[k]);
-        const uint2 packed = pack4(acc);
-        float gr[CPT];
-        unpack4(packed, gr);
-#pragma unroll
-        for (int k = 0; k < CPT; ++k) {
-          stats[0][k] += gr[k];
-          stats[1][k] = fmaf(gr[k], yp[k], stats[1][k]);
-        }
-        stg8(gout + off, packed);
       }
     } else {
       // stride 2.  Column: even iw -> ow = iw/2 (dw=1); odd iw -> ow = (iw+1)/2 (dw=0), (iw-1)/2 (dw=2)
