@@ -1,10 +1,12 @@
 #!/bin/bash
 # PMC counter passes (kernel-trace only; never combined with sys/runtime traces).
+# FETCH_SIZE must run alone: with WRITE_SIZE/TCC counters in the same pass the
+# request exceeds the hardware counter budget and rocprofv3 hangs.
 cd /tmp && export TMPDIR=/tmp
 R="$GRAFT_REPO_ROOT"; mkdir -p "$R/gpurun_out/pmc"
 rm -rf "$R/gpurun_out/pmc/p"*
 i=0
-for set in "FETCH_SIZE WRITE_SIZE TCC_HIT_sum TCC_MISS_sum" \
+for set in "FETCH_SIZE" "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum" \
            "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS" \
            "SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_WAIT_ANY SQ_INSTS_SALU"; do
   i=$((i+1))
