@@ -52,6 +52,8 @@ def main():
                          "with the weight-gradient side stream, whose branches the graph replay serialises)")
     ap.add_argument("--side-stream", type=int, default=1, help="weight gradients on a second HIP stream")
     ap.add_argument("--img-size", type=int, default=224)
+    ap.add_argument("--fp8", type=int, default=0,
+                    help="BASELINE config 5: forward 1x1 convs on e4m3 MFMA (use with --batch-size 512)")
     args = ap.parse_args()
 
     info, device, backend = init_distributed()
@@ -62,7 +64,7 @@ def main():
     from pgdist.engine.bench_step import build_bench_step
     step_fn, meta = build_bench_step(args.model, args.batch_size, device, backend=args.backend,
                                      img_size=args.img_size, use_graph=bool(args.graph), side_stream=bool(args.side_stream),
-                                     world_size=world, rank=info.rank)
+                                     fp8=bool(args.fp8), world_size=world, rank=info.rank)
 
     def sync():
         if device.type == "cuda":
@@ -87,11 +89,14 @@ def main():
 
     ms_per_step = elapsed / args.steps * 1e3
     imgs_per_s = args.batch_size * world * args.steps / elapsed
+    # the BASELINE.json metric is MobileNetV2 bs128/GPU bf16; other configs report their own metric
+    headline = args.model == "mobilenet_v2" and args.batch_size == 128 and not args.fp8
     if info.rank == 0:
         out = {
             "metric": ("images/sec (whole node) MobileNetV2/CIFAR-10 224² bs128 at 1/2/4/8 MI355X; val acc"
-                       if args.model == "mobilenet_v2" else
-                       f"images/sec (whole node) {args.model} 224² synthetic bs{args.batch_size}/GPU"),
+                       if headline else
+                       f"images/sec (whole node) {args.model} 224² synthetic {'fp8 ' if args.fp8 else ''}"
+                       f"bs{args.batch_size}/GPU"),
             "value": round(imgs_per_s, 2),
             "unit": "images/s",
             "n_gpus": world,
@@ -100,13 +105,14 @@ def main():
             "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(imgs_per_s / ref_for(world), 3) if args.model == "mobilenet_v2" else None,
-            "dtype": "bf16",
+            "vs_baseline": round(imgs_per_s / ref_for(world), 3) if headline else None,
+            "dtype": "fp8-e4m3 fwd GEMMs / bf16" if args.fp8 else "bf16",
             "data": "synthetic (device-resident uint8 32x32x3 CIFAR-shaped images, GPU-augmented to 224x224; random-init weights)",
             "config": {"model": args.model, "global_batch": args.batch_size * world,
                        "per_gpu_batch": args.batch_size, "seq_len": None, "img_size": args.img_size,
                        "parallelism": f"dp{world}", "backend": meta.get("backend"),
-                       "hip_graph": meta.get("graph"), "side_stream": meta.get("side_stream")},
+                       "hip_graph": meta.get("graph"), "side_stream": meta.get("side_stream"),
+                       "fp8": bool(args.fp8)},
         }
         print(json.dumps(out), flush=True)
     cleanup()

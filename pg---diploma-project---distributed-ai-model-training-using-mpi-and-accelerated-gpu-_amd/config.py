@@ -42,7 +42,7 @@ class TrainConfig:
     # execution
     device: str = "auto"                      # auto | cpu | cuda
     backend: str = "auto"                     # auto (hip on GPU, torch on CPU) | hip | torch
-    precision: str = "bf16"                   # bf16 | fp32 (torch backend only)
+    precision: str = "bf16"                   # bf16 | fp32 (torch backend only) | fp8 (hip: e4m3 forward 1x1 GEMMs)
     seed: Optional[int] = 42
     graph: bool = False                       # hipGraph capture of the step (hip backend; eager + side stream measured faster)
     deterministic: bool = False
@@ -77,6 +77,9 @@ PRESETS = {
                    log_format="serial", seed=None),
     # cifar10_mpi_mobilenet_224.py
     "mpi": dict(batch_size=128, save_path="best_mobilenetv2_cifar10_224_mpi.pth", log_format="ddp", seed=42),
+    # BASELINE.json config 5: MobileNetV2 fp8 (e4m3 forward GEMMs), bs 512 per GPU, DDP
+    "mpi_fp8": dict(batch_size=512, precision="fp8", backend="hip",
+                    save_path="best_mobilenetv2_cifar10_224_mpi_fp8.pth", log_format="ddp", seed=42),
 }
 
 

@@ -49,6 +49,9 @@ void launch_pw_bwd(int, const bf16_t *, const bf16_t *, const float *, const flo
                    const bf16_t *, bf16_t *, const bf16_t *, const float *, const float *, const bf16_t *,
                    const bf16_t *, float *, float *, float *, int, int, int, hipStream_t);
 void launch_wt_transpose(const bf16_t *, bf16_t *, const int *, int, hipStream_t);
+void launch_pw_gemm_f8(int, const bf16_t *, const float *, const float *, const uint8_t *, int, const float *,
+                       float, bf16_t *, float *, int, int, int, hipStream_t);
+void launch_w8_quant(const float *, uint8_t *, float *, const int *, int, hipStream_t);
 void launch_pw_gemm(int, int, const bf16_t *, const bf16_t *, const float *, const float *,
                     const float *, const bf16_t *, bf16_t *, const bf16_t *, const float *,
                     const float *, const bf16_t *, float *, int, int, int, bf16_t *, hipStream_t);
@@ -152,6 +155,14 @@ PYBIND11_MODULE(_pgdist_C, m) {
     launch_pw_gemm(pro, epi, ptr<bf16_t>(A), ptr<bf16_t>(A2), ptr<float>(pa), ptr<float>(pb),
                    ptr<float>(pc), ptr<bf16_t>(W), ptr<bf16_t>(out), ptr<bf16_t>(Yt), ptr<float>(es),
                    ptr<float>(et), ptr<bf16_t>(R), ptr<float>(part), M, N, K, ptr<bf16_t>(Aout), S(s));
+  });
+  m.def("pw_gemm_f8", [](int pro, P A, P pa, P pb, P W8, int ldw8, P wsc, float asc, P out, P part, int M,
+                         int N, int K, P s) {
+    launch_pw_gemm_f8(pro, ptr<bf16_t>(A), ptr<float>(pa), ptr<float>(pb), ptr<uint8_t>(W8), ldw8,
+                      ptr<float>(wsc), asc, ptr<bf16_t>(out), ptr<float>(part), M, N, K, S(s));
+  });
+  m.def("w8_quant", [](P src, P dst, P wsc, P tab, int n, P s) {
+    launch_w8_quant(ptr<float>(src), ptr<uint8_t>(dst), ptr<float>(wsc), ptr<int>(tab), n, S(s));
   });
   m.def("wt_transpose", [](P src, P dst, P tab, int n, P s) {
     launch_wt_transpose(ptr<bf16_t>(src), ptr<bf16_t>(dst), ptr<int>(tab), n, S(s));

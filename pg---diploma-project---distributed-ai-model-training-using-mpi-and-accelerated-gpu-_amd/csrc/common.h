@@ -89,4 +89,21 @@ PG_DEVICE float relu6_mask(float y, float s, float t) {
   return (a > 0.f && a < 6.f) ? 1.f : 0.f;
 }
 
+// OCP fp8 e4m3fn (gfx950 native format): largest finite magnitude
+constexpr float kFp8Max = 448.f;
+
+// 8 floats -> 8 e4m3 bytes (element j in byte j), scaled by sc and saturated to +-448:
+// the A/B fragment of v_mfma_f32_16x16x32_fp8_fp8 (k = 8*(lane>>4) .. +7 of one row)
+PG_DEVICE long pack_fp8x8(const float (&v)[8], float sc) {
+  float q[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) q[j] = fminf(fmaxf(v[j] * sc, -kFp8Max), kFp8Max);
+  int lo = 0, hi = 0;
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(q[0], q[1], lo, false);
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(q[2], q[3], lo, true);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(q[4], q[5], hi, false);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(q[6], q[7], hi, true);
+  return (long)(unsigned)lo | ((long)(unsigned)hi << 32);
+}
+
 #define PG_CHECK_LAUNCH() ((void)hipGetLastError())

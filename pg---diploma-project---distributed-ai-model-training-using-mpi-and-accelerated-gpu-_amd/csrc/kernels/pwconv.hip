@@ -61,18 +61,21 @@ struct PwArgs {
   float *part;          // [gridDim.x][2][N]
   int M, N, K;
   bf16_t *Aout;         // optional [M][K]: the transformed A (block output), written by N-tile 0
+  // fp8 forward (F8 instantiations): e4m3 weights [N][ldw8] (zero-padded k), per-n dequant
+  // scale wsc[n]; the prologue output is multiplied by asc before its e4m3 conversion
+  const uint8_t *W8;
+  const float *wsc;
+  float asc;
+  int ldw8;
 };
 }  // namespace
 
 // transform one raw 16-B A fragment (8 consecutive k of one row) by the fused prologue;
 // per-k parameters come from LDS (zero for k >= K, so padded k stay exactly 0)
 template <int PRO>
-PG_DEVICE s16x8_t a_transform(const uint4 &raw, const uint4 &raw2, const float *Ps, int Kp, int kl) {
-  if constexpr (PRO == ACT_NONE) {
-    return __builtin_bit_cast(s16x8_t, raw);
-  } else {
-    float v[8];
-    unpack8(raw, v);
+PG_DEVICE void a_transform_f(const uint4 &raw, const uint4 &raw2, const float *Ps, int Kp, int kl, float (&v)[8]) {
+  unpack8(raw, v);
+  if constexpr (PRO != ACT_NONE) {
     const float4 a0 = *reinterpret_cast<const float4 *>(Ps + kl), a1 = *reinterpret_cast<const float4 *>(Ps + kl + 4);
     const float4 b0 = *reinterpret_cast<const float4 *>(Ps + Kp + kl), b1 = *reinterpret_cast<const float4 *>(Ps + Kp + kl + 4);
     const float aa[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
@@ -93,6 +96,15 @@ PG_DEVICE s16x8_t a_transform(const uint4 &raw, const uint4 &raw2, const float *
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = act_apply<PRO>(v[j], aa[j], bb[j]);
     }
+  }
+}
+template <int PRO>
+PG_DEVICE s16x8_t a_transform(const uint4 &raw, const uint4 &raw2, const float *Ps, int Kp, int kl) {
+  if constexpr (PRO == ACT_NONE) {
+    return __builtin_bit_cast(s16x8_t, raw);
+  } else {
+    float v[8];
+    a_transform_f<PRO>(raw, raw2, Ps, Kp, kl, v);
     return __builtin_bit_cast(s16x8_t, pack8(v));
   }
 }
@@ -107,8 +119,12 @@ struct PwRaw {
   uint4 b[SUBS][CTB > 0 ? CTB : 1];
 };
 
-template <int PRO, int EPI, int BN, int KS, bool BDIRECT>
+// F8: e4m3 forward (v_mfma_f32_16x16x32_fp8_fp8): the weight tile is staged as e4m3
+// bytes and each transformed A fragment is converted to e4m3 in registers; the fp32
+// accumulators are dequantised by wsc[n] / asc before the bf16 C tile.
+template <int PRO, int EPI, int BN, int KS, bool BDIRECT, bool F8 = false>
 __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
+  static_assert(!F8 || (!BDIRECT && EPI == EPI_FWD && PRO != PRO_BNBWD && PRO != PRO_BNRES), "fp8: forward only");
   constexpr int CT = BN / 16;               // col tiles per wave
   constexpr int RG = 4 / KS;                // wave row groups (each 32 rows)
   constexpr int BM = 32 * RG;               // rows per M tile
@@ -130,16 +146,28 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
   const int Kp = (p.K + KSTEP - 1) / KSTEP * KSTEP;
   const int nsteps = Kp / KSTEP;
   const int LDB = Kp + kBPad;
+  const int LDB8 = Kp + 16;                 // e4m3 weight row pitch (bytes)
+  const int bs_bytes = BDIRECT ? 0 : (F8 ? BN * LDB8 : BN * LDB * 2);
   const int nmt = (p.M + BM - 1) / BM;
   bf16_t *Bs = reinterpret_cast<bf16_t *>(smem);                                      // [BN][LDB]
-  float *Ps = reinterpret_cast<float *>(smem + (BDIRECT ? 0 : BN * LDB * 2));           // [NPAR][Kp]
-  char *cbase = smem + (BDIRECT ? 0 : BN * LDB * 2) + NPAR * Kp * 4;
+  uint8_t *Bs8 = reinterpret_cast<uint8_t *>(smem);                                   // [BN][LDB8] (F8)
+  float *Ps = reinterpret_cast<float *>(smem + bs_bytes);                             // [NPAR][Kp]
+  char *cbase = smem + bs_bytes + NPAR * Kp * 4;
   bf16_t *Cs = reinterpret_cast<bf16_t *>(cbase);                                      // [BM][LDC]
   float *Cf = reinterpret_cast<float *>(cbase);                                        // [KS][BM][LDF]
   float *Red = reinterpret_cast<float *>(cbase);                                       // [RSTEP][BN] (end)
 
   // ---- stage the weight tile (once per workgroup) and the per-k prologue parameters
-  if constexpr (!BDIRECT) {
+  if constexpr (F8) {
+    const int per_row = Kp / 16;            // W8 rows are zero-padded to ldw8 >= Kp
+    for (int i = tid; i < BN * per_row; i += 256) {
+      const int r = i / per_row, c16 = (i % per_row) * 16;
+      const int n = n0 + r;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (n < p.N) v = ldg16(p.W8 + (size_t)n * p.ldw8 + c16);
+      *reinterpret_cast<uint4 *>(Bs8 + r * LDB8 + c16) = v;
+    }
+  } else if constexpr (!BDIRECT) {
     const int per_row = Kp / 8;
     for (int i = tid; i < BN * per_row; i += 256) {
       const int r = i / per_row, c8 = (i % per_row) * 8;
@@ -198,10 +226,33 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
 
   f32x4_t acc[2][CT];
   int cur_m0 = 0;
+  float csc[CT];                            // F8: per-column dequant scale of this lane's C columns
+#pragma unroll
+  for (int c = 0; c < CT; ++c) {
+    const int n = n0 + c * 16 + (lane & 15);
+    csc[c] = (F8 && n < p.N) ? p.wsc[n] / p.asc : 1.f;
+  }
   auto compute = [&](const Raw &r, int s) {
 #pragma unroll
     for (int ss = 0; ss < SUBS; ++ss) {
       const int kl = s * KSTEP + ss * 32 + 8 * (lane >> 4);
+      if constexpr (F8) {
+        long a8[2];
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          float v[8];
+          a_transform_f<PRO>(r.a[ss][f], r.y[0][f], Ps, Kp, kl, v);
+          a8[f] = pack_fp8x8(v, p.asc);
+        }
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+          const long b8 = *reinterpret_cast<const long *>(Bs8 + (c * 16 + (lane & 15)) * LDB8 + kl);
+#pragma unroll
+          for (int f = 0; f < 2; ++f)
+            acc[f][c] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a8[f], b8, acc[f][c], 0, 0, 0);
+        }
+        continue;
+      }
       s16x8_t af[2];
 #pragma unroll
       for (int f = 0; f < 2; ++f) af[f] = a_transform<PRO>(r.a[ss][f], r.y[HAS_A2 ? ss : 0][f], Ps, Kp, kl);
@@ -250,7 +301,7 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int r = rg * 32 + f * 16 + 4 * (lane >> 4) + j, col = c * 16 + (lane & 15);
-          if constexpr (KS == 1) Cs[r * LDC + col] = f2bf(acc[f][c][j]);
+          if constexpr (KS == 1) Cs[r * LDC + col] = f2bf(F8 ? acc[f][c][j] * csc[c] : acc[f][c][j]);
           else Cf[(kp * BM + r) * LDF + col] = acc[f][c][j];
         }
     __syncthreads();
@@ -662,6 +713,68 @@ void launch_pw_gemm(int pro, int epi, const bf16_t *A, const bf16_t *A2, const f
   PW_CASE(PRO_BNBWD, EPI_BWD_RELU6)
   PW_CASE(PRO_BNBWD, EPI_BWD_LIN)
 #undef PW_CASE
+}
+
+void launch_pw_tile_f8(int pro, const bf16_t *A, const float *pa, const float *pb, const uint8_t *W8, int ldw8,
+                       const float *wsc, float asc, bf16_t *out, float *part, int M, int N, int K,
+                       hipStream_t st);
+
+// fp8 forward GEMM (fwd epilogue only): out = dequant(e4m3(asc * prologue(A)) . W8^T)
+void launch_pw_gemm_f8(int pro, const bf16_t *A, const float *pa, const float *pb, const uint8_t *W8, int ldw8,
+                       const float *wsc, float asc, bf16_t *out, float *part, int M, int N, int K,
+                       hipStream_t st) {
+  PwGeom g = pw_geom(M, N, K, pro);
+  if (g.bdirect) {
+    launch_pw_tile_f8(pro, A, pa, pb, W8, ldw8, wsc, asc, out, part, M, N, K, st);
+    return;
+  }
+  PwArgs a{A, nullptr, pa, pb, nullptr, nullptr, out, nullptr, nullptr, nullptr, nullptr, part, M, N, K, nullptr,
+           W8, wsc, asc, ldw8};
+  const int Kp = (K + 63) / 64 * 64;
+  g.lds -= (size_t)g.BN * (Kp + kBPad) * 2;
+  g.lds += (size_t)g.BN * (Kp + 16);
+#define PW8_CASE(P)                                                                                          \
+  if (pro == P) {                                                                                            \
+    if (g.BN == 32) hipLaunchKernelGGL((pw_gemm_kernel<P, EPI_FWD, 32, 1, false, true>), dim3(g.gx, g.nt),   \
+                                       dim3(256), g.lds, st, a);                                             \
+    else hipLaunchKernelGGL((pw_gemm_kernel<P, EPI_FWD, 64, 1, false, true>), dim3(g.gx, g.nt), dim3(256),   \
+                            g.lds, st, a);                                                                   \
+    return;                                                                                                  \
+  }
+  PW8_CASE(ACT_NONE)
+  PW8_CASE(ACT_BN_RELU6)
+  PW8_CASE(ACT_BN)
+#undef PW8_CASE
+}
+
+// Per-output-channel e4m3 quantisation of the 1x1 conv weights (fp32 master), one wave
+// per weight row; tab int32 [n][5] = (src element offset, rows N, cols K, dst byte offset,
+// scale offset); each layer's e4m3 rows have pitch ldw8 = K rounded up to 64 (zero padded).
+// w8[n][k] = e4m3(w[n][k] / s_n), s_n = max_k |w[n][k]| / 448 (1 for an all-zero row).
+__global__ __launch_bounds__(256) void w8_quant_kernel(const float *__restrict__ src, uint8_t *__restrict__ dst,
+                                                       float *__restrict__ wsc, const int *__restrict__ tab) {
+  const int *e = tab + blockIdx.y * 5;
+  const int N = e[1], K = e[2], ldw8 = (K + 63) / 64 * 64;
+  const int lane = threadIdx.x & 63;
+  for (int n = blockIdx.x * 4 + (threadIdx.x >> 6); n < N; n += gridDim.x * 4) {
+    const float *w = src + e[0] + (size_t)n * K;
+    float amax = 0.f;
+    for (int k = lane; k < K; k += 64) amax = fmaxf(amax, fabsf(w[k]));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+    const float s = amax > 0.f ? amax / kFp8Max : 1.f, inv = 1.f / s;
+    uint8_t *d = dst + e[3] + (size_t)n * ldw8;
+    for (int k = lane; k < ldw8; k += 64) {
+      const float q = k < K ? fminf(fmaxf(w[k] * inv, -kFp8Max), kFp8Max) : 0.f;
+      d[k] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(q, 0.f, 0, false) & 0xff);
+    }
+    if (lane == 0) wsc[e[4] + n] = s;
+  }
+}
+
+void launch_w8_quant(const float *src, uint8_t *dst, float *wsc, const int *tab, int n, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(w8_quant_kernel, dim3(64, n), dim3(256), 0, st, src, dst, wsc, tab);
 }
 
 // tab: int32 [n][3] = (element offset, rows R = Cout, cols C = Cin) into src/dst

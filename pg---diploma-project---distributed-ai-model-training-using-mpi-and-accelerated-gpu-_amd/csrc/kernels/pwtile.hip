@@ -32,14 +32,24 @@ struct PwTArgs {
   float *part;          // [nmt][2][N]
   int M, N, K;
   bf16_t *Aout;         // optional [M][K]: transformed A (block output), written by N-tile 0
+  const uint8_t *W8;    // F8: e4m3 weights [N][ldw8] (k zero-padded), dequant scale wsc[n]
+  const float *wsc;
+  float asc;            // F8: the prologue output is scaled by asc before its e4m3 conversion
+  int ldw8;
 };
 }  // namespace
 
 // KSTEP: k per pipeline step (32, or 64 for long K: half the steps / barriers, twice the
 // bytes in flight per step)
-template <int PRO, int EPI, int BM, int BN, int KSTEP>
+// F8: forward in e4m3 (v_mfma_f32_16x16x32_fp8_fp8): A is converted to e4m3 after the
+// prologue while it is staged, B is staged from the e4m3 weight copy; both LDS tiles are
+// half the bytes of the bf16 ones.
+template <int PRO, int EPI, int BM, int BN, int KSTEP, bool F8 = false>
 __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
+  static_assert(!F8 || (EPI == EPI_FWD_T && PRO != PRO_BNBWD_T && PRO != PRO_BNRES_T), "fp8: forward only");
   constexpr int kLDK = KSTEP + 8;                      // staged operand row pitch (bf16)
+  constexpr int kLDK8 = KSTEP + 16;                    // F8 staged row pitch (bytes)
+  constexpr int B8CH = BN * KSTEP / 16, B8PT = (B8CH + 255) / 256;   // F8 16-B weight chunks
   constexpr int KCH = KSTEP / 8;                       // 16-B chunks per staged row
   constexpr int NPAR = PRO == ACT_NONE ? 0 : (PRO == PRO_BNBWD_T ? 3 : 2);
   constexpr int RT = BM / 32, CTW = BN / 32;          // per-wave 16x16 tiles (rows, cols)
@@ -51,7 +61,10 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t *As = reinterpret_cast<bf16_t *>(smem);                         // [2][BM][kLDK]
   bf16_t *Bs = As + 2 * BM * kLDK;                                       // [2][BN][kLDK]
-  float *Ps = reinterpret_cast<float *>(Bs + 2 * BN * kLDK);             // [NPAR][Kp]
+  uint8_t *As8 = reinterpret_cast<uint8_t *>(smem);                      // F8: [2][BM][kLDK8]
+  uint8_t *Bs8 = As8 + 2 * BM * kLDK8;                                   // F8: [2][BN][kLDK8]
+  float *Ps = F8 ? reinterpret_cast<float *>(Bs8 + 2 * BN * kLDK8)
+                 : reinterpret_cast<float *>(Bs + 2 * BN * kLDK);        // [NPAR][Kp]
   bf16_t *Cs = reinterpret_cast<bf16_t *>(smem);                         // [BM][LDC] (after the K loop)
   float *Red = reinterpret_cast<float *>(smem);                          // [RSTEP][BN] (at the end)
 
@@ -86,7 +99,7 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
   }
 
   constexpr bool HAS_A2 = PRO == PRO_BNBWD_T || PRO == PRO_BNRES_T;
-  uint4 ra[ACH], ry[HAS_A2 ? ACH : 1], rb[BCH];
+  uint4 ra[ACH], ry[HAS_A2 ? ACH : 1], rb[F8 ? B8PT : BCH];
   auto load = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
@@ -97,11 +110,21 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
       ra[i] = ok ? ldg16(p.A + off) : make_uint4(0, 0, 0, 0);
       if constexpr (HAS_A2) ry[i] = ok ? ldg16(p.A2 + off) : make_uint4(0, 0, 0, 0);
     }
+    if constexpr (F8) {
 #pragma unroll
-    for (int i = 0; i < BCH; ++i) {
-      const int c = tid + i * 256, n = c / KCH, kk = (c % KCH) * 8;
-      const int gn = n0 + n, k = k0 + kk;
-      rb[i] = (gn < p.N && k < p.K) ? ldg16(p.W + (size_t)gn * p.K + k) : make_uint4(0, 0, 0, 0);
+      for (int i = 0; i < B8PT; ++i) {
+        const int c = tid + i * 256, n = c / (KSTEP / 16), kk = (c % (KSTEP / 16)) * 16;
+        const int gn = n0 + n;
+        rb[i] = (c < B8CH && gn < p.N && k0 + kk < p.ldw8) ? ldg16(p.W8 + (size_t)gn * p.ldw8 + k0 + kk)
+                                                           : make_uint4(0, 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < BCH; ++i) {
+        const int c = tid + i * 256, n = c / KCH, kk = (c % KCH) * 8;
+        const int gn = n0 + n, k = k0 + kk;
+        rb[i] = (gn < p.N && k < p.K) ? ldg16(p.W + (size_t)gn * p.K + k) : make_uint4(0, 0, 0, 0);
+      }
     }
   };
   auto write = [&](int buf, int k0) {
@@ -129,18 +152,37 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) x[j] = act_apply<PRO>(x[j], Ps[k + j], Ps[Kp + k + j]);
         }
+        if constexpr (F8) {
+          const long q = pack_fp8x8(x, p.asc);
+          *reinterpret_cast<long *>(As8 + (buf * BM + row) * kLDK8 + kk) = q;
+          continue;
+        }
         v = pack8(x);
         if (p.Aout && nt == 0) {   // materialise the block output once (N-tile 0)
           const int gr = m0 + row;
           if (gr < p.M && k < p.K) stg16(p.Aout + (size_t)gr * p.K + k, v);
         }
       }
-      *reinterpret_cast<uint4 *>(Ab + row * kLDK + kk) = v;
+      if constexpr (F8) {   // ACT_NONE: convert the raw bf16 A
+        float x[8];
+        unpack8(v, x);
+        *reinterpret_cast<long *>(As8 + (buf * BM + row) * kLDK8 + kk) = pack_fp8x8(x, p.asc);
+      } else {
+        *reinterpret_cast<uint4 *>(Ab + row * kLDK + kk) = v;
+      }
     }
+    if constexpr (F8) {
 #pragma unroll
-    for (int i = 0; i < BCH; ++i) {
-      const int c = tid + i * 256, n = c / KCH, kk = (c % KCH) * 8;
-      *reinterpret_cast<uint4 *>(Bb + n * kLDK + kk) = rb[i];
+      for (int i = 0; i < B8PT; ++i) {
+        const int c = tid + i * 256, n = c / (KSTEP / 16), kk = (c % (KSTEP / 16)) * 16;
+        if (c < B8CH) *reinterpret_cast<uint4 *>(Bs8 + (buf * BN + n) * kLDK8 + kk) = rb[i];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < BCH; ++i) {
+        const int c = tid + i * 256, n = c / KCH, kk = (c % KCH) * 8;
+        *reinterpret_cast<uint4 *>(Bb + n * kLDK + kk) = rb[i];
+      }
     }
   };
 
@@ -161,6 +203,23 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
     const bf16_t *Bb = Bs + buf * BN * kLDK;
 #pragma unroll
     for (int sub = 0; sub < KSTEP / 32; ++sub) {
+      if constexpr (F8) {
+        const uint8_t *A8 = As8 + buf * BM * kLDK8, *B8 = Bs8 + buf * BN * kLDK8;
+        long af8[RT];
+#pragma unroll
+        for (int r = 0; r < RT; ++r)
+          af8[r] = *reinterpret_cast<const long *>(A8 + (wm * (BM / 2) + r * 16 + (lane & 15)) * kLDK8 + sub * 32 +
+                                                   8 * (lane >> 4));
+#pragma unroll
+        for (int c = 0; c < CTW; ++c) {
+          const long bf8 = *reinterpret_cast<const long *>(B8 + (wn * (BN / 2) + c * 16 + (lane & 15)) * kLDK8 +
+                                                           sub * 32 + 8 * (lane >> 4));
+#pragma unroll
+          for (int r = 0; r < RT; ++r)
+            acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(af8[r], bf8, acc[r][c], 0, 0, 0);
+        }
+        continue;
+      }
       s16x8_t af[RT];
 #pragma unroll
       for (int r = 0; r < RT; ++r)
@@ -182,13 +241,15 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
 
   // ---- epilogue: bf16 C tile in LDS, then 16-B row chunks (same contract as pw_gemm_kernel)
 #pragma unroll
-  for (int r = 0; r < RT; ++r)
+  for (int c = 0; c < CTW; ++c) {
+    const int col = wn * (BN / 2) + c * 16 + (lane & 15);
+    const float csc = (F8 && n0 + col < p.N) ? p.wsc[n0 + col] / p.asc : 1.f;
 #pragma unroll
-    for (int c = 0; c < CTW; ++c)
+    for (int r = 0; r < RT; ++r)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        Cs[(wm * (BM / 2) + r * 16 + 4 * (lane >> 4) + j) * LDC + wn * (BN / 2) + c * 16 + (lane & 15)] =
-            f2bf(acc[r][c][j]);
+        Cs[(wm * (BM / 2) + r * 16 + 4 * (lane >> 4) + j) * LDC + col] = f2bf(F8 ? acc[r][c][j] * csc : acc[r][c][j]);
+  }
   __syncthreads();
   const int my_chunk = tid % CH, ncol0 = n0 + my_chunk * 8;
   float st0[8], st1[8], es[8], et[8];
@@ -295,18 +356,18 @@ TileGeom tile_geom(int M, int N, int K, int pro) {
   return g;
 }
 
-template <int PRO, int EPI, int BM, int BN>
+template <int PRO, int EPI, int BM, int BN, bool F8>
 void launch_tile_t(const PwTArgs &a, const TileGeom &g, hipStream_t st) {
-  if (g.KS == 64) hipLaunchKernelGGL((pw_tile_kernel<PRO, EPI, BM, BN, 64>), dim3(g.nmt * g.nt), dim3(256), g.lds, st, a);
-  else hipLaunchKernelGGL((pw_tile_kernel<PRO, EPI, BM, BN, 32>), dim3(g.nmt * g.nt), dim3(256), g.lds, st, a);
+  if (g.KS == 64) hipLaunchKernelGGL((pw_tile_kernel<PRO, EPI, BM, BN, 64, F8>), dim3(g.nmt * g.nt), dim3(256), g.lds, st, a);
+  else hipLaunchKernelGGL((pw_tile_kernel<PRO, EPI, BM, BN, 32, F8>), dim3(g.nmt * g.nt), dim3(256), g.lds, st, a);
 }
 
-template <int PRO, int EPI>
+template <int PRO, int EPI, bool F8 = false>
 void launch_tile_pe(const PwTArgs &a, const TileGeom &g, hipStream_t st) {
-  if (g.BM == 128 && g.BN == 128) launch_tile_t<PRO, EPI, 128, 128>(a, g, st);
-  else if (g.BM == 64 && g.BN == 128) launch_tile_t<PRO, EPI, 64, 128>(a, g, st);
-  else if (g.BM == 128 && g.BN == 64) launch_tile_t<PRO, EPI, 128, 64>(a, g, st);
-  else launch_tile_t<PRO, EPI, 64, 64>(a, g, st);
+  if (g.BM == 128 && g.BN == 128) launch_tile_t<PRO, EPI, 128, 128, F8>(a, g, st);
+  else if (g.BM == 64 && g.BN == 128) launch_tile_t<PRO, EPI, 64, 128, F8>(a, g, st);
+  else if (g.BM == 128 && g.BN == 64) launch_tile_t<PRO, EPI, 128, 64, F8>(a, g, st);
+  else launch_tile_t<PRO, EPI, 64, 64, F8>(a, g, st);
 }
 }  // namespace
 
@@ -327,4 +388,15 @@ void launch_pw_tile(int pro, int epi, const bf16_t *A, const bf16_t *A2, const f
   PT_CASE(PRO_BNBWD_T, EPI_BWD_RELU6_T)
   PT_CASE(PRO_BNBWD_T, EPI_BWD_LIN_T)
 #undef PT_CASE
+}
+
+void launch_pw_tile_f8(int pro, const bf16_t *A, const float *pa, const float *pb, const uint8_t *W8, int ldw8,
+                       const float *wsc, float asc, bf16_t *out, float *part, int M, int N, int K,
+                       hipStream_t st) {
+  PwTArgs a{A, nullptr, pa, pb, nullptr, nullptr, out, nullptr, nullptr, nullptr, nullptr, part, M, N, K,
+            nullptr, W8, wsc, asc, ldw8};
+  TileGeom g = tile_geom(M, N, K, pro);   // the bf16 LDS size bounds the e4m3 one
+  if (pro == ACT_NONE) launch_tile_pe<ACT_NONE, EPI_FWD_T, true>(a, g, st);
+  else if (pro == ACT_BN_RELU6) launch_tile_pe<ACT_BN_RELU6, EPI_FWD_T, true>(a, g, st);
+  else if (pro == ACT_BN) launch_tile_pe<ACT_BN, EPI_FWD_T, true>(a, g, st);
 }

@@ -21,14 +21,17 @@ def _resolve_backend(backend: str, device: torch.device) -> str:
 
 def build_bench_step(model_name: str, batch_size: int, device: torch.device, backend: str = "auto",
                      img_size: int = 224, use_graph: bool = True, world_size: int = 1, rank: int = 0,
-                     side_stream: bool = True):
+                     side_stream: bool = True, fp8: bool = False):
     backend = _resolve_backend(backend, device)
     if backend == "hip":
         from .native_step import NativeTrainStep
         step = NativeTrainStep.for_benchmark(model_name, batch_size, device, img_size=img_size,
                                              use_graph=use_graph, world_size=world_size, rank=rank,
-                                             side_stream=side_stream)
-        return step.bench_step, {"backend": "hip", "graph": step.graph_enabled, "side_stream": side_stream}
+                                             side_stream=side_stream, fp8=fp8)
+        return step.bench_step, {"backend": "hip", "graph": step.graph_enabled, "side_stream": side_stream,
+                                 "fp8": fp8}
+    if fp8:
+        raise NotImplementedError("fp8 runs on the native (hip) backend")
     return _torch_bench_step(model_name, batch_size, device, img_size, world_size, rank)
 
 

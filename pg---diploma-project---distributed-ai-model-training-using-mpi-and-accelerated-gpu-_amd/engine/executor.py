@@ -112,11 +112,14 @@ class MobileNetV2Executor:
     # block outputs materialised by the consumer GEMM instead of a BN-apply pass: measured neutral
     # on MI355X (the consumer reads y_p and the residual per N tile), so off by default
     FUSE_BLOCK_OUTPUT = os.environ.get("PGDIST_FUSE_BLOCK_OUT", "0") == "1"
+    # fp8 mode: every forward 1x1 conv runs on e4m3 MFMA (weights per output channel, activations
+    # scaled by ops.kernels.FP8_ASC), backward and depthwise/BN stay bf16/fp32
 
     def __init__(self, model: MobileNetV2, batch: int, img_size: int, device: torch.device,
                  flat: Optional[FlatParams] = None, dropout_seed: int = 0,
-                 hyper: Optional[torch.Tensor] = None, side_stream: bool = True):
+                 hyper: Optional[torch.Tensor] = None, side_stream: bool = True, fp8: bool = False):
         assert device.type == "cuda", "the native executor runs on the GPU"
+        self.fp8 = fp8
         self.model = model.to(device)
         self.B, self.S, self.device = batch, img_size, device
         self.flat = flat or FlatParams(self.model, device)
@@ -221,6 +224,22 @@ class MobileNetV2Executor:
         tab.append((self.flat.offsets[self.w_last][0], self.C_last, self.C_last_in))
         self.wt_tab = torch.tensor(tab, dtype=torch.int32, device=device).contiguous()
         self.wt_n = len(tab)
+        # fp8 forward (BASELINE config 5): per-output-channel e4m3 copies of every 1x1 weight,
+        # re-quantised from the fp32 master at the start of each forward (one batched launch)
+        self.w8 = {}
+        if fp8:
+            qtab, dst, sc = [], 0, 0
+            for off, n, k in tab:
+                qtab.append((off, n, k, dst, sc))
+                dst += n * K.fp8_pitch(k)
+                sc += n
+            self.w8_buf = torch.zeros(dst + 64, dtype=torch.uint8, device=device)
+            self.w8_scale = torch.ones(sc, dtype=torch.float32, device=device)
+            self.w8_tab = torch.tensor(qtab, dtype=torch.int32, device=device).contiguous()
+            names = [n for bp in self.blocks for n in ((bp.w_e, bp.w_p) if bp.expand else (bp.w_p,))]
+            names.append(self.w_last)
+            for name, (off, n, k, d0, c0) in zip(names, qtab):
+                self.w8[name] = (self.w8_buf[d0:d0 + n * K.fp8_pitch(k)], self.w8_scale[c0:c0 + n])
 
     # ------------------------------------------------------------------ helpers
     def _ready(self, names):
@@ -255,6 +274,14 @@ class MobileNetV2Executor:
         else:
             K.pw_gemm(K.ACT_BN, K.EPI_FWD, bn.y, W, out, ws, M, N, K_, pa=bn.scale, pb=bn.shift, Aout=o)
 
+    def _pw_fwd(self, pro, A, wname, out, ws, M, N, K_, pa=None, pb=None):
+        """Forward 1x1 conv: bf16 MFMA GEMM, or the e4m3 one in fp8 mode."""
+        if self.fp8:
+            W8, wsc = self.w8[wname]
+            K.pw_gemm_f8(pro, A, W8, wsc, out, ws, M, N, K_, pa=pa, pb=pb)
+        else:
+            K.pw_gemm(pro, K.EPI_FWD, A, self.flat.b(wname), out, ws, M, N, K_, pa=pa, pb=pb)
+
     def _fin_fwd(self, bn: BNState, P: int, train: bool):
         if train:
             bn.finalize_fwd(self.ws_part, P)
@@ -264,6 +291,8 @@ class MobileNetV2Executor:
         """Runs the forward pass on ``self.img`` (and, when training, the head backward)."""
         f, B, S = self.flat, self.B, self.S
         ws = self.ws_part
+        if self.fp8:
+            K.w8_quant(f.master, self.w8_buf, self.w8_scale, self.w8_tab, self.w8_tab.shape[0])
         # stem
         K.stem_fwd(self.img, f.b(self.stem_w), self.bn0.y, ws, B, S, S)
         self._fin_fwd(self.bn0, K.stem_num_partials(B, S, S), train)
@@ -279,10 +308,10 @@ class MobileNetV2Executor:
                 if pend is not None:
                     self._consume_output(pend, f.b(bp.w_e), bp.bn_e.y, ws, Min, bp.hidden, bp.cin)
                 elif inp_t is None:
-                    K.pw_gemm(K.ACT_BN_RELU6, K.EPI_FWD, inp_bn.y, f.b(bp.w_e), bp.bn_e.y, ws, Min, bp.hidden,
-                              bp.cin, pa=inp_bn.scale, pb=inp_bn.shift)
+                    self._pw_fwd(K.ACT_BN_RELU6, inp_bn.y, bp.w_e, bp.bn_e.y, ws, Min, bp.hidden, bp.cin,
+                                 pa=inp_bn.scale, pb=inp_bn.shift)
                 else:
-                    K.pw_gemm(K.ACT_NONE, K.EPI_FWD, inp_t, f.b(bp.w_e), bp.bn_e.y, ws, Min, bp.hidden, bp.cin)
+                    self._pw_fwd(K.ACT_NONE, inp_t, bp.w_e, bp.bn_e.y, ws, Min, bp.hidden, bp.cin)
                 self._fin_fwd(bp.bn_e, K.pw_num_partials(Min, bp.hidden, bp.cin), train)
                 dw_in = bp.bn_e
             else:
@@ -292,10 +321,10 @@ class MobileNetV2Executor:
                      bp.hidden, bp.stride)
             self._fin_fwd(bp.bn_d, K.dw_num_partials("fwd", B, Hin, Hin, bp.hidden, bp.stride), train)
             Mout = B * bp.Ho * bp.Wo
-            K.pw_gemm(K.ACT_BN_RELU6, K.EPI_FWD, bp.bn_d.y, f.b(bp.w_p), bp.bn_p.y, ws, Mout, bp.cout, bp.hidden,
-                      pa=bp.bn_d.scale, pb=bp.bn_d.shift)
+            self._pw_fwd(K.ACT_BN_RELU6, bp.bn_d.y, bp.w_p, bp.bn_p.y, ws, Mout, bp.cout, bp.hidden,
+                         pa=bp.bn_d.scale, pb=bp.bn_d.shift)
             self._fin_fwd(bp.bn_p, K.pw_num_partials(Mout, bp.cout, bp.hidden), train)
-            if self.FUSE_BLOCK_OUTPUT:
+            if self.FUSE_BLOCK_OUTPUT and not self.fp8:
                 pend = (bp.bn_p, inp_t if bp.residual else None, bp.o)
             else:
                 K.bn_apply(bp.bn_p.y, bp.bn_p.scale, bp.bn_p.shift, bp.o, relu6=False,
@@ -306,8 +335,7 @@ class MobileNetV2Executor:
         if pend is not None:
             self._consume_output(pend, f.b(self.w_last), self.bn_last.y, ws, Mf, self.C_last, self.C_last_in)
         else:
-            K.pw_gemm(K.ACT_NONE, K.EPI_FWD, inp_t, f.b(self.w_last), self.bn_last.y, ws, Mf, self.C_last,
-                      self.C_last_in)
+            self._pw_fwd(K.ACT_NONE, inp_t, self.w_last, self.bn_last.y, ws, Mf, self.C_last, self.C_last_in)
         self._fin_fwd(self.bn_last, K.pw_num_partials(Mf, self.C_last, self.C_last_in), train)
         # head (+ its backward when training)
         K.head(self.bn_last.y, self.bn_last.scale, self.bn_last.shift, f.w(self.w_lin), f.w(self.b_lin),

@@ -47,11 +47,11 @@ class NativeTrainStep:
                  rank: int = 0, use_graph: bool = True, seed: int = 0, bucket_mb: float = 4.0,
                  first_bucket_mb: float = 1.0, reduce_dtype: torch.dtype = torch.float32,
                  double_resize: bool = True, augment: bool = True, train_augment: bool = True,
-                 side_stream: bool = True, bn_broadcast: bool = False):
+                 side_stream: bool = True, bn_broadcast: bool = False, fp8: bool = False):
         self.device, self.B, self.S = device, batch, img_size
         self.world, self.rank = world_size, rank
         self.exe = MobileNetV2Executor(model, batch, img_size, device, dropout_seed=(seed * 7919) ^ rank,
-                                       side_stream=side_stream)
+                                       side_stream=side_stream, fp8=fp8)
         self.flat = self.exe.flat
         self.betas, self.eps, self.wd = betas, eps, weight_decay
         self.seed = seed
@@ -88,14 +88,14 @@ class NativeTrainStep:
     # ------------------------------------------------------------------ setup
     @classmethod
     def for_benchmark(cls, model_name: str, batch: int, device, img_size=224, use_graph=True,
-                      world_size=1, rank=0, n_data=50000, side_stream=True):
+                      world_size=1, rank=0, n_data=50000, side_stream=True, fp8=False):
         if model_name != "mobilenet_v2":
             raise NotImplementedError("native executor implements mobilenet_v2; use --backend torch for "
                                       f"{model_name}")
         torch.manual_seed(42)  # identical random-init weights on every rank (then rank-0 broadcast)
         model = build_model("mobilenet_v2", num_classes=10)
         st = cls(model, batch, device, img_size=img_size, world_size=world_size, rank=rank,
-                 use_graph=use_graph, seed=42, side_stream=side_stream)
+                 use_graph=use_graph, seed=42, side_stream=side_stream, fp8=fp8)
         g = torch.Generator(device=device).manual_seed(1234 + rank)
         src = torch.randint(0, 256, (n_data, 32, 32, 3), dtype=torch.uint8, device=device, generator=g)
         labels = torch.randint(0, 10, (n_data,), dtype=torch.int64, device=device, generator=g)

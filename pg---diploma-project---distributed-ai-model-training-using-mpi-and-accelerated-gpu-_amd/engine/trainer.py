@@ -118,7 +118,7 @@ class Trainer:
                                     first_bucket_mb=cfg.first_bucket_mb,
                                     reduce_dtype=torch.bfloat16 if cfg.grad_reduce_dtype == "bf16" else torch.float32,
                                     augment=True, train_augment=cfg.augment != "none",
-                                    bn_broadcast=cfg.bn_sync == "broadcast")
+                                    bn_broadcast=cfg.bn_sync == "broadcast", fp8=cfg.precision == "fp8")
         self.flat = self.step.flat
         self.train_src = torch.from_numpy(self.train_data.images).to(self.device)
         self.train_labels = torch.from_numpy(self.train_data.labels).to(self.device)

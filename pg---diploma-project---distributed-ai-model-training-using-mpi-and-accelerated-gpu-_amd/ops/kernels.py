@@ -212,6 +212,51 @@ def pw_gemm(pro, epi, A, W, out, part, M, N, K, A2=None, pa=None, pb=None, pc=No
                   _p(es), _p(et), _p(R), _p(part), M, N, K, _p(Aout), _s())
 
 
+FP8 = torch.uint8   # raw OCP e4m3fn bytes (torch.float8_e4m3fn views share the encoding)
+
+# activation scale applied before the e4m3 conversion of a GEMM's A operand: ReLU6 outputs
+# lie in [0, 6] (x64 -> [0, 384], inside the normal e4m3 range up to 448); BN-linear /
+# materialised block outputs are O(1) after BatchNorm (x8 -> saturation only beyond |x| = 56)
+FP8_ASC = {ACT_BN_RELU6: 64.0, ACT_BN: 8.0, ACT_NONE: 8.0}
+
+
+def fp8_pitch(K: int) -> int:
+    """Row pitch (bytes) of an e4m3 weight matrix: K rounded up to 64, zero padded."""
+    return (K + 63) // 64 * 64
+
+
+def pw_gemm_f8(pro, A, W8, wsc, out, part, M, N, K, pa=None, pb=None, asc=None):
+    """fp8 forward 1x1 conv: out[M,N] = bf16( (e4m3(asc*prologue(A)) . W8^T) * wsc[n] / asc ).
+
+    W8 is the per-output-channel e4m3 weight copy [N][fp8_pitch(K)] (see :func:`w8_quant`),
+    wsc[n] its dequantisation scale; the BN statistics partials are those of the
+    dequantised output (same contract as :func:`pw_gemm` with EPI_FWD)."""
+    if K % 8 or N % 8:
+        raise ValueError(f"pw_gemm_f8: K={K}, N={N} must be multiples of 8")
+    if pro not in (ACT_NONE, ACT_BN, ACT_BN_RELU6):
+        raise ValueError("pw_gemm_f8: forward prologues only")
+    ld = fp8_pitch(K)
+    _chk(A, BF16, M * K, "A")
+    _chk(W8, FP8, N * ld, "W8")
+    _chk(wsc, F32, N, "wsc")
+    _chk(out, BF16, M * N, "out")
+    _chk(part, F32, pw_num_partials(M, N, K) * 2 * N, "part")
+    if pro != ACT_NONE:
+        assert pa is not None and pb is not None and pa.numel() >= K
+    a = float(FP8_ASC[pro] if asc is None else asc)
+    lib().pw_gemm_f8(int(pro), _p(A), _p(pa), _p(pb), _p(W8), ld, _p(wsc), a, _p(out), _p(part), M, N, K, _s())
+
+
+def w8_quant(src, dst, wsc, tab, n):
+    """Per-output-channel e4m3 quantisation of fp32 1x1 weights, batched over the int32
+    table ``tab`` [n,5] = (src offset, N, K, dst byte offset, scale offset)."""
+    _chk(src, F32, 1, "src")
+    _chk(dst, FP8, 1, "dst")
+    _chk(wsc, F32, 1, "wsc")
+    assert tab.dtype == torch.int32 and tab.is_contiguous() and tab.numel() >= 5 * n
+    lib().w8_quant(_p(src), _p(dst), _p(wsc), _p(tab), int(n), _s())
+
+
 def wt_transpose(src, dst, tab, n):
     """Batched bf16 transpose of 1x1 conv weights: for each row (off, R, C) of the int32
     table ``tab`` [n,3], dst[off + c*R + r] = src[off + r*C + c]."""

@@ -219,6 +219,71 @@ def test_pw_fwd(dev, M, K_, N, pro):
     assert rel(st[1], (ref * ref).sum(0)) < 1e-2
 
 
+def e4m3(x):
+    """fp32 -> OCP e4m3fn (saturating) -> fp32, PyTorch's conversion as the reference."""
+    return x.clamp(-448.0, 448.0).to(torch.float8_e4m3fn).float()
+
+
+def test_w8_quant_matches_torch_e4m3(dev):
+    """Per-output-channel e4m3 weight quantisation: bytes equal PyTorch's float8_e4m3fn
+    encoding of w / (amax/448), rows zero-padded to the 64-byte pitch, two layers in one launch."""
+    shapes = [(96, 24), (1280, 320)]
+    ws = [rnd(n, k, dev=dev, seed=n) * 0.1 for n, k in shapes]
+    ws[0][3].zero_()                                    # all-zero row -> scale 1, zero bytes
+    src = torch.cat([w.flatten() for w in ws])
+    tab, so, do, co = [], 0, 0, 0
+    for n, k in shapes:
+        tab.append([so, n, k, do, co])
+        so += n * k
+        do += n * K.fp8_pitch(k)
+        co += n
+    dst = torch.full((do,), 0xAB, dtype=torch.uint8, device=dev)
+    wsc = torch.zeros(co, device=dev)
+    K.w8_quant(src, dst, wsc, torch.tensor(tab, dtype=torch.int32, device=dev), len(tab))
+    for (n, k), w, (_, _, _, d0, c0) in zip(shapes, ws, tab):
+        ld = K.fp8_pitch(k)
+        amax = w.abs().amax(1)
+        s = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
+        assert torch.allclose(wsc[c0:c0 + n], s)
+        q = dst[d0:d0 + n * ld].view(n, ld)
+        ref = (w / s[:, None]).clamp(-448, 448).to(torch.float8_e4m3fn).view(torch.uint8)
+        assert torch.equal(q[:, :k], ref)
+        assert int(q[:, k:].count_nonzero()) == 0
+
+
+@pytest.mark.parametrize("M,K_,N", [(70001, 16, 96), (100352, 24, 144), (66000, 192, 64), (6272, 960, 160),
+                                    (25088, 64, 384), (3000, 320, 1280), (777, 96, 24)])
+@pytest.mark.parametrize("pro", [K.ACT_NONE, K.ACT_BN_RELU6, K.ACT_BN])
+def test_pw_fwd_fp8(dev, M, K_, N, pro):
+    """fp8 forward GEMM (v_mfma_f32_16x16x32_fp8_fp8): equals the fp32 GEMM of the e4m3-rounded
+    operands (PyTorch float8_e4m3fn conversion) up to the bf16 output rounding."""
+    A = bf(rnd(M, K_, dev=dev, seed=M))
+    s, t = bn_params(K_, dev)
+    W = rnd(N, K_, dev=dev, seed=5) / math.sqrt(K_)
+    ld = K.fp8_pitch(K_)
+    W8 = torch.empty(N * ld, dtype=torch.uint8, device=dev)
+    wsc = torch.empty(N, device=dev)
+    K.w8_quant(W.flatten(), W8, wsc, torch.tensor([[0, N, K_, 0, 0]], dtype=torch.int32, device=dev), 1)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    P = K.pw_num_partials(M, N, K_)
+    part = torch.zeros(P * 2 * N, device=dev)
+    K.pw_gemm_f8(pro, A, W8, wsc, out, part, M, N, K_, pa=s, pb=t)
+    asc = K.FP8_ASC[pro]
+    x = A.float()
+    if pro == K.ACT_BN_RELU6:
+        x = relu6(x * s + t)
+    elif pro == K.ACT_BN:
+        x = x * s + t
+    xq = e4m3(x * asc) / asc
+    wq = W8.view(N, ld)[:, :K_].view(torch.float8_e4m3fn).float() * wsc[:, None]
+    ref = xq @ wq.t()
+    assert rel(out, ref) < 6e-3
+    assert rel(ref, x @ W.t()) < 0.08          # e4m3 vs exact: a few % (3 mantissa bits)
+    st = sum_parts(part, P, N)
+    assert rel(st[0], ref.sum(0)) < 1e-2
+    assert rel(st[1], (ref * ref).sum(0)) < 1e-2
+
+
 @pytest.mark.parametrize("M,K_,N", [(70001, 24, 144), (25088, 64, 384), (6272, 320, 1280), (100352, 32, 192)])
 @pytest.mark.parametrize("res", [False, True])
 def test_pw_fwd_block_output(dev, M, K_, N, res):
