@@ -77,6 +77,32 @@ void launch_wgrad_reduce(float *, int, long long, float *, hipStream_t);
 long long bn_part_floats(int, int);
 void register_side_stream(hipStream_t);
 void launch_reduce_metrics(const float *, const float *, int, double *, hipStream_t);
+// ---- dense convolutions (ResNet-50), kernels/conv.hip ----
+int conv_fwd_num_partials(int, int, int, int, int, int);
+int conv_dgrad_num_partials(int, int, int, int, int, int, int, int);
+void launch_conv_fwd(int, const bf16_t *, const float *, const float *, const bf16_t *, bf16_t *, float *, int,
+                     int, int, int, int, int, int, int, int, hipStream_t);
+void launch_conv_dgrad(int, const bf16_t *, const bf16_t *, const float *, const float *, const float *,
+                       const bf16_t *, bf16_t *, const bf16_t *, const float *, const float *, const bf16_t *,
+                       const bf16_t *, const bf16_t *, float *, float *, int, int, int, int, int, int, int, int,
+                       int, hipStream_t);
+long long conv_wgrad_workspace_floats(int, int, int, int, int, int, int, int, int);
+void launch_conv_wgrad(const bf16_t *, const bf16_t *, const float *, const float *, const float *,
+                       const bf16_t *, const float *, const float *, int, float *, float *, int, int, int, int,
+                       int, int, int, int, int, hipStream_t);
+void launch_conv_wt(const bf16_t *, bf16_t *, const int *, int, hipStream_t);
+void launch_res_out(const bf16_t *, const float *, const float *, const bf16_t *, const float *, const float *,
+                    bf16_t *, long long, int, hipStream_t);
+void launch_maxpool_fwd(const bf16_t *, const float *, const float *, bf16_t *, uint8_t *, int, int, int, int,
+                        hipStream_t);
+int maxpool_bwd_num_partials(int, int, int);
+void launch_maxpool_bwd(const bf16_t *, const uint8_t *, const bf16_t *, const float *, const float *, bf16_t *,
+                        float *, int, int, int, int, hipStream_t);
+void launch_avgpool(const bf16_t *, float *, int, int, int, hipStream_t);
+void launch_head_bwd(const float *, const bf16_t *, const bf16_t *, bf16_t *, float *, int, int, int, hipStream_t);
+void launch_softmax_ce(const float *, const long long *, int, int, float, float *, float *, float *, hipStream_t);
+void launch_image_prep(const uint8_t *, const long long *, const long long *, int, int, int, unsigned long long,
+                       const float *, bf16_t *, long long *, hipStream_t);
 
 template <typename T>
 static T *ptr(P p) { return reinterpret_cast<T *>(p); }
@@ -214,6 +240,62 @@ PYBIND11_MODULE(_pgdist_C, m) {
     launch_augment(ptr<unsigned char>(src), ptr<long long>(idx), ptr<long long>(labels_src), nsrc, B,
                    out_hw, train, double_resize, ptr<float>(params), seed, ptr<float>(hyper),
                    epoch_ctr, ptr<bf16_t>(out), ptr<long long>(labels_out), ptr<float>(params_out), S(s));
+  });
+
+  // ---- dense convolutions (ResNet-50) ----
+  m.def("conv_fwd_num_partials", &conv_fwd_num_partials);
+  m.def("conv_dgrad_num_partials", &conv_dgrad_num_partials);
+  m.def("conv_fwd", [](int pro, P x, P pa, P pb, P w, P y, P part, int Nb, int H, int W, int Ci, int N, int R,
+                       int Sk, int st, int pad, P s) {
+    launch_conv_fwd(pro, ptr<bf16_t>(x), ptr<float>(pa), ptr<float>(pb), ptr<bf16_t>(w), ptr<bf16_t>(y),
+                    ptr<float>(part), Nb, H, W, Ci, N, R, Sk, st, pad, S(s));
+  });
+  m.def("conv_dgrad", [](int epi, P G, P Y, P ga, P gb, P gc, P wt, P dx, P Yt, P es, P et, P Rg, P X, P Yt2,
+                         P part, P part2, int Nb, int H, int W, int Cin, int Cout, int R, int Sk, int st, int pad,
+                         P s) {
+    launch_conv_dgrad(epi, ptr<bf16_t>(G), ptr<bf16_t>(Y), ptr<float>(ga), ptr<float>(gb), ptr<float>(gc),
+                      ptr<bf16_t>(wt), ptr<bf16_t>(dx), ptr<bf16_t>(Yt), ptr<float>(es), ptr<float>(et),
+                      ptr<bf16_t>(Rg), ptr<bf16_t>(X), ptr<bf16_t>(Yt2), ptr<float>(part), ptr<float>(part2), Nb,
+                      H, W, Cin, Cout, R, Sk, st, pad, S(s));
+  });
+  m.def("conv_wgrad_workspace_floats", &conv_wgrad_workspace_floats);
+  m.def("conv_wgrad", [](P G, P Y, P ga, P gb, P gc, P x, P xs, P xt, int xpro, P ws, P grad, int Nb, int H,
+                         int W, int Ci, int N, int R, int Sk, int st, int pad, P s) {
+    launch_conv_wgrad(ptr<bf16_t>(G), ptr<bf16_t>(Y), ptr<float>(ga), ptr<float>(gb), ptr<float>(gc),
+                      ptr<bf16_t>(x), ptr<float>(xs), ptr<float>(xt), xpro, ptr<float>(ws), ptr<float>(grad), Nb,
+                      H, W, Ci, N, R, Sk, st, pad, S(s));
+  });
+  m.def("conv_wt", [](P src, P dst, P tab, int n, P s) {
+    launch_conv_wt(ptr<bf16_t>(src), ptr<bf16_t>(dst), ptr<int>(tab), n, S(s));
+  });
+  m.def("res_out", [](P y, P sc, P sh, P r, P rs, P rt, P out, long long M, int C, P s) {
+    launch_res_out(ptr<bf16_t>(y), ptr<float>(sc), ptr<float>(sh), ptr<bf16_t>(r), ptr<float>(rs),
+                   ptr<float>(rt), ptr<bf16_t>(out), M, C, S(s));
+  });
+  m.def("maxpool_fwd", [](P y, P sc, P sh, P out, P idx, int Nb, int H, int W, int C, P s) {
+    launch_maxpool_fwd(ptr<bf16_t>(y), ptr<float>(sc), ptr<float>(sh), ptr<bf16_t>(out), ptr<uint8_t>(idx), Nb,
+                       H, W, C, S(s));
+  });
+  m.def("maxpool_bwd_num_partials", &maxpool_bwd_num_partials);
+  m.def("maxpool_bwd", [](P gp, P idx, P y, P sc, P sh, P g, P part, int Nb, int H, int W, int C, P s) {
+    launch_maxpool_bwd(ptr<bf16_t>(gp), ptr<uint8_t>(idx), ptr<bf16_t>(y), ptr<float>(sc), ptr<float>(sh),
+                       ptr<bf16_t>(g), ptr<float>(part), Nb, H, W, C, S(s));
+  });
+  m.def("avgpool", [](P x, P out, int Nb, int HW, int C, P s) {
+    launch_avgpool(ptr<bf16_t>(x), ptr<float>(out), Nb, HW, C, S(s));
+  });
+  m.def("head_bwd", [](P dpool, P x, P y, P G, P part, int Nb, int HW, int C, P s) {
+    launch_head_bwd(ptr<float>(dpool), ptr<bf16_t>(x), ptr<bf16_t>(y), ptr<bf16_t>(G), ptr<float>(part), Nb,
+                    HW, C, S(s));
+  });
+  m.def("softmax_ce", [](P logits, P labels, int B, int NC, float scale, P loss, P correct, P dlogits, P s) {
+    launch_softmax_ce(ptr<float>(logits), ptr<long long>(labels), B, NC, scale, ptr<float>(loss),
+                      ptr<float>(correct), ptr<float>(dlogits), S(s));
+  });
+  m.def("image_prep", [](P src, P idx, P lab_src, int B, int H, int W, unsigned long long seed, P hyper, P out,
+                         P lab_out, P s) {
+    launch_image_prep(ptr<uint8_t>(src), ptr<long long>(idx), ptr<long long>(lab_src), B, H, W, seed,
+                      ptr<float>(hyper), ptr<bf16_t>(out), ptr<long long>(lab_out), S(s));
   });
 
   // ---- native runtime (host) ----

@@ -1,0 +1,1165 @@
+// Dense convolutions for ResNet-50 (BASELINE.json config 4) on gfx950 MFMA.
+//
+// The reference trains through cuDNN ("cuDNN conv fwd/bwd"); here every
+// dense convolution of a bottleneck network (7x7 s2 stem, 1x1, 3x3 s1/s2, 1x1 s2
+// projection shortcut) is an NHWC implicit GEMM on v_mfma_f32_16x16x32_bf16:
+//
+//   forward   y[m][n]  = sum_k A[m][k] W[n][k]        m = (b, oh, ow), k = (r, s, ci)
+//             A gathered from x at (oh*st - pad + r, ow*st - pad + s), zero outside;
+//             optional BN+ReLU of the producer applied while the tile is staged
+//             (padding stays zero); epilogue: bf16 y + per-tile BN partial sums.
+//   dgrad     dx = conv^T(dy): the output pixels are split into st x st parity classes;
+//             class (ph, pw) only meets the taps with (ph + pad - r) % st == 0, so a
+//             stride-2 3x3 layer does 9 taps of work over its 4 classes instead of 36
+//             (no MFMA time on the structural zeros of the transposed convolution).
+//             A = BN-backward(dy) (a*G + b*Y + c, this layer's BN) applied while staging;
+//             B = W^T [ci][r][s][co] (transposed once per step); epilogue: ReLU mask of
+//             the producer's BN (+ BN partials), or (acc + shortcut grad) * (x > 0) with
+//             partials against up to two pre-BN tensors (bn3 and the projection BN of
+//             the previous block share that gradient).
+//   wgrad     dW[n][k] = sum_m dy[m][n] x[m][k]: split over m (deterministic partial
+//             slabs + one reduction launch), both operands transposed into m-contiguous
+//             LDS rows while staged, BN-backward on dy and BN+ReLU on x in the staging pass.
+//
+// Tiles: 4 waves (2 x 2), BM x BN in {128, 64}^2, k-steps of 32 or 64 bf16 with both
+// operand tiles double-buffered in LDS and the next step's global loads in flight during
+// the current step's MFMAs.  When Ci % KSTEP == 0 a k-step lies inside one filter tap, so
+// the tap decomposition is one scalar division per step.  Workgroup ids put the N tiles
+// of one M tile 8 ids apart (same XCD L2; T1 of the CDNA guide).
+#include "../common.h"
+
+#include <cstdlib>
+#include <type_traits>
+
+namespace {
+enum { CM_FWD = 0, CM_DGRAD = 1 };
+enum { CP_NONE = 0, CP_BN_RELU = 1, CP_BNBWD = 3 };
+enum { CE_FWD = 0, CE_BWD_RELU = 1, CE_BWD_RES = 2 };
+
+struct ConvArgs {
+  const bf16_t *A;      // gathered image [Nb][Hi][Wi][Ci]  (fwd: x, dgrad: G of this layer's BN)
+  const bf16_t *A2;     // dgrad: pre-BN output Y of this layer (same layout as A)
+  const float *pa, *pb, *pc;   // per-Ci prologue parameters
+  const bf16_t *W;      // fwd: [N][R][S][Ci] ; dgrad: [N=Cin][R][S][Ci=Cout]
+  bf16_t *out;          // [Nb][Ho][Wo][N]
+  const bf16_t *Yt;     // epilogue statistics partner [Nb][Ho][Wo][N]
+  const bf16_t *Yt2;    // second partner (CE_BWD_RES)
+  const bf16_t *X;      // CE_BWD_RES: mask tensor (x > 0), may be null
+  const bf16_t *Rg;     // CE_BWD_RES: added gradient, may be null
+  const float *es, *et; // CE_BWD_RELU: producer BN scale / shift (mask y*s+t > 0)
+  float *part, *part2;  // [P][2][N]
+  int Hi, Wi, Ci;
+  int Ho, Wo, N;
+  int R, S, stride, pad;
+  int Kw;               // weight row pitch (elements)
+  int K;                // GEMM K of class 0 (fwd) ; dgrad: per class ntap * Ci
+  int Mc;               // GEMM rows per class
+  int Hc, Wc;           // dgrad: class image (Ho / st, Wo / st); fwd: Ho, Wo
+  int nmt;              // M tiles per class
+  int ntap[4];
+  signed char tr[4][9], ts[4][9], tdh[4][9], tdw[4][9];
+};
+
+// 16x16x32 bf16 MFMA on raw 8 x bf16 fragments
+PG_DEVICE f32x4_t mfma16(const s16x8_t &a, const s16x8_t &b, const f32x4_t &c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
+                                                 0, 0, 0);
+}
+
+PG_DEVICE float reluf(float x) { return fmaxf(x, 0.f); }
+
+// load 8 floats (two float4) of a per-channel vector
+PG_DEVICE void ld8f(const float *p, float (&v)[8]) {
+  const float4 a = *reinterpret_cast<const float4 *>(p), b = *reinterpret_cast<const float4 *>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+}  // namespace
+
+// ===========================================================================
+// forward / dgrad implicit GEMM
+// ===========================================================================
+// CV: channels per gathered chunk (8 = one 16-B load; 4 = the 4-channel padded stem input,
+// one 8-B load per chunk).  UT: Ci % KSTEP == 0 (uniform tap per k-step).
+template <int MODE, int PRO, int EPI, int BM, int BN, int KSTEP, int CV, bool UT>
+__global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs p) {
+  static_assert(CV == 8 || (CV == 4 && PRO == CP_NONE && MODE == CM_FWD), "4-channel chunks: stem forward only");
+  constexpr int kLDK = KSTEP + 8;                    // staged row pitch (bf16): 16-B pad
+  constexpr int KCH = KSTEP / CV;                    // chunks per staged row
+  constexpr int RT = BM / 32, CTW = BN / 32;         // per-wave 16x16 tiles
+  constexpr int ACH = BM * KCH / 256, BCH = BN * KCH / 256;
+  constexpr int LDC = BN + 8;
+  constexpr int CH = BN / 8, RSTEP = 256 / CH, NP = BM / RSTEP;
+  constexpr bool HAS_A2 = PRO == CP_BNBWD;
+  static_assert(ACH >= 1 && BCH >= 1 && NP >= 1, "tile too small for 256 threads");
+  typedef typename std::conditional<CV == 8, uint4, uint2>::type chunk_t;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t *As = reinterpret_cast<bf16_t *>(smem);     // [2][BM][kLDK]
+  bf16_t *Bs = As + 2 * BM * kLDK;                   // [2][BN][kLDK]
+  bf16_t *Cs = reinterpret_cast<bf16_t *>(smem);     // [BM][LDC] (after the K loop)
+  float *Red = reinterpret_cast<float *>(smem);      // [RSTEP][BN] (end)
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int NT = (p.N + BN - 1) / BN;
+  const int nmt = p.nmt;
+  // workgroup -> (class, mt, nt): N tiles of one M tile 8 ids apart
+  const int cls = MODE == CM_DGRAD ? blockIdx.y : 0;
+  int mt, nt;
+  {
+    const int L = blockIdx.x, full = (nmt / 8) * 8 * NT;
+    if (L < full) {
+      mt = (L / (8 * NT)) * 8 + L % 8;
+      nt = (L / 8) % NT;
+    } else {
+      const int rem = nmt % 8, Lr = L - full;
+      mt = (nmt / 8) * 8 + Lr % rem;
+      nt = Lr / rem;
+    }
+  }
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int ph = MODE == CM_DGRAD ? cls / p.stride : 0, pw = MODE == CM_DGRAD ? cls % p.stride : 0;
+  const int Kc = MODE == CM_DGRAD ? p.ntap[cls] * p.Ci : p.K;
+  const int nk = (Kc + KSTEP - 1) / KSTEP;
+  const int HWc = p.Hc * p.Wc;
+
+  // ---- per-chunk row state (rows are fixed across k-steps)
+  int rb[ACH], rh[ACH], rw[ACH];     // image index, base h, base w; rb < 0: row out of range
+#pragma unroll
+  for (int i = 0; i < ACH; ++i) {
+    const int c = tid + i * 256, row = c / KCH;
+    const int m = m0 + row;
+    if (m < p.Mc) {
+      const int b = m / HWc, rem = m % HWc, hh = rem / p.Wc, ww = rem % p.Wc;
+      rb[i] = b;
+      if constexpr (MODE == CM_FWD) {
+        rh[i] = hh * p.stride - p.pad;
+        rw[i] = ww * p.stride - p.pad;
+      } else {
+        rh[i] = hh;
+        rw[i] = ww;
+      }
+    } else {
+      rb[i] = -1; rh[i] = 0; rw[i] = 0;
+    }
+  }
+
+  chunk_t ra[ACH], ry[HAS_A2 ? ACH : 1], rbw[BCH];
+  bool va[ACH];
+  float pa8[8], pb8[8], pc8[8];
+  // tap of a k offset: (dh, dw, weight tap index)
+  auto tap_of = [&](int j, int &dh, int &dw, int &wt) {
+    if constexpr (MODE == CM_FWD) {
+      const int r = j / p.S, s = j - r * p.S;
+      dh = r; dw = s; wt = j;
+    } else {
+      dh = p.tdh[cls][j]; dw = p.tdw[cls][j];
+      wt = p.tr[cls][j] * p.S + p.ts[cls][j];
+    }
+  };
+  auto load = [&](int k0) {
+    int u_dh = 0, u_dw = 0, u_wt = 0, u_c0 = 0;
+    if constexpr (UT) {
+      const int j = k0 / p.Ci;
+      u_c0 = k0 - j * p.Ci;
+      tap_of(j, u_dh, u_dw, u_wt);
+    }
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int c = tid + i * 256, kk = (c % KCH) * CV;
+      int dh, dw, ci;
+      bool ok = rb[i] >= 0 && k0 + kk < Kc;
+      if constexpr (UT) {
+        dh = u_dh; dw = u_dw; ci = u_c0 + kk;
+      } else {
+        const int k = k0 + kk, j = k / p.Ci;
+        int wt;
+        ci = k - j * p.Ci;
+        if (MODE == CM_FWD && j >= p.R * p.S) ok = false;
+        tap_of(ok ? j : 0, dh, dw, wt);
+      }
+      const int ih = rh[i] + dh, iw = rw[i] + dw;
+      ok = ok && ih >= 0 && ih < p.Hi && iw >= 0 && iw < p.Wi;
+      va[i] = ok;
+      const size_t off = (((size_t)rb[i] * p.Hi + ih) * p.Wi + iw) * p.Ci + ci;
+      if constexpr (CV == 8) {
+        ra[i] = ok ? ldg16(p.A + off) : make_uint4(0, 0, 0, 0);
+        if constexpr (HAS_A2) ry[i] = ok ? ldg16(p.A2 + off) : make_uint4(0, 0, 0, 0);
+      } else {
+        ra[i] = ok ? *reinterpret_cast<const uint2 *>(p.A + off) : make_uint2(0, 0);
+      }
+    }
+    if constexpr (PRO != CP_NONE) {
+      // every chunk of this thread sits at the same kk (ACH rows apart) -> one parameter set
+      const int kk = (tid % KCH) * CV;
+      int ci;
+      if constexpr (UT) ci = u_c0 + kk;
+      else { const int k = k0 + kk; ci = k % p.Ci; }
+      ld8f(p.pa + ci, pa8);
+      ld8f(p.pb + ci, pb8);
+      if constexpr (PRO == CP_BNBWD) ld8f(p.pc + ci, pc8);
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int c = tid + i * 256, n = c / KCH, kk = (c % KCH) * CV;
+      const int gn = n0 + n, k = k0 + kk;
+      bool ok = gn < p.N && k < Kc;
+      size_t off;
+      if constexpr (MODE == CM_FWD) {
+        off = (size_t)gn * p.Kw + k;
+        if constexpr (CV == 4) ok = ok && k < p.Kw;
+      } else {
+        int dh, dw, wt, ci;
+        if constexpr (UT) { dh = u_dh; dw = u_dw; wt = u_wt; ci = u_c0 + kk; }
+        else { const int j = k / p.Ci; ci = k - j * p.Ci; tap_of(ok ? j : 0, dh, dw, wt); }
+        off = (size_t)gn * p.Kw + (size_t)wt * p.Ci + ci;
+      }
+      if constexpr (CV == 8) rbw[i] = ok ? ldg16(p.W + off) : make_uint4(0, 0, 0, 0);
+      else rbw[i] = ok ? *reinterpret_cast<const uint2 *>(p.W + off) : make_uint2(0, 0);
+    }
+  };
+  auto write = [&](int buf) {
+    bf16_t *Ab = As + buf * BM * kLDK;
+    bf16_t *Bb = Bs + buf * BN * kLDK;
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int c = tid + i * 256, row = c / KCH, kk = (c % KCH) * CV;
+      if constexpr (CV == 8) {
+        uint4 v = ra[i];
+        if constexpr (PRO != CP_NONE) {
+          float x[8];
+          unpack8(ra[i], x);
+          if constexpr (PRO == CP_BNBWD) {
+            float y[8];
+            unpack8(ry[i], y);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) x[j] = fmaf(pa8[j], x[j], fmaf(pb8[j], y[j], pc8[j]));
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) x[j] = reluf(fmaf(x[j], pa8[j], pb8[j]));
+          }
+          if (!va[i]) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) x[j] = 0.f;
+          }
+          v = pack8(x);
+        }
+        *reinterpret_cast<uint4 *>(Ab + row * kLDK + kk) = v;
+      } else {
+        *reinterpret_cast<uint2 *>(Ab + row * kLDK + kk) = ra[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int c = tid + i * 256, n = c / KCH, kk = (c % KCH) * CV;
+      if constexpr (CV == 8) *reinterpret_cast<uint4 *>(Bb + n * kLDK + kk) = rbw[i];
+      else *reinterpret_cast<uint2 *>(Bb + n * kLDK + kk) = rbw[i];
+    }
+  };
+
+  f32x4_t acc[RT][CTW];
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int c = 0; c < CTW; ++c) acc[r][c] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) {
+    load(0);
+    write(0);
+  }
+  __syncthreads();
+  for (int ks = 0; ks < nk; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nk) load((ks + 1) * KSTEP);
+    const bf16_t *Ab = As + buf * BM * kLDK;
+    const bf16_t *Bb = Bs + buf * BN * kLDK;
+#pragma unroll
+    for (int sub = 0; sub < KSTEP / 32; ++sub) {
+      s16x8_t af[RT];
+#pragma unroll
+      for (int r = 0; r < RT; ++r)
+        af[r] = *reinterpret_cast<const s16x8_t *>(Ab + (wm * (BM / 2) + r * 16 + (lane & 15)) * kLDK + sub * 32 +
+                                                   8 * (lane >> 4));
+#pragma unroll
+      for (int c = 0; c < CTW; ++c) {
+        const s16x8_t bf = *reinterpret_cast<const s16x8_t *>(Bb + (wn * (BN / 2) + c * 16 + (lane & 15)) * kLDK +
+                                                              sub * 32 + 8 * (lane >> 4));
+#pragma unroll
+        for (int r = 0; r < RT; ++r) acc[r][c] = mfma16(af[r], bf, acc[r][c]);
+      }
+    }
+    if (ks + 1 < nk) write(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: bf16 C tile in LDS, then 16-B row chunks
+#pragma unroll
+  for (int c = 0; c < CTW; ++c) {
+    const int col = wn * (BN / 2) + c * 16 + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) Cs[(wm * (BM / 2) + r * 16 + 4 * (lane >> 4) + j) * LDC + col] = f2bf(acc[r][c][j]);
+  }
+  __syncthreads();
+  const int my_chunk = tid % CH, ncol0 = n0 + my_chunk * 8;
+  const bool colok = ncol0 < p.N;
+  float s0[8], s1[8], s2[8], es[8], et[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s0[j] = s1[j] = s2[j] = 0.f;
+  if constexpr (EPI == CE_BWD_RELU) {
+    if (colok) { ld8f(p.es + ncol0, es); ld8f(p.et + ncol0, et); }
+  }
+  const bool has_yt = EPI == CE_FWD || p.Yt != nullptr;
+  const bool has_yt2 = EPI == CE_BWD_RES && p.Yt2 != nullptr;
+#pragma unroll 2
+  for (int i0 = 0; i0 < NP; ++i0) {
+    const int rr = tid / CH + i0 * RSTEP, m = m0 + rr;
+    if (m >= p.Mc || !colok) continue;
+    size_t pix;
+    if constexpr (MODE == CM_FWD) {
+      pix = m;
+    } else {
+      const int b = m / HWc, rem = m % HWc, hh = rem / p.Wc, ww = rem % p.Wc;
+      pix = ((size_t)b * p.Ho + hh * p.stride + ph) * p.Wo + ww * p.stride + pw;
+    }
+    const size_t off = pix * p.N + ncol0;
+    float v[8];
+    unpack8(*reinterpret_cast<const uint4 *>(Cs + rr * LDC + my_chunk * 8), v);
+    if constexpr (EPI == CE_FWD) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { s0[j] += v[j]; s1[j] = fmaf(v[j], v[j], s1[j]); }
+    } else if constexpr (EPI == CE_BWD_RELU) {
+      float yt[8];
+      unpack8(ldg16(p.Yt + off), yt);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[j] = fmaf(yt[j], es[j], et[j]) > 0.f ? v[j] : 0.f;
+        v[j] = bf2f(f2bf(v[j]));
+        s0[j] += v[j];
+        s1[j] = fmaf(v[j], yt[j], s1[j]);
+      }
+    } else {
+      if (p.Rg) {
+        float rv[8];
+        unpack8(ldg16(p.Rg + off), rv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += rv[j];
+      }
+      if (p.X) {
+        float xv[8];
+        unpack8(ldg16(p.X + off), xv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = xv[j] > 0.f ? v[j] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = bf2f(f2bf(v[j]));
+      if (has_yt) {
+        float yt[8];
+        unpack8(ldg16(p.Yt + off), yt);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { s0[j] += v[j]; s1[j] = fmaf(v[j], yt[j], s1[j]); }
+      }
+      if (has_yt2) {
+        float y2[8];
+        unpack8(ldg16(p.Yt2 + off), y2);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s2[j] = fmaf(v[j], y2[j], s2[j]);
+      }
+    }
+    stg16(p.out + off, pack8(v));
+  }
+  if (!has_yt) return;   // uniform: no statistics requested
+  __syncthreads();
+  // ---- BN partials of this tile's columns -> part[cls*nmt + mt][2][N] (and part2)
+  const int prow = cls * nmt + mt;
+  const int nstat = has_yt2 ? 3 : 2;
+  for (int s = 0; s < nstat; ++s) {
+    const int rgrp = tid / CH;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Red[rgrp * BN + my_chunk * 8 + j] = s == 0 ? s0[j] : (s == 1 ? s1[j] : s2[j]);
+    __syncthreads();
+    for (int c = tid; c < BN; c += 256) {
+      float a = 0.f;
+      for (int g = 0; g < RSTEP; ++g) a += Red[g * BN + c];
+      if (n0 + c < p.N) {
+        if (s < 2) p.part[((size_t)prow * 2 + s) * p.N + n0 + c] = a;
+        if (s == 0 && has_yt2) p.part2[((size_t)prow * 2) * p.N + n0 + c] = a;
+        if (s == 2) p.part2[((size_t)prow * 2 + 1) * p.N + n0 + c] = a;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ===========================================================================
+// weight gradient (split over m):  part[z][n][k] = sum_{m in split z} dy[m][n] * x[m][k]
+//   dy = a[n]*G + b[n]*Y + c[n]      (this layer's BN backward)
+//   x  = gather(X) at the forward taps, with ReLU(BN of the producer) (XPRO) or as stored
+// ===========================================================================
+namespace {
+struct WgArgs {
+  const bf16_t *G, *Y;
+  const float *ga, *gb, *gc;
+  const bf16_t *X;
+  const float *xs, *xt;
+  float *out;           // [nsplit][N][Kw]  (or the gradient itself when nsplit == 1)
+  int N;                // output channels (dy channels)
+  int Hi, Wi, Ci;       // x image
+  int Ho, Wo;           // dy image
+  int R, S, stride, pad;
+  int Kw;               // R*S*Ci
+  int M;                // Nb*Ho*Wo
+  int rows_per_split;
+};
+constexpr int kWgMK = 32;             // m rows per step
+constexpr int kWgLD = kWgMK + 8;      // transposed row pitch (bf16)
+}  // namespace
+
+template <int XPRO, int TN, int TK, int CV>
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs p) {
+  constexpr int QN = TN / 2, QK = TK / 2, RN = QN / 16, RK = QK / 16;
+  constexpr int M4 = kWgMK / 4;
+  constexpr int IDY = M4 * (TN / 8), IX = M4 * (TK / 8);   // items: 4 rows x 8 columns
+  constexpr int PD = (IDY + 255) / 256, PX = (IX + 255) / 256;
+  static_assert(IDY % 64 == 0 && IX % 64 == 0, "items are handed out in whole waves");
+  __shared__ __attribute__((aligned(16))) bf16_t Tdy[2][TN * kWgLD];
+  __shared__ __attribute__((aligned(16))) bf16_t Tx[2][TK * kWgLD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave >> 1, wk = wave & 1;
+  const int n0 = blockIdx.x * TN, k0 = blockIdx.y * TK;
+  const int mbeg = blockIdx.z * p.rows_per_split;
+  const int mend = min(p.M, mbeg + p.rows_per_split);
+  const int HWo = p.Ho * p.Wo;
+  // dy items on threads [0, IDY), x items start at thread IDY % 256 (whole waves either way)
+  const int xtid = (tid + 256 - (IDY % 256)) % 256;
+
+  // ---- dy items: fixed (m4, 8 output channels)
+  int d_col[PD], d_m4[PD];
+  bool d_on[PD];
+  float ga8[PD][8], gb8[PD][8], gc8[PD][8];
+#pragma unroll
+  for (int i = 0; i < PD; ++i) {
+    const int it = tid + i * 256;
+    d_on[i] = it < IDY;
+    d_m4[i] = it % M4;
+    d_col[i] = n0 + (it / M4) * 8;
+    const bool ok = d_on[i] && d_col[i] < p.N;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ga8[i][j] = gb8[i][j] = gc8[i][j] = 0.f;
+    if (ok) {
+      ld8f(p.ga + d_col[i], ga8[i]);
+      ld8f(p.gb + d_col[i], gb8[i]);
+      ld8f(p.gc + d_col[i], gc8[i]);
+    }
+  }
+  // ---- x items: fixed (m4, 8 columns of k = (r, s, ci)); CV == 4: two taps of 4 channels
+  constexpr int NH = CV == 8 ? 1 : 2;
+  int x_col[PX], x_m4[PX], x_dh[PX][NH], x_dw[PX][NH], x_ci[PX][NH];
+  bool x_on[PX], x_kok[PX][NH];
+  float xs8[PX][8], xt8[PX][8];
+#pragma unroll
+  for (int i = 0; i < PX; ++i) {
+    const int xi = xtid + i * 256;
+    x_on[i] = xi < IX;
+    x_m4[i] = xi % M4;
+    const int k = k0 + (xi / M4) * 8;
+    x_col[i] = k;
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+      const int kh = k + 4 * h;
+      const int j = kh / p.Ci;
+      x_kok[i][h] = x_on[i] && kh < p.Kw;
+      x_ci[i][h] = kh - j * p.Ci;
+      const int r = j / p.S;
+      x_dh[i][h] = r - p.pad;
+      x_dw[i][h] = j - r * p.S - p.pad;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xs8[i][j] = xt8[i][j] = 0.f;
+    if constexpr (XPRO == CP_BN_RELU) {
+      if (x_kok[i][0]) {
+        ld8f(p.xs + x_ci[i][0], xs8[i]);
+        ld8f(p.xt + x_ci[i][0], xt8[i]);
+      }
+    }
+  }
+
+  f32x4_t acc[RN][RK];
+#pragma unroll
+  for (int a = 0; a < RN; ++a)
+#pragma unroll
+    for (int b = 0; b < RK; ++b) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  uint4 dg[PD][4], dyv[PD][4], xv[PX][4];
+  uint32_t dvm[PD], xvm[PX];   // validity bits of the staged rows
+  auto load_step = [&](int m0) {
+#pragma unroll
+    for (int i = 0; i < PD; ++i) {
+      const int mr = m0 + d_m4[i] * 4;
+      const bool cok = d_on[i] && d_col[i] < p.N;
+      dvm[i] = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool ok = cok && mr + q < mend;
+        dvm[i] |= ok ? 1u << q : 0u;
+        const size_t off = (size_t)(mr + q) * p.N + d_col[i];
+        dg[i][q] = ok ? ldg16(p.G + off) : make_uint4(0, 0, 0, 0);
+        dyv[i][q] = ok ? ldg16(p.Y + off) : make_uint4(0, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < PX; ++i) {
+      int m = m0 + x_m4[i] * 4;
+      int b = m / HWo, rem = m - b * HWo, oh = rem / p.Wo, ow = rem - oh * p.Wo;
+      xvm[i] = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool mok = x_on[i] && m < mend;
+        const int bh = oh * p.stride, bw = ow * p.stride;
+        if constexpr (CV == 8) {
+          const int ih = bh + x_dh[i][0], iw = bw + x_dw[i][0];
+          const bool ok = mok && x_kok[i][0] && ih >= 0 && ih < p.Hi && iw >= 0 && iw < p.Wi;
+          xvm[i] |= ok ? 1u << q : 0u;
+          xv[i][q] = ok ? ldg16(p.X + (((size_t)b * p.Hi + ih) * p.Wi + iw) * p.Ci + x_ci[i][0])
+                        : make_uint4(0, 0, 0, 0);
+        } else {
+          uint2 h2[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int ih = bh + x_dh[i][h], iw = bw + x_dw[i][h];
+            const bool ok = mok && x_kok[i][h] && ih >= 0 && ih < p.Hi && iw >= 0 && iw < p.Wi;
+            h2[h] = ok ? *reinterpret_cast<const uint2 *>(p.X + (((size_t)b * p.Hi + ih) * p.Wi + iw) * p.Ci +
+                                                          x_ci[i][h])
+                       : make_uint2(0, 0);
+          }
+          xv[i][q] = make_uint4(h2[0].x, h2[0].y, h2[1].x, h2[1].y);
+        }
+        ++m; ++ow;
+        if (ow == p.Wo) { ow = 0; ++oh; if (oh == p.Ho) { oh = 0; ++b; } }
+      }
+    }
+  };
+  // 4 rows x 8 columns -> T[col][m] (8 x ds_write_b64)
+  auto put = [&](bf16_t *T, int tcol, int tm, const float (&v)[4][8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      uint2 w;
+      w.x = pack2(v[0][j], v[1][j]);
+      w.y = pack2(v[2][j], v[3][j]);
+      *reinterpret_cast<uint2 *>(T + (tcol + j) * kWgLD + tm) = w;
+    }
+  };
+  auto write_step = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < PD; ++i) {
+      if (!d_on[i]) continue;
+      float v[4][8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float g[8], y[8];
+        unpack8(dg[i][q], g);
+        unpack8(dyv[i][q], y);
+        const bool ok = (dvm[i] >> q) & 1u;   // a*0 + b*0 + c != 0: invalid rows must be zeroed
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[q][j] = ok ? fmaf(ga8[i][j], g[j], fmaf(gb8[i][j], y[j], gc8[i][j])) : 0.f;
+      }
+      put(Tdy[buf], d_col[i] - n0, d_m4[i] * 4, v);
+    }
+#pragma unroll
+    for (int i = 0; i < PX; ++i) {
+      if (!x_on[i]) continue;
+      float v[4][8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        unpack8(xv[i][q], v[q]);
+        if constexpr (XPRO == CP_BN_RELU) {
+          const bool ok = (xvm[i] >> q) & 1u;   // padding stays zero (not relu(shift))
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[q][j] = ok ? reluf(fmaf(v[q][j], xs8[i][j], xt8[i][j])) : 0.f;
+        }
+      }
+      put(Tx[buf], x_col[i] - k0, x_m4[i] * 4, v);
+    }
+  };
+
+  int buf = 0;
+  if (mbeg < mend) {
+    load_step(mbeg);
+    write_step(0);
+  }
+  __syncthreads();
+  for (int m0 = mbeg; m0 < mend; m0 += kWgMK) {
+    const bool has_next = m0 + kWgMK < mend;
+    if (has_next) load_step(m0 + kWgMK);
+    const bf16_t *Td = Tdy[buf], *Tq = Tx[buf];
+    s16x8_t af[RN], bfr[RK];
+#pragma unroll
+    for (int a = 0; a < RN; ++a)
+      af[a] = *reinterpret_cast<const s16x8_t *>(Td + (wn * QN + a * 16 + (lane & 15)) * kWgLD + 8 * (lane >> 4));
+#pragma unroll
+    for (int b = 0; b < RK; ++b)
+      bfr[b] = *reinterpret_cast<const s16x8_t *>(Tq + (wk * QK + b * 16 + (lane & 15)) * kWgLD + 8 * (lane >> 4));
+#pragma unroll
+    for (int a = 0; a < RN; ++a)
+#pragma unroll
+      for (int b = 0; b < RK; ++b) acc[a][b] = mfma16(af[a], bfr[b], acc[a][b]);
+    if (has_next) write_step(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  float *dst = p.out + (size_t)blockIdx.z * p.N * p.Kw;
+#pragma unroll
+  for (int a = 0; a < RN; ++a)
+#pragma unroll
+    for (int b = 0; b < RK; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wn * QN + a * 16 + 4 * (lane >> 4) + j;
+        const int k = k0 + wk * QK + b * 16 + (lane & 15);
+        if (n < p.N && k < p.Kw) dst[(size_t)n * p.Kw + k] = acc[a][b][j];
+      }
+}
+
+
+// ===========================================================================
+// weight transposes for dgrad: dst[ci][t][co] = src[co][t][ci]  (bf16, batched by table)
+// tab int32 [n][5] = (src offset, dst offset, Cout, taps, Cin)
+// ===========================================================================
+__global__ __launch_bounds__(256) void conv_wt_kernel(const bf16_t *__restrict__ src, bf16_t *__restrict__ dst,
+                                                      const int *__restrict__ tab) {
+  __shared__ bf16_t T[32][33];
+  const int *e = tab + blockIdx.y * 5;
+  const long long so = e[0], dof = e[1];
+  const int Co = e[2], RS = e[3], Ci = e[4];
+  const int tco = (Co + 31) / 32, tci = (Ci + 31) / 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int t = blockIdx.x; t < tco * tci * RS; t += gridDim.x) {
+    const int tap = t / (tco * tci), rem = t % (tco * tci);
+    const int co0 = (rem / tci) * 32, ci0 = (rem % tci) * 32;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int co = co0 + ty + 8 * i, ci = ci0 + tx;
+      T[ty + 8 * i][tx] = (co < Co && ci < Ci) ? src[so + ((long long)co * RS + tap) * Ci + ci] : bf16_t(0);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ci = ci0 + ty + 8 * i, co = co0 + tx;
+      if (co < Co && ci < Ci) dst[dof + ((long long)ci * RS + tap) * Co + co] = T[tx][ty + 8 * i];
+    }
+    __syncthreads();
+  }
+}
+
+// ===========================================================================
+// bottleneck output:  o = relu(y3*s3 + t3 + (yd*sd + td  |  x))       [M][C]
+// ===========================================================================
+template <bool PROJ>
+__global__ __launch_bounds__(256) void res_out_kernel(const bf16_t *__restrict__ y, const float *__restrict__ s,
+                                                      const float *__restrict__ t, const bf16_t *__restrict__ r,
+                                                      const float *__restrict__ rs, const float *__restrict__ rt,
+                                                      bf16_t *__restrict__ out, long long n8, int C8) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % C8) * 8;
+    float v[8], rv[8], a[8], b[8];
+    unpack8(ldg16(y + i * 8), v);
+    unpack8(ldg16(r + i * 8), rv);
+    ld8f(s + c0, a);
+    ld8f(t + c0, b);
+    if constexpr (PROJ) {
+      float ra[8], rb[8];
+      ld8f(rs + c0, ra);
+      ld8f(rt + c0, rb);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) rv[k] = fmaf(rv[k], ra[k], rb[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = reluf(fmaf(v[k], a[k], b[k]) + rv[k]);
+    stg16(out + i * 8, pack8(v));
+  }
+}
+
+// ===========================================================================
+// 3x3 s2 p1 max-pool of relu(bn(y)) (stem output), forward with the arg-max tap (uint8)
+// and backward (gather over the <= 4 windows that contain an input pixel) fused with the
+// stem BN's ReLU mask and its backward partial sums.  8 channels per thread.
+// ===========================================================================
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16_t *__restrict__ y, const float *__restrict__ s,
+                                                          const float *__restrict__ t, bf16_t *__restrict__ out,
+                                                          uint8_t *__restrict__ idx, int Nb, int H, int W, int C,
+                                                          int Ho, int Wo) {
+  const int C8 = C / 8;
+  const long long total = (long long)Nb * Ho * Wo * C8;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % C8) * 8;
+    const long long pix = i / C8;
+    const int ow = (int)(pix % Wo), oh = (int)((pix / Wo) % Ho), b = (int)(pix / ((long long)Wo * Ho));
+    float a[8], sh[8], best[8];
+    int bi[8];
+    ld8f(s + c0, a);
+    ld8f(t + c0, sh);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { best[k] = -1.f; bi[k] = 0; }
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int ih = oh * 2 - 1 + r, iw = ow * 2 - 1 + q;
+        if (ih < 0 || ih >= H || iw < 0 || iw >= W) continue;
+        float v[8];
+        unpack8(ldg16(y + (((size_t)b * H + ih) * W + iw) * C + c0), v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float z = reluf(fmaf(v[k], a[k], sh[k]));
+          if (z > best[k]) { best[k] = z; bi[k] = r * 3 + q; }
+        }
+      }
+    stg16(out + pix * C + c0, pack8(best));
+    uint2 u;
+    u.x = (uint32_t)bi[0] | ((uint32_t)bi[1] << 8) | ((uint32_t)bi[2] << 16) | ((uint32_t)bi[3] << 24);
+    u.y = (uint32_t)bi[4] | ((uint32_t)bi[5] << 8) | ((uint32_t)bi[6] << 16) | ((uint32_t)bi[7] << 24);
+    *reinterpret_cast<uint2 *>(idx + pix * C + c0) = u;
+  }
+}
+
+// one workgroup per (image, strip of rows): 256 threads = 32 pixels x 8 channel chunks (C = 64)
+// part[blockIdx][2][C]: sum g, sum g*y
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16_t *__restrict__ gp, const uint8_t *__restrict__ idx,
+                                                          const bf16_t *__restrict__ y, const float *__restrict__ s,
+                                                          const float *__restrict__ t, bf16_t *__restrict__ g,
+                                                          float *__restrict__ part, int Nb, int H, int W, int C,
+                                                          int Ho, int Wo, int pix_per_wg) {
+  __shared__ float red[2][32][64];
+  const int C8 = C / 8;   // == 8
+  const int cc = threadIdx.x % C8, pl = threadIdx.x / C8, PPI = 256 / C8;
+  const int c0 = cc * 8;
+  float a[8], sh[8], s0[8], s1[8];
+  ld8f(s + c0, a);
+  ld8f(t + c0, sh);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s0[k] = s1[k] = 0.f;
+  const long long total = (long long)Nb * H * W;
+  const long long p0 = (long long)blockIdx.x * pix_per_wg;
+  for (long long pix = p0 + pl; pix < min(total, p0 + pix_per_wg); pix += PPI) {
+    const int w = (int)(pix % W), h = (int)((pix / W) % H), b = (int)(pix / ((long long)W * H));
+    float acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+    // windows (oh, ow) with oh*2-1 <= h <= oh*2+1
+    const int oh_lo = h >= 1 ? (h - 1 + 1) / 2 : 0, oh_hi = min(Ho - 1, (h + 1) / 2);
+    const int ow_lo = w >= 1 ? (w - 1 + 1) / 2 : 0, ow_hi = min(Wo - 1, (w + 1) / 2);
+    for (int oh = oh_lo; oh <= oh_hi; ++oh)
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const int tap = (h - (oh * 2 - 1)) * 3 + (w - (ow * 2 - 1));
+        if (tap < 0 || tap > 8) continue;
+        const size_t o = (((size_t)b * Ho + oh) * Wo + ow) * C + c0;
+        const uint2 u = *reinterpret_cast<const uint2 *>(idx + o);
+        float gv[8];
+        unpack8(ldg16(gp + o), gv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t word = k < 4 ? u.x : u.y;
+          const int ti = (word >> (8 * (k & 3))) & 0xff;
+          if (ti == tap) acc[k] += gv[k];
+        }
+      }
+    float yv[8];
+    const size_t io = pix * C + c0;
+    unpack8(ldg16(y + io), yv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float gk = fmaf(yv[k], a[k], sh[k]) > 0.f ? acc[k] : 0.f;
+      gk = bf2f(f2bf(gk));
+      acc[k] = gk;
+      s0[k] += gk;
+      s1[k] = fmaf(gk, yv[k], s1[k]);
+    }
+    stg16(g + io, pack8(acc));
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { red[0][pl][c0 + k] = s0[k]; red[1][pl][c0 + k] = s1[k]; }
+  __syncthreads();
+  if (threadIdx.x < 2 * C) {
+    const int st = threadIdx.x / C, c = threadIdx.x % C;
+    float v = 0.f;
+    for (int q = 0; q < PPI; ++q) v += red[st][q][c];
+    part[((size_t)blockIdx.x * 2 + st) * C + c] = v;
+  }
+}
+
+// ===========================================================================
+// head: global average pool (fp32 [B][C]) and the pooled-gradient broadcast back
+// through the last ReLU, fused with the last BN's backward partial sums
+// ===========================================================================
+__global__ __launch_bounds__(256) void avgpool_kernel(const bf16_t *__restrict__ x, float *__restrict__ out, int HW,
+                                                      int C) {
+  const int b = blockIdx.x;
+  for (int c8 = threadIdx.x; c8 < C / 8; c8 += blockDim.x) {
+    float acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+    for (int i = 0; i < HW; ++i) {
+      float v[8];
+      unpack8(ldg16(x + ((size_t)b * HW + i) * C + c8 * 8), v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += v[k];
+    }
+    float *o = out + (size_t)b * C + c8 * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = acc[k] / (float)HW;
+  }
+}
+
+// G[b][i][c] = dpool[b][c] / HW * (x > 0);  part[b][2][C] = (sum G, sum G*y) over the image
+__global__ __launch_bounds__(256) void head_bwd_kernel(const float *__restrict__ dpool, const bf16_t *__restrict__ x,
+                                                       const bf16_t *__restrict__ y, bf16_t *__restrict__ G,
+                                                       float *__restrict__ part, int HW, int C) {
+  const int b = blockIdx.x;
+  for (int c8 = threadIdx.x; c8 < C / 8; c8 += blockDim.x) {
+    float d[8], s0[8], s1[8];
+    ld8f(dpool + (size_t)b * C + c8 * 8, d);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { d[k] /= (float)HW; s0[k] = s1[k] = 0.f; }
+    for (int i = 0; i < HW; ++i) {
+      const size_t o = ((size_t)b * HW + i) * C + c8 * 8;
+      float xv[8], yv[8], g[8];
+      unpack8(ldg16(x + o), xv);
+      unpack8(ldg16(y + o), yv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        g[k] = bf2f(f2bf(xv[k] > 0.f ? d[k] : 0.f));
+        s0[k] += g[k];
+        s1[k] = fmaf(g[k], yv[k], s1[k]);
+      }
+      stg16(G + o, pack8(g));
+    }
+    float *p0 = part + (size_t)b * 2 * C + c8 * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { p0[k] = s0[k]; p0[C + k] = s1[k]; }
+  }
+}
+
+// softmax cross-entropy over NC classes, one wave per image: loss[b], correct[b],
+// dlogits[b][:] = (softmax - onehot) * scale
+__global__ __launch_bounds__(64) void softmax_ce_kernel(const float *__restrict__ logits, const long long *__restrict__ labels,
+                                                        int NC, float scale, float *__restrict__ loss,
+                                                        float *__restrict__ correct, float *__restrict__ dlogits) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const float *z = logits + (size_t)b * NC;
+  float mx = -INFINITY;
+  int am = 0;
+  for (int i = lane; i < NC; i += 64) if (z[i] > mx) { mx = z[i]; am = i; }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(mx, o, 64);
+    const int oa = __shfl_xor(am, o, 64);
+    if (om > mx || (om == mx && oa < am)) { mx = om; am = oa; }
+  }
+  float se = 0.f;
+  for (int i = lane; i < NC; i += 64) se += __expf(z[i] - mx);
+  se = wave_sum(se);
+  const int lab = (int)labels[b];
+  const float lse = mx + __logf(se);
+  if (lane == 0) {
+    loss[b] = lse - z[lab];
+    correct[b] = am == lab ? 1.f : 0.f;
+  }
+  if (dlogits) {
+    for (int i = lane; i < NC; i += 64) dlogits[(size_t)b * NC + i] = (__expf(z[i] - lse) - (i == lab ? 1.f : 0.f)) * scale;
+  }
+}
+
+// ===========================================================================
+// synthetic ImageNet-shaped input: uint8 [n][H][W][3] pool -> random horizontal flip,
+// ImageNet normalisation, NHWC bf16 with a zero 4th channel
+// ===========================================================================
+__global__ __launch_bounds__(256) void image_prep_kernel(const uint8_t *__restrict__ src, const long long *__restrict__ idx,
+                                                         const long long *__restrict__ lab_src, int HW, int W,
+                                                         unsigned long long seed, const float *__restrict__ hyper,
+                                                         bf16_t *__restrict__ out, long long *__restrict__ lab_out) {
+  const int b = blockIdx.y;
+  const long long si = idx[b];
+  const uint64_t step = hyper ? (uint64_t)hyper[1] : 0;
+  const bool flip = pg_uniform(seed ^ (step * 0x9E3779B97F4A7C15ull), (uint64_t)b) < 0.5f;
+  const float mean[3] = {0.485f, 0.456f, 0.406f}, inv[3] = {1.f / 0.229f, 1.f / 0.224f, 1.f / 0.225f};
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < HW; p += gridDim.x * blockDim.x) {
+    const int h = p / W, w = p % W;
+    const int sw = flip ? W - 1 - w : w;
+    const uint8_t *s = src + ((size_t)si * HW + (size_t)h * W + sw) * 3;
+    float v[4];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) v[c] = ((float)s[c] * (1.f / 255.f) - mean[c]) * inv[c];
+    v[3] = 0.f;
+    uint2 u;
+    u.x = pack2(v[0], v[1]);
+    u.y = pack2(v[2], v[3]);
+    *reinterpret_cast<uint2 *>(out + ((size_t)b * HW + p) * 4) = u;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) lab_out[b] = lab_src[si];
+}
+
+// ===========================================================================
+// host side
+// ===========================================================================
+namespace {
+struct Geom {
+  int BM, BN, KS, nmt, nt, ncls;
+  size_t lds;
+};
+
+Geom igemm_geom(int M, int N, int Kmax, int Ci, int ncls) {
+  Geom g{};
+  const int cand[4][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}};
+  int pick = 3;
+  for (int i = 0; i < 4; ++i) {
+    if (cand[i][1] == 128 && N <= 64) continue;   // no half-empty N tiles
+    const long long wgs = (long long)((M + cand[i][0] - 1) / cand[i][0]) * ((N + cand[i][1] - 1) / cand[i][1]) * ncls;
+    if (wgs >= 512) { pick = i; break; }
+  }
+  g.BM = cand[pick][0];
+  g.BN = cand[pick][1];
+  g.nmt = (M + g.BM - 1) / g.BM;
+  g.nt = (N + g.BN - 1) / g.BN;
+  g.ncls = ncls;
+  g.KS = (Kmax >= 256 && Ci % 64 == 0) ? 64 : 32;
+  const size_t ops = (size_t)2 * (g.BM + g.BN) * (g.KS + 8) * 2;
+  const size_t ctile = (size_t)g.BM * (g.BN + 8) * 2;
+  const size_t red = (size_t)(256 / (g.BN / 8)) * g.BN * 4;
+  g.lds = ops > ctile ? ops : ctile;
+  if (red > g.lds) g.lds = red;
+  return g;
+}
+
+template <int MODE, int PRO, int EPI, int BM, int BN, int KS, int CV>
+void launch_t(const ConvArgs &a, const Geom &g, bool ut, hipStream_t st) {
+  const dim3 grid(g.nmt * g.nt, g.ncls);
+  if (ut) hipLaunchKernelGGL((conv_igemm_kernel<MODE, PRO, EPI, BM, BN, KS, CV, true>), grid, dim3(256), g.lds, st, a);
+  else hipLaunchKernelGGL((conv_igemm_kernel<MODE, PRO, EPI, BM, BN, KS, CV, false>), grid, dim3(256), g.lds, st, a);
+}
+
+template <int MODE, int PRO, int EPI, int CV>
+void launch_geom(const ConvArgs &a, const Geom &g, hipStream_t st) {
+  const bool ut = a.Ci % g.KS == 0;
+  if constexpr (CV == 4) {   // stem: K = 196 -> 32-wide k-steps
+    if (g.BM == 128 && g.BN == 64) { launch_t<MODE, PRO, EPI, 128, 64, 32, CV>(a, g, false, st); return; }
+    launch_t<MODE, PRO, EPI, 64, 64, 32, CV>(a, g, false, st);
+    return;
+  } else {
+#define LG_TILE(BM_, BN_)                                                                              \
+  if (g.BM == BM_ && g.BN == BN_) {                                                                    \
+    if (g.KS == 64) launch_t<MODE, PRO, EPI, BM_, BN_, 64, CV>(a, g, ut, st);                          \
+    else launch_t<MODE, PRO, EPI, BM_, BN_, 32, CV>(a, g, ut, st);                                     \
+    return;                                                                                            \
+  }
+    LG_TILE(128, 128)
+    LG_TILE(128, 64)
+    LG_TILE(64, 128)
+    LG_TILE(64, 64)
+#undef LG_TILE
+  }
+}
+
+// dgrad parity classes of a (R, S, stride, pad) convolution
+void dgrad_classes(ConvArgs &a, int R, int S, int st, int pad) {
+  for (int cls = 0; cls < st * st; ++cls) {
+    const int ph = cls / st, pw = cls % st;
+    int n = 0;
+    for (int r = 0; r < R; ++r) {
+      if (((ph + pad - r) % st + st) % st) continue;
+      for (int s = 0; s < S; ++s) {
+        if (((pw + pad - s) % st + st) % st) continue;
+        a.tr[cls][n] = (signed char)r;
+        a.ts[cls][n] = (signed char)s;
+        a.tdh[cls][n] = (signed char)((ph + pad - r) / st);   // exact division (multiple of st)
+        a.tdw[cls][n] = (signed char)((pw + pad - s) / st);
+        ++n;
+      }
+    }
+    a.ntap[cls] = n;
+  }
+}
+}  // namespace
+
+// BN partial rows a forward conv writes (per M tile)
+int conv_fwd_num_partials(int Nb, int Ho, int Wo, int N, int K, int Ci) {
+  const int M = Nb * Ho * Wo;
+  return igemm_geom(M, N, K, Ci, 1).nmt;
+}
+// ... and a dgrad (all parity classes)
+int conv_dgrad_num_partials(int Nb, int H, int W, int N, int Cout, int R, int S, int st) {
+  const int M = Nb * (H / st) * (W / st);
+  return igemm_geom(M, N, R * S * Cout, Cout, st * st).nmt * st * st;
+}
+
+// forward conv.  x [Nb][H][W][Ci] (Ci % 8 == 0, or Ci == 4 for the stem), w [N][R][S][Ci]
+// pro: 0 none, 1 relu(x*pa+pb) of the producer BN
+void launch_conv_fwd(int pro, const bf16_t *x, const float *pa, const float *pb, const bf16_t *w, bf16_t *y,
+                     float *part, int Nb, int H, int W, int Ci, int N, int R, int S, int st, int pad,
+                     hipStream_t stream) {
+  ConvArgs a{};
+  a.A = x; a.pa = pa; a.pb = pb; a.W = w; a.out = y; a.part = part;
+  a.Hi = H; a.Wi = W; a.Ci = Ci;
+  a.Ho = (H + 2 * pad - R) / st + 1;
+  a.Wo = (W + 2 * pad - S) / st + 1;
+  a.N = N; a.R = R; a.S = S; a.stride = st; a.pad = pad;
+  a.Kw = R * S * Ci;
+  a.K = Ci == 4 ? (a.Kw + 31) / 32 * 32 : a.Kw;
+  a.Mc = Nb * a.Ho * a.Wo;
+  a.Hc = a.Ho; a.Wc = a.Wo;
+  const Geom g = igemm_geom(a.Mc, N, a.Kw, Ci, 1);
+  a.nmt = g.nmt;
+  if (Ci == 4) { launch_geom<CM_FWD, CP_NONE, CE_FWD, 4>(a, g, stream); return; }
+  if (pro == CP_BN_RELU) launch_geom<CM_FWD, CP_BN_RELU, CE_FWD, 8>(a, g, stream);
+  else launch_geom<CM_FWD, CP_NONE, CE_FWD, 8>(a, g, stream);
+}
+
+// dgrad.  G, Y [Nb][Ho][Wo][Cout] (this layer's BN-backward: dy = ga*G + gb*Y + gc),
+// wt [Cin][R][S][Cout]; out dx [Nb][H][W][Cin]   (H % st == 0, W % st == 0)
+// epi 1: dx * (Yt*es + et > 0) + partials (sum, sum*Yt)
+// epi 2: (dx + Rg) * (X > 0) + partials against Yt (part) and Yt2 (part2); null pointers skip
+void launch_conv_dgrad(int epi, const bf16_t *G, const bf16_t *Y, const float *ga, const float *gb, const float *gc,
+                       const bf16_t *wt, bf16_t *dx, const bf16_t *Yt, const float *es, const float *et,
+                       const bf16_t *Rg, const bf16_t *X, const bf16_t *Yt2, float *part, float *part2, int Nb, int H,
+                       int W, int Cin, int Cout, int R, int S, int st, int pad, hipStream_t stream) {
+  ConvArgs a{};
+  a.A = G; a.A2 = Y; a.pa = ga; a.pb = gb; a.pc = gc; a.W = wt; a.out = dx;
+  a.Yt = Yt; a.Yt2 = Yt2; a.X = X; a.Rg = Rg; a.es = es; a.et = et; a.part = part; a.part2 = part2;
+  a.Hi = (H + 2 * pad - R) / st + 1;
+  a.Wi = (W + 2 * pad - S) / st + 1;
+  a.Ci = Cout;
+  a.Ho = H; a.Wo = W; a.N = Cin;
+  a.R = R; a.S = S; a.stride = st; a.pad = pad;
+  a.Kw = R * S * Cout;
+  a.Hc = H / st; a.Wc = W / st;
+  a.Mc = Nb * a.Hc * a.Wc;
+  dgrad_classes(a, R, S, st, pad);
+  int kmax = 0;
+  for (int c = 0; c < st * st; ++c) kmax = a.ntap[c] * Cout > kmax ? a.ntap[c] * Cout : kmax;
+  a.K = kmax;
+  const Geom g = igemm_geom(a.Mc, Cin, kmax, Cout, st * st);
+  a.nmt = g.nmt;
+  if (epi == CE_BWD_RELU) launch_geom<CM_DGRAD, CP_BNBWD, CE_BWD_RELU, 8>(a, g, stream);
+  else launch_geom<CM_DGRAD, CP_BNBWD, CE_BWD_RES, 8>(a, g, stream);
+}
+
+// ---- weight gradient
+namespace {
+struct WgGeom {
+  int TN, TK, nsplit, rows;
+};
+WgGeom wg_geom(int N, int Kw, int M) {
+  WgGeom g{};
+  g.TN = N >= 128 ? 128 : 64;
+  g.TK = Kw >= 128 ? 128 : 64;
+  const long long tiles = (long long)((N + g.TN - 1) / g.TN) * ((Kw + g.TK - 1) / g.TK);
+  long long ns = (1024 + tiles - 1) / tiles;
+  const long long max_ns = (M + 4 * kWgMK - 1) / (4 * kWgMK);   // >= 4 steps per split
+  if (ns > max_ns) ns = max_ns;
+  if (ns < 1) ns = 1;
+  g.rows = (int)(((M + ns - 1) / ns + kWgMK - 1) / kWgMK * kWgMK);
+  g.nsplit = (M + g.rows - 1) / g.rows;
+  return g;
+}
+}  // namespace
+
+int colsum_rows(int R);
+void launch_wgrad_reduce(float *part, int S, long long n, float *grad, hipStream_t st);
+
+long long conv_wgrad_workspace_floats(int Nb, int H, int W, int Ci, int N, int R, int S, int st, int pad) {
+  const int Ho = (H + 2 * pad - R) / st + 1, Wo = (W + 2 * pad - S) / st + 1;
+  const WgGeom g = wg_geom(N, R * S * Ci, Nb * Ho * Wo);
+  if (g.nsplit == 1) return 0;
+  return (long long)(g.nsplit + colsum_rows(g.nsplit)) * N * R * S * Ci;
+}
+
+// dW [N][R][S][Ci] (fp32, overwritten) of y = conv(x);  G, Y [Nb][Ho][Wo][N];  x [Nb][H][W][Ci]
+// xpro 1: x = relu(x*xs + xt) (producer BN), 0: as stored
+void launch_conv_wgrad(const bf16_t *G, const bf16_t *Y, const float *ga, const float *gb, const float *gc,
+                       const bf16_t *x, const float *xs, const float *xt, int xpro, float *ws, float *grad, int Nb,
+                       int H, int W, int Ci, int N, int R, int S, int st, int pad, hipStream_t stream) {
+  WgArgs a{};
+  a.G = G; a.Y = Y; a.ga = ga; a.gb = gb; a.gc = gc; a.X = x; a.xs = xs; a.xt = xt;
+  a.N = N; a.Hi = H; a.Wi = W; a.Ci = Ci;
+  a.Ho = (H + 2 * pad - R) / st + 1;
+  a.Wo = (W + 2 * pad - S) / st + 1;
+  a.R = R; a.S = S; a.stride = st; a.pad = pad;
+  a.Kw = R * S * Ci;
+  a.M = Nb * a.Ho * a.Wo;
+  const WgGeom g = wg_geom(N, a.Kw, a.M);
+  a.rows_per_split = g.rows;
+  a.out = g.nsplit == 1 ? grad : ws;
+  const dim3 grid((N + g.TN - 1) / g.TN, (a.Kw + g.TK - 1) / g.TK, g.nsplit);
+#define WG_L(XP, TN_, TK_, CV_) hipLaunchKernelGGL((conv_wgrad_kernel<XP, TN_, TK_, CV_>), grid, dim3(256), 0, stream, a)
+  if (Ci == 4) {
+    if (g.TN == 128) WG_L(CP_NONE, 128, 128, 4); else WG_L(CP_NONE, 64, 128, 4);
+  } else if (xpro == CP_BN_RELU) {
+    if (g.TN == 128 && g.TK == 128) WG_L(CP_BN_RELU, 128, 128, 8);
+    else if (g.TN == 128) WG_L(CP_BN_RELU, 128, 64, 8);
+    else if (g.TK == 128) WG_L(CP_BN_RELU, 64, 128, 8);
+    else WG_L(CP_BN_RELU, 64, 64, 8);
+  } else {
+    if (g.TN == 128 && g.TK == 128) WG_L(CP_NONE, 128, 128, 8);
+    else if (g.TN == 128) WG_L(CP_NONE, 128, 64, 8);
+    else if (g.TK == 128) WG_L(CP_NONE, 64, 128, 8);
+    else WG_L(CP_NONE, 64, 64, 8);
+  }
+#undef WG_L
+  if (g.nsplit > 1) launch_wgrad_reduce(ws, g.nsplit, (long long)N * a.Kw, grad, stream);
+}
+
+void launch_conv_wt(const bf16_t *src, bf16_t *dst, const int *tab, int n, hipStream_t st) {
+  hipLaunchKernelGGL(conv_wt_kernel, dim3(256, n), dim3(256), 0, st, src, dst, tab);
+}
+
+void launch_res_out(const bf16_t *y, const float *s, const float *t, const bf16_t *r, const float *rs,
+                    const float *rt, bf16_t *out, long long M, int C, hipStream_t st) {
+  const long long n8 = M * (C / 8);
+  int grid = (int)((n8 + 255) / 256);
+  if (grid > 16384) grid = 16384;
+  if (rs) hipLaunchKernelGGL((res_out_kernel<true>), dim3(grid), dim3(256), 0, st, y, s, t, r, rs, rt, out, n8, C / 8);
+  else hipLaunchKernelGGL((res_out_kernel<false>), dim3(grid), dim3(256), 0, st, y, s, t, r, rs, rt, out, n8, C / 8);
+}
+
+void launch_maxpool_fwd(const bf16_t *y, const float *s, const float *t, bf16_t *out, uint8_t *idx, int Nb, int H,
+                        int W, int C, hipStream_t st) {
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  const long long total = (long long)Nb * Ho * Wo * (C / 8);
+  int grid = (int)((total + 255) / 256);
+  if (grid > 16384) grid = 16384;
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid), dim3(256), 0, st, y, s, t, out, idx, Nb, H, W, C, Ho, Wo);
+}
+
+constexpr int kMpPix = 512;   // input pixels per backward workgroup
+int maxpool_bwd_num_partials(int Nb, int H, int W) {
+  return (int)(((long long)Nb * H * W + kMpPix - 1) / kMpPix);
+}
+
+void launch_maxpool_bwd(const bf16_t *gp, const uint8_t *idx, const bf16_t *y, const float *s, const float *t,
+                        bf16_t *g, float *part, int Nb, int H, int W, int C, hipStream_t st) {
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(maxpool_bwd_num_partials(Nb, H, W)), dim3(256), 0, st, gp, idx, y, s, t,
+                     g, part, Nb, H, W, C, Ho, Wo, kMpPix);
+}
+
+void launch_avgpool(const bf16_t *x, float *out, int Nb, int HW, int C, hipStream_t st) {
+  hipLaunchKernelGGL(avgpool_kernel, dim3(Nb), dim3(256), 0, st, x, out, HW, C);
+}
+
+void launch_head_bwd(const float *dpool, const bf16_t *x, const bf16_t *y, bf16_t *G, float *part, int Nb, int HW,
+                     int C, hipStream_t st) {
+  hipLaunchKernelGGL(head_bwd_kernel, dim3(Nb), dim3(256), 0, st, dpool, x, y, G, part, HW, C);
+}
+
+void launch_softmax_ce(const float *logits, const long long *labels, int B, int NC, float scale, float *loss,
+                       float *correct, float *dlogits, hipStream_t st) {
+  hipLaunchKernelGGL(softmax_ce_kernel, dim3(B), dim3(64), 0, st, logits, labels, NC, scale, loss, correct, dlogits);
+}
+
+void launch_image_prep(const uint8_t *src, const long long *idx, const long long *lab_src, int B, int H, int W,
+                       unsigned long long seed, const float *hyper, bf16_t *out, long long *lab_out,
+                       hipStream_t st) {
+  const int HW = H * W;
+  hipLaunchKernelGGL(image_prep_kernel, dim3((HW + 255) / 256 < 64 ? (HW + 255) / 256 : 64, B), dim3(256), 0, st, src,
+                     idx, lab_src, HW, W, seed, hyper, out, lab_out);
+}

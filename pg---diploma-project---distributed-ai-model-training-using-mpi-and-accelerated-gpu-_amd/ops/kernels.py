@@ -398,3 +398,199 @@ def augment(src, idx, labels_src, out, labels_out, params_out, train=True, doubl
     lib().augment(_p(src), _p(idx), _p(labels_src), src.shape[0], B, out_hw, int(bool(train)),
                   int(bool(double_resize)), _p(given_params), int(seed) & ((1 << 64) - 1), _p(hyper),
                   int(epoch_ctr), _p(out), _p(labels_out), _p(params_out), _s())
+
+
+# --------------------------------------------------------------------------- dense conv (ResNet-50)
+CP_NONE, CP_BN_RELU, CP_BNBWD = 0, 1, 3
+CE_BWD_RELU, CE_BWD_RES = 1, 2
+
+
+def conv_out_hw(H, W, R, S, stride, pad):
+    return (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
+
+
+def _conv_check(Ci, N, what):
+    if not (Ci % 8 == 0 or Ci == 4) or N % 8:
+        raise ValueError(f"{what}: Ci={Ci} must be a multiple of 8 (or 4 for the padded stem input) and "
+                         f"N={N} a multiple of 8")
+
+
+def conv_fwd_num_partials(B, Ho, Wo, N, K, Ci):
+    """BN partial rows a forward conv with output [B,Ho,Wo,N] and GEMM depth K writes."""
+    return lib().conv_fwd_num_partials(B, Ho, Wo, N, K, Ci)
+
+
+def conv_dgrad_num_partials(B, H, W, Cin, Cout, R, S, stride):
+    return lib().conv_dgrad_num_partials(B, H, W, Cin, Cout, R, S, stride)
+
+
+def conv_fwd(pro, x, w, y, part, B, H, W, Ci, N, R, S, stride, pad, pa=None, pb=None):
+    """NHWC implicit-GEMM convolution  y = conv(pro(x), w)  on MFMA, plus per-tile BN
+    partial sums of y.  x [B,H,W,Ci] bf16, w [N,R,S,Ci] bf16, y [B,Ho,Wo,N] bf16;
+    pro = CP_BN_RELU applies relu(x*pa + pb) to in-bounds taps (padding stays 0)."""
+    _conv_check(Ci, N, "conv_fwd")
+    if Ci == 4 and pro != CP_NONE:
+        raise ValueError("conv_fwd: the 4-channel (stem) path has no prologue")
+    Ho, Wo = conv_out_hw(H, W, R, S, stride, pad)
+    _chk(x, BF16, B * H * W * Ci, "x")
+    _chk(w, BF16, N * R * S * Ci, "w")
+    _chk(y, BF16, B * Ho * Wo * N, "y")
+    _chk(part, F32, conv_fwd_num_partials(B, Ho, Wo, N, R * S * Ci, Ci) * 2 * N, "part")
+    if pro == CP_BN_RELU:
+        _chk(pa, F32, Ci, "pa")
+        _chk(pb, F32, Ci, "pb")
+    lib().conv_fwd(int(pro), _p(x), _p(pa), _p(pb), _p(w), _p(y), _p(part), B, H, W, Ci, N, R, S, stride, pad,
+                   _s())
+
+
+def conv_dgrad(epi, G, Y, ga, gb, gc, wt, dx, part, B, H, W, Cin, Cout, R, S, stride, pad, Yt=None, es=None,
+               et=None, Rg=None, X=None, Yt2=None, part2=None):
+    """Data gradient of y = conv(x, w) with this layer's BN backward fused on the way in:
+    dy = ga*G + gb*Y + gc  ([B,Ho,Wo,Cout]),  dx = conv^T(dy, wt)  ([B,H,W,Cin]), where
+    wt = w transposed to [Cin,R,S,Cout] (:func:`conv_wt`).  Epilogues:
+      CE_BWD_RELU  dx *= 1[Yt*es + et > 0];  part <- (sum dx, sum dx*Yt)
+      CE_BWD_RES   dx = (dx + Rg) * 1[X > 0]  (null operands skipped);
+                   part <- (sum dx, sum dx*Yt), part2 <- (sum dx, sum dx*Yt2) when given."""
+    _conv_check(Cout, Cin, "conv_dgrad")
+    if H % stride or W % stride:
+        raise ValueError("conv_dgrad: H and W must be multiples of the stride")
+    if R > 3 or S > 3:
+        raise ValueError("conv_dgrad: filters up to 3x3")
+    Ho, Wo = conv_out_hw(H, W, R, S, stride, pad)
+    for t, nm in ((G, "G"), (Y, "Y")):
+        _chk(t, BF16, B * Ho * Wo * Cout, nm)
+    for t, nm in ((ga, "ga"), (gb, "gb"), (gc, "gc")):
+        _chk(t, F32, Cout, nm)
+    _chk(wt, BF16, Cin * R * S * Cout, "wt")
+    for t, nm in ((dx, "dx"), (Yt, "Yt"), (Rg, "Rg"), (X, "X"), (Yt2, "Yt2")):
+        _chk(t, BF16, B * H * W * Cin, nm)
+    P = conv_dgrad_num_partials(B, H, W, Cin, Cout, R, S, stride)
+    if epi == CE_BWD_RELU:
+        if Yt is None or es is None or et is None:
+            raise ValueError("conv_dgrad(CE_BWD_RELU) needs Yt, es, et")
+        _chk(part, F32, P * 2 * Cin, "part")
+    elif epi == CE_BWD_RES:
+        if Yt is not None:
+            _chk(part, F32, P * 2 * Cin, "part")
+        if Yt2 is not None:
+            if Yt is None:
+                raise ValueError("conv_dgrad: Yt2 needs Yt")
+            _chk(part2, F32, P * 2 * Cin, "part2")
+    else:
+        raise ValueError(f"conv_dgrad: bad epilogue {epi}")
+    lib().conv_dgrad(int(epi), _p(G), _p(Y), _p(ga), _p(gb), _p(gc), _p(wt), _p(dx), _p(Yt), _p(es), _p(et),
+                     _p(Rg), _p(X), _p(Yt2), _p(part), _p(part2), B, H, W, Cin, Cout, R, S, stride, pad, _s())
+
+
+def conv_wgrad_workspace(B, H, W, Ci, N, R, S, stride, pad):
+    return lib().conv_wgrad_workspace_floats(B, H, W, Ci, N, R, S, stride, pad)
+
+
+def conv_wgrad(G, Y, ga, gb, gc, x, ws, grad, B, H, W, Ci, N, R, S, stride, pad, xpro=CP_NONE, xs=None, xt=None):
+    """grad [N,R,S,Ci] (fp32, overwritten) = sum_m dy[m] (x) im2col(x')[m] with
+    dy = ga*G + gb*Y + gc and x' = relu(x*xs + xt) (xpro = CP_BN_RELU) or x."""
+    _conv_check(Ci, N, "conv_wgrad")
+    Ho, Wo = conv_out_hw(H, W, R, S, stride, pad)
+    _chk(G, BF16, B * Ho * Wo * N, "G")
+    _chk(Y, BF16, B * Ho * Wo * N, "Y")
+    for t, nm in ((ga, "ga"), (gb, "gb"), (gc, "gc")):
+        _chk(t, F32, N, nm)
+    _chk(x, BF16, B * H * W * Ci, "x")
+    if xpro == CP_BN_RELU:
+        _chk(xs, F32, Ci, "xs")
+        _chk(xt, F32, Ci, "xt")
+    _chk(ws, F32, conv_wgrad_workspace(B, H, W, Ci, N, R, S, stride, pad), "ws")
+    _chk(grad, F32, N * R * S * Ci, "grad")
+    lib().conv_wgrad(_p(G), _p(Y), _p(ga), _p(gb), _p(gc), _p(x), _p(xs), _p(xt), int(xpro), _p(ws), _p(grad),
+                     B, H, W, Ci, N, R, S, stride, pad, _s())
+
+
+def conv_wt(src, dst, tab, n):
+    """Batched bf16 weight transpose for dgrad: for each row (src_off, dst_off, Cout, taps, Cin)
+    of the int32 table ``tab`` [n,5], dst[ci][t][co] = src[co][t][ci]."""
+    _chk(src, BF16, 1, "src")
+    _chk(dst, BF16, 1, "dst")
+    assert tab.dtype == torch.int32 and tab.is_contiguous() and tab.numel() >= 5 * n
+    lib().conv_wt(_p(src), _p(dst), _p(tab), int(n), _s())
+
+
+def res_out(y, s, t, r, out, rs=None, rt=None):
+    """Bottleneck output out = relu(y*s + t + r'), r' = r*rs + rt (projection shortcut BN) or r."""
+    M, C = y.shape
+    if C % 8:
+        raise ValueError("res_out: C % 8")
+    for x_, nm in ((y, "y"), (r, "r"), (out, "out")):
+        _chk(x_, BF16, M * C, nm)
+    lib().res_out(_p(y), _p(s), _p(t), _p(r), _p(rs), _p(rt), _p(out), M, C, _s())
+
+
+def maxpool_fwd(y, s, t, out, idx, B, H, W, C):
+    """3x3 s2 p1 max-pool of relu(y*s+t) -> out [B,Ho,Wo,C] bf16 + arg-max tap (uint8)."""
+    Ho, Wo = conv_out_hw(H, W, 3, 3, 2, 1)
+    if C % 8:
+        raise ValueError("maxpool: C % 8")
+    _chk(y, BF16, B * H * W * C, "y")
+    _chk(out, BF16, B * Ho * Wo * C, "out")
+    _chk(idx, torch.uint8, B * Ho * Wo * C, "idx")
+    lib().maxpool_fwd(_p(y), _p(s), _p(t), _p(out), _p(idx), B, H, W, C, _s())
+
+
+def maxpool_bwd_num_partials(B, H, W):
+    return lib().maxpool_bwd_num_partials(B, H, W)
+
+
+def maxpool_bwd(gp, idx, y, s, t, g, part, B, H, W, C):
+    """Max-pool backward fused with the stem BN's ReLU mask: g = route(gp) * 1[y*s+t > 0],
+    part <- (sum g, sum g*y) per workgroup (C == 64)."""
+    if C != 64:
+        raise ValueError("maxpool_bwd: C must be 64")
+    Ho, Wo = conv_out_hw(H, W, 3, 3, 2, 1)
+    _chk(gp, BF16, B * Ho * Wo * C, "gp")
+    _chk(idx, torch.uint8, B * Ho * Wo * C, "idx")
+    _chk(y, BF16, B * H * W * C, "y")
+    _chk(g, BF16, B * H * W * C, "g")
+    _chk(part, F32, maxpool_bwd_num_partials(B, H, W) * 2 * C, "part")
+    lib().maxpool_bwd(_p(gp), _p(idx), _p(y), _p(s), _p(t), _p(g), _p(part), B, H, W, C, _s())
+
+
+def avgpool(x, out, B, HW, C):
+    if C % 8 or C // 8 > 256:
+        raise ValueError("avgpool: C % 8 and C <= 2048")
+    _chk(x, BF16, B * HW * C, "x")
+    _chk(out, F32, B * C, "out")
+    lib().avgpool(_p(x), _p(out), B, HW, C, _s())
+
+
+def head_bwd(dpool, x, y, G, part, B, HW, C):
+    """G = dpool/HW broadcast * 1[x > 0];  part[B][2][C] <- (sum G, sum G*y) per image."""
+    if C % 8 or C // 8 > 256:
+        raise ValueError("head_bwd: C % 8 and C <= 2048")
+    _chk(dpool, F32, B * C, "dpool")
+    for t, nm in ((x, "x"), (y, "y"), (G, "G")):
+        _chk(t, BF16, B * HW * C, nm)
+    _chk(part, F32, B * 2 * C, "part")
+    lib().head_bwd(_p(dpool), _p(x), _p(y), _p(G), _p(part), B, HW, C, _s())
+
+
+def softmax_ce(logits, labels, loss, correct, dlogits=None, scale=1.0):
+    B, NC = logits.shape
+    _chk(logits, F32, B * NC, "logits")
+    _chk(labels, torch.int64, B, "labels")
+    _chk(loss, F32, B, "loss")
+    _chk(correct, F32, B, "correct")
+    _chk(dlogits, F32, B * NC, "dlogits")
+    lib().softmax_ce(_p(logits), _p(labels), B, NC, float(scale), _p(loss), _p(correct), _p(dlogits), _s())
+
+
+def image_prep(src, idx, labels_src, out, labels_out, seed=0, hyper=None):
+    """uint8 [N,H,W,3] pool gathered by idx [B] -> random h-flip, ImageNet normalisation,
+    NHWC bf16 [B,H,W,4] (4th channel 0)."""
+    B = idx.numel()
+    if src.dtype != torch.uint8 or src.dim() != 4 or src.shape[3] != 3 or not src.is_contiguous():
+        raise ValueError("image_prep: src must be contiguous uint8 [N,H,W,3]")
+    H, W = src.shape[1], src.shape[2]
+    _chk(idx, torch.int64, B, "idx")
+    _chk(out, BF16, B * H * W * 4, "out")
+    _chk(labels_out, torch.int64, B, "labels_out")
+    lib().image_prep(_p(src), _p(idx), _p(labels_src), B, H, W, int(seed) & ((1 << 64) - 1), _p(hyper), _p(out),
+                     _p(labels_out), _s())
