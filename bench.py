@@ -107,7 +107,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": round(imgs_per_s / ref_for(world), 3) if headline else None,
             "dtype": "fp8-e4m3 fwd GEMMs / bf16" if args.fp8 else "bf16",
-            "data": "synthetic (device-resident uint8 32x32x3 CIFAR-shaped images, GPU-augmented to 224x224; random-init weights)",
+            "data": ("synthetic (device-resident uint8 32x32x3 CIFAR-shaped images, GPU-augmented to 224x224; "
+                     "random-init weights)" if args.model == "mobilenet_v2" else
+                     "synthetic (device-resident uint8 224x224x3 ImageNet-shaped images, GPU flip + normalise; "
+                     "random-init weights, 1000 classes)"),
             "config": {"model": args.model, "global_batch": args.batch_size * world,
                        "per_gpu_batch": args.batch_size, "seq_len": None, "img_size": args.img_size,
                        "parallelism": f"dp{world}", "backend": meta.get("backend"),

@@ -881,7 +881,7 @@ __global__ __launch_bounds__(256) void image_prep_kernel(const uint8_t *__restri
   const int b = blockIdx.y;
   const long long si = idx[b];
   const uint64_t step = hyper ? (uint64_t)hyper[1] : 0;
-  const bool flip = pg_uniform(seed ^ (step * 0x9E3779B97F4A7C15ull), (uint64_t)b) < 0.5f;
+  const bool flip = hyper != nullptr && pg_uniform(seed ^ (step * 0x9E3779B97F4A7C15ull), (uint64_t)b) < 0.5f;   // no hyper: test transform
   const float mean[3] = {0.485f, 0.456f, 0.406f}, inv[3] = {1.f / 0.229f, 1.f / 0.224f, 1.f / 0.225f};
   for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < HW; p += gridDim.x * blockDim.x) {
     const int h = p / W, w = p % W;

@@ -16,6 +16,11 @@ Depthwise 3x3 weights ``[C,1,3,3]`` are stored *tap-major* ``[9][C]`` so the
 depthwise kernels read the 4 channels of one tap with a single 8-byte load; the
 Parameter is a strided view of that storage, so ``state_dict()`` still yields
 torchvision-layout tensors.
+
+With ``conv_nhwc=True`` (dense-conv networks, ResNet-50) every dense R x S (R*S > 1)
+conv weight ``[Cout,Cin,R,S]`` is stored ``[Cout][R][S][Cp]`` — the implicit-GEMM
+kernels' K order (r, s, ci) — with Cp = 4 for a 3-channel input (the zero 4th
+channel matches the 4-channel NHWC image; its gradient is exactly zero, so it stays 0).
 """
 from typing import Dict, List, Tuple
 
@@ -33,17 +38,29 @@ def is_depthwise3x3(p: torch.Tensor) -> bool:
 
 
 class FlatParams:
-    def __init__(self, model: torch.nn.Module, device: torch.device, with_shadow: bool = True):
+    def __init__(self, model: torch.nn.Module, device: torch.device, with_shadow: bool = True,
+                 conv_nhwc: bool = False):
         named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
         order = list(reversed(named))
+        # dense R x S conv weights in NHWC storage: name -> (Cout, R, S, Cin, Cp)
+        self.nhwc = {}
+        if conv_nhwc:
+            for n, p in order:
+                if p.dim() == 4 and p.shape[2] * p.shape[3] > 1 and not is_depthwise3x3(p):
+                    co, ci, r, s_ = p.shape
+                    self.nhwc[n] = (co, r, s_, ci, 4 if ci == 3 else ci)
         self.offsets: Dict[str, Tuple[int, int]] = {}
         self.order: List[str] = []
         off = 0
         for name, p in order:
             off = _align(off)
-            self.offsets[name] = (off, p.numel())
+            numel = p.numel()
+            if name in self.nhwc:
+                co, r, s_, ci, cp = self.nhwc[name]
+                numel = co * r * s_ * cp
+            self.offsets[name] = (off, numel)
             self.order.append(name)
-            off += p.numel()
+            off += numel
         self.numel = _align(off)
         self.device = device
         self.master = torch.zeros(self.numel, dtype=torch.float32, device=device)
@@ -54,7 +71,7 @@ class FlatParams:
         # transposed bf16 copies of the 1x1 conv weights (same offsets; filled by the executor)
         self.shadow_t = torch.zeros_like(self.shadow) if with_shadow else None
         self.params = {}
-        self.tap_major = {n for n, p in order if is_depthwise3x3(p)}
+        self.tap_major = {n for n, p in order if is_depthwise3x3(p)} - set(self.nhwc)
         with torch.no_grad():
             for name, p in order:
                 w_view, g_view = self.view(self.master, name, p.shape), self.view(self.grad, name, p.shape)
@@ -71,6 +88,9 @@ class FlatParams:
         if name in self.tap_major:
             C = shape[0]
             return buf[o:o + n].view(9, C).t().view(*shape)
+        if name in self.nhwc:
+            co, r, s_, ci, cp = self.nhwc[name]
+            return buf[o:o + n].view(co, r, s_, cp)[..., :ci].permute(0, 3, 1, 2)
         return buf[o:o + n].view(shape)
 
     def w(self, name: str) -> torch.Tensor:

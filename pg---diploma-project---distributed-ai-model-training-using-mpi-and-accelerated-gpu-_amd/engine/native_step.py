@@ -19,6 +19,15 @@ from ..parallel.ddp import BucketedGradReducer, broadcast_parameters
 from .executor import MobileNetV2Executor
 
 
+def executor_class(model):
+    """Static-plan executor of a model family (MobileNetV2 or ResNet)."""
+    from ..models.resnet import ResNet
+    if isinstance(model, ResNet):
+        from .resnet_executor import ResNet50Executor
+        return ResNet50Executor
+    return MobileNetV2Executor
+
+
 def coalesce_bn_buffers(model: torch.nn.Module):
     """Re-home every BatchNorm running_mean / running_var into one flat fp32 tensor and every
     num_batches_tracked into one int64 tensor (module buffers become views), so the per-step
@@ -50,8 +59,8 @@ class NativeTrainStep:
                  side_stream: bool = True, bn_broadcast: bool = False, fp8: bool = False):
         self.device, self.B, self.S = device, batch, img_size
         self.world, self.rank = world_size, rank
-        self.exe = MobileNetV2Executor(model, batch, img_size, device, dropout_seed=(seed * 7919) ^ rank,
-                                       side_stream=side_stream, fp8=fp8)
+        self.exe = executor_class(model)(model, batch, img_size, device, dropout_seed=(seed * 7919) ^ rank,
+                                         side_stream=side_stream, fp8=fp8)
         self.flat = self.exe.flat
         self.betas, self.eps, self.wd = betas, eps, weight_decay
         self.seed = seed
@@ -89,16 +98,24 @@ class NativeTrainStep:
     @classmethod
     def for_benchmark(cls, model_name: str, batch: int, device, img_size=224, use_graph=True,
                       world_size=1, rank=0, n_data=50000, side_stream=True, fp8=False):
-        if model_name != "mobilenet_v2":
-            raise NotImplementedError("native executor implements mobilenet_v2; use --backend torch for "
-                                      f"{model_name}")
+        if model_name not in ("mobilenet_v2", "resnet50"):
+            raise NotImplementedError(f"native executors: mobilenet_v2, resnet50 (not {model_name}); "
+                                      "use --backend torch")
         torch.manual_seed(42)  # identical random-init weights on every rank (then rank-0 broadcast)
-        model = build_model("mobilenet_v2", num_classes=10)
+        g = torch.Generator(device=device).manual_seed(1234 + rank)
+        if model_name == "resnet50":
+            # BASELINE config 4: ImageNet-shaped synthetic data (uint8 224x224x3 pool, 1000 classes)
+            model = build_model("resnet50", num_classes=1000)
+            n_data = min(n_data, 2048)
+            src = torch.randint(0, 256, (n_data, img_size, img_size, 3), dtype=torch.uint8, device=device,
+                                generator=g)
+            labels = torch.randint(0, 1000, (n_data,), dtype=torch.int64, device=device, generator=g)
+        else:
+            model = build_model("mobilenet_v2", num_classes=10)
+            src = torch.randint(0, 256, (n_data, 32, 32, 3), dtype=torch.uint8, device=device, generator=g)
+            labels = torch.randint(0, 10, (n_data,), dtype=torch.int64, device=device, generator=g)
         st = cls(model, batch, device, img_size=img_size, world_size=world_size, rank=rank,
                  use_graph=use_graph, seed=42, side_stream=side_stream, fp8=fp8)
-        g = torch.Generator(device=device).manual_seed(1234 + rank)
-        src = torch.randint(0, 256, (n_data, 32, 32, 3), dtype=torch.uint8, device=device, generator=g)
-        labels = torch.randint(0, 10, (n_data,), dtype=torch.int64, device=device, generator=g)
         st.set_data(src, labels)
         st._perm = torch.randperm(n_data, device=device, generator=g)
         st._pos = 0
@@ -111,8 +128,8 @@ class NativeTrainStep:
         st = NativeTrainStep.__new__(NativeTrainStep)
         st.__dict__.update(self.__dict__)
         st.B = batch
-        st.exe = MobileNetV2Executor(self.exe.model, batch, self.S, self.device, flat=self.flat,
-                                     dropout_seed=self.exe.dropout_seed, hyper=self.hyper)
+        st.exe = type(self.exe)(self.exe.model, batch, self.S, self.device, flat=self.flat,
+                                dropout_seed=self.exe.dropout_seed, hyper=self.hyper)
         st.exe.on_params_ready = self.exe.on_params_ready
         st.idx = torch.zeros(batch, dtype=torch.int64, device=self.device)
         st.aug_params = torch.zeros(batch, K.AUG_NPARAMS, dtype=torch.float32, device=self.device)
@@ -120,7 +137,10 @@ class NativeTrainStep:
         return st
 
     def set_data(self, src_u8: torch.Tensor, labels: torch.Tensor):
-        assert src_u8.is_cuda and src_u8.dtype == torch.uint8 and src_u8.shape[1:] == (32, 32, 3)
+        """Device-resident uint8 NHWC images: CIFAR-shaped [N,32,32,3] (GPU augmentation to
+        the training resolution) or full-resolution [N,S,S,3] (flip + normalise only)."""
+        assert src_u8.is_cuda and src_u8.dtype == torch.uint8 and src_u8.dim() == 4 and src_u8.shape[3] == 3
+        assert tuple(src_u8.shape[1:3]) in ((32, 32), (self.S, self.S)), "source images: 32x32 or SxS"
         self.src = src_u8.contiguous()
         self.src_labels = labels.to(self.device, torch.int64).contiguous()
 
@@ -137,7 +157,11 @@ class NativeTrainStep:
     def _body(self):
         exe = self.exe
         K.step_begin(self.hyper)
-        if self.augment_enabled:
+        if self.augment_enabled and self.src.shape[1] != 32:
+            K.image_prep(self.src, self.idx, self.src_labels, exe.img, exe.labels,
+                         seed=self.seed + 17 * self.rank if self.train_augment else 0,
+                         hyper=self.hyper if self.train_augment else None)
+        elif self.augment_enabled:
             K.augment(self.src, self.idx, self.src_labels, exe.img, exe.labels, self.aug_params,
                       train=self.train_augment,
                       double_resize=self.double_resize, seed=self.seed + 17 * self.rank, hyper=self.hyper,

@@ -1,0 +1,317 @@
+"""Static-plan executor: ResNet-50 training step on the gfx950 dense-conv kernels
+(BASELINE.json config 4, "ResNet-50 ImageNet-shape 224x224 synthetic DDP").
+
+Same design as the MobileNetV2 executor (engine/executor.py): the network is compiled
+once into a fixed schedule of HIP kernels over preallocated NHWC bf16 buffers, BN
+statistics come out of the producing conv's epilogue as per-tile partial sums and a
+per-channel finalize, and BN-apply + ReLU is fused into the consumer's operand staging:
+
+forward, per bottleneck (x = block input, materialised)
+  conv1 1x1       y1 = conv(x)                           + BN1 partials -> finalize
+  conv2 3x3 s     y2 = conv(relu(BN1(y1)))               + BN2 partials -> finalize
+  conv3 1x1       y3 = conv(relu(BN2(y2)))               + BN3 partials -> finalize
+  [projection]    yd = conv_s(x)                         + BNd partials -> finalize
+  output          o = relu(BN3(y3) + (BNd(yd) | x))      (materialised, bf16)
+stem: 7x7 s2 conv on the 4-channel image, BN0, fused relu + 3x3 s2 max-pool (arg-max kept)
+head: average pool -> fc (hipBLASLt GEMM through torch.addmm, fp32) -> softmax CE kernel
+
+backward walks the schedule in reverse.  Gz = dL/d(BN3(y3) + shortcut) is produced by
+the NEXT block's conv1 dgrad epilogue ((dx + shortcut grad) * 1[o > 0], with the BN3 and
+BNd partial sums of the previous block computed on the way), each dgrad applies its
+layer's BN backward (a*G + b*Y + c) while staging dy and the producer's ReLU mask in its
+epilogue, and weight gradients (split-M, BN-backward / BN+ReLU fused in the staging)
+run on a side stream, reporting finished parameters to the DDP bucket reducer.
+
+Reference call stack for the model forward: SURVEY.md §3.3 (cuDNN conv / BN / ReLU
+launches per layer); this executor replaces all of them.
+"""
+from dataclasses import dataclass
+from typing import Callable, List, Optional
+
+import torch
+
+from ..models.resnet import ResNet, Bottleneck
+from ..ops import kernels as K
+from .executor import BNState
+from .flat import FlatParams
+
+
+@dataclass
+class ConvSpec:
+    name: str       # weight parameter name
+    cin: int
+    cout: int
+    k: int          # kernel size (square)
+    stride: int
+    pad: int
+    H: int          # input spatial size (square)
+
+    @property
+    def Ho(self) -> int:
+        return (self.H + 2 * self.pad - self.k) // self.stride + 1
+
+
+@dataclass
+class BlockPlan:
+    prefix: str
+    cin: int
+    planes: int
+    cout: int
+    stride: int
+    H: int
+    Ho: int
+    c1: ConvSpec
+    c2: ConvSpec
+    c3: ConvSpec
+    cd: Optional[ConvSpec]
+    bn1: BNState
+    bn2: BNState
+    bn3: BNState
+    bnd: Optional[BNState]
+    x_in: torch.Tensor = None     # block input (previous output or max-pool output)
+    out: torch.Tensor = None      # block output o (materialised)
+    Rd: torch.Tensor = None       # projection-shortcut data gradient (dgrad of cd)
+
+
+class ResNet50Executor:
+    def __init__(self, model: ResNet, batch: int, img_size: int, device: torch.device,
+                 flat: Optional[FlatParams] = None, hyper: Optional[torch.Tensor] = None,
+                 side_stream: bool = True, dropout_seed: int = 0, fp8: bool = False):
+        assert device.type == "cuda", "the native executor runs on the GPU"
+        if fp8:
+            raise NotImplementedError("fp8 is implemented for the MobileNetV2 executor")
+        self.model = model.to(device)
+        self.B, self.S, self.device = batch, img_size, device
+        self.dropout_seed = dropout_seed
+        self.flat = flat or FlatParams(self.model, device, conv_nhwc=True)
+        assert self.flat.nhwc, "ResNet executor needs FlatParams(conv_nhwc=True)"
+        B = batch
+        f32 = dict(dtype=torch.float32, device=device)
+        bf16 = dict(dtype=torch.bfloat16, device=device)
+        parts, wgs = [], []
+
+        def fwd_parts(c: ConvSpec):
+            ci = 4 if c.cin == 3 else c.cin
+            parts.append((K.conv_fwd_num_partials(B, c.Ho, c.Ho, c.cout, c.k * c.k * ci, ci), c.cout))
+            wgs.append(K.conv_wgrad_workspace(B, c.H, c.H, ci, c.cout, c.k, c.k, c.stride, c.pad))
+
+        def dgrad_parts(c: ConvSpec):
+            parts.append((K.conv_dgrad_num_partials(B, c.H, c.H, c.cin, c.cout, c.k, c.k, c.stride), c.cin))
+
+        # ---------------- stem + max-pool
+        self.stem = ConvSpec("conv1.weight", 3, 64, 7, 2, 3, img_size)
+        H0 = self.stem.Ho
+        self.H0 = H0
+        self.bn0 = BNState(self.flat, model.bn1, "bn1", B * H0 * H0, 64, device)
+        fwd_parts(self.stem)
+        self.Hp = (H0 - 1) // 2 + 1
+        self.pool = torch.empty(B * self.Hp * self.Hp, 64, **bf16)
+        self.pool_idx = torch.empty(B * self.Hp * self.Hp, 64, dtype=torch.uint8, device=device)
+        self.Gpool = torch.empty(B * self.Hp * self.Hp, 64, **bf16)
+        parts.append((K.maxpool_bwd_num_partials(B, H0, H0), 64))
+        # ---------------- bottlenecks
+        self.blocks: List[BlockPlan] = []
+        H, x_in = self.Hp, self.pool
+        for li, layer in enumerate((model.layer1, model.layer2, model.layer3, model.layer4)):
+            for bi, blk in enumerate(layer):
+                blk: Bottleneck
+                pre = f"layer{li + 1}.{bi}"
+                cin, planes, cout, s = blk.conv1.in_channels, blk.conv1.out_channels, blk.conv3.out_channels, blk.stride
+                Ho = (H - 1) // s + 1
+                Min, Mout = B * H * H, B * Ho * Ho
+                c1 = ConvSpec(f"{pre}.conv1.weight", cin, planes, 1, 1, 0, H)
+                c2 = ConvSpec(f"{pre}.conv2.weight", planes, planes, 3, s, 1, H)
+                c3 = ConvSpec(f"{pre}.conv3.weight", planes, cout, 1, 1, 0, Ho)
+                cd = ConvSpec(f"{pre}.downsample.0.weight", cin, cout, 1, s, 0, H) if blk.downsample is not None else None
+                bn1 = BNState(self.flat, blk.bn1, f"{pre}.bn1", Min, planes, device)
+                bn2 = BNState(self.flat, blk.bn2, f"{pre}.bn2", Mout, planes, device)
+                bn3 = BNState(self.flat, blk.bn3, f"{pre}.bn3", Mout, cout, device)
+                bnd = (BNState(self.flat, blk.downsample[1], f"{pre}.downsample.1", Mout, cout, device, need_g=False)
+                       if cd is not None else None)
+                bp = BlockPlan(pre, cin, planes, cout, s, H, Ho, c1, c2, c3, cd, bn1, bn2, bn3, bnd)
+                bp.x_in = x_in
+                bp.out = torch.empty(Mout, cout, **bf16)
+                if cd is not None:
+                    bp.Rd = torch.empty(Min, cin, **bf16)
+                for c in (c1, c2, c3) + ((cd,) if cd else ()):
+                    fwd_parts(c)
+                    dgrad_parts(c)
+                self.blocks.append(bp)
+                H, x_in = Ho, bp.out
+        # ---------------- head
+        self.Hf = H
+        self.C_last = self.blocks[-1].cout
+        self.NC = model.fc.out_features
+        parts.append((B, self.C_last))
+        self.pooled = torch.zeros(B, self.C_last, **f32)
+        self.logits = torch.zeros(B, self.NC, **f32)
+        self.dlogits = torch.zeros(B, self.NC, **f32)
+        self.dpool = torch.zeros(B, self.C_last, **f32)
+        self.loss = torch.zeros(B, **f32)
+        self.correct = torch.zeros(B, **f32)
+        self.fc_w = self.flat.w("fc.weight").view(self.NC, self.C_last)
+        self.fc_b = self.flat.w("fc.bias")
+        self.fc_gw = self.flat.g("fc.weight").view(self.NC, self.C_last)
+        self.fc_gb = self.flat.g("fc.bias")
+        # ---------------- workspaces (stream-ordered reuse)
+        pf = max(K.bn_part_floats(P, C) for P, C in parts) + 1024
+        self.ws_part = torch.zeros(pf, **f32)
+        self.ws_part2 = torch.zeros(pf, **f32)
+        self.ws_wgrad = torch.zeros(max(wgs) + 1024, **f32)
+        self.side = None
+        if side_stream:
+            self.side = torch.cuda.Stream(device)
+            K.register_side_stream(self.side)
+        self.img = torch.zeros(B, img_size, img_size, 4, **bf16)
+        self.labels = torch.zeros(B, dtype=torch.int64, device=device)
+        self.hyper = hyper if hyper is not None else torch.zeros(2, **f32)
+        self.on_params_ready: Optional[Callable[[List[str]], None]] = None
+        # dgrad weights: every conv but the stem transposed to [Cin][R][S][Cout] (one launch)
+        tab = []
+        for bp in self.blocks:
+            for c in (bp.c1, bp.c2, bp.c3) + ((bp.cd,) if bp.cd else ()):
+                off = self.flat.offsets[c.name][0]
+                tab.append((off, off, c.cout, c.k * c.k, c.cin))
+        self.wt_tab = torch.tensor(tab, dtype=torch.int32, device=device).contiguous()
+
+    # ------------------------------------------------------------------ helpers
+    def _ready(self, names):
+        if self.on_params_ready is None:
+            return
+        if self.side is None:
+            self.on_params_ready(names)
+            return
+        self.side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.side):
+            self.on_params_ready(names)
+
+    def _wgrad(self, fn):
+        if self.side is None:
+            fn()
+            return
+        self.side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.side):
+            fn()
+
+    def _fin(self, bn: BNState, P: int, train: bool):
+        if train:
+            bn.finalize_fwd(self.ws_part, P)
+
+    def _conv(self, c: ConvSpec, pro, x, y, train, bn_out: BNState, bn_in: Optional[BNState] = None):
+        B = self.B
+        ci = 4 if c.cin == 3 else c.cin
+        K.conv_fwd(pro, x, self.flat.b(c.name), y, self.ws_part, B, c.H, c.H, ci, c.cout, c.k, c.k, c.stride,
+                   c.pad, pa=bn_in.scale if bn_in is not None else None,
+                   pb=bn_in.shift if bn_in is not None else None)
+        self._fin(bn_out, K.conv_fwd_num_partials(B, c.Ho, c.Ho, c.cout, c.k * c.k * ci, ci), train)
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, train: bool = True):
+        B = self.B
+        self._conv(self.stem, K.CP_NONE, self.img, self.bn0.y, train, self.bn0)
+        K.maxpool_fwd(self.bn0.y, self.bn0.scale, self.bn0.shift, self.pool, self.pool_idx, B, self.H0, self.H0, 64)
+        for bp in self.blocks:
+            self._conv(bp.c1, K.CP_NONE, bp.x_in, bp.bn1.y, train, bp.bn1)
+            self._conv(bp.c2, K.CP_BN_RELU, bp.bn1.y, bp.bn2.y, train, bp.bn2, bp.bn1)
+            self._conv(bp.c3, K.CP_BN_RELU, bp.bn2.y, bp.bn3.y, train, bp.bn3, bp.bn2)
+            if bp.cd is not None:
+                self._conv(bp.cd, K.CP_NONE, bp.x_in, bp.bnd.y, train, bp.bnd)
+                K.res_out(bp.bn3.y, bp.bn3.scale, bp.bn3.shift, bp.bnd.y, bp.out, rs=bp.bnd.scale, rt=bp.bnd.shift)
+            else:
+                K.res_out(bp.bn3.y, bp.bn3.scale, bp.bn3.shift, bp.x_in, bp.out)
+        # head
+        HW = self.Hf * self.Hf
+        K.avgpool(self.blocks[-1].out, self.pooled, B, HW, self.C_last)
+        torch.addmm(self.fc_b, self.pooled, self.fc_w.t(), out=self.logits)
+        K.softmax_ce(self.logits, self.labels, self.loss, self.correct, self.dlogits if train else None,
+                     scale=1.0 / B)
+
+    # ------------------------------------------------------------------ backward
+    def backward(self):
+        f, B, ws, ws2, wg = self.flat, self.B, self.ws_part, self.ws_part2, self.ws_wgrad
+        K.conv_wt(f.shadow, f.shadow_t, self.wt_tab, self.wt_tab.shape[0])
+        # head: fc gradients (fp32 GEMMs) and the pooled gradient through the last ReLU
+        torch.mm(self.dlogits.t(), self.pooled, out=self.fc_gw)
+        torch.sum(self.dlogits, 0, out=self.fc_gb)
+        torch.mm(self.dlogits, self.fc_w, out=self.dpool)
+        self._ready(["fc.weight", "fc.bias"])
+        last = self.blocks[-1]
+        HW = self.Hf * self.Hf
+        K.head_bwd(self.dpool, last.out, last.bn3.y, last.bn3.g, ws, B, HW, self.C_last)
+        last.bn3.finalize_bwd(ws, B)
+        self._ready(last.bn3.param_names)
+        for i in range(len(self.blocks) - 1, -1, -1):
+            bp = self.blocks[i]
+            prev = self.blocks[i - 1] if i > 0 else None
+            bn1, bn2, bn3, bnd = bp.bn1, bp.bn2, bp.bn3, bp.bnd
+            H, Ho = bp.H, bp.Ho
+            c1, c2, c3, cd = bp.c1, bp.c2, bp.c3, bp.cd
+            # conv3 dgrad -> G2 (ReLU mask of BN2) + BN2 partials
+            K.conv_dgrad(K.CE_BWD_RELU, bn3.g, bn3.y, bn3.a, bn3.b, bn3.c, f.bt(c3.name), bn2.g, ws, B, Ho, Ho,
+                         c3.cin, c3.cout, 1, 1, 1, 0, Yt=bn2.y, es=bn2.scale, et=bn2.shift)
+            bn2.finalize_bwd(ws, K.conv_dgrad_num_partials(B, Ho, Ho, c3.cin, c3.cout, 1, 1, 1))
+            self._wgrad(lambda bp=bp: K.conv_wgrad(bp.bn3.g, bp.bn3.y, bp.bn3.a, bp.bn3.b, bp.bn3.c, bp.bn2.y, wg,
+                                                   f.g(bp.c3.name), B, bp.Ho, bp.Ho, bp.c3.cin, bp.c3.cout, 1, 1, 1,
+                                                   0, xpro=K.CP_BN_RELU, xs=bp.bn2.scale, xt=bp.bn2.shift))
+            self._ready([c3.name] + bn2.param_names)
+            # projection shortcut: data gradient (summed in conv1's dgrad epilogue) + weight gradient
+            if cd is not None:
+                K.conv_dgrad(K.CE_BWD_RES, bn3.g, bnd.y, bnd.a, bnd.b, bnd.c, f.bt(cd.name), bp.Rd, None, B, H, H,
+                             cd.cin, cd.cout, 1, 1, cd.stride, 0)
+                self._wgrad(lambda bp=bp: K.conv_wgrad(bp.bn3.g, bp.bnd.y, bp.bnd.a, bp.bnd.b, bp.bnd.c, bp.x_in,
+                                                       wg, f.g(bp.cd.name), B, bp.H, bp.H, bp.cd.cin, bp.cd.cout,
+                                                       1, 1, bp.cd.stride, 0))
+                self._ready([cd.name])
+            # conv2 dgrad -> G1 (ReLU mask of BN1) + BN1 partials
+            K.conv_dgrad(K.CE_BWD_RELU, bn2.g, bn2.y, bn2.a, bn2.b, bn2.c, f.bt(c2.name), bn1.g, ws, B, H, H,
+                         c2.cin, c2.cout, 3, 3, c2.stride, 1, Yt=bn1.y, es=bn1.scale, et=bn1.shift)
+            bn1.finalize_bwd(ws, K.conv_dgrad_num_partials(B, H, H, c2.cin, c2.cout, 3, 3, c2.stride))
+            self._wgrad(lambda bp=bp: K.conv_wgrad(bp.bn2.g, bp.bn2.y, bp.bn2.a, bp.bn2.b, bp.bn2.c, bp.bn1.y, wg,
+                                                   f.g(bp.c2.name), B, bp.H, bp.H, bp.c2.cin, bp.c2.cout, 3, 3,
+                                                   bp.c2.stride, 1, xpro=K.CP_BN_RELU, xs=bp.bn1.scale,
+                                                   xt=bp.bn1.shift))
+            self._ready([c2.name] + bn1.param_names)
+            # conv1 dgrad + shortcut gradient -> gradient of the block input:
+            #   previous block: Gz_prev = (dx + sc) * 1[o_prev > 0], BN3 (+BNd) partials of that block
+            #   first block: gradient of the max-pool output (no ReLU in between)
+            sc = bp.Rd if cd is not None else bn3.g
+            P1 = K.conv_dgrad_num_partials(B, H, H, c1.cin, c1.cout, 1, 1, 1)
+            if prev is not None:
+                pds = prev.bnd is not None
+                K.conv_dgrad(K.CE_BWD_RES, bn1.g, bn1.y, bn1.a, bn1.b, bn1.c, f.bt(c1.name), prev.bn3.g, ws, B, H,
+                             H, c1.cin, c1.cout, 1, 1, 1, 0, Yt=prev.bn3.y, Rg=sc, X=prev.out,
+                             Yt2=prev.bnd.y if pds else None, part2=ws2 if pds else None)
+                prev.bn3.finalize_bwd(ws, P1)
+                if pds:
+                    prev.bnd.finalize_bwd(ws2, P1)
+            else:
+                K.conv_dgrad(K.CE_BWD_RES, bn1.g, bn1.y, bn1.a, bn1.b, bn1.c, f.bt(c1.name), self.Gpool, None, B,
+                             H, H, c1.cin, c1.cout, 1, 1, 1, 0, Rg=sc)
+            self._wgrad(lambda bp=bp: K.conv_wgrad(bp.bn1.g, bp.bn1.y, bp.bn1.a, bp.bn1.b, bp.bn1.c, bp.x_in, wg,
+                                                   f.g(bp.c1.name), B, bp.H, bp.H, bp.c1.cin, bp.c1.cout, 1, 1, 1,
+                                                   0))
+            names = [c1.name]
+            if prev is not None:
+                names += prev.bn3.param_names + (prev.bnd.param_names if prev.bnd is not None else [])
+            self._ready(names)
+        # max-pool + stem
+        bn0 = self.bn0
+        K.maxpool_bwd(self.Gpool, self.pool_idx, bn0.y, bn0.scale, bn0.shift, bn0.g, ws, B, self.H0, self.H0, 64)
+        bn0.finalize_bwd(ws, K.maxpool_bwd_num_partials(B, self.H0, self.H0))
+        st = self.stem
+        self._wgrad(lambda: K.conv_wgrad(bn0.g, bn0.y, bn0.a, bn0.b, bn0.c, self.img, wg, f.g(st.name), B, st.H,
+                                         st.H, 4, st.cout, 7, 7, 2, 3))
+        self._ready([st.name] + bn0.param_names)
+        if self.side is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.side)
+
+    # ------------------------------------------------------------------ eval
+    def all_bns(self):
+        out = [self.bn0]
+        for bp in self.blocks:
+            out += [bp.bn1, bp.bn2, bp.bn3] + ([bp.bnd] if bp.bnd is not None else [])
+        return out
+
+    def eval_prepare(self):
+        for bn in self.all_bns():
+            bn.eval_prepare()
