@@ -15,7 +15,6 @@ constexpr int kMaxDev = 64, kLaneCtrs = 65536;
 int *g_ctr[kMaxDev] = {};
 std::vector<hipStream_t> g_side;
 std::mutex g_mu;
-constexpr int kWredMinRows = 8;
 }  // namespace
 
 void register_side_stream(hipStream_t st) {
@@ -39,45 +38,109 @@ int *reduce_counters(int n, hipStream_t st) {
   return g_ctr[dev] + (side ? kLaneCtrs : 0);
 }
 
-// level-1 rows the wgrad reduction of R partial rows needs after the partials
-int colsum_rows(int R) { return red_nch(R, kWredMinRows); }
+// Geometry: a workgroup covers 16 column groups of V floats x 16 row stripes (each row
+// read as 16 x 16-B pieces = 256 contiguous bytes); the rows are split into nch chunks so
+// the grid has ~2k workgroups, and the last-arriving workgroup of a column block sums the
+// nch level-1 rows (<= kWredMaxChunks) the same way.
+constexpr int kWredMaxChunks = 128;
+constexpr int kWredTargetWgs = 2048;
 
-__global__ __launch_bounds__(256) void col_reduce_kernel(const float *__restrict__ part, int R, long long n,
-                                                         int rch, int nch, float *__restrict__ lvl1,
-                                                         int *__restrict__ ctr, float *__restrict__ out) {
+// level-1 rows the wgrad reduction of R partial rows may need after the partials
+int colsum_rows(int R) {
+  const int c = (R + 15) / 16;
+  return c < 1 ? 1 : (c > kWredMaxChunks ? kWredMaxChunks : c);
+}
+
+template <int V>
+__global__ __launch_bounds__(256) void col_reduce_kernel(const float *__restrict__ part, int R, long long n, int rch,
+                                                         int nch, float *__restrict__ lvl1, int *__restrict__ ctr,
+                                                         float *__restrict__ out) {
+  __shared__ float sh[16][16 * V + 1];
   __shared__ int flag;
-  const long long i = blockIdx.x * 256ll + threadIdx.x;
-  const int r0 = blockIdx.y * rch, r1 = min(R, r0 + rch);
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-  if (i < n) {
-    int r = r0;
-    for (; r + 3 < r1; r += 4) {
-      a0 += part[(size_t)r * n + i];
-      a1 += part[(size_t)(r + 1) * n + i];
-      a2 += part[(size_t)(r + 2) * n + i];
-      a3 += part[(size_t)(r + 3) * n + i];
+  const int cg = threadIdx.x & 15, stripe = threadIdx.x >> 4;
+  const long long c0 = ((long long)blockIdx.x * 16 + cg) * V;
+  const bool cok = c0 < n;
+  float acc[V], acc2[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) acc[j] = acc2[j] = 0.f;
+  auto ld = [&](const float *p, float (&v)[V]) {
+    if constexpr (V == 4) {
+      const float4 q = *reinterpret_cast<const float4 *>(p);
+      v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+    } else {
+      v[0] = *p;
     }
-    for (; r < r1; ++r) a0 += part[(size_t)r * n + i];
+  };
+  const int r0 = blockIdx.y * rch, r1 = min(R, r0 + rch);
+  if (cok) {
+    int r = r0 + stripe;
+    for (; r + 16 < r1; r += 32) {   // two rows in flight per thread, fixed order
+      float a[V], b[V];
+      ld(part + (size_t)r * n + c0, a);
+      ld(part + (size_t)(r + 16) * n + c0, b);
+#pragma unroll
+      for (int j = 0; j < V; ++j) { acc[j] += a[j]; acc2[j] += b[j]; }
+    }
+    if (r < r1) {
+      float a[V];
+      ld(part + (size_t)r * n + c0, a);
+#pragma unroll
+      for (int j = 0; j < V; ++j) acc[j] += a[j];
+    }
   }
-  const float s1 = (a0 + a1) + (a2 + a3);
+#pragma unroll
+  for (int j = 0; j < V; ++j) sh[stripe][cg * V + j] = acc[j] + acc2[j];
+  __syncthreads();
+  const int col = threadIdx.x;   // < 16 * V: one output column per thread
+  const long long oc = (long long)blockIdx.x * 16 * V + col;
+  float s1 = 0.f;
+  if (col < 16 * V) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s1 += sh[k][col];
+  }
   if (nch == 1) {
-    if (i < n) out[i] = s1;
+    if (col < 16 * V && oc < n) out[oc] = s1;
     return;
   }
-  if (i < n) st_sc1(lvl1 + (size_t)blockIdx.y * n + i, s1);
+  if (col < 16 * V && oc < n) st_sc1(lvl1 + (size_t)blockIdx.y * n + oc, s1);
   if (!arrive_last(ctr, nch, &flag)) return;
-  if (i < n) {
+  float b[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) b[j] = 0.f;
+  if (cok) {
+    for (int k = stripe; k < nch; k += 16) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) b[j] += ld_sc1(lvl1 + (size_t)k * n + c0 + j);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < V; ++j) sh[stripe][cg * V + j] = b[j];
+  __syncthreads();
+  if (col < 16 * V && oc < n) {
     float s = 0.f;
-    for (int k = 0; k < nch; ++k) s += ld_sc1(lvl1 + (size_t)k * n + i);
-    out[i] = s;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += sh[k][col];
+    out[oc] = s;
   }
 }
 
 // grad[n] = sum over S split rows of part[S][n] (fixed order); part needs S + colsum_rows(S) rows
 void launch_wgrad_reduce(float *part, int S, long long n, float *grad, hipStream_t st) {
-  const int rch = red_rch(S, kWredMinRows), nch = red_nch(S, kWredMinRows);
-  const unsigned nb = (unsigned)((n + 255) / 256);
+  const bool vec = (n % 4 == 0) && ((uintptr_t)part % 16 == 0) && ((uintptr_t)grad % 16 == 0);
+  const int V = vec ? 4 : 1;
+  const long long nb = (n + 16 * V - 1) / (16 * V);
+  long long want = kWredTargetWgs / (nb > 0 ? nb : 1);
+  int nch = (int)(want < 1 ? 1 : want);
+  const int cap = colsum_rows(S);
+  if (nch > cap) nch = cap;
+  const int rch = (S + nch - 1) / nch;
+  nch = (S + rch - 1) / rch;
   int *ctr = nch > 1 ? reduce_counters((int)nb, st) : nullptr;
-  hipLaunchKernelGGL(col_reduce_kernel, dim3(nb, nch), dim3(256), 0, st, part, S, n, rch, nch,
-                     part + (size_t)S * n, ctr, grad);
+  if (vec)
+    hipLaunchKernelGGL(col_reduce_kernel<4>, dim3((unsigned)nb, nch), dim3(256), 0, st, part, S, n, rch, nch,
+                       part + (size_t)S * n, ctr, grad);
+  else
+    hipLaunchKernelGGL(col_reduce_kernel<1>, dim3((unsigned)nb, nch), dim3(256), 0, st, part, S, n, rch, nch,
+                       part + (size_t)S * n, ctr, grad);
 }

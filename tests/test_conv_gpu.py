@@ -321,3 +321,23 @@ def test_image_prep(dev):
         assert ok
     assert out[..., 3].abs().max().item() == 0
     assert torch.equal(lab, labels[idx])
+
+
+@pytest.mark.parametrize("S,n", [(1, 4096), (7, 1000), (3136, 512), (3000, 36864), (200, 4717), (5000, 64),
+                                 (8, 2359296)])
+def test_wgrad_reduce(dev, S, n):
+    """Split-M weight-gradient reduction: grad = sum of the S partial rows, repeated launches
+    (counters re-armed), fixed summation order (bitwise repeatable)."""
+    rows = S + K.lib().colsum_rows(S)
+    part = torch.zeros(rows * n, device=dev)
+    for it in range(3):
+        vals = rnd(S, n, dev=dev, seed=70 + it)
+        part[: S * n] = vals.reshape(-1)
+        grad = torch.full((n,), float("nan"), device=dev)
+        K.wgrad_reduce(part, S, n, grad)
+        g2 = torch.full((n,), float("nan"), device=dev)
+        K.wgrad_reduce(part, S, n, g2)
+        torch.cuda.synchronize()
+        ref = vals.double().sum(0)
+        assert torch.allclose(grad.double(), ref, rtol=1e-4, atol=1e-3 * (S ** 0.5))
+        assert torch.equal(grad, g2)
