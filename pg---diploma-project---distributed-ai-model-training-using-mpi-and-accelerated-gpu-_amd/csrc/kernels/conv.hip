@@ -34,7 +34,9 @@
 namespace {
 enum { CM_FWD = 0, CM_DGRAD = 1 };
 enum { CP_NONE = 0, CP_BN_RELU = 1, CP_BNBWD = 3 };
-enum { CE_FWD = 0, CE_BWD_RELU = 1, CE_BWD_RES = 2 };
+// backward epilogues: ReLU mask of the producer BN, or (+R) (*1[X>0]) with statistics against
+// Yt (and Yt2); the operand set is a template choice so every epilogue load is unconditional
+enum { CE_FWD = 0, CE_BWD_RELU = 1, CE_BWD_PLAIN = 2, CE_BWD_R = 3, CE_BWD_RXY = 4, CE_BWD_RXYY = 5 };
 
 struct ConvArgs {
   const bf16_t *A;      // gathered image [Nb][Hi][Wi][Ci]  (fwd: x, dgrad: G of this layer's BN)
@@ -144,8 +146,11 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs p) {
     }
   }
 
-  chunk_t ra[ACH], ry[HAS_A2 ? ACH : 1], rbw[BCH];
-  bool va[ACH];
+  struct Stage {
+    chunk_t ra[ACH], ry[HAS_A2 ? ACH : 1], rbw[BCH];
+    bool va[ACH];
+  };
+  Stage S0;
   float pa8[8], pb8[8], pc8[8];
   // tap of a k offset: (dh, dw, weight tap index)
   auto tap_of = [&](int j, int &dh, int &dw, int &wt) {
@@ -157,7 +162,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs p) {
       wt = p.tr[cls][j] * p.S + p.ts[cls][j];
     }
   };
-  auto load = [&](int k0) {
+  auto load = [&](Stage &st, int k0) {
     int u_dh = 0, u_dw = 0, u_wt = 0, u_c0 = 0;
     if constexpr (UT) {
       const int j = k0 / p.Ci;
@@ -180,24 +185,14 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs p) {
       }
       const int ih = rh[i] + dh, iw = rw[i] + dw;
       ok = ok && ih >= 0 && ih < p.Hi && iw >= 0 && iw < p.Wi;
-      va[i] = ok;
+      st.va[i] = ok;
       const size_t off = (((size_t)rb[i] * p.Hi + ih) * p.Wi + iw) * p.Ci + ci;
       if constexpr (CV == 8) {
-        ra[i] = ok ? ldg16(p.A + off) : make_uint4(0, 0, 0, 0);
-        if constexpr (HAS_A2) ry[i] = ok ? ldg16(p.A2 + off) : make_uint4(0, 0, 0, 0);
+        st.ra[i] = ok ? ldg16(p.A + off) : make_uint4(0, 0, 0, 0);
+        if constexpr (HAS_A2) st.ry[i] = ok ? ldg16(p.A2 + off) : make_uint4(0, 0, 0, 0);
       } else {
-        ra[i] = ok ? *reinterpret_cast<const uint2 *>(p.A + off) : make_uint2(0, 0);
+        st.ra[i] = ok ? *reinterpret_cast<const uint2 *>(p.A + off) : make_uint2(0, 0);
       }
-    }
-    if constexpr (PRO != CP_NONE) {
-      // every chunk of this thread sits at the same kk (ACH rows apart) -> one parameter set
-      const int kk = (tid % KCH) * CV;
-      int ci;
-      if constexpr (UT) ci = u_c0 + kk;
-      else { const int k = k0 + kk; ci = k % p.Ci; }
-      ld8f(p.pa + ci, pa8);
-      ld8f(p.pb + ci, pb8);
-      if constexpr (PRO == CP_BNBWD) ld8f(p.pc + ci, pc8);
     }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
@@ -214,31 +209,44 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs p) {
         else { const int j = k / p.Ci; ci = k - j * p.Ci; tap_of(ok ? j : 0, dh, dw, wt); }
         off = (size_t)gn * p.Kw + (size_t)wt * p.Ci + ci;
       }
-      if constexpr (CV == 8) rbw[i] = ok ? ldg16(p.W + off) : make_uint4(0, 0, 0, 0);
-      else rbw[i] = ok ? *reinterpret_cast<const uint2 *>(p.W + off) : make_uint2(0, 0);
+      if constexpr (CV == 8) st.rbw[i] = ok ? ldg16(p.W + off) : make_uint4(0, 0, 0, 0);
+      else st.rbw[i] = ok ? *reinterpret_cast<const uint2 *>(p.W + off) : make_uint2(0, 0);
     }
   };
-  auto write = [&](int buf) {
+  // per-channel prologue parameters of the k-step written next (every chunk of this thread
+  // sits at the same kk, ACH rows apart -> one parameter set)
+  auto load_par = [&](int k0) {
+    if constexpr (PRO != CP_NONE) {
+      const int kk = (tid % KCH) * CV;
+      int ci;
+      if constexpr (UT) ci = k0 % p.Ci + kk;
+      else ci = (k0 + kk) % p.Ci;
+      ld8f(p.pa + ci, pa8);
+      ld8f(p.pb + ci, pb8);
+      if constexpr (PRO == CP_BNBWD) ld8f(p.pc + ci, pc8);
+    }
+  };
+  auto write = [&](Stage &st, int buf) {
     bf16_t *Ab = As + buf * BM * kLDK;
     bf16_t *Bb = Bs + buf * BN * kLDK;
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
       const int c = tid + i * 256, row = c / KCH, kk = (c % KCH) * CV;
       if constexpr (CV == 8) {
-        uint4 v = ra[i];
+        uint4 v = st.ra[i];
         if constexpr (PRO != CP_NONE) {
           float x[8];
-          unpack8(ra[i], x);
+          unpack8(st.ra[i], x);
           if constexpr (PRO == CP_BNBWD) {
             float y[8];
-            unpack8(ry[i], y);
+            unpack8(st.ry[i], y);
 #pragma unroll
             for (int j = 0; j < 8; ++j) x[j] = fmaf(pa8[j], x[j], fmaf(pb8[j], y[j], pc8[j]));
           } else {
 #pragma unroll
             for (int j = 0; j < 8; ++j) x[j] = reluf(fmaf(x[j], pa8[j], pb8[j]));
           }
-          if (!va[i]) {
+          if (!st.va[i]) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) x[j] = 0.f;
           }
@@ -246,14 +254,14 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs p) {
         }
         *reinterpret_cast<uint4 *>(Ab + row * kLDK + kk) = v;
       } else {
-        *reinterpret_cast<uint2 *>(Ab + row * kLDK + kk) = ra[i];
+        *reinterpret_cast<uint2 *>(Ab + row * kLDK + kk) = st.ra[i];
       }
     }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
       const int c = tid + i * 256, n = c / KCH, kk = (c % KCH) * CV;
-      if constexpr (CV == 8) *reinterpret_cast<uint4 *>(Bb + n * kLDK + kk) = rbw[i];
-      else *reinterpret_cast<uint2 *>(Bb + n * kLDK + kk) = rbw[i];
+      if constexpr (CV == 8) *reinterpret_cast<uint4 *>(Bb + n * kLDK + kk) = st.rbw[i];
+      else *reinterpret_cast<uint2 *>(Bb + n * kLDK + kk) = st.rbw[i];
     }
   };
 
@@ -262,15 +270,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs p) {
   for (int r = 0; r < RT; ++r)
 #pragma unroll
     for (int c = 0; c < CTW; ++c) acc[r][c] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  if (nk > 0) {
-    load(0);
-    write(0);
-  }
-  __syncthreads();
-  for (int ks = 0; ks < nk; ++ks) {
-    const int buf = ks & 1;
-    if (ks + 1 < nk) load((ks + 1) * KSTEP);
+  auto mma = [&](int buf) {
     const bf16_t *Ab = As + buf * BM * kLDK;
     const bf16_t *Bb = Bs + buf * BN * kLDK;
 #pragma unroll
@@ -288,11 +288,72 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs p) {
         for (int r = 0; r < RT; ++r) acc[r][c] = mfma16(af[r], bf, acc[r][c]);
       }
     }
-    if (ks + 1 < nk) write(buf ^ 1);
+  };
+
+  // one register stage: the loads of step k+1 are in flight during the MFMAs of step k (a
+  // two-stage variant -- loads two steps ahead -- measured slower on MI355X: it needs ~400
+  // registers for the 128 x 128 tile, i.e. one wave per SIMD)
+  if (nk > 0) {
+    load(S0, 0);
+    load_par(0);
+    write(S0, 0);
+  }
+  __syncthreads();
+  for (int ks = 0; ks < nk; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nk) {
+      load_par((ks + 1) * KSTEP);
+      load(S0, (ks + 1) * KSTEP);
+    }
+    mma(buf);
+    if (ks + 1 < nk) write(S0, buf ^ 1);
     __syncthreads();
   }
 
-  // ---- epilogue: bf16 C tile in LDS, then 16-B row chunks
+  // ---- epilogue: bf16 C tile in LDS, then 16-B row chunks.  The epilogue operands of the
+  // first EB rows are loaded before the C tile is staged; rows past the end are clamped to
+  // a valid row (loads are unconditional, results discarded) so hipcc keeps them in flight.
+  constexpr bool E_R = EPI == CE_BWD_R || EPI == CE_BWD_RXY || EPI == CE_BWD_RXYY;
+  constexpr bool E_X = EPI == CE_BWD_RXY || EPI == CE_BWD_RXYY;
+  constexpr bool E_YT = EPI == CE_BWD_RELU || EPI == CE_BWD_RXY || EPI == CE_BWD_RXYY;
+  constexpr bool E_YT2 = EPI == CE_BWD_RXYY;
+  constexpr bool STATS = EPI == CE_FWD || E_YT;
+  constexpr int EB = NP < 4 ? NP : 4;
+  const int my_chunk = tid % CH;
+  const bool colok = n0 + my_chunk * 8 < p.N;
+  const int ncol0 = colok ? n0 + my_chunk * 8 : 0;
+  float s0[8], s1[8], s2[8], es[8], et[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s0[j] = s1[j] = s2[j] = 0.f;
+  if constexpr (EPI == CE_BWD_RELU) {
+    ld8f(p.es + ncol0, es);
+    ld8f(p.et + ncol0, et);
+  }
+  uint4 oy[EB], orr[EB], ox[EB], oy2[EB];
+  size_t offs[EB];
+  bool okr[EB];
+  auto issue = [&](int i0) {
+#pragma unroll
+    for (int e = 0; e < EB; ++e) {
+      const int rr = tid / CH + (i0 + e) * RSTEP;
+      int m = m0 + rr;
+      okr[e] = m < p.Mc && colok;
+      if (m >= p.Mc) m = p.Mc - 1;
+      size_t pix;
+      if constexpr (MODE == CM_FWD) {
+        pix = m;
+      } else {
+        const int b = m / HWc, rem = m % HWc, hh = rem / p.Wc, ww = rem % p.Wc;
+        pix = ((size_t)b * p.Ho + hh * p.stride + ph) * p.Wo + ww * p.stride + pw;
+      }
+      offs[e] = pix * p.N + ncol0;
+      if constexpr (E_YT) oy[e] = ldg16(p.Yt + offs[e]);
+      if constexpr (E_R) orr[e] = ldg16(p.Rg + offs[e]);
+      if constexpr (E_X) ox[e] = ldg16(p.X + offs[e]);
+      if constexpr (E_YT2) oy2[e] = ldg16(p.Yt2 + offs[e]);
+    }
+  };
+  issue(0);
 #pragma unroll
   for (int c = 0; c < CTW; ++c) {
     const int col = wn * (BN / 2) + c * 16 + (lane & 15);
@@ -302,74 +363,58 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs p) {
       for (int j = 0; j < 4; ++j) Cs[(wm * (BM / 2) + r * 16 + 4 * (lane >> 4) + j) * LDC + col] = f2bf(acc[r][c][j]);
   }
   __syncthreads();
-  const int my_chunk = tid % CH, ncol0 = n0 + my_chunk * 8;
-  const bool colok = ncol0 < p.N;
-  float s0[8], s1[8], s2[8], es[8], et[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) s0[j] = s1[j] = s2[j] = 0.f;
-  if constexpr (EPI == CE_BWD_RELU) {
-    if (colok) { ld8f(p.es + ncol0, es); ld8f(p.et + ncol0, et); }
-  }
-  const bool has_yt = EPI == CE_FWD || p.Yt != nullptr;
-  const bool has_yt2 = EPI == CE_BWD_RES && p.Yt2 != nullptr;
-#pragma unroll 2
-  for (int i0 = 0; i0 < NP; ++i0) {
-    const int rr = tid / CH + i0 * RSTEP, m = m0 + rr;
-    if (m >= p.Mc || !colok) continue;
-    size_t pix;
-    if constexpr (MODE == CM_FWD) {
-      pix = m;
-    } else {
-      const int b = m / HWc, rem = m % HWc, hh = rem / p.Wc, ww = rem % p.Wc;
-      pix = ((size_t)b * p.Ho + hh * p.stride + ph) * p.Wo + ww * p.stride + pw;
-    }
-    const size_t off = pix * p.N + ncol0;
-    float v[8];
-    unpack8(*reinterpret_cast<const uint4 *>(Cs + rr * LDC + my_chunk * 8), v);
-    if constexpr (EPI == CE_FWD) {
+  for (int i0 = 0; i0 < NP; i0 += EB) {
+    if (i0 > 0) issue(i0);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { s0[j] += v[j]; s1[j] = fmaf(v[j], v[j], s1[j]); }
-    } else if constexpr (EPI == CE_BWD_RELU) {
-      float yt[8];
-      unpack8(ldg16(p.Yt + off), yt);
+    for (int e = 0; e < EB; ++e) {
+      const int rr = tid / CH + (i0 + e) * RSTEP;
+      float v[8];
+      unpack8(*reinterpret_cast<const uint4 *>(Cs + rr * LDC + my_chunk * 8), v);
+      if constexpr (EPI == CE_FWD) {
+        if (okr[e]) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        v[j] = fmaf(yt[j], es[j], et[j]) > 0.f ? v[j] : 0.f;
-        v[j] = bf2f(f2bf(v[j]));
-        s0[j] += v[j];
-        s1[j] = fmaf(v[j], yt[j], s1[j]);
-      }
-    } else {
-      if (p.Rg) {
-        float rv[8];
-        unpack8(ldg16(p.Rg + off), rv);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] += rv[j];
-      }
-      if (p.X) {
-        float xv[8];
-        unpack8(ldg16(p.X + off), xv);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = xv[j] > 0.f ? v[j] : 0.f;
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = bf2f(f2bf(v[j]));
-      if (has_yt) {
+          for (int j = 0; j < 8; ++j) { s0[j] += v[j]; s1[j] = fmaf(v[j], v[j], s1[j]); }
+        }
+      } else {
         float yt[8];
-        unpack8(ldg16(p.Yt + off), yt);
+        if constexpr (E_YT) unpack8(oy[e], yt);
+        if constexpr (EPI == CE_BWD_RELU) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { s0[j] += v[j]; s1[j] = fmaf(v[j], yt[j], s1[j]); }
-      }
-      if (has_yt2) {
-        float y2[8];
-        unpack8(ldg16(p.Yt2 + off), y2);
+          for (int j = 0; j < 8; ++j) v[j] = fmaf(yt[j], es[j], et[j]) > 0.f ? v[j] : 0.f;
+        }
+        if constexpr (E_R) {
+          float rv[8];
+          unpack8(orr[e], rv);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) s2[j] = fmaf(v[j], y2[j], s2[j]);
+          for (int j = 0; j < 8; ++j) v[j] += rv[j];
+        }
+        if constexpr (E_X) {
+          float xv[8];
+          unpack8(ox[e], xv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = xv[j] > 0.f ? v[j] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = bf2f(f2bf(v[j]));
+        if (okr[e]) {
+          if constexpr (E_YT) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { s0[j] += v[j]; s1[j] = fmaf(v[j], yt[j], s1[j]); }
+          }
+          if constexpr (E_YT2) {
+            float y2[8];
+            unpack8(oy2[e], y2);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s2[j] = fmaf(v[j], y2[j], s2[j]);
+          }
+        }
       }
+      if (okr[e]) stg16(p.out + offs[e], pack8(v));
     }
-    stg16(p.out + off, pack8(v));
   }
-  if (!has_yt) return;   // uniform: no statistics requested
+  if constexpr (!STATS) return;
+  const bool has_yt2 = E_YT2;
   __syncthreads();
   // ---- BN partials of this tile's columns -> part[cls*nmt + mt][2][N] (and part2)
   const int prow = cls * nmt + mt;
@@ -412,7 +457,7 @@ struct WgArgs {
   int M;                // Nb*Ho*Wo
   int rows_per_split;
 };
-constexpr int kWgMK = 32;             // m rows per step
+constexpr int kWgMK = 64;             // m rows per step
 constexpr int kWgLD = kWgMK + 8;      // transposed row pitch (bf16)
 }  // namespace
 
@@ -593,17 +638,22 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs p) {
     const bool has_next = m0 + kWgMK < mend;
     if (has_next) load_step(m0 + kWgMK);
     const bf16_t *Td = Tdy[buf], *Tq = Tx[buf];
-    s16x8_t af[RN], bfr[RK];
 #pragma unroll
-    for (int a = 0; a < RN; ++a)
-      af[a] = *reinterpret_cast<const s16x8_t *>(Td + (wn * QN + a * 16 + (lane & 15)) * kWgLD + 8 * (lane >> 4));
+    for (int sub = 0; sub < kWgMK / 32; ++sub) {
+      s16x8_t af[RN], bfr[RK];
 #pragma unroll
-    for (int b = 0; b < RK; ++b)
-      bfr[b] = *reinterpret_cast<const s16x8_t *>(Tq + (wk * QK + b * 16 + (lane & 15)) * kWgLD + 8 * (lane >> 4));
+      for (int a = 0; a < RN; ++a)
+        af[a] = *reinterpret_cast<const s16x8_t *>(Td + (wn * QN + a * 16 + (lane & 15)) * kWgLD + sub * 32 +
+                                                   8 * (lane >> 4));
 #pragma unroll
-    for (int a = 0; a < RN; ++a)
+      for (int b = 0; b < RK; ++b)
+        bfr[b] = *reinterpret_cast<const s16x8_t *>(Tq + (wk * QK + b * 16 + (lane & 15)) * kWgLD + sub * 32 +
+                                                    8 * (lane >> 4));
 #pragma unroll
-      for (int b = 0; b < RK; ++b) acc[a][b] = mfma16(af[a], bfr[b], acc[a][b]);
+      for (int a = 0; a < RN; ++a)
+#pragma unroll
+        for (int b = 0; b < RK; ++b) acc[a][b] = mfma16(af[a], bfr[b], acc[a][b]);
+    }
     if (has_next) write_step(buf ^ 1);
     __syncthreads();
     buf ^= 1;
@@ -1017,7 +1067,8 @@ void launch_conv_fwd(int pro, const bf16_t *x, const float *pa, const float *pb,
 // dgrad.  G, Y [Nb][Ho][Wo][Cout] (this layer's BN-backward: dy = ga*G + gb*Y + gc),
 // wt [Cin][R][S][Cout]; out dx [Nb][H][W][Cin]   (H % st == 0, W % st == 0)
 // epi 1: dx * (Yt*es + et > 0) + partials (sum, sum*Yt)
-// epi 2: (dx + Rg) * (X > 0) + partials against Yt (part) and Yt2 (part2); null pointers skip
+// epi 2: (dx + Rg) * (X > 0) + partials against Yt (part) and Yt2 (part2); operand sets:
+//        {} | {Rg} | {Rg, X, Yt} | {Rg, X, Yt, Yt2}
 void launch_conv_dgrad(int epi, const bf16_t *G, const bf16_t *Y, const float *ga, const float *gb, const float *gc,
                        const bf16_t *wt, bf16_t *dx, const bf16_t *Yt, const float *es, const float *et,
                        const bf16_t *Rg, const bf16_t *X, const bf16_t *Yt2, float *part, float *part2, int Nb, int H,
@@ -1039,8 +1090,12 @@ void launch_conv_dgrad(int epi, const bf16_t *G, const bf16_t *Y, const float *g
   a.K = kmax;
   const Geom g = igemm_geom(a.Mc, Cin, kmax, Cout, st * st);
   a.nmt = g.nmt;
-  if (epi == CE_BWD_RELU) launch_geom<CM_DGRAD, CP_BNBWD, CE_BWD_RELU, 8>(a, g, stream);
-  else launch_geom<CM_DGRAD, CP_BNBWD, CE_BWD_RES, 8>(a, g, stream);
+  if (epi == CE_BWD_RELU) { launch_geom<CM_DGRAD, CP_BNBWD, CE_BWD_RELU, 8>(a, g, stream); return; }
+  // (dx + Rg) * 1[X > 0] with statistics against Yt (, Yt2): supported operand sets
+  if (!Rg && !X && !Yt && !Yt2) launch_geom<CM_DGRAD, CP_BNBWD, CE_BWD_PLAIN, 8>(a, g, stream);
+  else if (Rg && !X && !Yt && !Yt2) launch_geom<CM_DGRAD, CP_BNBWD, CE_BWD_R, 8>(a, g, stream);
+  else if (Rg && X && Yt && !Yt2) launch_geom<CM_DGRAD, CP_BNBWD, CE_BWD_RXY, 8>(a, g, stream);
+  else if (Rg && X && Yt && Yt2) launch_geom<CM_DGRAD, CP_BNBWD, CE_BWD_RXYY, 8>(a, g, stream);
 }
 
 // ---- weight gradient

@@ -470,6 +470,10 @@ def conv_dgrad(epi, G, Y, ga, gb, gc, wt, dx, part, B, H, W, Cin, Cout, R, S, st
             raise ValueError("conv_dgrad(CE_BWD_RELU) needs Yt, es, et")
         _chk(part, F32, P * 2 * Cin, "part")
     elif epi == CE_BWD_RES:
+        ops = (Rg is not None, X is not None, Yt is not None, Yt2 is not None)
+        if ops not in ((False, False, False, False), (True, False, False, False), (True, True, True, False),
+                       (True, True, True, True)):
+            raise ValueError("conv_dgrad(CE_BWD_RES): operand sets {} | {Rg} | {Rg,X,Yt} | {Rg,X,Yt,Yt2}")
         if Yt is not None:
             _chk(part, F32, P * 2 * Cin, "part")
         if Yt2 is not None:
