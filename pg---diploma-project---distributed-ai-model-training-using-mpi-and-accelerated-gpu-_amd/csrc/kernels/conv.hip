@@ -960,12 +960,15 @@ struct Geom {
 
 Geom igemm_geom(int M, int N, int Kmax, int Ci, int ncls) {
   Geom g{};
-  const int cand[4][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}};
+  // largest tile that still gives min_wgs workgroups (128 x 128 tiles run at 1.3-1.8x the
+  // MFMA rate of the smaller ones on MI355X, so the bar is about one workgroup per CU)
+  static const int min_wgs = [] { const char *e = getenv("PGDIST_CONV_MINWG"); return e ? atoi(e) : 256; }();
+  const int cand[4][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}};
   int pick = 3;
   for (int i = 0; i < 4; ++i) {
     if (cand[i][1] == 128 && N <= 64) continue;   // no half-empty N tiles
     const long long wgs = (long long)((M + cand[i][0] - 1) / cand[i][0]) * ((N + cand[i][1] - 1) / cand[i][1]) * ncls;
-    if (wgs >= 512) { pick = i; break; }
+    if (wgs >= min_wgs) { pick = i; break; }
   }
   g.BM = cand[pick][0];
   g.BN = cand[pick][1];
@@ -1108,7 +1111,8 @@ WgGeom wg_geom(int N, int Kw, int M) {
   g.TN = N >= 128 ? 128 : 64;
   g.TK = Kw >= 128 ? 128 : 64;
   const long long tiles = (long long)((N + g.TN - 1) / g.TN) * ((Kw + g.TK - 1) / g.TK);
-  long long ns = (1024 + tiles - 1) / tiles;
+  static const int target = [] { const char *e = getenv("PGDIST_WG_TARGET"); return e ? atoi(e) : 1024; }();
+  long long ns = (target + tiles - 1) / tiles;
   const long long max_ns = (M + 4 * kWgMK - 1) / (4 * kWgMK);   // >= 4 steps per split
   if (ns > max_ns) ns = max_ns;
   if (ns < 1) ns = 1;
