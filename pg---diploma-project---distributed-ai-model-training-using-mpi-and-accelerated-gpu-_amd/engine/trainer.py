@@ -109,8 +109,8 @@ class Trainer:
     def _init_hip(self):
         from .native_step import NativeTrainStep
         cfg = self.cfg
-        if cfg.model != "mobilenet_v2":
-            raise NotImplementedError("the native HIP executor implements mobilenet_v2")
+        if cfg.model not in ("mobilenet_v2", "resnet50"):
+            raise NotImplementedError("native HIP executors: mobilenet_v2, resnet50")
         self.step = NativeTrainStep(self.model, cfg.batch_size, self.device, img_size=cfg.img_size,
                                     lr=self.base_lr, betas=cfg.betas, eps=cfg.eps,
                                     weight_decay=cfg.weight_decay, world_size=self.world, rank=self.rank,

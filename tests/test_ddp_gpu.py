@@ -25,18 +25,18 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, model_name):
     import pgdist  # noqa: F401
-    from pgdist.models import mobilenet_v2
+    from pgdist.models import build_model
     from pgdist.engine.native_step import NativeTrainStep
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cuda", 0)
     torch.manual_seed(100 + rank)            # different init per rank: the broadcast must fix it
-    model = mobilenet_v2(10)
+    model = build_model(model_name, num_classes=10)
     st = NativeTrainStep(model, 8, dev, img_size=64, lr=1e-3, world_size=world, rank=rank,
-                         bucket_mb=0.5, first_bucket_mb=0.1)
+                         bucket_mb=0.5 if model_name == "mobilenet_v2" else 8.0, first_bucket_mb=0.1)
     g = torch.Generator(device=dev).manual_seed(7)
     src = torch.randint(0, 256, (64, 32, 32, 3), dtype=torch.uint8, device=dev, generator=g)
     labels = torch.randint(0, 10, (64,), device=dev, generator=g)
@@ -53,11 +53,12 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_native_ddp_two_ranks_one_gpu():
+@pytest.mark.parametrize("model_name", ["mobilenet_v2", "resnet50"])
+def test_native_ddp_two_ranks_one_gpu(model_name):
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, model_name)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=400) for _ in range(world)]

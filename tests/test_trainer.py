@@ -82,3 +82,20 @@ def test_native_training_hip_backend(tmp_path, capsys):
     tr2 = Trainer(cfg.replace(epochs=4, resume="auto"))
     assert tr2.start_epoch == 3
     assert int(tr2.step.hyper[1].item()) == 30
+
+
+@pytest.mark.gpu
+def test_native_training_resnet50(tmp_path, capsys):
+    """ResNet-50 (BASELINE config 4) through the same trainer on the native dense-conv executor:
+    CIFAR-shaped data GPU-augmented to 64x64, tail batch, eval, torchvision-keyed checkpoint."""
+    cfg = _cfg(tmp_path, device="cuda", backend="hip", precision="bf16", augment="gpu", model="resnet50",
+               synthetic_train_size=100, synthetic_test_size=40, batch_size=16, epochs=2, img_size=64,
+               lr=1e-3, ckpt_dir=str(tmp_path / "ck"))
+    tr = Trainer(cfg)
+    hist = tr.fit()
+    out = capsys.readouterr().out.splitlines()
+    assert sum(1 for l in out if SERIAL_RE.match(l)) == 2
+    assert hist[-1]["train_images"] == 100          # 6 full batches + a native tail batch of 4
+    assert all(h["train_loss"] == h["train_loss"] and h["test_loss"] == h["test_loss"] for h in hist)
+    sd = torch.load(tmp_path / "best.pth", weights_only=True)
+    assert len(sd) == 320 and tuple(sd["conv1.weight"].shape) == (64, 3, 7, 7)
