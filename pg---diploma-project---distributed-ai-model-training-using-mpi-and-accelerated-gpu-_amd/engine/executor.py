@@ -112,6 +112,7 @@ class MobileNetV2Executor:
     # block outputs materialised by the consumer GEMM instead of a BN-apply pass: measured neutral
     # on MI355X (the consumer reads y_p and the residual per N tile), so off by default
     FUSE_BLOCK_OUTPUT = os.environ.get("PGDIST_FUSE_BLOCK_OUT", "0") == "1"
+    STEM_WGRAD_SIDE = os.environ.get("PGDIST_STEM_WGRAD_SIDE", "0") == "1"
     # fp8 mode: every forward 1x1 conv runs on e4m3 MFMA (weights per output channel, activations
     # scaled by ops.kernels.FP8_ASC), backward and depthwise/BN stay bf16/fp32
 
@@ -204,6 +205,9 @@ class MobileNetV2Executor:
         # ---------------- workspaces (stream-ordered reuse)
         self.ws_part = torch.zeros(max(K.bn_part_floats(P, C) for P, C in parts) + 1024, **f32)
         self.ws_wgrad = torch.zeros(max(wg) + 1024, **f32)
+        # the stem weight gradient may run on the main stream concurrently with side-stream
+        # weight gradients: its own split-M workspace
+        self.ws_stem = torch.zeros(K.stem_wgrad_workspace(B, img_size, img_size, 32) + 1024, **f32)
         self._wpart = {k: torch.zeros(v + 1024, **f32) for k, v in wparts.items()}
         # weight gradients that are not fused into a dgrad run on a side stream, overlapping
         # the dgrad -> BN-finalize chain (the backward's critical path)
@@ -431,10 +435,16 @@ class MobileNetV2Executor:
                                                    K.ACT_NONE, wg, f.g(bp.w_e), Min, bp.hidden, bp.cin))
                 self._ready([bp.w_e] + prev.bn_p.param_names)
             else:
-                # t=1 block: its input is relu6(BN0(stem)) -> stem weight gradient
+                # t=1 block: its input is relu6(BN0(stem)) -> stem weight gradient.  It is the last
+                # work of the backward: on the main stream it runs beside the side stream's backlog
+                # instead of queueing behind it (PGDIST_STEM_WGRAD_SIDE=1: side stream)
                 bn0 = self.bn0
-                self._wgrad(lambda: K.stem_wgrad(bn0.g, bn0.y, bn0.a, bn0.b, bn0.c, self.img, wg,
-                                                 f.g(self.stem_w), B, S, S, 32))
+                stem_wg = lambda: K.stem_wgrad(bn0.g, bn0.y, bn0.a, bn0.b, bn0.c, self.img, self.ws_stem,  # noqa: E731
+                                               f.g(self.stem_w), B, S, S, 32)
+                if self.STEM_WGRAD_SIDE:
+                    self._wgrad(stem_wg)
+                else:
+                    stem_wg()
                 self._ready([self.stem_w])
         if self.side is not None:   # join: the optimizer (main stream) needs every gradient
             torch.cuda.current_stream(self.device).wait_stream(self.side)
