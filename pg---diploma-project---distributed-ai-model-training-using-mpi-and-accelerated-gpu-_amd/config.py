@@ -48,7 +48,7 @@ class TrainConfig:
     deterministic: bool = False
     # distributed
     dist_backend: str = "auto"                # auto (nccl on GPU = RCCL, gloo on CPU)
-    bucket_mb: float = 4.0                    # gradient all-reduce bucket cap (MiB)
+    bucket_mb: Optional[float] = None         # gradient all-reduce bucket cap (MiB); None: ~total/6
     first_bucket_mb: float = 1.0
     grad_reduce_dtype: str = "fp32"           # fp32 | bf16
     bn_sync: str = "eval"                     # broadcast (every step, reference DDP default) | eval (before eval/save) | none

@@ -53,7 +53,7 @@ def coalesce_bn_buffers(model: torch.nn.Module):
 class NativeTrainStep:
     def __init__(self, model, batch: int, device: torch.device, img_size: int = 224, lr: float = 1e-4,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, world_size: int = 1,
-                 rank: int = 0, use_graph: bool = True, seed: int = 0, bucket_mb: float = 4.0,
+                 rank: int = 0, use_graph: bool = True, seed: int = 0, bucket_mb: Optional[float] = None,
                  first_bucket_mb: float = 1.0, reduce_dtype: torch.dtype = torch.float32,
                  double_resize: bool = True, augment: bool = True, train_augment: bool = True,
                  side_stream: bool = True, bn_broadcast: bool = False, fp8: bool = False):

@@ -51,10 +51,20 @@ def build_buckets(ranges: Sequence[Tuple[str, int, int]], cap_bytes: int, first_
     return buckets
 
 
+def auto_bucket_mb(grad_bytes: int) -> float:
+    """Bucket cap for a gradient of ``grad_bytes``: ~6 buckets (1-32 MiB).  The bucket holding the
+    stem-side parameters completes last and its all-reduce is exposed after the backward, so it
+    should be small; too many buckets pay RCCL's per-call latency (MobileNetV2: 8.95 MB ->
+    1.5 MiB buckets, the last one 0.3 MiB; ResNet-50: 102 MB -> 16 MiB)."""
+    return min(32.0, max(1.0, grad_bytes / 2 ** 20 / 6))
+
+
 class BucketedGradReducer:
     def __init__(self, flat_grad: torch.Tensor, ranges: Sequence[Tuple[str, int, int]],
-                 bucket_cap_mb: float = 4.0, first_bucket_mb: float = 1.0,
+                 bucket_cap_mb: Optional[float] = None, first_bucket_mb: float = 1.0,
                  reduce_dtype: torch.dtype = torch.float32, group=None):
+        if bucket_cap_mb is None:
+            bucket_cap_mb = auto_bucket_mb(flat_grad.numel() * flat_grad.element_size())
         self.grad = flat_grad
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
