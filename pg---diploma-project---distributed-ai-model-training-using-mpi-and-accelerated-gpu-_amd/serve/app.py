@@ -75,8 +75,9 @@ def main(argv=None):
     ap.add_argument("--port", type=int, default=7861)
     ap.add_argument("--normalize", choices=("imagenet", "cifar"), default="imagenet")
     ap.add_argument("--device", default="auto")
+    ap.add_argument("--model", default="mobilenet_v2", help="mobilenet_v2 | resnet50 (checkpoint architecture)")
     a = ap.parse_args(argv)
-    pred = Predictor(a.checkpoint, device=a.device, normalize=a.normalize)
+    pred = Predictor(a.checkpoint, device=a.device, normalize=a.normalize, model_name=a.model)
     try:
         demo = build_gradio(pred)
         demo.launch(server_name=a.host, server_port=a.port)

@@ -47,12 +47,12 @@ class Predictor:
     def __init__(self, checkpoint: Optional[str] = None, model: Optional[torch.nn.Module] = None,
                  device: Union[str, torch.device] = "auto", classes: Sequence[str] = CIFAR10_CLASSES,
                  img_size: int = 224, backend: str = "auto", normalize: str = "imagenet",
-                 max_batch: int = 16):
+                 max_batch: int = 16, model_name: str = "mobilenet_v2"):
         dev = torch.device("cuda" if (device == "auto" and torch.cuda.is_available()) else
                            ("cpu" if device == "auto" else device))
         self.device, self.classes, self.img_size = dev, tuple(classes), img_size
         if model is None:
-            model = build_model("mobilenet_v2", num_classes=len(classes))
+            model = build_model(model_name, num_classes=len(classes))
             if checkpoint:
                 from ..engine.checkpoint import load_model_weights
                 load_model_weights(model, checkpoint)
@@ -65,9 +65,9 @@ class Predictor:
             backend = "hip" if dev.type == "cuda" else "torch"
         self.backend = backend
         self.max_batch = max_batch
-        if backend == "hip":
-            from ..engine.executor import MobileNetV2Executor
-            self.exe = MobileNetV2Executor(self.model, max_batch, img_size, dev)
+        if backend == "hip":   # native eval executor of the model family (BN from running statistics)
+            from ..engine.native_step import executor_class
+            self.exe = executor_class(self.model)(self.model, max_batch, img_size, dev)
             self.exe.eval_prepare()
 
     @torch.no_grad()

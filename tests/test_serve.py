@@ -73,3 +73,22 @@ def test_native_predictor_matches_torch(tmp_path, ckpt):
     nat = Predictor(str(p), device="cuda", backend="hip", max_batch=4).probs([img, img])
     assert torch.allclose(nat, ref, atol=0.05)
     assert nat.argmax(1).tolist() == ref.argmax(1).tolist()
+
+
+@pytest.mark.gpu
+def test_native_predictor_resnet50(tmp_path):
+    """ResNet-50 checkpoint served through its native eval executor (BN from running stats)."""
+    from pgdist.models import build_model
+    torch.manual_seed(0)
+    m = build_model("resnet50", num_classes=10)
+    with torch.no_grad():   # non-trivial running statistics
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.BatchNorm2d):
+                mod.running_mean.uniform_(-0.1, 0.1)
+                mod.running_var.uniform_(0.5, 1.5)
+    p = tmp_path / "r50.pth"
+    torch.save(m.state_dict(), p)
+    img = str(_png(tmp_path, (20, 180, 60)))
+    ref = Predictor(str(p), device="cpu", model_name="resnet50").probs([img])
+    nat = Predictor(str(p), device="cuda", backend="hip", max_batch=2, model_name="resnet50").probs([img])
+    assert torch.allclose(nat, ref, atol=0.05)
