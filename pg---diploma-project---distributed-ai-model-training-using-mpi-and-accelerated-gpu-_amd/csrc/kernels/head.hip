@@ -11,6 +11,7 @@
 
 namespace {
 constexpr int kMaxNC = 16;
+constexpr int kPix = 8;   // pixel rows loaded per batch in the pooling / gradient loops
 }
 
 __global__ __launch_bounds__(256) void head_kernel(
@@ -36,11 +37,19 @@ __global__ __launch_bounds__(256) void head_kernel(
       sh[k] = t[c0 + k];
       pd[k] = 0.f;
     }
-    for (int hw = 0; hw < HW; ++hw) {
+    const bf16_t *yb = y + (size_t)b * HW * C + c0;
+    for (int h0 = 0; h0 < HW; h0 += kPix) {   // kPix pixel loads in flight (a serial load chain before)
+     uint4 raw[kPix];
+#pragma unroll
+     for (int u = 0; u < kPix; ++u) raw[u] = ldg16(yb + (size_t)min(h0 + u, HW - 1) * C);   // clamped, unconditional
+#pragma unroll
+     for (int u = 0; u < kPix; ++u) {
+      if (h0 + u >= HW) break;
       float v[8];
-      unpack8(ldg16(y + ((size_t)b * HW + hw) * C + c0), v);
+      unpack8(raw[u], v);
 #pragma unroll
       for (int k = 0; k < 8; ++k) pd[k] += relu6f(fmaf(v[k], sc[k], sh[k]));
+     }
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -100,10 +109,16 @@ __global__ __launch_bounds__(256) void head_kernel(
   float st0[8], st1[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) st0[k] = st1[k] = 0.f;
-  for (int hw = 0; hw < HW; ++hw) {
-    const size_t off = ((size_t)b * HW + hw) * C + c0;
+  for (int h0 = 0; h0 < HW; h0 += kPix) {
+   uint4 raw[kPix];
+#pragma unroll
+   for (int u = 0; u < kPix; ++u) raw[u] = ldg16(y + ((size_t)b * HW + min(h0 + u, HW - 1)) * C + c0);
+#pragma unroll
+   for (int u = 0; u < kPix; ++u) {
+    if (h0 + u >= HW) break;
+    const size_t off = ((size_t)b * HW + h0 + u) * C + c0;
     float v[8], g[8];
-    unpack8(ldg16(y + off), v);
+    unpack8(raw[u], v);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       g[k] = dz[k] * relu6_mask(v[k], sc[k], sh[k]);
@@ -118,6 +133,7 @@ __global__ __launch_bounds__(256) void head_kernel(
       st1[k] = fmaf(gr[k], v[k], st1[k]);
     }
     stg16(g_out + off, gp);
+   }
   }
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -134,9 +150,14 @@ __global__ __launch_bounds__(256) void head_wgrad_kernel(const float *__restrict
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i < NC * C) {
     const int j = i / C, c = i % C;
-    float a = 0.f;
-    for (int b = 0; b < B; ++b) a = fmaf(dlogits[b * NC + j], pd[(size_t)b * C + c], a);
-    dW[i] = a;
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // 16 loads in flight per step
+    int b = 0;
+    for (; b + 8 <= B; b += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] = fmaf(dlogits[(b + u) * NC + j], pd[(size_t)(b + u) * C + c], a[u]);
+    }
+    for (; b < B; ++b) a[0] = fmaf(dlogits[b * NC + j], pd[(size_t)b * C + c], a[0]);
+    dW[i] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
   } else if (i < NC * C + NC) {
     const int j = i - NC * C;
     float a = 0.f;
