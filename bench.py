@@ -63,7 +63,7 @@ def main():
 
     from pgdist.engine.bench_step import build_bench_step
     step_fn, meta = build_bench_step(args.model, args.batch_size, device, backend=args.backend,
-                                     img_size=args.img_size, use_graph=bool(args.graph), side_stream=bool(args.side_stream),
+                                     img_size=args.img_size, use_graph=args.graph, side_stream=bool(args.side_stream),
                                      fp8=bool(args.fp8), world_size=world, rank=info.rank)
 
     def sync():

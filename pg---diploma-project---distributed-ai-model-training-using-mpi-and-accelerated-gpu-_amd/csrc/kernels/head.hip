@@ -1,7 +1,7 @@
 // Fused classifier head + loss: BN-apply/ReLU6 of the last 1x1 conv ->
 // global average pool -> Dropout(p) -> Linear(C, NC) -> softmax cross-entropy
 // (mean over the local batch) -> argmax/correct, AND its backward down to the
-// BN-backward partials of features.18 — one workgroup per image.
+// BN-backward partials of features.18 (pool / CE / backward launches, below).
 //
 // Reference ops: AdaptiveAvgPool2d(1) + flatten, Dropout(0.2),
 // Linear(1280, 10), CrossEntropyLoss, torch.max + .item() metrics
@@ -11,134 +11,184 @@
 
 namespace {
 constexpr int kMaxNC = 16;
-constexpr int kPix = 8;   // pixel rows loaded per batch in the pooling / gradient loops
-}
+constexpr int kSlots = 8;        // pixel slots per workgroup (32 channel lanes x 8 slots = 256 threads)
+constexpr int kChunk = 32 * 8;   // channels per workgroup (8 per lane)
 
-__global__ __launch_bounds__(256) void head_kernel(
-    const bf16_t *__restrict__ y, const float *__restrict__ s, const float *__restrict__ t,
-    const float *__restrict__ Wl, const float *__restrict__ bl, const long long *__restrict__ labels,
-    int HW, int C, int NC, float drop_p, unsigned long long seed, const float *__restrict__ hyper,
-    int train, float loss_scale, float *__restrict__ logits_out, float *__restrict__ loss_out,
-    float *__restrict__ correct_out, float *__restrict__ dlogits, float *__restrict__ pd_out,
-    bf16_t *__restrict__ g_out, float *__restrict__ part) {
-  __shared__ float red[4][kMaxNC];
-  __shared__ float dl[kMaxNC];
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int C8 = C / 8;
-  const bool active = tid < C8;
-  const int c0 = tid * 8;
-  const float inv_hw = 1.f / (float)HW;
-  const unsigned long long ctr = hyper ? (unsigned long long)hyper[1] : 0ull;
-  float sc[8], sh[8], pd[8], keep[8];
+PG_DEVICE float drop_keep(int train, float drop_p, unsigned long long seed, unsigned long long ctr, size_t i) {
+  if (!train || drop_p <= 0.f) return 1.f;
+  const float u = pg_uniform(seed ^ (ctr * 0x9E3779B97F4A7C15ull), (unsigned long long)i);
+  return u >= drop_p ? 1.f / (1.f - drop_p) : 0.f;
+}
+}  // namespace
+
+// The head runs as three launches so the 16 MB feature map is streamed by B x C/256
+// workgroups (640 at B=128) instead of one workgroup per image (128 workgroups, half the
+// CUs idle, a 49-deep per-thread load chain):
+//   pool:  z = relu6(BN(y)) averaged over HW, dropout -> pd[B][C]      grid (B, C/256)
+//   ce:    logits = pd W^T + b, softmax-CE, argmax, dlogits            grid B
+//   bwd:   g = (dlogits W) * keep / HW * relu6'(BN(y)), BN partials    grid (B, C/256)
+// Within a workgroup lane l owns channels [8l, 8l+8) of the chunk and slot k the pixels
+// k, k+8, ...; the slot sums are combined in LDS in a fixed order (deterministic).
+__global__ __launch_bounds__(256) void head_pool_kernel(
+    const bf16_t *__restrict__ y, const float *__restrict__ s, const float *__restrict__ t, int HW, int C,
+    float drop_p, unsigned long long seed, const float *__restrict__ hyper, int train, float *__restrict__ pd_out) {
+  __shared__ float red[kSlots][kChunk + 4];
+  const int b = blockIdx.x, tid = threadIdx.x, cl = tid & 31, slot = tid >> 5;
+  const int cbase = blockIdx.y * kChunk;
+  const int c0 = cbase + cl * 8;
+  const bool active = c0 < C;
+  float pd[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) pd[k] = 0.f;
   if (active) {
+    float sc[8], sh[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       sc[k] = s[c0 + k];
       sh[k] = t[c0 + k];
-      pd[k] = 0.f;
     }
     const bf16_t *yb = y + (size_t)b * HW * C + c0;
-    for (int h0 = 0; h0 < HW; h0 += kPix) {   // kPix pixel loads in flight (a serial load chain before)
-     uint4 raw[kPix];
+    for (int h0 = slot; h0 < HW; h0 += 4 * kSlots) {   // 4 independent 16-B loads in flight
+      uint4 raw[4];
 #pragma unroll
-     for (int u = 0; u < kPix; ++u) raw[u] = ldg16(yb + (size_t)min(h0 + u, HW - 1) * C);   // clamped, unconditional
+      for (int u = 0; u < 4; ++u) raw[u] = ldg16(yb + (size_t)min(h0 + u * kSlots, HW - 1) * C);
 #pragma unroll
-     for (int u = 0; u < kPix; ++u) {
-      if (h0 + u >= HW) break;
-      float v[8];
-      unpack8(raw[u], v);
+      for (int u = 0; u < 4; ++u) {
+        if (h0 + u * kSlots < HW) {
+          float v[8];
+          unpack8(raw[u], v);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) pd[k] += relu6f(fmaf(v[k], sc[k], sh[k]));
-     }
-    }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      pd[k] *= inv_hw;
-      keep[k] = 1.f;
-      if (train && drop_p > 0.f) {
-        const float u = pg_uniform(seed ^ (ctr * 0x9E3779B97F4A7C15ull), (unsigned long long)b * C + c0 + k);
-        keep[k] = u >= drop_p ? 1.f / (1.f - drop_p) : 0.f;
+          for (int k = 0; k < 8; ++k) pd[k] += relu6f(fmaf(v[k], sc[k], sh[k]));
+        }
       }
-      pd[k] *= keep[k];
-      if (pd_out) pd_out[(size_t)b * C + c0 + k] = pd[k];
     }
   }
-  // logits
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[slot][cl * 8 + k] = pd[k];
+  __syncthreads();
+  const int c = cbase + tid;   // one channel per thread for the slot combine
+  if (c < C) {
+    float a = 0.f;
+#pragma unroll
+    for (int k = 0; k < kSlots; ++k) a += red[k][tid];
+    const unsigned long long ctr = hyper ? (unsigned long long)hyper[1] : 0ull;
+    pd_out[(size_t)b * C + c] = a * (1.f / (float)HW) * drop_keep(train, drop_p, seed, ctr, (size_t)b * C + c);
+  }
+}
+
+__global__ __launch_bounds__(256) void head_ce_kernel(
+    const float *__restrict__ pd, const float *__restrict__ Wl, const float *__restrict__ bl,
+    const long long *__restrict__ labels, int C, int NC, float loss_scale, float *__restrict__ logits_out,
+    float *__restrict__ loss_out, float *__restrict__ correct_out, float *__restrict__ dlogits) {
+  __shared__ float red[4][kMaxNC];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c0 = tid * 8;
+  const bool active = c0 < C;
+  float p[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) p[k] = active ? pd[(size_t)b * C + c0 + k] : 0.f;
   for (int j = 0; j < NC; ++j) {
     float a = 0.f;
     if (active) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) a = fmaf(Wl[(size_t)j * C + c0 + k], pd[k], a);
+      for (int k = 0; k < 8; ++k) a = fmaf(Wl[(size_t)j * C + c0 + k], p[k], a);
     }
     a = wave_sum(a);
     if (lane == 0) red[wave][j] = a;
   }
   __syncthreads();
-  if (tid == 0) {
-    float lg[kMaxNC];
-    float mx = -INFINITY;
-    int arg = 0;
-    for (int j = 0; j < NC; ++j) {
-      lg[j] = red[0][j] + red[1][j] + red[2][j] + red[3][j] + bl[j];
-      if (lg[j] > mx) { mx = lg[j]; arg = j; }
-      if (logits_out) logits_out[(size_t)b * NC + j] = lg[j];
-    }
-    float se = 0.f;
-    for (int j = 0; j < NC; ++j) se += __expf(lg[j] - mx);
-    const float lse = mx + __logf(se);
-    const int lab = labels ? (int)labels[b] : 0;
-    if (loss_out) loss_out[b] = lse - lg[lab];
-    if (correct_out) correct_out[b] = (arg == lab) ? 1.f : 0.f;
-    for (int j = 0; j < NC; ++j) {
-      const float pj = __expf(lg[j] - lse);
-      const float d = (pj - (j == lab ? 1.f : 0.f)) * loss_scale;
-      dl[j] = d;
-      if (dlogits) dlogits[(size_t)b * NC + j] = d;
-    }
+  if (tid != 0) return;
+  float lg[kMaxNC];
+  float mx = -INFINITY;
+  int arg = 0;
+  for (int j = 0; j < NC; ++j) {
+    lg[j] = red[0][j] + red[1][j] + red[2][j] + red[3][j] + bl[j];
+    if (lg[j] > mx) { mx = lg[j]; arg = j; }
+    if (logits_out) logits_out[(size_t)b * NC + j] = lg[j];
   }
-  if (!train) return;
-  __syncthreads();
-  if (!active) return;
-  float dz[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    float a = 0.f;
-    for (int j = 0; j < NC; ++j) a = fmaf(dl[j], Wl[(size_t)j * C + c0 + k], a);
-    dz[k] = a * keep[k] * inv_hw;
+  float se = 0.f;
+  for (int j = 0; j < NC; ++j) se += __expf(lg[j] - mx);
+  const float lse = mx + __logf(se);
+  const int lab = labels ? (int)labels[b] : 0;
+  if (loss_out) loss_out[b] = lse - lg[lab];
+  if (correct_out) correct_out[b] = (arg == lab) ? 1.f : 0.f;
+  if (dlogits) {
+    for (int j = 0; j < NC; ++j)
+      dlogits[(size_t)b * NC + j] = (__expf(lg[j] - lse) - (j == lab ? 1.f : 0.f)) * loss_scale;
   }
+}
+
+__global__ __launch_bounds__(256) void head_bwd_kernel(
+    const bf16_t *__restrict__ y, const float *__restrict__ s, const float *__restrict__ t,
+    const float *__restrict__ Wl, const float *__restrict__ dlogits, int HW, int C, int NC, float drop_p,
+    unsigned long long seed, const float *__restrict__ hyper, bf16_t *__restrict__ g_out,
+    float *__restrict__ part) {
+  __shared__ float r0[kSlots][kChunk + 4];
+  __shared__ float r1[kSlots][kChunk + 4];
+  const int b = blockIdx.x, tid = threadIdx.x, cl = tid & 31, slot = tid >> 5;
+  const int cbase = blockIdx.y * kChunk;
+  const int c0 = cbase + cl * 8;
+  const bool active = c0 < C;
   float st0[8], st1[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) st0[k] = st1[k] = 0.f;
-  for (int h0 = 0; h0 < HW; h0 += kPix) {
-   uint4 raw[kPix];
-#pragma unroll
-   for (int u = 0; u < kPix; ++u) raw[u] = ldg16(y + ((size_t)b * HW + min(h0 + u, HW - 1)) * C + c0);
-#pragma unroll
-   for (int u = 0; u < kPix; ++u) {
-    if (h0 + u >= HW) break;
-    const size_t off = ((size_t)b * HW + h0 + u) * C + c0;
-    float v[8], g[8];
-    unpack8(raw[u], v);
+  if (active) {
+    const unsigned long long ctr = hyper ? (unsigned long long)hyper[1] : 0ull;
+    const float inv_hw = 1.f / (float)HW;
+    float sc[8], sh[8], dz[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      g[k] = dz[k] * relu6_mask(v[k], sc[k], sh[k]);
+      sc[k] = s[c0 + k];
+      sh[k] = t[c0 + k];
+      dz[k] = 0.f;
     }
-    // statistics over the bf16 value actually stored
-    const uint4 gp = pack8(g);
-    float gr[8];
-    unpack8(gp, gr);
+    for (int j = 0; j < NC; ++j) {
+      const float d = dlogits[(size_t)b * NC + j];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      st0[k] += gr[k];
-      st1[k] = fmaf(gr[k], v[k], st1[k]);
+      for (int k = 0; k < 8; ++k) dz[k] = fmaf(d, Wl[(size_t)j * C + c0 + k], dz[k]);
     }
-    stg16(g_out + off, gp);
-   }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dz[k] *= drop_keep(1, drop_p, seed, ctr, (size_t)b * C + c0 + k) * inv_hw;
+    const size_t base = (size_t)b * HW * C + c0;
+    for (int h0 = slot; h0 < HW; h0 += 4 * kSlots) {
+      uint4 raw[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) raw[u] = ldg16(y + base + (size_t)min(h0 + u * kSlots, HW - 1) * C);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (h0 + u * kSlots < HW) {
+          float v[8], g[8], gr[8];
+          unpack8(raw[u], v);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) g[k] = dz[k] * relu6_mask(v[k], sc[k], sh[k]);
+          const uint4 gp = pack8(g);   // statistics over the bf16 value actually stored
+          unpack8(gp, gr);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            st0[k] += gr[k];
+            st1[k] = fmaf(gr[k], v[k], st1[k]);
+          }
+          stg16(g_out + base + (size_t)(h0 + u * kSlots) * C, gp);
+        }
+      }
+    }
   }
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    part[((size_t)b * 2 + 0) * C + c0 + k] = st0[k];
-    part[((size_t)b * 2 + 1) * C + c0 + k] = st1[k];
+    r0[slot][cl * 8 + k] = st0[k];
+    r1[slot][cl * 8 + k] = st1[k];
+  }
+  __syncthreads();
+  const int c = cbase + tid;
+  if (c < C) {
+    float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+    for (int k = 0; k < kSlots; ++k) {
+      a0 += r0[k][tid];
+      a1 += r1[k][tid];
+    }
+    part[((size_t)b * 2 + 0) * C + c] = a0;
+    part[((size_t)b * 2 + 1) * C + c] = a1;
   }
 }
 
@@ -171,10 +221,13 @@ void launch_head(const bf16_t *y, const float *s, const float *t, const float *W
                  unsigned long long seed, const float *hyper, int train, float loss_scale,
                  float *logits, float *loss, float *correct, float *dlogits, float *pd,
                  bf16_t *g_out, float *part, float *dW, float *db, hipStream_t st) {
-  hipLaunchKernelGGL(head_kernel, dim3(B), dim3(256), 0, st, y, s, t, Wl, bl, labels, HW, C, NC,
-                     drop_p, seed, hyper, train, loss_scale, logits, loss, correct, dlogits, pd,
-                     g_out, part);
-  if (train)
-    hipLaunchKernelGGL(head_wgrad_kernel, dim3((NC * C + NC + 255) / 256), dim3(256), 0, st, dlogits,
-                       pd, B, C, NC, dW, db);
+  const dim3 grid2(B, (C + kChunk - 1) / kChunk);
+  hipLaunchKernelGGL(head_pool_kernel, grid2, dim3(256), 0, st, y, s, t, HW, C, drop_p, seed, hyper, train, pd);
+  hipLaunchKernelGGL(head_ce_kernel, dim3(B), dim3(256), 0, st, pd, Wl, bl, labels, C, NC, loss_scale, logits,
+                     loss, correct, train ? dlogits : nullptr);
+  if (!train) return;
+  hipLaunchKernelGGL(head_bwd_kernel, grid2, dim3(256), 0, st, y, s, t, Wl, dlogits, HW, C, NC, drop_p, seed,
+                     hyper, g_out, part);
+  hipLaunchKernelGGL(head_wgrad_kernel, dim3((NC * C + NC + 255) / 256), dim3(256), 0, st, dlogits, pd, B, C,
+                     NC, dW, db);
 }

@@ -25,10 +25,12 @@ def build_bench_step(model_name: str, batch_size: int, device: torch.device, bac
     backend = _resolve_backend(backend, device)
     if backend == "hip":
         from .native_step import NativeTrainStep
+        # use_graph: 0 eager, 1 whole step in one hipGraph, 2 forward in a hipGraph + eager backward
         step = NativeTrainStep.for_benchmark(model_name, batch_size, device, img_size=img_size,
-                                             use_graph=use_graph, world_size=world_size, rank=rank,
-                                             side_stream=side_stream, fp8=fp8)
-        return step.bench_step, {"backend": "hip", "graph": step.graph_enabled, "side_stream": side_stream,
+                                             use_graph=int(use_graph) == 1, world_size=world_size, rank=rank,
+                                             side_stream=side_stream, fp8=fp8, graph_forward=int(use_graph) == 2)
+        graph = "forward" if step.graph_forward else step.graph_enabled
+        return step.bench_step, {"backend": "hip", "graph": graph, "side_stream": side_stream,
                                  "fp8": fp8}
     if fp8:
         raise NotImplementedError("fp8 runs on the native (hip) backend")

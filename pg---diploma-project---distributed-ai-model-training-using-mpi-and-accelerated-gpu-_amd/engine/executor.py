@@ -345,7 +345,7 @@ class MobileNetV2Executor:
         K.head(self.bn_last.y, self.bn_last.scale, self.bn_last.shift, f.w(self.w_lin), f.w(self.b_lin),
                self.labels, B, self.Hf * self.Hf, self.C_last, self.NC, self.drop_p, self.dropout_seed,
                self.hyper, train, 1.0 / B, logits=self.logits, loss=self.loss, correct=self.correct,
-               dlogits=self.dlogits if train else None, pd=self.pd if train else None,
+               dlogits=self.dlogits if train else None, pd=self.pd,
                g_out=self.bn_last.g if train else None, part=ws if train else None,
                dW=f.g(self.w_lin) if train else None, db=f.g(self.b_lin) if train else None)
 

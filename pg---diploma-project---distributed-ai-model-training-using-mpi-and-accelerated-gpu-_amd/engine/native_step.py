@@ -56,7 +56,8 @@ class NativeTrainStep:
                  rank: int = 0, use_graph: bool = True, seed: int = 0, bucket_mb: Optional[float] = None,
                  first_bucket_mb: float = 1.0, reduce_dtype: torch.dtype = torch.float32,
                  double_resize: bool = True, augment: bool = True, train_augment: bool = True,
-                 side_stream: bool = True, bn_broadcast: bool = False, fp8: bool = False):
+                 side_stream: bool = True, bn_broadcast: bool = False, fp8: bool = False,
+                 graph_forward: bool = False):
         self.device, self.B, self.S = device, batch, img_size
         self.world, self.rank = world_size, rank
         self.exe = executor_class(model)(model, batch, img_size, device, dropout_seed=(seed * 7919) ^ rank,
@@ -93,11 +94,18 @@ class NativeTrainStep:
         self.use_graph = use_graph and world_size == 1
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self._eager_runs = 0
+        # forward-only graph: augment + forward (+ fused head backward) are one main-stream
+        # chain of ~170 short kernels whose eager launch is host-bound on the small late layers;
+        # replaying them as one graph lets the host run ahead and queue the (eager, two-stream)
+        # backward while the GPU is still in the forward.  No collective is captured, so it
+        # applies to data-parallel runs too (not with the per-step BN buffer broadcast).
+        self.graph_forward = graph_forward and not self.use_graph and not self.bn_broadcast
+        self.fwd_graph: Optional[torch.cuda.CUDAGraph] = None
 
     # ------------------------------------------------------------------ setup
     @classmethod
     def for_benchmark(cls, model_name: str, batch: int, device, img_size=224, use_graph=True,
-                      world_size=1, rank=0, n_data=50000, side_stream=True, fp8=False):
+                      world_size=1, rank=0, n_data=50000, side_stream=True, fp8=False, graph_forward=False):
         if model_name not in ("mobilenet_v2", "resnet50"):
             raise NotImplementedError(f"native executors: mobilenet_v2, resnet50 (not {model_name}); "
                                       "use --backend torch")
@@ -115,7 +123,7 @@ class NativeTrainStep:
             src = torch.randint(0, 256, (n_data, 32, 32, 3), dtype=torch.uint8, device=device, generator=g)
             labels = torch.randint(0, 10, (n_data,), dtype=torch.int64, device=device, generator=g)
         st = cls(model, batch, device, img_size=img_size, world_size=world_size, rank=rank,
-                 use_graph=use_graph, seed=42, side_stream=side_stream, fp8=fp8)
+                 use_graph=use_graph, seed=42, side_stream=side_stream, fp8=fp8, graph_forward=graph_forward)
         st.set_data(src, labels)
         st._perm = torch.randperm(n_data, device=device, generator=g)
         st._pos = 0
@@ -134,6 +142,7 @@ class NativeTrainStep:
         st.idx = torch.zeros(batch, dtype=torch.int64, device=self.device)
         st.aug_params = torch.zeros(batch, K.AUG_NPARAMS, dtype=torch.float32, device=self.device)
         st.use_graph, st.graph, st._eager_runs = False, None, 0
+        st.graph_forward, st.fwd_graph = False, None
         return st
 
     def set_data(self, src_u8: torch.Tensor, labels: torch.Tensor):
@@ -155,6 +164,11 @@ class NativeTrainStep:
 
     # ------------------------------------------------------------------ step
     def _body(self):
+        self._front()
+        self._back()
+
+    def _front(self):
+        """Step counter, augmentation and the training forward (main stream only)."""
         exe = self.exe
         K.step_begin(self.hyper)
         if self.augment_enabled and self.src.shape[1] != 32:
@@ -166,11 +180,15 @@ class NativeTrainStep:
                       train=self.train_augment,
                       double_resize=self.double_resize, seed=self.seed + 17 * self.rank, hyper=self.hyper,
                       epoch_ctr=0, out_hw=self.S)
-        if self.reducer is not None:
-            self.reducer.begin()
         if self.bn_broadcast:
             broadcast_parameters([self.bn_flat, self.bn_nbt])
         exe.forward(train=True)
+
+    def _back(self):
+        """Backward (+ bucketed all-reduce), Adam and metrics."""
+        exe = self.exe
+        if self.reducer is not None:
+            self.reducer.begin()
         exe.backward()
         if self.reducer is not None:
             self.reducer.finish()
@@ -182,6 +200,19 @@ class NativeTrainStep:
     def run(self, idx: torch.Tensor):
         """One training step on the batch ``src[idx]`` (idx: int64 [B] on device)."""
         self.idx.copy_(idx, non_blocking=True)
+        if self.graph_forward:
+            if self.fwd_graph is None:
+                if self._eager_runs < 2:
+                    self._eager_runs += 1
+                    self._body()
+                    return
+                torch.cuda.synchronize(self.device)
+                self.fwd_graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.fwd_graph):
+                    self._front()
+            self.fwd_graph.replay()
+            self._back()
+            return
         if not self.use_graph:
             self._body()
             return

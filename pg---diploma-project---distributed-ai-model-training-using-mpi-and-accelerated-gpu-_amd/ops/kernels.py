@@ -370,6 +370,9 @@ def head(y, s, t, Wl, bl, labels, B, HW, C, NC, drop_p, seed, hyper, train, loss
         raise ValueError("head kernel supports NC <= 16 and C <= 2048 (C % 8 == 0)")
     _chk(y, BF16, B * HW * C, "y")
     _chk(Wl, F32, NC * C, "Wl")
+    if pd is None:
+        raise ValueError("head needs pd [B, C] (pooled features; the CE launch reads them)")
+    _chk(pd, F32, B * C, "pd")
     if train:
         for t_, n in ((dlogits, "dlogits"), (pd, "pd"), (g_out, "g_out"), (part, "part"), (dW, "dW"),
                       (db, "db")):

@@ -155,3 +155,28 @@ def test_native_train_step_fp8_loss_decreases(dev):
             l, c, n = st.read_metrics()
             losses.append(l / n)
     assert losses[-1] < losses[0] * 0.5, losses
+
+
+@pytest.mark.parametrize("mode", ["forward_graph", "full_graph"])
+def test_graph_modes_match_eager(dev, mode):
+    """The forward-only hipGraph (replayed forward + eager two-stream backward) and the
+    whole-step graph give the same weights as eager launching after several steps."""
+    from pgdist.engine.native_step import NativeTrainStep
+    src = torch.randint(0, 256, (16, 32, 32, 3), dtype=torch.uint8, device=dev,
+                        generator=torch.Generator(device=dev).manual_seed(3))
+    labels = torch.arange(16, device=dev) % 10
+    out = {}
+    for m in ("eager", mode):
+        torch.manual_seed(0)
+        model = mobilenet_v2(10)
+        st = NativeTrainStep(model, 8, dev, img_size=64, lr=1e-3, train_augment=False,
+                             use_graph=(m == "full_graph"), graph_forward=(m == "forward_graph"))
+        st.set_data(src, labels)
+        for i in range(5):
+            st.run((torch.arange(8, device=dev) + 3 * i) % 16)
+        torch.cuda.synchronize()
+        out[m] = (st.flat.master.clone(), st.read_metrics())
+        if m == "forward_graph":
+            assert st.fwd_graph is not None
+    assert torch.allclose(out["eager"][0], out[mode][0], rtol=0, atol=1e-6)
+    assert abs(out["eager"][1][0] - out[mode][1][0]) < 1e-4 * max(1.0, abs(out["eager"][1][0]))

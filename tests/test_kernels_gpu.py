@@ -559,3 +559,39 @@ def test_augment_flip_identity(dev):
     given[:, 9] = 0 | (1 << 2) | (2 << 4) | (3 << 6)
     K.augment(src, idx, labels, tr, lab, prm, train=True, given_params=given, out_hw=S)
     assert rel(tr, ev.flip(2)) < 1e-3
+
+
+def test_head_dropout_consistent(dev):
+    """Dropout in the split head: the pool launch draws the mask, the backward launch redraws
+    the same one (same seed / step counter), so g is zero exactly on dropped channels and
+    scaled by 1/(1-p) elsewhere."""
+    B, HW, C, NC, p = 4, 49, 1280, 10, 0.2
+    y = bf(rnd(B, HW, C, dev=dev, seed=11) * 3)
+    s, t = bn_params(C, dev, 12)
+    Wl = (rnd(NC, C, dev=dev, seed=13) * 0.05).contiguous()
+    bl = torch.zeros(NC, device=dev)
+    labels = torch.randint(0, NC, (B,), device=dev)
+    f32 = dict(device=dev, dtype=torch.float32)
+    hyper = torch.tensor([1e-3, 7.0], **f32)
+    logits, loss, correct = torch.zeros(B, NC, **f32), torch.zeros(B, **f32), torch.zeros(B, **f32)
+    dlog, pd = torch.zeros(B, NC, **f32), torch.zeros(B, C, **f32)
+    g = torch.empty(B, HW, C, dtype=torch.bfloat16, device=dev)
+    part = torch.zeros(B * 2 * C, **f32)
+    dW, db = torch.zeros(NC * C, **f32), torch.zeros(NC, **f32)
+    K.head(y, s, t, Wl, bl, labels, B, HW, C, NC, p, 1234, hyper, True, 1.0 / B, logits=logits, loss=loss,
+           correct=correct, dlogits=dlog, pd=pd, g_out=g, part=part, dW=dW, db=db)
+    a = y.float() * s + t
+    pooled = relu6(a).mean(1)
+    keep = torch.where(pooled.abs() > 1e-6, pd / pooled, torch.ones_like(pd))
+    dropped = (pd == 0) & (pooled.abs() > 1e-6)
+    frac = dropped.float().mean().item()
+    assert 0.1 < frac < 0.3, frac
+    kept = ~dropped & (pooled.abs() > 1e-6)
+    assert torch.allclose(keep[kept], torch.full_like(keep[kept], 1 / (1 - p)), rtol=1e-4)
+    lg = pd @ Wl.t() + bl
+    assert rel(logits, lg) < 1e-4
+    mask = ((a > 0) & (a < 6)).float()
+    keepm = torch.where(dropped, torch.zeros_like(pd), torch.full_like(pd, 1 / (1 - p)))
+    dpool = ((torch.softmax(lg, 1) - F.one_hot(labels, NC)) / B) @ Wl * keepm
+    gref = dpool[:, None, :] / HW * mask
+    assert rel(g, gref) < 8e-3
