@@ -219,6 +219,9 @@ class MobileNetV2Executor:
         self.labels = torch.zeros(B, dtype=torch.int64, device=device)
         self.hyper = hyper if hyper is not None else torch.zeros(2, **f32)   # [lr, step] (device)
         self.on_params_ready: Optional[Callable[[List[str]], None]] = None
+        # ready_probe(names) -> True when marking ``names`` launches a gradient bucket; other
+        # calls only do host bookkeeping (no side-stream event record / wait per layer)
+        self.ready_probe: Optional[Callable[[List[str]], bool]] = None
         # 1x1 weights transposed for dgrad: table rows (offset, Cout, Cin)
         tab = []
         for bp in self.blocks:
@@ -252,7 +255,7 @@ class MobileNetV2Executor:
         stream, so the collective is ordered after both streams' producers."""
         if self.on_params_ready is None:
             return
-        if self.side is None:
+        if self.side is None or (self.ready_probe is not None and not self.ready_probe(names)):
             self.on_params_ready(names)
             return
         self.side.wait_stream(torch.cuda.current_stream(self.device))

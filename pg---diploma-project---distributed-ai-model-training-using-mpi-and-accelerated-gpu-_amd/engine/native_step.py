@@ -82,6 +82,7 @@ class NativeTrainStep:
             ranges = [(n,) + self.flat.range_of(n) for n in self.flat.order]
             self.reducer = BucketedGradReducer(self.flat.grad, ranges, bucket_mb, first_bucket_mb, reduce_dtype)
             self.exe.on_params_ready = self.reducer.mark_ready
+            self.exe.ready_probe = self.reducer.would_launch
             self.sync_from_rank0()
         # reference DDP default (broadcast_buffers=True): rank 0's BN running statistics are
         # broadcast before every training forward; the buffers are coalesced into one flat
@@ -139,6 +140,7 @@ class NativeTrainStep:
         st.exe = type(self.exe)(self.exe.model, batch, self.S, self.device, flat=self.flat,
                                 dropout_seed=self.exe.dropout_seed, hyper=self.hyper)
         st.exe.on_params_ready = self.exe.on_params_ready
+        st.exe.ready_probe = self.exe.ready_probe
         st.idx = torch.zeros(batch, dtype=torch.int64, device=self.device)
         st.aug_params = torch.zeros(batch, K.AUG_NPARAMS, dtype=torch.float32, device=self.device)
         st.use_graph, st.graph, st._eager_runs = False, None, 0

@@ -166,6 +166,9 @@ class ResNet50Executor:
         self.labels = torch.zeros(B, dtype=torch.int64, device=device)
         self.hyper = hyper if hyper is not None else torch.zeros(2, **f32)
         self.on_params_ready: Optional[Callable[[List[str]], None]] = None
+        # ready_probe(names) -> True when marking ``names`` launches a gradient bucket; other
+        # calls only do host bookkeeping (no side-stream event record / wait per layer)
+        self.ready_probe: Optional[Callable[[List[str]], bool]] = None
         # dgrad weights: every conv but the stem transposed to [Cin][R][S][Cout] (one launch)
         tab = []
         for bp in self.blocks:
@@ -178,7 +181,7 @@ class ResNet50Executor:
     def _ready(self, names):
         if self.on_params_ready is None:
             return
-        if self.side is None:
+        if self.side is None or (self.ready_probe is not None and not self.ready_probe(names)):
             self.on_params_ready(names)
             return
         self.side.wait_stream(torch.cuda.current_stream(self.device))

@@ -95,6 +95,17 @@ class BucketedGradReducer:
         self._next = 0
         self._works = []
 
+    def would_launch(self, names: Sequence[str]) -> bool:
+        """True if ``mark_ready(names)`` would launch at least one bucket (buckets launch in
+        order, so exactly when the next unlaunched bucket becomes complete).  Lets the executor
+        skip the side-stream join for the ~100 per-layer calls that launch nothing."""
+        if not self.enabled or self._next >= len(self.buckets):
+            return False
+        if self._ready[self._next]:
+            return True
+        hit = sum(1 for n in names if self.owner.get(n) == self._next)
+        return self._pending[self._next] - hit == 0
+
     def mark_ready(self, names: Sequence[str]):
         if not self.enabled:
             return

@@ -132,3 +132,36 @@ def test_trainer_two_ranks_keeps_replicas_in_sync(tmp_path, bn_sync):
     assert (tmp_path / "best_mpi.pth").exists()
     sd = torch.load(tmp_path / "best_mpi.pth", weights_only=True)
     assert not any(k.startswith("module.") for k in sd) and len(sd) == 314
+
+
+def test_would_launch_predicts_bucket_launches():
+    """The executor skips the side-stream join for per-layer ready calls that launch no
+    bucket; ``would_launch`` must predict exactly the calls after which ``mark_ready`` launches."""
+    import random
+    from pgdist.parallel.ddp import BucketedGradReducer
+    ranges, o = [], 0
+    for i in range(40):
+        n = 1000 * (1 + i % 7)
+        ranges.append((f"p{i}", o, o + n))
+        o += n
+    red = BucketedGradReducer(torch.zeros(o), ranges, bucket_cap_mb=0.05, first_bucket_mb=0.01)
+    red.world = 2   # pretend data parallel; collectives are recorded instead of issued
+    launched = []
+    red._launch = lambda bi: launched.append(bi)
+    assert len(red.buckets) > 3
+    rng = random.Random(0)
+    for trial in range(5):
+        red.begin()
+        launched.clear()
+        names = [r[0] for r in ranges][::-1]
+        groups = []
+        while names:
+            k = rng.randint(1, 4)
+            groups.append(names[:k])
+            names = names[k:]
+        for g in groups:
+            pred = red.would_launch(g)
+            before = len(launched)
+            red.mark_ready(g)
+            assert pred == (len(launched) > before), (trial, g)
+        assert launched == list(range(len(red.buckets)))
