@@ -56,7 +56,9 @@ def main():
                     help="BASELINE config 5: forward 1x1 convs on e4m3 MFMA (use with --batch-size 512)")
     args = ap.parse_args()
 
-    info, device, backend = init_distributed()
+    # PGDIST_DIST_BACKEND=gloo: rehearse the multi-rank bench with several ranks on one GPU
+    # (RCCL needs one GPU per rank); the default picks RCCL ("nccl") on GPUs
+    info, device, backend = init_distributed(backend=os.environ.get("PGDIST_DIST_BACKEND", "auto"))
     world = info.world_size
     if world != args.gpus and info.rank == 0:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)

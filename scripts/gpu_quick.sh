@@ -1,2 +1,3 @@
 cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out && export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_ddp_gpu.py -m gpu -x -v --timeout 500 --timeout-method thread > gpurun_out/t_q.log 2>&1; rc=$?; tail -5 gpurun_out/t_q.log; [ $rc -eq 0 ] || { grep -B5 -A25 "Error\|assert" gpurun_out/t_q.log | head -60; exit $rc; }
+PGDIST_DIST_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --steps 10 --warmup 3 > gpurun_out/b2.json 2> gpurun_out/b2.err || { tail -30 gpurun_out/b2.err; exit 3; }
+cat gpurun_out/b2.json
