@@ -1,3 +1,10 @@
 cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out && export TMPDIR=/tmp
-PGDIST_DIST_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --steps 10 --warmup 3 > gpurun_out/b2.json 2> gpurun_out/b2.err || { tail -30 gpurun_out/b2.err; exit 3; }
-cat gpurun_out/b2.json
+timeout -k 10 60 python -c "import torch; print('prio range', torch.cuda.Stream.priority_range())"
+for e in PGDIST_NOOP=1 PGDIST_SIDE_PRIO=-1 PGDIST_NOOP=1 PGDIST_SIDE_PRIO=-1; do
+  env $e timeout -k 10 120 python bench.py --steps 30 --warmup 10 > gpurun_out/sw.json 2> gpurun_out/sw.err || { tail gpurun_out/sw.err; exit 5; }
+  echo "$e $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/sw.json)"
+done
+for e in PGDIST_NOOP=1 PGDIST_SIDE_PRIO=-1; do
+  env $e timeout -k 10 120 python bench.py --model resnet50 --steps 20 --warmup 5 > gpurun_out/sw.json 2> gpurun_out/sw.err || { tail gpurun_out/sw.err; exit 5; }
+  echo "resnet $e $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/sw.json)"
+done
