@@ -1,4 +1,2 @@
 cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out && export TMPDIR=/tmp
-(cd /tmp && timeout -k 10 60 rocprofv3 --list-avail > "$GRAFT_REPO_ROOT/gpurun_out/avail.txt" 2>&1); echo "list rc=$?"
-grep -i -o "SQ_[A-Z_]*MFMA[A-Z0-9_]*\|GRBM_GUI_ACTIVE" gpurun_out/avail.txt | sort -u | head -30
-bash scripts/gpu_pmc.sh
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -k "head" > gpurun_out/t_q.log 2>&1; rc=$?; tail -3 gpurun_out/t_q.log; [ $rc -eq 0 ] || { grep -B5 -A25 "Error\|assert" gpurun_out/t_q.log | head -60; exit $rc; }

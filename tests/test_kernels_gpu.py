@@ -432,8 +432,9 @@ def test_stem(dev, B, S):
 
 # ----------------------------------------------------------------------------- head
 @pytest.mark.parametrize("train", [True, False])
-def test_head(dev, train):
-    B, HW, C, NC = 6, 49, 1280, 10
+@pytest.mark.parametrize("HW,C", [(49, 1280), (9, 1000)])
+def test_head(dev, train, HW, C):
+    B, NC = 6, 10
     y = bf(rnd(B, HW, C, dev=dev, seed=1) * 3)
     s, t = bn_params(C, dev, 2)
     Wl = (rnd(NC, C, dev=dev, seed=3) * 0.05).contiguous()
