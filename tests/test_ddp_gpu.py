@@ -69,3 +69,59 @@ def test_native_ddp_two_ranks_one_gpu(model_name):
         assert diff == 0.0, f"replicas diverged on rank {rank}: {diff}"
         assert n == 32
         assert nb >= 3
+
+
+def _grad_worker(rank, world, port, q):
+    import pgdist  # noqa: F401
+    from pgdist.models import build_model
+    from pgdist.engine.native_step import NativeTrainStep
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(7)
+    src = torch.randint(0, 256, (32, 32, 32, 3), dtype=torch.uint8, device=dev, generator=g)
+    labels = torch.randint(0, 10, (32,), device=dev, generator=g)
+
+    def make(world_size, r):
+        torch.manual_seed(100)
+        st = NativeTrainStep(build_model("mobilenet_v2", num_classes=10), 8, dev, img_size=64, lr=1e-3,
+                             world_size=world_size, rank=r, bucket_mb=0.5, first_bucket_mb=0.1)
+        st.set_data(src, labels)
+        return st
+
+    shard = lambda r: torch.arange(8, device=dev) + 8 * r   # noqa: E731
+    st = make(world, rank)
+    st.run(shard(rank))
+    torch.cuda.synchronize()
+    reduced = st.flat.grad.clone()
+    if rank == 0:
+        # the same first step on each shard alone (same weights, dropout / augmentation seeds)
+        singles = []
+        for r in range(world):
+            s1 = make(1, r)
+            s1.run(shard(r))
+            torch.cuda.synchronize()
+            singles.append(s1.flat.grad.clone())
+        expect = singles[0] + singles[1]
+        err = ((reduced - expect).abs().max() / (expect.abs().max() + 1e-12)).item()
+        q.put(("err", err, len(st.reducer.buckets)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_native_ddp_reduced_gradient_equals_sum_of_shards():
+    """After one data-parallel step the flat gradient buffer holds the SUM of the per-shard
+    gradients (the 1/world is folded into Adam): checks the bucket launches are ordered after
+    every producer of their gradients (main-stream dgrad-side BN grads and side-stream wgrads)."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_grad_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    tag, err, nb = q.get(timeout=400)
+    for p in procs:
+        p.join(timeout=120)
+    assert nb >= 3
+    assert err < 1e-5, err
