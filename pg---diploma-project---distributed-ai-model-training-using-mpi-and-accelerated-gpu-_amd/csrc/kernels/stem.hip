@@ -11,16 +11,20 @@
 // (launch_stem_wgrad).  No input gradient is needed.
 #include "../common.h"
 
+#include <cstdlib>
+
 namespace {
 constexpr int kCo = 32;
 }
 
+template <int kPx>
 __global__ __launch_bounds__(256) void stem_fwd_kernel(const bf16_t *__restrict__ img,
                                                       const bf16_t *__restrict__ w,  // [32][3][3][3]
                                                       bf16_t *__restrict__ y, float *__restrict__ part,
                                                       int B, int H, int W, int Ho, int Wo) {
-  // thread = (output pixel, group of 8 output channels): 4 threads per pixel, so
-  // accumulators + BN partials stay in ~40 VGPRs and each thread stores one 16-B vector
+  // thread = (group of kPx output pixels, group of 8 output channels): 4 threads per pixel
+  // group; each pair of LDS weight reads (8 channels of one input channel x tap) feeds the
+  // kPx pixels; each thread stores one 16-B vector per pixel.
   __shared__ __attribute__((aligned(16))) float ws[27][kCo];  // [c*9+tap][o]
   __shared__ float red[64][kCo];
   const int tid = threadIdx.x;
@@ -34,42 +38,63 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(const bf16_t *__restrict_
 #pragma unroll
   for (int j = 0; j < 8; ++j) s0[j] = s1[j] = 0.f;
   const long long npix = (long long)B * Ho * Wo;
-  for (long long pix = blockIdx.x * 64ll + (tid >> 2); pix < npix; pix += (long long)gridDim.x * 64) {
-    const int b = (int)(pix / (Ho * Wo));
-    const int rem = (int)(pix % (Ho * Wo));
-    const int oh = rem / Wo, ow = rem % Wo;
-    float acc[8];
+  const long long step = (long long)gridDim.x * 64 * kPx;
+  for (long long pbase = (blockIdx.x * 64ll + (tid >> 2)) * kPx; pbase < npix; pbase += step) {
+    int ih0[kPx], iw0[kPx];
+    size_t ibase[kPx];
+    bool pok[kPx];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    for (int q = 0; q < kPx; ++q) {
+      const long long pix = pbase + q;
+      pok[q] = pix < npix;
+      const long long pp = pok[q] ? pix : npix - 1;
+      const int b = (int)(pp / (Ho * Wo));
+      const int rem = (int)(pp % (Ho * Wo));
+      ih0[q] = (rem / Wo) * 2 - 1;
+      iw0[q] = (rem % Wo) * 2 - 1;
+      ibase[q] = (size_t)b * H * W;
+    }
+    float acc[kPx][8];
 #pragma unroll
+    for (int q = 0; q < kPx; ++q)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[q][j] = 0.f;
+#pragma unroll 1   // (a 3- or 9-tap unrolled body keeps ~200 VGPRs live)
     for (int tap = 0; tap < 9; ++tap) {
-      const int ih = oh * 2 - 1 + tap / 3, iw = ow * 2 - 1 + tap % 3;
-      if (ih < 0 || ih >= H || iw < 0 || iw >= W) continue;
-      const uint2 u = *reinterpret_cast<const uint2 *>(img + (((size_t)b * H + ih) * W + iw) * 4);
-      const float x[3] = {__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
-                          __uint_as_float(u.y << 16)};
+      float x[kPx][3];
+#pragma unroll
+      for (int q = 0; q < kPx; ++q) {
+        const int ih = ih0[q] + tap / 3, iw = iw0[q] + tap % 3;
+        const bool in = ih >= 0 && ih < H && iw >= 0 && iw < W;
+        uint2 u = make_uint2(0u, 0u);
+        if (in) u = *reinterpret_cast<const uint2 *>(img + (ibase[q] + (size_t)ih * W + iw) * 4);
+        x[q][0] = __uint_as_float(u.x << 16);
+        x[q][1] = __uint_as_float(u.x & 0xffff0000u);
+        x[q][2] = __uint_as_float(u.y << 16);
+      }
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
         const float4 wa = *reinterpret_cast<const float4 *>(&ws[c * 9 + tap][o0]);
         const float4 wb = *reinterpret_cast<const float4 *>(&ws[c * 9 + tap][o0 + 4]);
-        acc[0] = fmaf(x[c], wa.x, acc[0]);
-        acc[1] = fmaf(x[c], wa.y, acc[1]);
-        acc[2] = fmaf(x[c], wa.z, acc[2]);
-        acc[3] = fmaf(x[c], wa.w, acc[3]);
-        acc[4] = fmaf(x[c], wb.x, acc[4]);
-        acc[5] = fmaf(x[c], wb.y, acc[5]);
-        acc[6] = fmaf(x[c], wb.z, acc[6]);
-        acc[7] = fmaf(x[c], wb.w, acc[7]);
+        const float wv[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
+#pragma unroll
+        for (int q = 0; q < kPx; ++q)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[q][j] = fmaf(x[q][c], wv[j], acc[q][j]);
       }
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      s0[j] += acc[j];
-      s1[j] = fmaf(acc[j], acc[j], s1[j]);
+    for (int q = 0; q < kPx; ++q) {
+      if (!pok[q]) continue;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s0[j] += acc[q][j];
+        s1[j] = fmaf(acc[q][j], acc[q][j], s1[j]);
+      }
+      stg16(y + (pbase + q) * kCo + o0, pack8(acc[q]));
     }
-    stg16(y + pix * kCo + o0, pack8(acc));
   }
-  // block reduction over the 64 pixel slots sharing a channel group
+  // block reduction over the 64 pixel-group slots sharing a channel group
   for (int s = 0; s < 2; ++s) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) red[tid >> 2][o0 + j] = s == 0 ? s0[j] : s1[j];
@@ -95,5 +120,10 @@ void launch_stem_fwd(const bf16_t *img, const bf16_t *w, bf16_t *y, float *part,
                      int W, hipStream_t st) {
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
   const int grid = stem_fwd_num_partials(B, H, W);
-  hipLaunchKernelGGL(stem_fwd_kernel, dim3(grid), dim3(256), 0, st, img, w, y, part, B, H, W, Ho, Wo);
+  // pixels per thread (PGDIST_STEM_PX): measured at bs128 224^2 on MI355X, rolled tap loop:
+  // 1 -> 83 us (32 VGPRs), 2 -> 92 us, 4 -> 89 us; the fully unrolled 1-pixel loop was 98 us
+  static const int px = [] { const char *e = getenv("PGDIST_STEM_PX"); return e ? atoi(e) : 1; }();
+  if (px == 1) hipLaunchKernelGGL(stem_fwd_kernel<1>, dim3(grid), dim3(256), 0, st, img, w, y, part, B, H, W, Ho, Wo);
+  else if (px == 2) hipLaunchKernelGGL(stem_fwd_kernel<2>, dim3(grid), dim3(256), 0, st, img, w, y, part, B, H, W, Ho, Wo);
+  else hipLaunchKernelGGL(stem_fwd_kernel<4>, dim3(grid), dim3(256), 0, st, img, w, y, part, B, H, W, Ho, Wo);
 }
