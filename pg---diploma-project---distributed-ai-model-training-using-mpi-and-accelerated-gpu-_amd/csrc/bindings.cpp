@@ -11,6 +11,7 @@
 #include <pybind11/numpy.h>
 
 #include <cstdint>
+#include <stdexcept>
 #include <string>
 
 #include "runtime/runtime.h"
@@ -63,7 +64,7 @@ long long stem_wgrad_workspace_floats(int, int);
 void launch_stem_wgrad(const bf16_t *, const bf16_t *, const float *, const float *, const float *,
                        const bf16_t *, float *, float *, int, int, int, int, hipStream_t);
 int stem_fwd_num_partials(int, int, int);
-void launch_stem_fwd(const bf16_t *, const bf16_t *, bf16_t *, float *, int, int, int, hipStream_t);
+bool launch_stem_fwd(const bf16_t *, const bf16_t *, bf16_t *, float *, int, int, int, int, hipStream_t);
 void launch_head(const bf16_t *, const float *, const float *, const float *, const float *,
                  const long long *, int, int, int, int, float, unsigned long long, const float *,
                  int, float, float *, float *, float *, float *, float *, bf16_t *, float *, float *,
@@ -215,8 +216,9 @@ PYBIND11_MODULE(_pgdist_C, m) {
   });
   // ---- stem ----
   m.def("stem_fwd_num_partials", &stem_fwd_num_partials);
-  m.def("stem_fwd", [](P img, P w, P y, P part, int B, int H, int W, P s) {
-    launch_stem_fwd(ptr<bf16_t>(img), ptr<bf16_t>(w), ptr<bf16_t>(y), ptr<float>(part), B, H, W, S(s));
+  m.def("stem_fwd", [](P img, P w, P y, P part, int B, int H, int W, int px, P s) {
+    if (!launch_stem_fwd(ptr<bf16_t>(img), ptr<bf16_t>(w), ptr<bf16_t>(y), ptr<float>(part), B, H, W, px, S(s)))
+      throw std::invalid_argument("stem_fwd: px must be 1, 2 or 4");
   });
   m.def("stem_wgrad_workspace_floats", &stem_wgrad_workspace_floats);
   m.def("stem_wgrad", [](P G, P Y, P ga, P gb, P gc, P img, P part, P grad, int B, int H, int W,

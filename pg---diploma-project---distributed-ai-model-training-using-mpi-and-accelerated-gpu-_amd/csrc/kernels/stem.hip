@@ -5,13 +5,15 @@
 // the output of the GPU augmentation kernel: NHWC with 4 channels (channel 3 is
 // an always-zero pad so each pixel is one aligned 8-byte load).
 //
-// Forward: four threads per output pixel, each computing 8 of the 32 channels
-// (27 taps x 8 FMAs, weights broadcast from LDS), storing one 16-B vector and
-// accumulating the BN0 partial sums.  The weight gradient is the im2col MFMA kernel in pwconv.hip
+// Forward: four threads per group of kPx output pixels, each computing 8 of the
+// 32 channels.  The 9 taps are a rolled loop (tap / 3, tap % 3 give the input
+// row / column; 32 VGPRs at kPx = 1); per tap the 3 input channels are one 8-B
+// load per pixel and each pair of LDS weight reads (8 channels, tap-major
+// layout ws[c*9+tap][o]) feeds the kPx pixels (register blocking; kPx = 1, 2 or
+// 4).  Each thread stores one 16-B vector per pixel and accumulates the BN0
+// partial sums.  The weight gradient is the im2col MFMA kernel in pwconv.hip
 // (launch_stem_wgrad).  No input gradient is needed.
 #include "../common.h"
-
-#include <cstdlib>
 
 namespace {
 constexpr int kCo = 32;
@@ -116,14 +118,16 @@ int stem_fwd_num_partials(int B, int H, int W) {
   return (int)g;
 }
 
-void launch_stem_fwd(const bf16_t *img, const bf16_t *w, bf16_t *y, float *part, int B, int H,
-                     int W, hipStream_t st) {
+// px = output pixels per thread (1, 2 or 4; anything else is rejected by the caller and here).
+// Measured at bs128 224^2 on MI355X, rolled tap loop: 1 -> 83 us (32 VGPRs), 2 -> 92 us,
+// 4 -> 89 us; the fully unrolled 1-pixel loop was 98 us.  The default (1) is chosen in ops.kernels.
+bool launch_stem_fwd(const bf16_t *img, const bf16_t *w, bf16_t *y, float *part, int B, int H,
+                     int W, int px, hipStream_t st) {
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
   const int grid = stem_fwd_num_partials(B, H, W);
-  // pixels per thread (PGDIST_STEM_PX): measured at bs128 224^2 on MI355X, rolled tap loop:
-  // 1 -> 83 us (32 VGPRs), 2 -> 92 us, 4 -> 89 us; the fully unrolled 1-pixel loop was 98 us
-  static const int px = [] { const char *e = getenv("PGDIST_STEM_PX"); return e ? atoi(e) : 1; }();
   if (px == 1) hipLaunchKernelGGL(stem_fwd_kernel<1>, dim3(grid), dim3(256), 0, st, img, w, y, part, B, H, W, Ho, Wo);
   else if (px == 2) hipLaunchKernelGGL(stem_fwd_kernel<2>, dim3(grid), dim3(256), 0, st, img, w, y, part, B, H, W, Ho, Wo);
-  else hipLaunchKernelGGL(stem_fwd_kernel<4>, dim3(grid), dim3(256), 0, st, img, w, y, part, B, H, W, Ho, Wo);
+  else if (px == 4) hipLaunchKernelGGL(stem_fwd_kernel<4>, dim3(grid), dim3(256), 0, st, img, w, y, part, B, H, W, Ho, Wo);
+  else return false;
+  return true;
 }

@@ -9,6 +9,7 @@ allocation, no synchronisation inside).
 Activations are NHWC bf16 tensors viewed as [M, C]; per-channel BN vectors are
 fp32 [C]; BN partial-sum buffers are fp32 [P, 2, C].
 """
+import os
 from typing import Optional
 
 import torch
@@ -339,13 +340,25 @@ def stem_num_partials(B, H, W):
     return lib().stem_fwd_num_partials(B, H, W)
 
 
-def stem_fwd(img, w, y, part, B, H, W):
+def _stem_px_default():
+    v = os.environ.get("PGDIST_STEM_PX", "1")
+    if v not in ("1", "2", "4"):
+        raise ValueError(f"PGDIST_STEM_PX={v!r}: must be 1, 2 or 4")
+    return int(v)
+
+
+def stem_fwd(img, w, y, part, B, H, W, px=None):
+    """Stem 3x3 s2 conv forward; ``px`` output pixels per thread (1, 2 or 4; default from
+    PGDIST_STEM_PX, else 1 — the measured fastest)."""
+    px = _stem_px_default() if px is None else int(px)
+    if px not in (1, 2, 4):
+        raise ValueError(f"stem_fwd: px={px} must be 1, 2 or 4")
     Ho, Wo = dw_out_hw(H, W, 2)
     _chk(img, BF16, B * H * W * 4, "img")
     _chk(w, BF16, 32 * 27, "w")
     _chk(y, BF16, B * Ho * Wo * 32, "y")
     _chk(part, F32, stem_num_partials(B, H, W) * 2 * 32, "part")
-    lib().stem_fwd(_p(img), _p(w), _p(y), _p(part), B, H, W, _s())
+    lib().stem_fwd(_p(img), _p(w), _p(y), _p(part), B, H, W, px, _s())
 
 
 def stem_wgrad_workspace(B, H, W, O=32):

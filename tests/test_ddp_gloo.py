@@ -6,22 +6,13 @@
 * the full Trainer (torch backend) runs 2 ranks and keeps replicas identical
 """
 import os
-import socket
 
 import pytest
 import torch
 import torch.distributed as dist
-import torch.multiprocessing as mp
 
+from mp_util import free_port as _free_port, run_ranks
 from pgdist.parallel.ddp import build_buckets
-
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
 
 
 def _init(rank, world, port):
@@ -67,26 +58,19 @@ def _worker_equivalence(rank, world, port, q):
     red.finish()
     flat.grad.mul_(1.0 / world)
     err = ((flat.grad - ref).norm() / ref.norm()).item()
-    q.put((rank, err, len(red.buckets)))
+    q.put(("ok", rank, err, len(red.buckets)))
     dist.destroy_process_group()
 
 
 def test_sharded_gradient_equals_full_batch():
     world, port = 2, _free_port()
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    procs = [ctx.Process(target=_worker_equivalence, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = [q.get(timeout=240) for _ in range(world)]
-    for p in procs:
-        p.join(timeout=60)
-    for rank, err, nb in res:
+    res = run_ranks(_worker_equivalence, world, (world, port), expect=world, timeout=240)
+    for _, rank, err, nb in res:
         assert err < 1e-5, (rank, err)
         assert nb > 3
 
 
-def _worker_trainer(rank, world, port, tmp, q, bn_sync="eval"):
+def _worker_trainer(rank, world, port, tmp, bn_sync, q):
     import pgdist  # noqa: F401
     from pgdist.config import TrainConfig
     from pgdist.engine.trainer import Trainer
@@ -105,7 +89,7 @@ def _worker_trainer(rank, world, port, tmp, q, bn_sync="eval"):
     rs = torch.cat([b.float().reshape(-1) for b in tr._bn_buffers()])
     allrs = [torch.zeros_like(rs) for _ in range(world)]
     dist.all_gather(allrs, rs)
-    q.put((rank, max((a - w).abs().max().item() for a in allw), tr.history[-1]["train_images"],
+    q.put(("ok", rank, max((a - w).abs().max().item() for a in allw), tr.history[-1]["train_images"],
            max((a - rs).abs().max().item() for a in allrs)))
     dist.destroy_process_group()
 
@@ -113,16 +97,8 @@ def _worker_trainer(rank, world, port, tmp, q, bn_sync="eval"):
 @pytest.mark.parametrize("bn_sync", ["eval", "broadcast", "none"])
 def test_trainer_two_ranks_keeps_replicas_in_sync(tmp_path, bn_sync):
     world, port = 2, _free_port()
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    procs = [ctx.Process(target=_worker_trainer, args=(r, world, port, str(tmp_path), q, bn_sync))
-             for r in range(world)]
-    for p in procs:
-        p.start()
-    res = [q.get(timeout=300) for _ in range(world)]
-    for p in procs:
-        p.join(timeout=60)
-    for rank, diff, n, bn_diff in res:
+    res = run_ranks(_worker_trainer, world, (world, port, str(tmp_path), bn_sync), expect=world, timeout=300)
+    for _, rank, diff, n, bn_diff in res:
         assert diff == 0.0
         assert n == 48
         if bn_sync == "none":       # rank-local running statistics (different shards)

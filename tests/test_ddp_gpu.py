@@ -7,25 +7,17 @@ all-reduce, 1/world folded into the fused Adam — is the one RCCL drives on a
 multi-GPU node (bench.py / train.py with backend nccl).
 """
 import os
-import socket
 
 import pytest
 import torch
 import torch.distributed as dist
-import torch.multiprocessing as mp
+
+from mp_util import free_port as _free_port, run_ranks as _run_ranks
 
 pytestmark = pytest.mark.gpu
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
-def _worker(rank, world, port, q, model_name):
+def _worker(rank, world, port, model_name, q):
     import pgdist  # noqa: F401
     from pgdist.models import build_model
     from pgdist.engine.native_step import NativeTrainStep
@@ -49,22 +41,15 @@ def _worker(rank, world, port, q, model_name):
     dist.all_gather(allw, w)
     diff = max((a - w).abs().max().item() for a in allw)
     l, c, n = st.read_metrics()
-    q.put((rank, diff, n, len(st.reducer.buckets), bool(torch.isfinite(w).all())))
+    q.put(("ok", rank, diff, n, len(st.reducer.buckets), bool(torch.isfinite(w).all())))
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("model_name", ["mobilenet_v2", "resnet50"])
 def test_native_ddp_two_ranks_one_gpu(model_name):
     world, port = 2, _free_port()
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, model_name)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = [q.get(timeout=400) for _ in range(world)]
-    for p in procs:
-        p.join(timeout=60)
-    for rank, diff, n, nb, finite in res:
+    res = _run_ranks(_worker, world, (world, port, model_name), expect=world)
+    for _, rank, diff, n, nb, finite in res:
         assert finite
         assert diff == 0.0, f"replicas diverged on rank {rank}: {diff}"
         assert n == 32
@@ -104,8 +89,15 @@ def _grad_worker(rank, world, port, q):
             torch.cuda.synchronize()
             singles.append(s1.flat.grad.clone())
         expect = singles[0] + singles[1]
-        err = ((reduced - expect).abs().max() / (expect.abs().max() + 1e-12)).item()
-        q.put(("err", err, len(st.reducer.buckets)))
+        # per bucket: every bucket must hold a nonzero gradient (a zeroed / never-written
+        # bucket would otherwise pass a relative check) and match the shard sum
+        per = []
+        for bi, (b0, b1, names) in enumerate(st.reducer.buckets):
+            e, r_ = expect[b0:b1], reduced[b0:b1]
+            scale = e.abs().max().item()
+            err = (r_ - e).abs().max().item() / (scale + 1e-12)
+            per.append((bi, names[0], names[-1], scale, err))
+        q.put(("ok", per))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -115,13 +107,8 @@ def test_native_ddp_reduced_gradient_equals_sum_of_shards():
     gradients (the 1/world is folded into Adam): checks the bucket launches are ordered after
     every producer of their gradients (main-stream dgrad-side BN grads and side-stream wgrads)."""
     world, port = 2, _free_port()
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    procs = [ctx.Process(target=_grad_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    tag, err, nb = q.get(timeout=400)
-    for p in procs:
-        p.join(timeout=120)
-    assert nb >= 3
-    assert err < 1e-5, err
+    (_, per), = _run_ranks(_grad_worker, world, (world, port), expect=1)
+    assert len(per) >= 3
+    for bi, first, last, scale, err in per:
+        assert scale > 0, f"bucket {bi} ({first} .. {last}) has an all-zero gradient"
+        assert err < 1e-5, f"bucket {bi} ({first} .. {last}): rel err {err}"

@@ -1,0 +1,21 @@
+"""Host-side argument validation of the HIP op wrappers (no GPU needed: the checks run
+before any kernel launch)."""
+import pytest
+import torch
+
+import pgdist  # noqa: F401
+from pgdist.ops import kernels as K
+
+
+@pytest.mark.parametrize("px", [0, 3, 8])
+def test_stem_px_rejected(px):
+    t = torch.zeros(1)
+    with pytest.raises(ValueError, match="px"):
+        K.stem_fwd(t, t, t, t, 1, 32, 32, px=px)
+
+
+def test_stem_px_env_rejected(monkeypatch):
+    monkeypatch.setenv("PGDIST_STEM_PX", "3")
+    t = torch.zeros(1)
+    with pytest.raises(ValueError, match="PGDIST_STEM_PX"):
+        K.stem_fwd(t, t, t, t, 1, 32, 32)
