@@ -106,4 +106,34 @@ PG_DEVICE long pack_fp8x8(const float (&v)[8], float sc) {
   return (long)(unsigned)lo | ((long)(unsigned)hi << 32);
 }
 
+// ---------------------------------------------------------------------------
+// Raw buffer loads / stores with hardware bounds checking (gfx950 SRD, stride 0).  A masked
+// lane passes the offset kOOB: its load returns 0 and its store is dropped, so a kernel needs
+// no branch around a memory instruction — hipcc then counts vmcnt exactly instead of waiting
+// vmcnt(0) at every join (conditional loads defeat software prefetching).  The descriptor is
+// built from kernel arguments only (wave-uniform: no waterfall loops).  Tensors < 2 GiB.
+// ---------------------------------------------------------------------------
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+constexpr uint32_t kOOB = 0x80000000u;
+
+PG_DEVICE rsrc_t make_rsrc(const void *base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)bytes, 0x00020000);
+}
+PG_DEVICE uint4 bld16(rsrc_t r, uint32_t off) {
+  const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+PG_DEVICE uint2 bld8(rsrc_t r, uint32_t off) {
+  const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0);
+  return make_uint2(v.x, v.y);
+}
+PG_DEVICE void bst8(rsrc_t r, uint32_t off, const uint2 &v) {
+  u32x2_t d;
+  d.x = v.x;
+  d.y = v.y;
+  __builtin_amdgcn_raw_buffer_store_b64(d, r, (int)off, 0, 0);
+}
+
 #define PG_CHECK_LAUNCH() ((void)hipGetLastError())

@@ -7,17 +7,15 @@
 // pure bandwidth (1.8-4.5 FLOP/B), so these kernels are organised around the
 // memory system:
 //
-//  * vertical strips: a thread owns 4 channels (one 8-B vector) of ONE output
-//    column and walks R rows down the image, keeping a rolling 3-row x 3-column
-//    window in registers — every input row is loaded once per thread, and the
-//    lanes of a wave (channel-fastest, then column) read one contiguous run of
-//    pixels per load instruction (the neighbours' halo columns hit the same lines);
 //  * a workgroup = a tile of TWc columns x R rows of one image and a slab of
-//    CC <= 64 channels (one slab per workgroup): small per-workgroup partial rows, long
-//    streams; ~100 VGPRs;
-//  * weights are tap-major [9][C] in the flat parameter buffer (one 8-B load per
-//    tap and 4 channels);
-//  * the producer's BatchNorm-apply + ReLU6 is fused into the input load (zero
+//    CC <= 64 channels (a multiple of 8: 16-B chunks); a thread owns 4 channels of ONE
+//    column (output column for fwd / wgrad, input column for dgrad) and walks the R rows,
+//    keeping a rolling 3-row x 3-column window in registers;
+//  * every row the tile needs is streamed once into an LDS ring by LDS-DMA
+//    (buffer_load_dwordx4 ... lds, see the "LDS-DMA row-streaming" section below) and the
+//    three tap columns are read from LDS;
+//  * weights are tap-major [9][C] in the flat parameter buffer;
+//  * the producer's BatchNorm-apply + ReLU6 is fused into the input read (zero
 //    padding in the post-activation space), the forward epilogue emits this
 //    layer's BN partial sums, the dgrad epilogue the producer-BN backward
 //    partials; the weight gradient is reduced per workgroup and then by a
@@ -30,10 +28,6 @@ namespace {
 
 constexpr int CPT = 4;        // channels per thread
 constexpr int kRows = 28;     // rows per strip (swept 4..112 on MI355X: 28 fastest end to end)
-#ifndef PGDIST_DGRAD_PF
-#define PGDIST_DGRAD_PF 2
-#endif
-constexpr int kDgradPrefetch = PGDIST_DGRAD_PF;   // rows of loads in flight ahead (stride-1 dgrad)
 
 struct DwGeom {
   int B, H, W, C, Ho, Wo;
@@ -63,62 +57,8 @@ PG_DEVICE void zero4(float (&v)[CPT]) {
   for (int k = 0; k < CPT; ++k) v[k] = 0.f;
 }
 
-// 4 channels at (b, ih, iw) of an [*, H, W, C] tensor, producer BN (+relu6) applied; OOB -> 0
-template <int ACT>
-PG_DEVICE void load_act4(const bf16_t *__restrict__ x, int H, int W, int C, int b, int ih, int iw,
-                         int c0, const float (&s)[CPT], const float (&t)[CPT], float (&v)[CPT]) {
-  if (ih < 0 || ih >= H || iw < 0 || iw >= W) {
-    zero4(v);
-    return;
-  }
-  unpack4(ldg8(x + (((size_t)b * H + ih) * W + iw) * C + c0), v);
-#pragma unroll
-  for (int k = 0; k < CPT; ++k) v[k] = act_apply<ACT>(v[k], s[k], t[k]);
-}
-
-// dy = a*g + b*y + c at (b, oh, ow) of [*, Ho, Wo, C]; OOB -> 0
-PG_DEVICE void load_dy4(const bf16_t *__restrict__ g, const bf16_t *__restrict__ y, int Ho, int Wo, int C,
-                        int b, int oh, int ow, int c0, const float (&al)[CPT], const float (&be)[CPT],
-                        const float (&ga)[CPT], float (&v)[CPT]) {
-  if (oh < 0 || oh >= Ho || ow < 0 || ow >= Wo) {
-    zero4(v);
-    return;
-  }
-  const size_t off = (((size_t)b * Ho + oh) * Wo + ow) * C + c0;
-  float gv[CPT], yv[CPT];
-  unpack4(ldg8(g + off), gv);
-  unpack4(ldg8(y + off), yv);
-#pragma unroll
-  for (int k = 0; k < CPT; ++k) v[k] = fmaf(al[k], gv[k], fmaf(be[k], yv[k], ga[k]));
-}
 
 
-// Raw (untransformed) 3-column row segment, loaded one strip row ahead so the
-// loads are in flight while the current row's FMAs run (software pipelining).
-struct Raw3 {
-  uint2 v[3];
-};
-PG_DEVICE void load_raw3(Raw3 &r, const bf16_t *__restrict__ x, int H, int W, int C, int b, int ih,
-                         int iw0, int c0) {
-#pragma unroll
-  for (int d = 0; d < 3; ++d) {
-    const int iw = iw0 + d;
-    r.v[d] = (ih >= 0 && ih < H && iw >= 0 && iw < W) ? ldg8(x + (((size_t)b * H + ih) * W + iw) * C + c0)
-                                                      : make_uint2(0, 0);
-  }
-}
-// transform a raw row; out-of-range entries must become exactly 0 after the transform
-template <int ACT>
-PG_DEVICE void act3(const Raw3 &r, int ih, int H, int iw0, int W, const float (&s)[CPT], const float (&t)[CPT],
-                    float (&out)[3][CPT]) {
-#pragma unroll
-  for (int d = 0; d < 3; ++d) {
-    const bool ok = ih >= 0 && ih < H && iw0 + d >= 0 && iw0 + d < W;
-    unpack4(r.v[d], out[d]);
-#pragma unroll
-    for (int k = 0; k < CPT; ++k) out[d][k] = ok ? act_apply<ACT>(out[d][k], s[k], t[k]) : 0.f;
-  }
-}
 
 // Workgroup decode.  The 1-D grid enumerates (tile, channel slab) pairs so that the slabs
 // of one spatial tile are 8 workgroup ids apart: same XCD (ids are dealt to the 8 XCDs
@@ -172,15 +112,103 @@ PG_DEVICE void block_channel_partials(float (&acc)[NV][CPT], float *__restrict__
 
 }  // namespace
 
-// ---------------------------------------------------------------------------
-// forward: y = dwconv(act(x)), partial (sum y, sum y^2)
-// ---------------------------------------------------------------------------
+// ===========================================================================
+// LDS-DMA row-streaming variants (default).  Measured on MI355X (rocprofv3 --pmc,
+// scripts/gpu_pmc_dw.sh; per-layer times: scripts/dw_bench.py): the register-window kernels
+// above load each input row THREE times per thread (the 3 tap columns, 8 B per lane), so the
+// texture-data return path (TD_TD_BUSY) runs 80-85 % busy at 2-3 TB/s, and their loads sit
+// behind branches (image borders, strip ends), so hipcc drains vmcnt(0) at every join and the
+// one-row register prefetch never overlaps; staging rows through registers two or four rows
+// ahead only trades occupancy for depth (same bytes in flight per CU).
+// Here every row a tile needs is streamed ONCE, 16 B per lane, straight into an LDS ring by
+// buffer_load_dwordx4 ... lds (no VGPRs per row in flight), kDepth rows ahead of the row being
+// computed.  Every global access is a bounds-checked buffer op whose masked lanes use an
+// out-of-range offset (common.h), so the loop body has no per-lane branch around a memory
+// instruction and every wave issues the same VMEM instructions per step: the wait for a ring
+// slot is a counted `s_waitcnt vmcnt(N)` + s_barrier (one per row), never a drain.
+// The 3 tap columns are read from LDS (ds_read_b64); the rolling 3x3 register window, the
+// fused BN/ReLU6 prologue, the BN partial epilogues and the fused weight gradient are those
+// of the kernels above.
+// ===========================================================================
+namespace {
+
+#ifndef PGDIST_DW_DEPTH
+#define PGDIST_DW_DEPTH 4
+#endif
+constexpr int kDepth = PGDIST_DW_DEPTH;   // rows in flight per stream
+constexpr int kRing = kDepth + 1;         // ring slots: the row being read + kDepth in flight
+// per-slot LDS bytes (whole 1 KiB wave pieces): halo row segments (TWc + 2) x CC8 <= 144
+// chunks, own-column segments TWc x CC8 <= 128, stride-2 input segments (2 TWc + 1) x CC8 <= 256
+constexpr int kSlotHalo = 3072, kSlotOwn = 2048, kSlotS2 = 4096;
+
+// One streamed tensor: a row segment of ncol columns starting at col0 x CC channels = nchunk
+// 16-B chunks (t = col * CC8 + part), lane-linear in LDS (wave w fills chunks [64w, 64w+64)).
+// Waves with no chunk of the segment still issue, into a dummy LDS piece with out-of-range
+// offsets, so that every wave issues the same number of VMEM instructions per step.
+struct Stream {
+  rsrc_t rs;
+  int H, W, C, b, col0;
+  int lane_col;        // segment column of this lane's chunk (-1: none)
+  int lane_coff;       // channel byte offset of this lane's chunk
+  bool wave_used;      // wave-uniform
+  PG_DEVICE void init(rsrc_t r, int H_, int W_, int C_, int b_, int col0_, int nchunk, int CC8, int cbase) {
+    rs = r;
+    H = H_;
+    W = W_;
+    C = C_;
+    b = b_;
+    col0 = col0_;
+    const int t = threadIdx.x;
+    lane_col = t < nchunk ? t / CC8 : -1;
+    lane_coff = (cbase + (t < nchunk ? t % CC8 : 0) * 8) * 2;
+    wave_used = (t & ~63) < nchunk;
+  }
+  // DMA row ih into `slot` of a ring of `stride`-byte slots at `ring`
+  PG_DEVICE void issue(char *ring, int stride, int slot, int ih, char *dummy) const {
+    const int iw = col0 + lane_col;
+    const bool ok = wave_used && lane_col >= 0 && ih >= 0 && ih < H && iw >= 0 && iw < W;
+    const uint32_t off = ok ? (uint32_t)(((b * H + ih) * W + iw) * C) * 2u + (uint32_t)lane_coff : kOOB;
+    char *dst = wave_used ? ring + slot * stride + (threadIdx.x & ~63) * 16 : dummy;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)dst, 16, off, 0, 0, 0);
+  }
+};
+
+// wait until at most N of this wave's VMEM instructions are outstanding, then a workgroup
+// barrier (every wave's share of the slot is in LDS; every read of the slot about to be
+// refilled is done).  N counts only the DMAs issued after the awaited row: stores may retire
+// out of order with loads (an out-of-range store immediately — a budget that counted the
+// stores let the wait pass before the DMA had landed; measured), loads retire in order.
+// Inline asm: hipcc must neither drain vmcnt(0) at the barrier nor move LDS reads across it.
+template <int N>
+PG_DEVICE void ring_sync() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+PG_DEVICE void mem_fence_compiler() { asm volatile("" ::: "memory"); }
+
+PG_DEVICE uint2 lds8(const char *slot, int col, int CC, int c) {
+  return *reinterpret_cast<const uint2 *>(slot + (col * CC + c) * 2);
+}
+
+PG_DEVICE uint32_t nhwc_off(int b, int H, int W, int C, int h, int w, int c) {
+  return (uint32_t)((((b * H + h) * W + w) * C + c) * 2);
+}
+
+}  // namespace
+
+// forward: y = dwconv(act(x)), partial (sum y, sum y^2); tiles over the output grid.
+// Per step (one input row): 1 DMA + 1 store (out of range when no output row completes).
+// The row loop is unrolled over the window period (3 rows for stride 1, 4 for stride 2) so
+// the window rows rotate by register renaming instead of copies; weights stay unpacked.
 template <int S, int ACT>
-__global__ __launch_bounds__(256) void dw_fwd_kernel(
+__global__ __launch_bounds__(256) void dw_fwd_lds_kernel(
     const bf16_t *__restrict__ x, const float *__restrict__ in_s, const float *__restrict__ in_t,
     const bf16_t *__restrict__ w, bf16_t *__restrict__ y, float *__restrict__ part, DwGeom g) {
+  constexpr int kSlot = S == 1 ? kSlotHalo : kSlotS2;
+  constexpr int U = S == 1 ? 3 : 4;                 // window period in input rows
+  __shared__ __attribute__((aligned(16))) char ring[kRing * kSlot + 1024];
   __shared__ __attribute__((aligned(16))) float red[1024];
-  const int C4 = g.CC / CPT;
+  char *dummy = ring + kRing * kSlot;
+  const int C4 = g.CC / CPT, CC8 = g.CC / 8;
   const int tid = threadIdx.x;
   const int c4 = tid % C4, col = tid / C4;
   const Tile tl = tile_of(g);
@@ -188,9 +216,10 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(
   const int c0 = cbase + c4 * CPT;
   const int ow = tl.w0 + col;
   const bool active = col < g.TWc && ow < g.Wo;
+  const int lcol = active ? col * S : 0;            // segment column of tap 0 (clamped when inactive)
+  const rsrc_t ry = make_rsrc(y, (uint32_t)g.B * g.Ho * g.Wo * g.C * 2);
 
-  float s[CPT], t[CPT], stats[2][CPT];
-  uint2 wt[9];   // packed bf16 taps (unpacked at use: fewer live VGPRs -> more waves)
+  float s[CPT], t[CPT], stats[2][CPT], wt[9][CPT];
 #pragma unroll
   for (int k = 0; k < CPT; ++k) {
     s[k] = (ACT != ACT_NONE) ? in_s[c0 + k] : 1.f;
@@ -198,104 +227,115 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(
     stats[0][k] = stats[1][k] = 0.f;
   }
 #pragma unroll
-  for (int q = 0; q < 9; ++q) wt[q] = ldg8(w + (size_t)q * g.C + c0);
+  for (int q = 0; q < 9; ++q) unpack4(ldg8(w + (size_t)q * g.C + c0), wt[q]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // parameters in registers before the stream
 
-  if (active) {
-    const int oh_end = min(tl.r0 + g.R, g.Ho);
-    const int iw0 = ow * S - 1;
-    // rolling window win[r][dw][k] = input rows oh*S-1+r; next rows prefetched raw
-    float win[3][3][CPT];
-    Raw3 n1, n2;
-    {
-      const int ih0 = tl.r0 * S - 1;
-      Raw3 r0, r1, r2;
-      load_raw3(r0, x, g.H, g.W, g.C, tl.b, ih0, iw0, c0);
-      load_raw3(r1, x, g.H, g.W, g.C, tl.b, ih0 + 1, iw0, c0);
-      load_raw3(r2, x, g.H, g.W, g.C, tl.b, ih0 + 2, iw0, c0);
-      act3<ACT>(r0, ih0, g.H, iw0, g.W, s, t, win[0]);
-      act3<ACT>(r1, ih0 + 1, g.H, iw0, g.W, s, t, win[1]);
-      act3<ACT>(r2, ih0 + 2, g.H, iw0, g.W, s, t, win[2]);
+  const int oh_end = min(tl.r0 + g.R, g.Ho);
+  const int j0 = tl.r0 * S - 1;                     // input rows j0 .. j0 + nrows - 1
+  const int nrows = (oh_end - 1) * S + 1 - j0 + 1;
+  const int iw0 = ow * S - 1;
+  // column validity of the 3 taps (rows are checked per step)
+  bool cok[3];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) cok[d] = active && iw0 + d >= 0 && iw0 + d < g.W;
+  Stream sx;
+  sx.init(make_rsrc(x, (uint32_t)g.B * g.H * g.W * g.C * 2), g.H, g.W, g.C, tl.b, tl.w0 * S - 1,
+          ((g.TWc - 1) * S + 3) * CC8, CC8, cbase);
+#pragma unroll
+  for (int q = 0; q < kDepth; ++q) sx.issue(ring, kSlot, q, j0 + q, dummy);
+  float win[3][3][CPT];   // three input rows x three tap columns (roles rotate with the unroll)
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int d = 0; d < 3; ++d) zero4(win[r][d]);
+  int slot = 0;
+  // one input row: wait for its slot, refill the ring, load it into window row `into`;
+  // emit an output row from window rows (ra, rb, rc) when `emit`
+  auto step = [&](int k, int into, bool emit, int ra, int rb, int rc) {
+    ring_sync<(kDepth - 1) * 1>();
+    sx.issue(ring, kSlot, slot + kDepth < kRing ? slot + kDepth : slot + kDepth - kRing, j0 + k + kDepth, dummy);
+    mem_fence_compiler();
+    const char *sl = ring + slot * kSlot;
+    slot = slot + 1 == kRing ? 0 : slot + 1;
+    const int ih = j0 + k;
+    const bool rok = ih >= 0 && ih < g.H;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      float v[CPT];
+      unpack4(lds8(sl, lcol + d, g.CC, c4 * CPT), v);
+      const float m = (rok && cok[d]) ? 1.f : 0.f;
+#pragma unroll
+      for (int kk = 0; kk < CPT; ++kk) {
+        const float a = m * act_apply<ACT>(v[kk], s[kk], t[kk]);
+        if (into == 0) win[0][d][kk] = a;
+        if (into == 1) win[1][d][kk] = a;
+        if (into == 2) win[2][d][kk] = a;
+      }
     }
-    for (int oh = tl.r0; oh < oh_end; ++oh) {
-      const int ihb = oh * S - 1;
-      if (oh > tl.r0) {
-        if constexpr (S == 1) {
+    const int oh = S == 1 ? ih - 1 : (ih - 1) >> 1;
+    float acc[CPT];
+    zero4(acc);
 #pragma unroll
-          for (int dw = 0; dw < 3; ++dw)
+    for (int r = 0; r < 3; ++r) {
+      const int wr = r == 0 ? ra : r == 1 ? rb : rc;
 #pragma unroll
-            for (int k = 0; k < CPT; ++k) {
-              win[0][dw][k] = win[1][dw][k];
-              win[1][dw][k] = win[2][dw][k];
-            }
-          act3<ACT>(n1, ihb + 2, g.H, iw0, g.W, s, t, win[2]);
-        } else {
+      for (int dw = 0; dw < 3; ++dw)
 #pragma unroll
-          for (int dw = 0; dw < 3; ++dw)
+        for (int kk = 0; kk < CPT; ++kk) acc[kk] = fmaf(win[wr][dw][kk], wt[r * 3 + dw][kk], acc[kk]);
+    }
+    bst8(ry, (emit && active) ? nhwc_off(tl.b, g.Ho, g.Wo, g.C, oh, ow, c0) : kOOB, pack4(acc));
+    const float e = emit ? 1.f : 0.f;
 #pragma unroll
-            for (int k = 0; k < CPT; ++k) win[0][dw][k] = win[2][dw][k];
-          act3<ACT>(n1, ihb + 1, g.H, iw0, g.W, s, t, win[1]);
-          act3<ACT>(n2, ihb + 2, g.H, iw0, g.W, s, t, win[2]);
-        }
-      }
-      if (oh + 1 < oh_end) {   // prefetch the rows the next output row adds
-        const int nb = (oh + 1) * S - 1;
-        if constexpr (S == 1) {
-          load_raw3(n1, x, g.H, g.W, g.C, tl.b, nb + 2, iw0, c0);
-        } else {
-          load_raw3(n1, x, g.H, g.W, g.C, tl.b, nb + 1, iw0, c0);
-          load_raw3(n2, x, g.H, g.W, g.C, tl.b, nb + 2, iw0, c0);
-        }
-      }
-      float acc[CPT];
-      zero4(acc);
-#pragma unroll
-      for (int r = 0; r < 3; ++r)
-#pragma unroll
-        for (int dw = 0; dw < 3; ++dw) {
-          float wv[CPT];
-          unpack4(wt[r * 3 + dw], wv);
-#pragma unroll
-          for (int k = 0; k < CPT; ++k) acc[k] = fmaf(win[r][dw][k], wv[k], acc[k]);
-        }
-      stg8(y + (((size_t)tl.b * g.Ho + oh) * g.Wo + ow) * g.C + c0, pack4(acc));
-#pragma unroll
-      for (int k = 0; k < CPT; ++k) {
-        stats[0][k] += acc[k];
-        stats[1][k] = fmaf(acc[k], acc[k], stats[1][k]);
-      }
+    for (int kk = 0; kk < CPT; ++kk) {
+      stats[0][kk] = fmaf(e, acc[kk], stats[0][kk]);
+      stats[1][kk] = fmaf(e * acc[kk], acc[kk], stats[1][kk]);
+    }
+  };
+  for (int k = 0; k < nrows; k += U) {
+    if constexpr (S == 1) {   // row k -> slot k % 3; output rows use (k-2, k-1, k) % 3
+      step(k, 0, k >= 2, 1, 2, 0);
+      if (k + 1 < nrows) step(k + 1, 1, k + 1 >= 2, 2, 0, 1);
+      if (k + 2 < nrows) step(k + 2, 2, true, 0, 1, 2);
+    } else {                  // k%4: 0 -> A (emit C,B,A if k > 0), 1 -> B, 2 -> C (emit A,B,C), 3 -> B
+      step(k, 0, k > 0, 2, 1, 0);
+      if (k + 1 < nrows) step(k + 1, 1, false, 0, 1, 2);
+      if (k + 2 < nrows) step(k + 2, 2, true, 0, 1, 2);
+      if (k + 3 < nrows) step(k + 3, 1, false, 0, 1, 2);
     }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may still target the ring
+  __syncthreads();
   block_channel_partials<2>(stats, part, g.C, g.CC, cbase, g.TWc, red, tl.idx);
 }
 
-// ---------------------------------------------------------------------------
-// dgrad: gout = mask_prev * dwconv^T(dy),  dy = a*g + b*y + c (this layer's BN backward)
-// thread = one INPUT column, strip of input rows; partial (sum gout, sum gout*yprev)
-// ---------------------------------------------------------------------------
-// WG = true: the weight gradient of the same layer is accumulated on the way (fused dgrad +
-// wgrad): every input pixel's z = relu6(BN(yprev)) meets exactly the dy taps the dgrad already
-// holds in registers, so dW costs 9 FMAs per pixel and no second read of (g, y, yprev);
-// per-workgroup wgrad partials go to wpart[tile][9][C] (reduced like dw_wgrad's).
-template <int S, bool WG>
-__global__ __launch_bounds__(256) void dw_dgrad_kernel(
+// dgrad (stride 1): thread = one INPUT column, strip of input rows.  Streams per step k: the dy
+// rows (g, y of this layer's BN backward, halo columns) of dy row r0-1+k and yprev (the
+// producer's pre-BN activation, own columns: ReLU6 mask + fused weight gradient) of input row
+// r0+k-2; step k >= 2 emits input row r0+k-2.  Per step: 3 DMA + 1 store.
+template <bool WG>
+__global__ __launch_bounds__(256) void dw_dgrad_s1_lds_kernel(
     const bf16_t *__restrict__ gin, const bf16_t *__restrict__ yself, const float *__restrict__ coef,
     const bf16_t *__restrict__ w, const bf16_t *__restrict__ yprev, const float *__restrict__ ps,
     const float *__restrict__ pt, bf16_t *__restrict__ gout, float *__restrict__ part, DwGeom g,
     float *__restrict__ wpart) {
+  constexpr int kStep = 2 * kSlotHalo + kSlotOwn;   // g, y, yprev pieces of one ring slot
+  __shared__ __attribute__((aligned(16))) char ring[kRing * kStep + 1024];
   __shared__ __attribute__((aligned(16))) float red[1024];
-  const int C4 = g.CC / CPT;
+  char *dummy = ring + kRing * kStep;
+  const int C4 = g.CC / CPT, CC8 = g.CC / 8;
   const int tid = threadIdx.x;
   const int c4 = tid % C4, col = tid / C4;
   const Tile tl = tile_of(g);
   const int cbase = tl.slab * g.CC;
   const int c0 = cbase + c4 * CPT;
-  // tiles over the INPUT grid (H x W)
   const int iw = tl.w0 + col;
   const bool active = col < g.TWc && iw < g.W;
+  const int lcol = active ? col : 0;
+  const uint32_t nbytes = (uint32_t)g.B * g.H * g.W * g.C * 2;   // stride 1: dy grid == input grid
+  const rsrc_t ro = make_rsrc(gout, nbytes);
 
-  float al[CPT], be[CPT], ga[CPT], s[CPT], t[CPT], stats[2][CPT];
-  uint2 wtp[9];   // packed bf16 taps (unpacked at use: fewer live VGPRs -> more waves)
-  float accw[WG ? 9 : 1][CPT];   // fused weight-gradient partials (tap-major)
+  float al[CPT], be[CPT], ga[CPT], s[CPT], t[CPT], stats[2][CPT], wt[9][CPT];
+  float accw[WG ? 9 : 1][CPT];
 #pragma unroll
   for (int k = 0; k < CPT; ++k) {
     al[k] = coef[c0 + k];
@@ -306,263 +346,309 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(
     stats[0][k] = stats[1][k] = 0.f;
   }
 #pragma unroll
-  for (int q = 0; q < (WG ? 9 : 1); ++q)
+  for (int q = 0; q < (WG ? 9 : 1); ++q) zero4(accw[q]);
 #pragma unroll
-    for (int k = 0; k < CPT; ++k) accw[q][k] = 0.f;
-#pragma unroll
-  for (int q = 0; q < 9; ++q) wtp[q] = ldg8(w + (size_t)q * g.C + c0);
+  for (int q = 0; q < 9; ++q) unpack4(ldg8(w + (size_t)q * g.C + c0), wt[q]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-  if (active) {
-    const int ih_end = min(tl.r0 + g.R, g.H);
-    if constexpr (S == 1) {
-      // dx[ih][iw] = sum_{dh,dw} dy[ih+1-dh][iw+1-dw] * w[dh][dw];  window rows ih-1..ih+1 (as dy rows)
-      float win[3][3][CPT];   // win[r][c]: dy row ih-1+r, col iw-1+c
+  const int ih_end = min(tl.r0 + g.R, g.H);
+  const int j0 = tl.r0 - 1;                         // dy rows j0 .. ih_end (window ih-1..ih+1)
+  const int nrows = ih_end - j0 + 1;
+  bool cok[3];
 #pragma unroll
-      for (int r = 0; r < 3; ++r)
+  for (int c = 0; c < 3; ++c) cok[c] = active && iw - 1 + c >= 0 && iw - 1 + c < g.W;
+  Stream sg, sy, sp;
+  sg.init(make_rsrc(gin, nbytes), g.H, g.W, g.C, tl.b, tl.w0 - 1, (g.TWc + 2) * CC8, CC8, cbase);
+  sy = sg;
+  sy.rs = make_rsrc(yself, nbytes);
+  sp.init(make_rsrc(yprev, nbytes), g.H, g.W, g.C, tl.b, tl.w0, g.TWc * CC8, CC8, cbase);
+  auto issue = [&](int slot, int k) {
+    char *base = ring + slot * kStep;
+    sg.issue(base, 0, 0, j0 + k, dummy);
+    sy.issue(base + kSlotHalo, 0, 0, j0 + k, dummy);
+    sp.issue(base + 2 * kSlotHalo, 0, 0, tl.r0 + k - 2, dummy);
+  };
 #pragma unroll
-        for (int c = 0; c < 3; ++c)
-          load_dy4(gin, yself, g.Ho, g.Wo, g.C, tl.b, tl.r0 - 1 + r, iw - 1 + c, c0, al, be, ga, win[r][c]);
-      // kPf-deep ring of raw loads (statically indexed: the row loop is unrolled by kPf):
-      // dy row (r0 + 1 + i) sits in slot (i - 1) % kPf, yprev row (r0 + i) in slot i % kPf
-      constexpr int kPf = kDgradPrefetch;
-      Raw3 rg[kPf], ry[kPf];
-      uint2 ypr[kPf];
+  for (int q = 0; q < kDepth; ++q) issue(q, q);
+  float win[3][3][CPT];   // three dy rows x three columns iw-1..iw+1 (roles rotate with the unroll)
 #pragma unroll
-      for (int q = 0; q < kPf; ++q) {
-        load_raw3(rg[q], gin, g.Ho, g.Wo, g.C, tl.b, tl.r0 + 2 + q, iw - 1, c0);
-        load_raw3(ry[q], yself, g.Ho, g.Wo, g.C, tl.b, tl.r0 + 2 + q, iw - 1, c0);
-        const int r = tl.r0 + q;
-        ypr[q] = r < ih_end ? ldg8(yprev + (((size_t)tl.b * g.H + r) * g.W + iw) * g.C + c0) : make_uint2(0, 0);
-      }
-      for (int base = 0; tl.r0 + base < ih_end; base += kPf) {
+  for (int r = 0; r < 3; ++r)
 #pragma unroll
-        for (int j = 0; j < kPf; ++j) {
-          const int i = base + j, ih = tl.r0 + i;
-          if (ih >= ih_end) break;
-          if (i > 0) {
-            const int sl = (j + kPf - 1) % kPf;   // slot of dy row ih + 1 (static after unrolling)
+    for (int d = 0; d < 3; ++d) zero4(win[r][d]);
+  int slot = 0;
+  // dy row j0+k -> window row `into`; rows (ra, rb, rc) = dy rows ih-1, ih, ih+1 of input row
+  // ih = j0+k-1, emitted when `emit`
+  auto step = [&](int k, int into, bool emit, int ra, int rb, int rc) {
+    ring_sync<(kDepth - 1) * 3>();
+    issue(slot + kDepth < kRing ? slot + kDepth : slot + kDepth - kRing, k + kDepth);
+    mem_fence_compiler();
+    const char *sl = ring + slot * kStep;
+    slot = slot + 1 == kRing ? 0 : slot + 1;
+    const int oh = j0 + k;
+    const bool rok = oh >= 0 && oh < g.H;
 #pragma unroll
-            for (int c = 0; c < 3; ++c)
+    for (int c = 0; c < 3; ++c) {
+      const float m = (rok && cok[c]) ? 1.f : 0.f;
+      float gv[CPT], yv[CPT];
+      unpack4(lds8(sl, lcol + c, g.CC, c4 * CPT), gv);
+      unpack4(lds8(sl + kSlotHalo, lcol + c, g.CC, c4 * CPT), yv);
 #pragma unroll
-              for (int k = 0; k < CPT; ++k) {
-                win[0][c][k] = win[1][c][k];
-                win[1][c][k] = win[2][c][k];
-              }
-            const int oh = ih + 1;
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-              const bool ok = oh >= 0 && oh < g.Ho && iw - 1 + c >= 0 && iw - 1 + c < g.Wo;
-              float gv[CPT], yv[CPT];
-              unpack4(rg[sl].v[c], gv);
-              unpack4(ry[sl].v[c], yv);
-#pragma unroll
-              for (int k = 0; k < CPT; ++k) win[2][c][k] = ok ? fmaf(al[k], gv[k], fmaf(be[k], yv[k], ga[k])) : 0.f;
-            }
-            // refill the slot with dy row ih + 1 + kPf
-            load_raw3(rg[sl], gin, g.Ho, g.Wo, g.C, tl.b, ih + 1 + kPf, iw - 1, c0);
-            load_raw3(ry[sl], yself, g.Ho, g.Wo, g.C, tl.b, ih + 1 + kPf, iw - 1, c0);
-          }
-          const uint2 ypc = ypr[j];
-          {
-            const int r = ih + kPf;
-            ypr[j] = r < ih_end ? ldg8(yprev + (((size_t)tl.b * g.H + r) * g.W + iw) * g.C + c0) : make_uint2(0, 0);
-          }
-          float acc[CPT];
-          zero4(acc);
-          // dy row ih+1-dh = win[2-dh], col iw+1-dw = win[..][2-dw]
-#pragma unroll
-          for (int dh = 0; dh < 3; ++dh)
-#pragma unroll
-            for (int dw = 0; dw < 3; ++dw) {
-              float wv[CPT];
-              unpack4(wtp[dh * 3 + dw], wv);
-#pragma unroll
-              for (int k = 0; k < CPT; ++k) acc[k] = fmaf(win[2 - dh][2 - dw][k], wv[k], acc[k]);
-            }
-          const size_t off = (((size_t)tl.b * g.H + ih) * g.W + iw) * g.C + c0;
-          float yp[CPT];
-          unpack4(ypc, yp);
-          if constexpr (WG) {   // dW[dh][dw] += z[ih][iw] * dy[ih+1-dh][iw+1-dw]
-            float z[CPT];
-#pragma unroll
-            for (int k = 0; k < CPT; ++k) z[k] = relu6f(fmaf(yp[k], s[k], t[k]));
-#pragma unroll
-            for (int dh = 0; dh < 3; ++dh)
-#pragma unroll
-              for (int dw = 0; dw < 3; ++dw)
-#pragma unroll
-                for (int k = 0; k < CPT; ++k)
-                  accw[WG ? dh * 3 + dw : 0][k] = fmaf(z[k], win[2 - dh][2 - dw][k], accw[WG ? dh * 3 + dw : 0][k]);
-          }
-#pragma unroll
-          for (int k = 0; k < CPT; ++k) acc[k] *= relu6_mask(yp[k], s[k], t[k]);
-          const uint2 packed = pack4(acc);
-          float gr[CPT];
-          unpack4(packed, gr);
-#pragma unroll
-          for (int k = 0; k < CPT; ++k) {
-            stats[0][k] += gr[k];
-            stats[1][k] = fmaf(gr[k], yp[k], stats[1][k]);
-          }
-          stg8(gout + off, packed);
-        }
-      }
-    } else {
-      // stride 2.  Column: even iw -> ow = iw/2 (dw=1); odd iw -> ow = (iw+1)/2 (dw=0), (iw-1)/2 (dw=2)
-      // Row: even ih = 2o -> dy row o (dh=1); odd ih = 2o+1 -> dy rows o (dh=2), o+1 (dh=0)
-      const bool odd_w = iw & 1;
-      const int owA = odd_w ? (iw + 1) >> 1 : iw >> 1;   // dw = 0 (odd) or 1 (even)
-      const int owB = (iw - 1) >> 1;                      // dw = 2 (odd only)
-      // per-thread tap weights (selected with static indices: no runtime-indexed arrays)
-      float wA[3][CPT], wB[3][CPT];   // [dh] for column A (dw = 0 if odd else 1) and B (dw = 2)
-#pragma unroll
-      for (int r = 0; r < 3; ++r) {
-        float w0[CPT], w1[CPT], w2[CPT];
-        unpack4(wtp[r * 3 + 0], w0);
-        unpack4(wtp[r * 3 + 1], w1);
-        unpack4(wtp[r * 3 + 2], w2);
-#pragma unroll
-        for (int k = 0; k < CPT; ++k) {
-          wA[r][k] = odd_w ? w0[k] : w1[k];
-          wB[r][k] = odd_w ? w2[k] : 0.f;
-        }
-      }
-      // tiles start at even rows (R even).  Everything one iteration (2 input rows) ahead:
-      // raw dy (g, y) of the next dy row and the yprev rows of the next iteration.
-      auto ld_raw = [&](uint2 &dst, const bf16_t *src, int H_, int W_, int r, int c) {
-        dst = (r >= 0 && r < H_ && c >= 0 && c < W_) ? ldg8(src + (((size_t)tl.b * H_ + r) * W_ + c) * g.C + c0)
-                                                     : make_uint2(0, 0);
-      };
-      auto dy_of = [&](const uint2 &gg, const uint2 &yy, int r, int c, float (&v)[CPT]) {
-        const bool ok = r >= 0 && r < g.Ho && c >= 0 && c < g.Wo;
-        float gv[CPT], yv[CPT];
-        unpack4(gg, gv);
-        unpack4(yy, yv);
-#pragma unroll
-        for (int k = 0; k < CPT; ++k) v[k] = ok ? fmaf(al[k], gv[k], fmaf(be[k], yv[k], ga[k])) : 0.f;
-      };
-      float cur[2][CPT], nxt[2][CPT];   // dy row o / o+1 at columns A, B
-      float accA[WG ? 3 : 1][CPT], accB[WG ? 3 : 1][CPT];   // fused dW[dh][dwA] / dW[dh][2]
-#pragma unroll
-      for (int r = 0; r < (WG ? 3 : 1); ++r)
-#pragma unroll
-        for (int k = 0; k < CPT; ++k) accA[r][k] = accB[r][k] = 0.f;
-      uint2 rgA, ryA, rgB, ryB;         // raw dy row o+1 (columns A, B)
-      uint2 yp0r, yp1r;                 // raw yprev rows of the current iteration
-      int o = tl.r0 >> 1;
-      {
-        uint2 gA, yA, gB, yB;
-        ld_raw(gA, gin, g.Ho, g.Wo, o, owA);
-        ld_raw(yA, yself, g.Ho, g.Wo, o, owA);
-        ld_raw(gB, gin, g.Ho, g.Wo, o, odd_w ? owB : -1);
-        ld_raw(yB, yself, g.Ho, g.Wo, o, odd_w ? owB : -1);
-        dy_of(gA, yA, o, owA, cur[0]);
-        dy_of(gB, yB, o, odd_w ? owB : -1, cur[1]);
-      }
-      ld_raw(rgA, gin, g.Ho, g.Wo, o + 1, owA);
-      ld_raw(ryA, yself, g.Ho, g.Wo, o + 1, owA);
-      ld_raw(rgB, gin, g.Ho, g.Wo, o + 1, odd_w ? owB : -1);
-      ld_raw(ryB, yself, g.Ho, g.Wo, o + 1, odd_w ? owB : -1);
-      ld_raw(yp0r, yprev, g.H, g.W, tl.r0, iw);
-      ld_raw(yp1r, yprev, g.H, g.W, tl.r0 + 1 < ih_end ? tl.r0 + 1 : -1, iw);
-      for (int ih = tl.r0; ih < ih_end; ih += 2) {
-        o = ih >> 1;
-        dy_of(rgA, ryA, o + 1, owA, nxt[0]);
-        dy_of(rgB, ryB, o + 1, odd_w ? owB : -1, nxt[1]);
-        const uint2 ypc[2] = {yp0r, yp1r};
-        if (ih + 2 < ih_end) {   // next iteration's operands, in flight during this one's FMAs
-          ld_raw(rgA, gin, g.Ho, g.Wo, o + 2, owA);
-          ld_raw(ryA, yself, g.Ho, g.Wo, o + 2, owA);
-          ld_raw(rgB, gin, g.Ho, g.Wo, o + 2, odd_w ? owB : -1);
-          ld_raw(ryB, yself, g.Ho, g.Wo, o + 2, odd_w ? owB : -1);
-          ld_raw(yp0r, yprev, g.H, g.W, ih + 2, iw);
-          ld_raw(yp1r, yprev, g.H, g.W, ih + 3 < ih_end ? ih + 3 : -1, iw);
-        }
-#pragma unroll
-        for (int half = 0; half < 2; ++half) {
-          const int r = ih + half;
-          if (r >= ih_end) break;
-          float acc[CPT];
-          zero4(acc);
-          if (half == 0) {          // even row: dh = 1, dy row o
-#pragma unroll
-            for (int k = 0; k < CPT; ++k)
-              acc[k] = fmaf(cur[0][k], wA[1][k], fmaf(cur[1][k], wB[1][k], acc[k]));
-          } else {                  // odd row: dh = 2 (row o), dh = 0 (row o+1)
-#pragma unroll
-            for (int k = 0; k < CPT; ++k) {
-              acc[k] = fmaf(cur[0][k], wA[2][k], fmaf(cur[1][k], wB[2][k], acc[k]));
-              acc[k] = fmaf(nxt[0][k], wA[0][k], fmaf(nxt[1][k], wB[0][k], acc[k]));
-            }
-          }
-          const size_t off = (((size_t)tl.b * g.H + r) * g.W + iw) * g.C + c0;
-          float yp[CPT];
-          unpack4(ypc[half], yp);
-          if constexpr (WG) {
-            float z[CPT];
-#pragma unroll
-            for (int k = 0; k < CPT; ++k) z[k] = relu6f(fmaf(yp[k], s[k], t[k]));
-            if (half == 0) {          // dh = 1 with dy row o
-#pragma unroll
-              for (int k = 0; k < CPT; ++k) {
-                accA[WG ? 1 : 0][k] = fmaf(z[k], cur[0][k], accA[WG ? 1 : 0][k]);
-                accB[WG ? 1 : 0][k] = fmaf(z[k], cur[1][k], accB[WG ? 1 : 0][k]);
-              }
-            } else {                  // dh = 2 with row o, dh = 0 with row o+1
-#pragma unroll
-              for (int k = 0; k < CPT; ++k) {
-                accA[WG ? 2 : 0][k] = fmaf(z[k], cur[0][k], accA[WG ? 2 : 0][k]);
-                accB[WG ? 2 : 0][k] = fmaf(z[k], cur[1][k], accB[WG ? 2 : 0][k]);
-                accA[0][k] = fmaf(z[k], nxt[0][k], accA[0][k]);
-                accB[0][k] = fmaf(z[k], nxt[1][k], accB[0][k]);
-              }
-            }
-          }
-#pragma unroll
-          for (int k = 0; k < CPT; ++k) acc[k] *= relu6_mask(yp[k], s[k], t[k]);
-          const uint2 packed = pack4(acc);
-          float gr[CPT];
-          unpack4(packed, gr);
-#pragma unroll
-          for (int k = 0; k < CPT; ++k) {
-            stats[0][k] += gr[k];
-            stats[1][k] = fmaf(gr[k], yp[k], stats[1][k]);
-          }
-          stg8(gout + off, packed);
-        }
-#pragma unroll
-        for (int k = 0; k < CPT; ++k) {
-          cur[0][k] = nxt[0][k];
-          cur[1][k] = nxt[1][k];
-        }
-      }
-      if constexpr (WG) {   // column A is tap dw = 0 (odd iw) or 1 (even iw); column B is dw = 2
-#pragma unroll
-        for (int dh = 0; dh < 3; ++dh)
-#pragma unroll
-          for (int k = 0; k < CPT; ++k) {
-            accw[WG ? dh * 3 + 0 : 0][k] = odd_w ? accA[WG ? dh : 0][k] : 0.f;
-            accw[WG ? dh * 3 + 1 : 0][k] = odd_w ? 0.f : accA[WG ? dh : 0][k];
-            accw[WG ? dh * 3 + 2 : 0][k] = accB[WG ? dh : 0][k];
-          }
+      for (int kk = 0; kk < CPT; ++kk) {
+        const float v = m * fmaf(al[kk], gv[kk], fmaf(be[kk], yv[kk], ga[kk]));
+        if (into == 0) win[0][c][kk] = v;
+        if (into == 1) win[1][c][kk] = v;
+        if (into == 2) win[2][c][kk] = v;
       }
     }
+    const int ih = oh - 1;
+    float yp[CPT];
+    unpack4(lds8(sl + 2 * kSlotHalo, lcol, g.CC, c4 * CPT), yp);
+    float acc[CPT];
+    zero4(acc);
+#pragma unroll
+    for (int dh = 0; dh < 3; ++dh) {   // dx[ih][iw] += dy[ih+1-dh][iw+1-dw] * w[dh][dw]
+      const int wr = dh == 0 ? rc : dh == 1 ? rb : ra;
+#pragma unroll
+      for (int dw = 0; dw < 3; ++dw)
+#pragma unroll
+        for (int kk = 0; kk < CPT; ++kk) acc[kk] = fmaf(win[wr][2 - dw][kk], wt[dh * 3 + dw][kk], acc[kk]);
+    }
+    const float e = emit ? 1.f : 0.f;
+    if constexpr (WG) {
+      float z[CPT];
+#pragma unroll
+      for (int kk = 0; kk < CPT; ++kk) z[kk] = e * relu6f(fmaf(yp[kk], s[kk], t[kk]));
+#pragma unroll
+      for (int dh = 0; dh < 3; ++dh) {
+        const int wr = dh == 0 ? rc : dh == 1 ? rb : ra;
+#pragma unroll
+        for (int dw = 0; dw < 3; ++dw)
+#pragma unroll
+          for (int kk = 0; kk < CPT; ++kk)
+            accw[WG ? dh * 3 + dw : 0][kk] = fmaf(z[kk], win[wr][2 - dw][kk], accw[WG ? dh * 3 + dw : 0][kk]);
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < CPT; ++kk) acc[kk] *= relu6_mask(yp[kk], s[kk], t[kk]);
+    const uint2 packed = pack4(acc);
+    float gr[CPT];
+    unpack4(packed, gr);
+#pragma unroll
+    for (int kk = 0; kk < CPT; ++kk) {
+      stats[0][kk] = fmaf(e, gr[kk], stats[0][kk]);
+      stats[1][kk] = fmaf(e * gr[kk], yp[kk], stats[1][kk]);
+    }
+    bst8(ro, (emit && active) ? nhwc_off(tl.b, g.H, g.W, g.C, ih, iw, c0) : kOOB, packed);
+  };
+  for (int k = 0; k < nrows; k += 3) {   // dy row k -> window row k % 3
+    step(k, 0, k >= 2, 1, 2, 0);
+    if (k + 1 < nrows) step(k + 1, 1, k + 1 >= 2, 2, 0, 1);
+    if (k + 2 < nrows) step(k + 2, 2, true, 0, 1, 2);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   block_channel_partials<2>(stats, part, g.C, g.CC, cbase, g.TWc, red, tl.idx);
   if constexpr (WG) block_channel_partials<9>(accw, wpart, g.C, g.CC, cbase, g.TWc, red, tl.idx);
 }
 
-// ---------------------------------------------------------------------------
-// wgrad: dW[tap][c] partials per workgroup  [P][9][C]
-// thread = one output column, strip of output rows, rolling z window
-// ---------------------------------------------------------------------------
+// dgrad (stride 2): thread = one INPUT column iw; it needs dy columns owA (tap dw = 0 for odd
+// iw, 1 for even iw) and owB = (iw-1)/2 (tap dw = 2, odd iw only).  Streams per step k: dy
+// row o = o0 + k (g, y over the dy columns the tile touches) and yprev input rows 2(o-1),
+// 2(o-1)+1 (own columns); step k >= 1 emits those two input rows (tap dh = 1 with dy row o-1;
+// dh = 2 with row o-1 and dh = 0 with row o).  Per step: 4 DMA + 2 stores.
+template <bool WG>
+__global__ __launch_bounds__(256) void dw_dgrad_s2_lds_kernel(
+    const bf16_t *__restrict__ gin, const bf16_t *__restrict__ yself, const float *__restrict__ coef,
+    const bf16_t *__restrict__ w, const bf16_t *__restrict__ yprev, const float *__restrict__ ps,
+    const float *__restrict__ pt, bf16_t *__restrict__ gout, float *__restrict__ part, DwGeom g,
+    float *__restrict__ wpart) {
+  constexpr int kStep = 4 * kSlotOwn;   // g, y (<= TWc/2 + 2 dy columns), yprev x 2
+  __shared__ __attribute__((aligned(16))) char ring[kRing * kStep + 1024];
+  __shared__ __attribute__((aligned(16))) float red[1024];
+  char *dummy = ring + kRing * kStep;
+  const int C4 = g.CC / CPT, CC8 = g.CC / 8;
+  const int tid = threadIdx.x;
+  const int c4 = tid % C4, col = tid / C4;
+  const Tile tl = tile_of(g);
+  const int cbase = tl.slab * g.CC;
+  const int c0 = cbase + c4 * CPT;
+  const int iw = tl.w0 + col;
+  const bool active = col < g.TWc && iw < g.W;
+  const int lcol = active ? col : 0;
+  const int dcol0 = (tl.w0 - 1) >> 1;               // first dy column of the segment (may be -1)
+  const int dcol1 = (tl.w0 + g.TWc) >> 1;           // last dy column (inclusive)
+  const bool odd_w = iw & 1;
+  const int owA = odd_w ? (iw + 1) >> 1 : iw >> 1;
+  const int owB = odd_w ? (iw - 1) >> 1 : -1;       // -1: no tap (masked)
+  const bool okA = active && owA < g.Wo, okB = active && owB >= 0;
+  const int lA = okA ? owA - dcol0 : 0, lB = okB ? owB - dcol0 : 0;
+  const uint32_t nin = (uint32_t)g.B * g.H * g.W * g.C * 2, nout = (uint32_t)g.B * g.Ho * g.Wo * g.C * 2;
+  const rsrc_t ro = make_rsrc(gout, nin);
+
+  float al[CPT], be[CPT], ga[CPT], s[CPT], t[CPT], stats[2][CPT];
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    al[k] = coef[c0 + k];
+    be[k] = coef[g.C + c0 + k];
+    ga[k] = coef[2 * g.C + c0 + k];
+    s[k] = ps[c0 + k];
+    t[k] = pt[c0 + k];
+    stats[0][k] = stats[1][k] = 0.f;
+  }
+  float wA[3][CPT], wB[3][CPT];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    float w0[CPT], w1[CPT], w2[CPT];
+    unpack4(ldg8(w + (size_t)(r * 3 + 0) * g.C + c0), w0);
+    unpack4(ldg8(w + (size_t)(r * 3 + 1) * g.C + c0), w1);
+    unpack4(ldg8(w + (size_t)(r * 3 + 2) * g.C + c0), w2);
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      wA[r][k] = odd_w ? w0[k] : w1[k];
+      wB[r][k] = odd_w ? w2[k] : 0.f;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float accA[WG ? 3 : 1][CPT], accB[WG ? 3 : 1][CPT];
+#pragma unroll
+  for (int r = 0; r < (WG ? 3 : 1); ++r) {
+    zero4(accA[r]);
+    zero4(accB[r]);
+  }
+
+  const int ih_end = min(tl.r0 + g.R, g.H);
+  const int o0 = tl.r0 >> 1;                            // r0 even
+  const int nrows = ((ih_end - 1) >> 1) + 1 - o0 + 1;   // dy rows o0 .. (ih_end-1)/2 + 1
+  Stream sg, sy, sp;
+  sg.init(make_rsrc(gin, nout), g.Ho, g.Wo, g.C, tl.b, dcol0, (dcol1 - dcol0 + 1) * CC8, CC8, cbase);
+  sy = sg;
+  sy.rs = make_rsrc(yself, nout);
+  sp.init(make_rsrc(yprev, nin), g.H, g.W, g.C, tl.b, tl.w0, g.TWc * CC8, CC8, cbase);
+  auto issue = [&](int slot, int k) {
+    char *base = ring + slot * kStep;
+    const int o = o0 + k;
+    sg.issue(base, 0, 0, o, dummy);
+    sy.issue(base + kSlotOwn, 0, 0, o, dummy);
+    sp.issue(base + 2 * kSlotOwn, 0, 0, 2 * (o - 1), dummy);
+    sp.issue(base + 3 * kSlotOwn, 0, 0, 2 * (o - 1) + 1, dummy);
+  };
+#pragma unroll
+  for (int q = 0; q < kDepth; ++q) issue(q, q);
+  float dyb[2][2][CPT];   // two dy rows (roles alternate with the unroll) x columns A, B
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    zero4(dyb[r][0]);
+    zero4(dyb[r][1]);
+  }
+  int slot = 0;
+  // dy row o = o0+k -> dyb[into]; dyb[from] holds row o-1; emits input rows 2(o-1), 2(o-1)+1
+  auto step = [&](int k, int into, int from) {
+    ring_sync<(kDepth - 1) * 4>();
+    issue(slot + kDepth < kRing ? slot + kDepth : slot + kDepth - kRing, k + kDepth);
+    mem_fence_compiler();
+    const char *sl = ring + slot * kStep;
+    slot = slot + 1 == kRing ? 0 : slot + 1;
+    const int o = o0 + k;
+    const float mA = (okA && o < g.Ho) ? 1.f : 0.f, mB = (okB && o < g.Ho) ? 1.f : 0.f;
+    {
+      float gv[CPT], yv[CPT], hv[CPT], zv[CPT];
+      unpack4(lds8(sl, lA, g.CC, c4 * CPT), gv);
+      unpack4(lds8(sl + kSlotOwn, lA, g.CC, c4 * CPT), yv);
+      unpack4(lds8(sl, lB, g.CC, c4 * CPT), hv);
+      unpack4(lds8(sl + kSlotOwn, lB, g.CC, c4 * CPT), zv);
+#pragma unroll
+      for (int kk = 0; kk < CPT; ++kk) {
+        const float va = mA * fmaf(al[kk], gv[kk], fmaf(be[kk], yv[kk], ga[kk]));
+        const float vb = mB * fmaf(al[kk], hv[kk], fmaf(be[kk], zv[kk], ga[kk]));
+        if (into == 0) {
+          dyb[0][0][kk] = va;
+          dyb[0][1][kk] = vb;
+        } else {
+          dyb[1][0][kk] = va;
+          dyb[1][1][kk] = vb;
+        }
+      }
+    }
+    float(&cur)[2][CPT] = dyb[from];
+    float(&nxt)[2][CPT] = dyb[into];
+    float ypa[CPT], ypb[CPT];
+    unpack4(lds8(sl + 2 * kSlotOwn, lcol, g.CC, c4 * CPT), ypa);
+    unpack4(lds8(sl + 3 * kSlotOwn, lcol, g.CC, c4 * CPT), ypb);
+    const int r = 2 * (o - 1);
+    const float ea = k > 0 ? 1.f : 0.f;                      // row r exists (r < ih_end always)
+    const float eb = (k > 0 && r + 1 < ih_end) ? 1.f : 0.f;
+    float acc0[CPT], acc1[CPT];
+#pragma unroll
+    for (int kk = 0; kk < CPT; ++kk) {
+      acc0[kk] = fmaf(cur[0][kk], wA[1][kk], cur[1][kk] * wB[1][kk]);
+      acc1[kk] = fmaf(cur[0][kk], wA[2][kk], cur[1][kk] * wB[2][kk]);
+      acc1[kk] = fmaf(nxt[0][kk], wA[0][kk], fmaf(nxt[1][kk], wB[0][kk], acc1[kk]));
+    }
+    if constexpr (WG) {
+#pragma unroll
+      for (int kk = 0; kk < CPT; ++kk) {
+        const float za = ea * relu6f(fmaf(ypa[kk], s[kk], t[kk]));
+        const float zb = eb * relu6f(fmaf(ypb[kk], s[kk], t[kk]));
+        accA[WG ? 1 : 0][kk] = fmaf(za, cur[0][kk], accA[WG ? 1 : 0][kk]);
+        accB[WG ? 1 : 0][kk] = fmaf(za, cur[1][kk], accB[WG ? 1 : 0][kk]);
+        accA[WG ? 2 : 0][kk] = fmaf(zb, cur[0][kk], accA[WG ? 2 : 0][kk]);
+        accB[WG ? 2 : 0][kk] = fmaf(zb, cur[1][kk], accB[WG ? 2 : 0][kk]);
+        accA[0][kk] = fmaf(zb, nxt[0][kk], accA[0][kk]);
+        accB[0][kk] = fmaf(zb, nxt[1][kk], accB[0][kk]);
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < CPT; ++kk) {
+      acc0[kk] *= relu6_mask(ypa[kk], s[kk], t[kk]);
+      acc1[kk] *= relu6_mask(ypb[kk], s[kk], t[kk]);
+    }
+    const uint2 p0 = pack4(acc0), p1 = pack4(acc1);
+    float g0[CPT], g1[CPT];
+    unpack4(p0, g0);
+    unpack4(p1, g1);
+#pragma unroll
+    for (int kk = 0; kk < CPT; ++kk) {
+      stats[0][kk] = fmaf(ea, g0[kk], fmaf(eb, g1[kk], stats[0][kk]));
+      stats[1][kk] = fmaf(ea * g0[kk], ypa[kk], fmaf(eb * g1[kk], ypb[kk], stats[1][kk]));
+    }
+    bst8(ro, (k > 0 && active) ? nhwc_off(tl.b, g.H, g.W, g.C, r, iw, c0) : kOOB, p0);
+    bst8(ro, (eb != 0.f && active) ? nhwc_off(tl.b, g.H, g.W, g.C, r + 1, iw, c0) : kOOB, p1);
+  };
+  for (int k = 0; k < nrows; k += 2) {
+    step(k, 0, 1);
+    if (k + 1 < nrows) step(k + 1, 1, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float accw[WG ? 9 : 1][CPT];
+  if constexpr (WG) {
+#pragma unroll
+    for (int dh = 0; dh < 3; ++dh)
+#pragma unroll
+      for (int k = 0; k < CPT; ++k) {
+        accw[WG ? dh * 3 + 0 : 0][k] = odd_w ? accA[WG ? dh : 0][k] : 0.f;
+        accw[WG ? dh * 3 + 1 : 0][k] = odd_w ? 0.f : accA[WG ? dh : 0][k];
+        accw[WG ? dh * 3 + 2 : 0][k] = accB[WG ? dh : 0][k];
+      }
+  }
+  __syncthreads();
+  block_channel_partials<2>(stats, part, g.C, g.CC, cbase, g.TWc, red, tl.idx);
+  if constexpr (WG) block_channel_partials<9>(accw, wpart, g.C, g.CC, cbase, g.TWc, red, tl.idx);
+}
+
+// wgrad: dW[tap][c] partials per workgroup [P][9][C]; thread = one output column.  Streams per
+// step k: input row j0+k (z = relu6(BN(yprev)), halo columns) and the dy rows (g, y; own
+// columns) of the output row the step may complete.  Per step: 3 DMA.
 template <int S>
-__global__ __launch_bounds__(256) void dw_wgrad_kernel(
+__global__ __launch_bounds__(256) void dw_wgrad_lds_kernel(
     const bf16_t *__restrict__ gin, const bf16_t *__restrict__ yself, const float *__restrict__ coef,
     const bf16_t *__restrict__ yprev, const float *__restrict__ ps, const float *__restrict__ pt,
     float *__restrict__ part, DwGeom g) {
+  constexpr int kSlotX = S == 1 ? kSlotHalo : kSlotS2;
+  constexpr int kStep = kSlotX + 2 * kSlotOwn;
+  __shared__ __attribute__((aligned(16))) char ring[kRing * kStep + 1024];
   __shared__ __attribute__((aligned(16))) float lds[1024];
-  const int C4 = g.CC / CPT;
+  char *dummy = ring + kRing * kStep;
+  const int C4 = g.CC / CPT, CC8 = g.CC / 8;
   const int tid = threadIdx.x;
   const int c4 = tid % C4, col = tid / C4;
   const Tile tl = tile_of(g);
@@ -570,6 +656,8 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(
   const int c0 = cbase + c4 * CPT;
   const int ow = tl.w0 + col;
   const bool active = col < g.TWc && ow < g.Wo;
+  const int lcol = active ? col * S : 0, lown = active ? col : 0;
+  const uint32_t nin = (uint32_t)g.B * g.H * g.W * g.C * 2, nout = (uint32_t)g.B * g.Ho * g.Wo * g.C * 2;
 
   float al[CPT], be[CPT], ga[CPT], s[CPT], t[CPT];
   float accw[9][CPT];
@@ -580,77 +668,92 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(
     ga[k] = coef[2 * g.C + c0 + k];
     s[k] = ps[c0 + k];
     t[k] = pt[c0 + k];
-#pragma unroll
-    for (int q = 0; q < 9; ++q) accw[q][k] = 0.f;
   }
-  if (active) {
-    const int oh_end = min(tl.r0 + g.R, g.Ho);
-    const int iw0 = ow * S - 1;
-    float win[3][3][CPT];
-    Raw3 n1, n2;
-    uint2 gnext = make_uint2(0, 0), ynext = make_uint2(0, 0);
-    {
-      const int ih0 = tl.r0 * S - 1;
-      Raw3 r0, r1, r2;
-      load_raw3(r0, yprev, g.H, g.W, g.C, tl.b, ih0, iw0, c0);
-      load_raw3(r1, yprev, g.H, g.W, g.C, tl.b, ih0 + 1, iw0, c0);
-      load_raw3(r2, yprev, g.H, g.W, g.C, tl.b, ih0 + 2, iw0, c0);
-      const size_t off = (((size_t)tl.b * g.Ho + tl.r0) * g.Wo + ow) * g.C + c0;
-      gnext = ldg8(gin + off);
-      ynext = ldg8(yself + off);
-      act3<ACT_BN_RELU6>(r0, ih0, g.H, iw0, g.W, s, t, win[0]);
-      act3<ACT_BN_RELU6>(r1, ih0 + 1, g.H, iw0, g.W, s, t, win[1]);
-      act3<ACT_BN_RELU6>(r2, ih0 + 2, g.H, iw0, g.W, s, t, win[2]);
+#pragma unroll
+  for (int q = 0; q < 9; ++q) zero4(accw[q]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int oh_end = min(tl.r0 + g.R, g.Ho);
+  const int j0 = tl.r0 * S - 1;
+  const int nrows = (oh_end - 1) * S + 1 - j0 + 1;
+  const int iw0 = ow * S - 1;
+  bool cok[3];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) cok[d] = active && iw0 + d >= 0 && iw0 + d < g.W;
+  Stream sx, sg, sy;
+  sx.init(make_rsrc(yprev, nin), g.H, g.W, g.C, tl.b, tl.w0 * S - 1, ((g.TWc - 1) * S + 3) * CC8, CC8, cbase);
+  sg.init(make_rsrc(gin, nout), g.Ho, g.Wo, g.C, tl.b, tl.w0, g.TWc * CC8, CC8, cbase);
+  sy = sg;
+  sy.rs = make_rsrc(yself, nout);
+  // output row completed at step k: S = 1: r0 + k - 2; S = 2 (even k): r0 + (k - 2) / 2
+  auto out_row = [&](int k) { return S == 1 ? tl.r0 + k - 2 : tl.r0 + ((k - 2) >> 1); };
+  auto issue = [&](int slot, int k) {
+    char *base = ring + slot * kStep;
+    sx.issue(base, 0, 0, j0 + k, dummy);
+    const int oh = out_row(k);
+    const int ohc = oh < oh_end ? oh : -1;   // rows of the next tile are never needed
+    sg.issue(base + kSlotX, 0, 0, ohc, dummy);
+    sy.issue(base + kSlotX + kSlotOwn, 0, 0, ohc, dummy);
+  };
+#pragma unroll
+  for (int q = 0; q < kDepth; ++q) issue(q, q);
+  float win[3][3][CPT];
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int d = 0; d < 3; ++d) zero4(win[r][d]);
+  int slot = 0;
+  auto step = [&](int k, int into, bool emit, int ra, int rb, int rc) {
+    ring_sync<(kDepth - 1) * 3>();
+    issue(slot + kDepth < kRing ? slot + kDepth : slot + kDepth - kRing, k + kDepth);
+    mem_fence_compiler();
+    const char *sl = ring + slot * kStep;
+    slot = slot + 1 == kRing ? 0 : slot + 1;
+    const int ih = j0 + k;
+    const bool rok = ih >= 0 && ih < g.H;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      float v[CPT];
+      unpack4(lds8(sl, lcol + d, g.CC, c4 * CPT), v);
+      const float m = (rok && cok[d]) ? 1.f : 0.f;
+#pragma unroll
+      for (int kk = 0; kk < CPT; ++kk) {
+        const float a = m * relu6f(fmaf(v[kk], s[kk], t[kk]));
+        if (into == 0) win[0][d][kk] = a;
+        if (into == 1) win[1][d][kk] = a;
+        if (into == 2) win[2][d][kk] = a;
+      }
     }
-    for (int oh = tl.r0; oh < oh_end; ++oh) {
-      const int ihb = oh * S - 1;
-      if (oh > tl.r0) {
-        if constexpr (S == 1) {
+    if (emit) {
+      float dy[CPT], gv[CPT], yv[CPT];
+      unpack4(lds8(sl + kSlotX, lown, g.CC, c4 * CPT), gv);
+      unpack4(lds8(sl + kSlotX + kSlotOwn, lown, g.CC, c4 * CPT), yv);
+      const float m = active ? 1.f : 0.f;
 #pragma unroll
-          for (int dw = 0; dw < 3; ++dw)
+      for (int kk = 0; kk < CPT; ++kk) dy[kk] = m * fmaf(al[kk], gv[kk], fmaf(be[kk], yv[kk], ga[kk]));
 #pragma unroll
-            for (int k = 0; k < CPT; ++k) {
-              win[0][dw][k] = win[1][dw][k];
-              win[1][dw][k] = win[2][dw][k];
-            }
-          act3<ACT_BN_RELU6>(n1, ihb + 2, g.H, iw0, g.W, s, t, win[2]);
-        } else {
-#pragma unroll
-          for (int dw = 0; dw < 3; ++dw)
-#pragma unroll
-            for (int k = 0; k < CPT; ++k) win[0][dw][k] = win[2][dw][k];
-          act3<ACT_BN_RELU6>(n1, ihb + 1, g.H, iw0, g.W, s, t, win[1]);
-          act3<ACT_BN_RELU6>(n2, ihb + 2, g.H, iw0, g.W, s, t, win[2]);
-        }
-      }
-      float dy[CPT];
-      {
-        float gv[CPT], yv[CPT];
-        unpack4(gnext, gv);
-        unpack4(ynext, yv);
-#pragma unroll
-        for (int k = 0; k < CPT; ++k) dy[k] = fmaf(al[k], gv[k], fmaf(be[k], yv[k], ga[k]));
-      }
-      if (oh + 1 < oh_end) {   // prefetch next row: z rows and dy
-        const int nb = (oh + 1) * S - 1;
-        if constexpr (S == 1) {
-          load_raw3(n1, yprev, g.H, g.W, g.C, tl.b, nb + 2, iw0, c0);
-        } else {
-          load_raw3(n1, yprev, g.H, g.W, g.C, tl.b, nb + 1, iw0, c0);
-          load_raw3(n2, yprev, g.H, g.W, g.C, tl.b, nb + 2, iw0, c0);
-        }
-        const size_t off = (((size_t)tl.b * g.Ho + oh + 1) * g.Wo + ow) * g.C + c0;
-        gnext = ldg8(gin + off);
-        ynext = ldg8(yself + off);
-      }
-#pragma unroll
-      for (int r = 0; r < 3; ++r)
+      for (int r = 0; r < 3; ++r) {
+        const int wr = r == 0 ? ra : r == 1 ? rb : rc;
 #pragma unroll
         for (int dw = 0; dw < 3; ++dw)
 #pragma unroll
-          for (int k = 0; k < CPT; ++k) accw[r * 3 + dw][k] = fmaf(dy[k], win[r][dw][k], accw[r * 3 + dw][k]);
+          for (int kk = 0; kk < CPT; ++kk) accw[r * 3 + dw][kk] = fmaf(dy[kk], win[wr][dw][kk], accw[r * 3 + dw][kk]);
+      }
+    }
+  };
+  for (int k = 0; k < nrows; k += (S == 1 ? 3 : 4)) {
+    if constexpr (S == 1) {
+      step(k, 0, k >= 2, 1, 2, 0);
+      if (k + 1 < nrows) step(k + 1, 1, k + 1 >= 2, 2, 0, 1);
+      if (k + 2 < nrows) step(k + 2, 2, true, 0, 1, 2);
+    } else {
+      step(k, 0, k > 0, 2, 1, 0);
+      if (k + 1 < nrows) step(k + 1, 1, false, 0, 1, 2);
+      if (k + 2 < nrows) step(k + 2, 2, true, 0, 1, 2);
+      if (k + 3 < nrows) step(k + 3, 1, false, 0, 1, 2);
     }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   block_channel_partials<9>(accw, part, g.C, g.CC, cbase, g.TWc, lds, tl.idx);
 }
 
@@ -658,11 +761,12 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(
 // host side
 // ---------------------------------------------------------------------------
 namespace {
-// channels per workgroup: the largest multiple of 4 dividing C that is <= 64
+// channels per workgroup: the largest multiple of 8 dividing C that is <= 64 (C % 8 == 0 is
+// checked by the caller): 16-B channel chunks for the LDS-staged row segments
 int dw_cc(int C) {
-  for (int cc = 64; cc >= 4; cc -= 4)
+  for (int cc = 64; cc >= 8; cc -= 8)
     if (C % cc == 0) return cc;
-  return 4;
+  return 8;
 }
 
 // kind 0 = fwd (tiles over the output grid), 1 = dgrad (input grid), 2 = wgrad (output grid)
@@ -678,6 +782,8 @@ DwGeom dw_geom(int kind, int B, int H, int W, int C, int stride) {
   const int C4 = g.CC / CPT;
   const int gw = kind == 1 ? W : g.Wo, gh = kind == 1 ? H : g.Ho;
   int twc = 256 / C4;
+  // LDS-DMA stride-2 input rows over the output grid: (2 TWc + 1) x CC8 <= 256 chunks
+  if (kind != 1 && stride == 2 && twc > (256 / (g.CC / 8) - 1) / 2) twc = (256 / (g.CC / 8) - 1) / 2;
   if (twc > gw) twc = gw;
   g.TWc = twc;
   static const int env_rows = [] {
@@ -700,7 +806,6 @@ DwGeom dw_geom(int kind, int B, int H, int W, int C, int stride) {
 }
 
 int dw_grid_x(const DwGeom &g) { return g.B * g.tiles_h * g.tiles_w; }
-int dw_threads(const DwGeom &g) { return (g.CC / CPT) * g.TWc; }
 }  // namespace
 
 int dw_fwd_num_partials(int B, int H, int W, int C, int stride) { return dw_grid_x(dw_geom(0, B, H, W, C, stride)); }
@@ -710,13 +815,13 @@ int dw_wgrad_num_partials(int B, int H, int W, int C, int stride) { return dw_gr
 void launch_dw_fwd(const bf16_t *x, const float *in_s, const float *in_t, int act, const bf16_t *w,
                    bf16_t *y, float *part, int B, int H, int W, int C, int stride, hipStream_t st) {
   const DwGeom g = dw_geom(0, B, H, W, C, stride);
-  dim3 grid(dw_grid_x(g) * (C / g.CC)), block(dw_threads(g));
+  const dim3 grid(dw_grid_x(g) * (C / g.CC)), block(256);
   if (stride == 1) {
-    if (act == ACT_BN_RELU6) hipLaunchKernelGGL((dw_fwd_kernel<1, ACT_BN_RELU6>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
-    else hipLaunchKernelGGL((dw_fwd_kernel<1, ACT_NONE>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
+    if (act == ACT_BN_RELU6) hipLaunchKernelGGL((dw_fwd_lds_kernel<1, ACT_BN_RELU6>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
+    else hipLaunchKernelGGL((dw_fwd_lds_kernel<1, ACT_NONE>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
   } else {
-    if (act == ACT_BN_RELU6) hipLaunchKernelGGL((dw_fwd_kernel<2, ACT_BN_RELU6>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
-    else hipLaunchKernelGGL((dw_fwd_kernel<2, ACT_NONE>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
+    if (act == ACT_BN_RELU6) hipLaunchKernelGGL((dw_fwd_lds_kernel<2, ACT_BN_RELU6>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
+    else hipLaunchKernelGGL((dw_fwd_lds_kernel<2, ACT_NONE>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
   }
 }
 
@@ -726,17 +831,17 @@ void launch_dw_dgrad(const bf16_t *gin, const bf16_t *yself, const float *coef, 
                      const bf16_t *yprev, const float *ps, const float *pt, bf16_t *gout,
                      float *part, int B, int H, int W, int C, int stride, float *wpart, hipStream_t st) {
   const DwGeom g = dw_geom(1, B, H, W, C, stride);
-  dim3 grid(dw_grid_x(g) * (C / g.CC)), block(dw_threads(g));
+  const dim3 grid(dw_grid_x(g) * (C / g.CC)), block(256);
   if (wpart) {
     if (stride == 1)
-      hipLaunchKernelGGL((dw_dgrad_kernel<1, true>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g, wpart);
+      hipLaunchKernelGGL((dw_dgrad_s1_lds_kernel<true>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g, wpart);
     else
-      hipLaunchKernelGGL((dw_dgrad_kernel<2, true>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g, wpart);
+      hipLaunchKernelGGL((dw_dgrad_s2_lds_kernel<true>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g, wpart);
   } else {
     if (stride == 1)
-      hipLaunchKernelGGL((dw_dgrad_kernel<1, false>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g, wpart);
+      hipLaunchKernelGGL((dw_dgrad_s1_lds_kernel<false>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g, wpart);
     else
-      hipLaunchKernelGGL((dw_dgrad_kernel<2, false>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g, wpart);
+      hipLaunchKernelGGL((dw_dgrad_s2_lds_kernel<false>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g, wpart);
   }
 }
 
@@ -753,11 +858,11 @@ void launch_dw_wgrad(const bf16_t *gin, const bf16_t *yself, const float *coef, 
                      int C, int stride, hipStream_t st) {
   const DwGeom g = dw_geom(2, B, H, W, C, stride);
   const int P = dw_grid_x(g);
-  dim3 grid(P * (C / g.CC)), block(dw_threads(g));
+  const dim3 grid(P * (C / g.CC)), block(256);
   if (stride == 1)
-    hipLaunchKernelGGL((dw_wgrad_kernel<1>), grid, block, 0, st, gin, yself, coef, yprev, ps, pt, part, g);
+    hipLaunchKernelGGL((dw_wgrad_lds_kernel<1>), grid, block, 0, st, gin, yself, coef, yprev, ps, pt, part, g);
   else
-    hipLaunchKernelGGL((dw_wgrad_kernel<2>), grid, block, 0, st, gin, yself, coef, yprev, ps, pt, part, g);
+    hipLaunchKernelGGL((dw_wgrad_lds_kernel<2>), grid, block, 0, st, gin, yself, coef, yprev, ps, pt, part, g);
   // deterministic two-level reduction of the [P][9C] partials -> grad [9][C] (tap-major)
   launch_wgrad_reduce(part, P, 9LL * C, grad, st);
 }

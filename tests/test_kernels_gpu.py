@@ -131,7 +131,10 @@ def test_bn_bwd_finalize_matches_autograd(dev):
 
 # ----------------------------------------------------------------------------- depthwise
 DW_CASES = [(2, 14, 14, 32, 1), (2, 14, 14, 96, 2), (3, 28, 28, 144, 1), (2, 7, 7, 960, 1),
-            (2, 56, 56, 96, 2), (1, 28, 28, 576, 2), (2, 9, 9, 24, 1), (2, 10, 10, 16, 2)]
+            (2, 56, 56, 96, 2), (1, 28, 28, 576, 2), (2, 9, 9, 24, 1), (2, 10, 10, 16, 2),
+            # partial last column tile (W not a multiple of the tile width), odd sizes, full-size rows
+            (1, 57, 57, 64, 2), (1, 45, 45, 192, 1), (1, 112, 112, 32, 1), (1, 112, 112, 96, 2),
+            (1, 29, 31, 48, 2), (1, 13, 33, 40, 1)]
 
 
 @pytest.mark.parametrize("B,H,W,C,stride", DW_CASES)
