@@ -136,4 +136,15 @@ PG_DEVICE void bst8(rsrc_t r, uint32_t off, const uint2 &v) {
   __builtin_amdgcn_raw_buffer_store_b64(d, r, (int)off, 0, 0);
 }
 
+PG_DEVICE void bst16(rsrc_t r, uint32_t off, const uint4 &v) {
+  u32x4_t d;
+  d.x = v.x;
+  d.y = v.y;
+  d.z = v.z;
+  d.w = v.w;
+  __builtin_amdgcn_raw_buffer_store_b128(d, r, (int)off, 0, 0);
+}
+// byte offset of element i of a bf16 tensor, or kOOB
+PG_DEVICE uint32_t boff(bool ok, size_t i) { return ok ? (uint32_t)(i * 2) : kOOB; }
+
 #define PG_CHECK_LAUNCH() ((void)hipGetLastError())

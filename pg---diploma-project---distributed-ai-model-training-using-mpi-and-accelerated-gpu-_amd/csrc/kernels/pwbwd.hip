@@ -128,7 +128,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
 
   // ---- staging registers (one tile ahead): G, Y; Yt (both modes); X and R (LIN)
   uint4 gq[IDY][4], yq[IDY][4], tq[IX][4], xq[LIN ? IX : 1][4], rq[LIN ? IX : 1][4];
-  auto load_tile = [&](int m0) {
+  // bounds-checked buffer loads issued unconditionally (masked lanes and the prefetch past the
+  // last tile read 0 through an out-of-range offset): no branch, so hipcc keeps the next
+  // tile's loads in flight instead of draining vmcnt(0) at a join
+  const uint32_t gbytes = (uint32_t)((size_t)p.M * p.Kg * 2), tbytes = (uint32_t)((size_t)p.M * p.Ng * 2);
+  const rsrc_t rG = make_rsrc(p.G, gbytes), rY = make_rsrc(p.Y, gbytes), rT = make_rsrc(p.Yt, tbytes);
+  const rsrc_t rX = make_rsrc(LIN ? p.X : p.Yt, tbytes), rR = make_rsrc(p.R, p.R ? tbytes : 0u);
+  auto load_tile = [&](int m0, bool valid) {
 #pragma unroll
     for (int i = 0; i < IDY; ++i) {
       const int it = tid + i * 256;
@@ -136,10 +142,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int row = m0 + m4 * 4 + q;
-        const bool ok = it < NDY && row < p.M && c8 < p.Kg;
-        const size_t off = (size_t)row * p.Kg + c8;
-        gq[i][q] = ok ? ldg16(p.G + off) : make_uint4(0, 0, 0, 0);
-        yq[i][q] = ok ? ldg16(p.Y + off) : make_uint4(0, 0, 0, 0);
+        const uint32_t off = boff(valid && it < NDY && row < p.M && c8 < p.Kg, (size_t)row * p.Kg + c8);
+        gq[i][q] = bld16(rG, off);
+        yq[i][q] = bld16(rY, off);
       }
     }
 #pragma unroll
@@ -149,18 +154,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int row = m0 + m4 * 4 + q;
-        const bool ok = it < NX && row < p.M && n0 + c8 < p.Ng;
-        const size_t off = (size_t)row * p.Ng + n0 + c8;
-        tq[i][q] = ok ? ldg16(p.Yt + off) : make_uint4(0, 0, 0, 0);
+        const uint32_t off = boff(valid && it < NX && row < p.M && n0 + c8 < p.Ng, (size_t)row * p.Ng + n0 + c8);
+        tq[i][q] = bld16(rT, off);
         if constexpr (LIN) {
-          xq[i][q] = ok ? ldg16(p.X + off) : make_uint4(0, 0, 0, 0);
-          rq[i][q] = (ok && p.R) ? ldg16(p.R + off) : make_uint4(0, 0, 0, 0);
+          xq[i][q] = bld16(rX, off);
+          rq[i][q] = bld16(rR, off);
         }
       }
     }
   };
 
-  if (blockIdx.x < nmt) load_tile(blockIdx.x * BM);
+  load_tile(blockIdx.x * BM, blockIdx.x < nmt);
   for (int mt = blockIdx.x; mt < nmt; mt += gridDim.x) {
     const int m0 = mt * BM;
     __syncthreads();                 // previous tile's epilogue is done with Cs (aliases the staging)
@@ -227,7 +231,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
       }
     }
     __syncthreads();
-    if (mt + gridDim.x < nmt) load_tile((mt + gridDim.x) * BM);   // next tile in flight from here on
+    load_tile((mt + gridDim.x) * BM, mt + gridDim.x < nmt);   // next tile in flight from here on
     // ---- dgrad MFMA: wave -> rows rw*16 .. +16, column tiles cw*CTW .. +CTW
     f32x4_t acc[RPW][CTW];
 #pragma unroll

@@ -202,23 +202,29 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
   }
 
   using Raw = PwRaw<PRO, SUBS, BDIRECT ? CT : 0>;
-  auto load = [&](Raw &r, int m0, int s) {
+  // Bounds-checked buffer loads, issued unconditionally (masked lanes / the prefetch past the
+  // last tile use an out-of-range offset and read 0): a load behind a branch makes hipcc wait
+  // vmcnt(0) at the join, which drained this one-step-ahead prefetch right after issuing it.
+  const rsrc_t rA = make_rsrc(p.A, (uint32_t)((size_t)p.M * p.K * 2));
+  const rsrc_t rA2 = make_rsrc(HAS_A2 ? p.A2 : p.A, (uint32_t)((size_t)p.M * p.K * 2));
+  const rsrc_t rW = make_rsrc(p.W, (uint32_t)((size_t)p.N * p.K * 2));
+  auto load = [&](Raw &r, int m0, int s, bool valid) {
 #pragma unroll
     for (int ss = 0; ss < SUBS; ++ss) {
       const int k = s * KSTEP + ss * 32 + 8 * (lane >> 4);
 #pragma unroll
       for (int f = 0; f < 2; ++f) {
         const int row = m0 + rg * 32 + f * 16 + (lane & 15);
-        const bool ok = row < p.M && k < p.K;
-        const size_t off = (size_t)row * p.K + k;
-        r.a[ss][f] = ok ? ldg16(p.A + off) : make_uint4(0, 0, 0, 0);
-        if constexpr (HAS_A2) r.y[ss][f] = ok ? ldg16(p.A2 + off) : make_uint4(0, 0, 0, 0);
+        const bool ok = valid && row < p.M && k < p.K;
+        const uint32_t off = ok ? (uint32_t)(((size_t)row * p.K + k) * 2) : kOOB;
+        r.a[ss][f] = bld16(rA, off);
+        if constexpr (HAS_A2) r.y[ss][f] = bld16(rA2, off);
       }
       if constexpr (BDIRECT) {
 #pragma unroll
         for (int c = 0; c < CT; ++c) {
           const int n = n0 + c * 16 + (lane & 15);
-          r.b[ss][c] = (n < p.N && k < p.K) ? ldg16(p.W + (size_t)n * p.K + k) : make_uint4(0, 0, 0, 0);
+          r.b[ss][c] = bld16(rW, (valid && n < p.N && k < p.K) ? (uint32_t)(((size_t)n * p.K + k) * 2) : kOOB);
         }
       }
     }
@@ -278,7 +284,7 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
 
   // ---- flattened (M tile, k step) stream, prefetching one step ahead (across tiles too)
   Raw cur, nxt;
-  if (blockIdx.x < nmt) load(cur, blockIdx.x * BM, kp);
+  load(cur, blockIdx.x * BM, kp, blockIdx.x < nmt);
   for (int mt = blockIdx.x; mt < nmt; mt += gridDim.x) {
     const int m0 = mt * BM;
     cur_m0 = m0;
@@ -289,7 +295,7 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
     for (int s = kp; s < nsteps; s += KS) {
       int ns = s + KS, nm = mt;
       if (ns >= nsteps) { ns = kp; nm = mt + gridDim.x; }
-      if (nm < nmt) load(nxt, nm * BM, ns);
+      load(nxt, nm * BM, ns, nm < nmt);
       compute(cur, s);
       cur = nxt;
     }

@@ -100,30 +100,34 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
 
   constexpr bool HAS_A2 = PRO == PRO_BNBWD_T || PRO == PRO_BNRES_T;
   uint4 ra[ACH], ry[HAS_A2 ? ACH : 1], rb[F8 ? B8PT : BCH];
-  auto load = [&](int k0) {
+  // bounds-checked buffer loads issued unconditionally (masked: out-of-range offset, reads 0),
+  // so the one-step-ahead prefetch is not drained by a vmcnt(0) at a branch join
+  const rsrc_t rA = make_rsrc(p.A, (uint32_t)((size_t)p.M * p.K * 2));
+  const rsrc_t rA2 = make_rsrc(HAS_A2 ? p.A2 : p.A, (uint32_t)((size_t)p.M * p.K * 2));
+  const rsrc_t rW = F8 ? make_rsrc(p.W8, (uint32_t)((size_t)p.N * p.ldw8)) : make_rsrc(p.W, (uint32_t)((size_t)p.N * p.K * 2));
+  auto load = [&](int k0, bool valid) {
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
       const int c = tid + i * 256, row = c / KCH, kk = (c % KCH) * 8;
       const int gr = m0 + row, k = k0 + kk;
-      const bool ok = gr < p.M && k < p.K;
-      const size_t off = (size_t)gr * p.K + k;
-      ra[i] = ok ? ldg16(p.A + off) : make_uint4(0, 0, 0, 0);
-      if constexpr (HAS_A2) ry[i] = ok ? ldg16(p.A2 + off) : make_uint4(0, 0, 0, 0);
+      const uint32_t off = boff(valid && gr < p.M && k < p.K, (size_t)gr * p.K + k);
+      ra[i] = bld16(rA, off);
+      if constexpr (HAS_A2) ry[i] = bld16(rA2, off);
     }
     if constexpr (F8) {
 #pragma unroll
       for (int i = 0; i < B8PT; ++i) {
         const int c = tid + i * 256, n = c / (KSTEP / 16), kk = (c % (KSTEP / 16)) * 16;
         const int gn = n0 + n;
-        rb[i] = (c < B8CH && gn < p.N && k0 + kk < p.ldw8) ? ldg16(p.W8 + (size_t)gn * p.ldw8 + k0 + kk)
-                                                           : make_uint4(0, 0, 0, 0);
+        const bool ok = valid && c < B8CH && gn < p.N && k0 + kk < p.ldw8;
+        rb[i] = bld16(rW, ok ? (uint32_t)((size_t)gn * p.ldw8 + k0 + kk) : kOOB);
       }
     } else {
 #pragma unroll
       for (int i = 0; i < BCH; ++i) {
         const int c = tid + i * 256, n = c / KCH, kk = (c % KCH) * 8;
         const int gn = n0 + n, k = k0 + kk;
-        rb[i] = (gn < p.N && k < p.K) ? ldg16(p.W + (size_t)gn * p.K + k) : make_uint4(0, 0, 0, 0);
+        rb[i] = bld16(rW, boff(valid && gn < p.N && k < p.K, (size_t)gn * p.K + k));
       }
     }
   };
@@ -192,13 +196,13 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
 #pragma unroll
     for (int c = 0; c < CTW; ++c) acc[r][c] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  load(0);
+  load(0, true);
   __syncthreads();   // Ps staged
   write(0, 0);
   __syncthreads();
   for (int ks = 0; ks < nk; ++ks) {
     const int buf = ks & 1;
-    if (ks + 1 < nk) load((ks + 1) * KSTEP);
+    load((ks + 1) * KSTEP, ks + 1 < nk);
     const bf16_t *Ab = As + buf * BM * kLDK;
     const bf16_t *Bb = Bs + buf * BN * kLDK;
 #pragma unroll
