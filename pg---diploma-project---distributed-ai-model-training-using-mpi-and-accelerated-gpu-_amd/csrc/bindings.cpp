@@ -32,6 +32,8 @@ void launch_adam_flat(float *, const float *, float *, float *, bf16_t *, long l
                       float, float, float, float, float, hipStream_t);
 void launch_f32_to_bf16(const float *, bf16_t *, long long, hipStream_t);
 int dw_fwd_num_partials(int, int, int, int, int);
+int bn_rep();
+void bn_set_rep(int rep);
 int dw_dgrad_num_partials(int, int, int, int, int);
 int dw_wgrad_num_partials(int, int, int, int, int);
 void launch_dw_fwd(const bf16_t *, const float *, const float *, int, const bf16_t *, bf16_t *,
@@ -155,6 +157,8 @@ PYBIND11_MODULE(_pgdist_C, m) {
   });
   // ---- depthwise ----
   m.def("dw_fwd_num_partials", &dw_fwd_num_partials);
+  m.def("bn_rep", &bn_rep, "replica rows of the atomic BN-statistics accumulators");
+  m.def("bn_set_rep", &bn_set_rep, "set the replica rows (large = one row per workgroup: deterministic)");
   m.def("dw_dgrad_num_partials", &dw_dgrad_num_partials);
   m.def("dw_wgrad_num_partials", &dw_wgrad_num_partials);
   m.def("dw_fwd", [](P x, P is, P it, int act, P w, P y, P part, int B, int H, int W, int C,

@@ -147,4 +147,22 @@ PG_DEVICE void bst16(rsrc_t r, uint32_t off, const uint4 &v) {
 // byte offset of element i of a bf16 tensor, or kOOB
 PG_DEVICE uint32_t boff(bool ok, size_t i) { return ok ? (uint32_t)(i * 2) : kOOB; }
 
+// ---------------------------------------------------------------------------
+// BatchNorm statistics of the MobileNetV2 producers: every workgroup adds its per-channel
+// partial sums (sum, sum of squares | sum g, sum g*y) with float atomics into one of
+// kBnRep replica rows of a zeroed accumulator [rows][2][C] (rows = min(kBnRep, workgroup
+// partial rows)); the finalize then reduces rows <= kBnRep instead of one row per workgroup
+// (up to ~2k), and the accumulator of every BN of a step is zeroed by one memset.
+// Replicas (row % rep) spread the same-address atomics over separate lines.
+// The replica count is a launch argument taken from g_bn_rep (host): kBnRep by default, or
+// "unbounded" in deterministic mode (bn_set_rep), where every workgroup owns its row, adds to
+// zero exactly once, and the finalize sums the rows in a fixed order (bitwise reproducible).
+// ---------------------------------------------------------------------------
+constexpr int kBnRep = 8;
+extern int g_bn_rep;   // host: replica rows the launchers pass to the producers
+PG_DEVICE void bn_part_add(float *part, int row, int nrows, int rep, int C, int s, int c, float v) {
+  rep = nrows < rep ? nrows : rep;
+  atomicAdd(part + ((size_t)(row % rep) * 2 + s) * C + c, v);
+}
+
 #define PG_CHECK_LAUNCH() ((void)hipGetLastError())

@@ -10,6 +10,8 @@
 // (SURVEY.md §2.6 "BatchNorm2d (train)", §2.8).
 #include "../reduce.h"
 
+#include <stdexcept>
+
 // ---------------------------------------------------------------------------
 // Reduction of the [P][2][C] partials (one launch, reduce.h): grid (ceil(C/16) channel
 // blocks, nch row chunks), 256 threads = 32 columns ({sum, sumsq} x 16 channels) x 8
@@ -153,6 +155,13 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t *__restrict_
 // ---------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------
+int g_bn_rep = kBnRep;
+int bn_rep() { return g_bn_rep; }
+void bn_set_rep(int rep) {
+  if (rep < 1) throw std::invalid_argument("bn_set_rep: rep must be >= 1");
+  g_bn_rep = rep;
+}
+
 // part: [P][2][C] followed by the level-1 scratch (bn_part_floats(P, C) floats in total)
 long long bn_part_floats(int P, int C) {
   const int nch = red_nch(P, kBnMinRows);

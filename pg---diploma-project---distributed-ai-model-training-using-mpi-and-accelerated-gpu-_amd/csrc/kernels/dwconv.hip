@@ -35,6 +35,7 @@ struct DwGeom {
   int TWc;    // columns per workgroup
   int R;      // rows per workgroup
   int tiles_w, tiles_h;
+  int bn_rep;  // BN-statistics replica rows (g_bn_rep)
 };
 
 PG_DEVICE void unpack4(const uint2 &u, float (&f)[CPT]) {
@@ -69,6 +70,7 @@ struct Tile {
   int idx;     // tile index (partial row)
   int slab;    // channel slab
 };
+PG_DEVICE int dw_tiles(const DwGeom &g) { return g.B * g.tiles_h * g.tiles_w; }   // partial rows
 PG_DEVICE Tile tile_of(const DwGeom &g) {
   const int L = blockIdx.x;
   const int nslab = g.C / g.CC;
@@ -91,9 +93,12 @@ PG_DEVICE Tile tile_of(const DwGeom &g) {
 
 // Block-level reduction of per-thread [NV][CPT] channel partials of this workgroup's CC
 // channels into part[prow][NV][C] (columns cbase..cbase+CC); tid = col * C4 + c4.
+// nrows > 0 (BN statistics, NV == 2): accumulated atomically into replica row prow % rep
+// (bn_part_add); nrows == 0: plain store of row prow (weight-gradient split partials).
 template <int NV>
 PG_DEVICE void block_channel_partials(float (&acc)[NV][CPT], float *__restrict__ part, int C, int CC,
-                                      int cbase, int ncol, float *lds, int prow) {
+                                      int cbase, int ncol, float *lds, int prow, int nrows = 0,
+                                      int rep = 0) {
   const int tid = threadIdx.x;
   const int C4 = CC / CPT;
   const int c4 = tid % C4, col = tid / C4;
@@ -104,7 +109,8 @@ PG_DEVICE void block_channel_partials(float (&acc)[NV][CPT], float *__restrict__
     for (int c = tid; c < CC; c += blockDim.x) {
       float s = 0.f;
       for (int w = 0; w < ncol; ++w) s += lds[w * CC + c];
-      part[((size_t)prow * NV + v) * C + cbase + c] = s;
+      if (NV == 2 && nrows > 0) bn_part_add(part, prow, nrows, rep, C, v, cbase + c, s);
+      else part[((size_t)prow * NV + v) * C + cbase + c] = s;
     }
     __syncthreads();
   }
@@ -305,7 +311,7 @@ __global__ __launch_bounds__(256) void dw_fwd_lds_kernel(
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may still target the ring
   __syncthreads();
-  block_channel_partials<2>(stats, part, g.C, g.CC, cbase, g.TWc, red, tl.idx);
+  block_channel_partials<2>(stats, part, g.C, g.CC, cbase, g.TWc, red, tl.idx, dw_tiles(g), g.bn_rep);
 }
 
 // dgrad (stride 1): thread = one INPUT column, strip of input rows.  Streams per step k: the dy
@@ -447,7 +453,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_s1_lds_kernel(
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  block_channel_partials<2>(stats, part, g.C, g.CC, cbase, g.TWc, red, tl.idx);
+  block_channel_partials<2>(stats, part, g.C, g.CC, cbase, g.TWc, red, tl.idx, dw_tiles(g), g.bn_rep);
   if constexpr (WG) block_channel_partials<9>(accw, wpart, g.C, g.CC, cbase, g.TWc, red, tl.idx);
 }
 
@@ -631,7 +637,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_s2_lds_kernel(
       }
   }
   __syncthreads();
-  block_channel_partials<2>(stats, part, g.C, g.CC, cbase, g.TWc, red, tl.idx);
+  block_channel_partials<2>(stats, part, g.C, g.CC, cbase, g.TWc, red, tl.idx, dw_tiles(g), g.bn_rep);
   if constexpr (WG) block_channel_partials<9>(accw, wpart, g.C, g.CC, cbase, g.TWc, red, tl.idx);
 }
 
@@ -772,6 +778,7 @@ int dw_cc(int C) {
 // kind 0 = fwd (tiles over the output grid), 1 = dgrad (input grid), 2 = wgrad (output grid)
 DwGeom dw_geom(int kind, int B, int H, int W, int C, int stride) {
   DwGeom g;
+  g.bn_rep = g_bn_rep;
   g.B = B;
   g.H = H;
   g.W = W;

@@ -122,7 +122,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
     const bf16_t *__restrict__ y, const float *__restrict__ s, const float *__restrict__ t,
     const float *__restrict__ Wl, const float *__restrict__ dlogits, int HW, int C, int NC, float drop_p,
     unsigned long long seed, const float *__restrict__ hyper, bf16_t *__restrict__ g_out,
-    float *__restrict__ part) {
+    float *__restrict__ part, int rep) {
   __shared__ float r0[kSlots][kChunk + 4];
   __shared__ float r1[kSlots][kChunk + 4];
   const int b = blockIdx.x, tid = threadIdx.x, cl = tid & 31, slot = tid >> 5;
@@ -187,8 +187,8 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
       a0 += r0[k][tid];
       a1 += r1[k][tid];
     }
-    part[((size_t)b * 2 + 0) * C + c] = a0;
-    part[((size_t)b * 2 + 1) * C + c] = a1;
+    bn_part_add(part, b, gridDim.x, rep, C, 0, c, a0);
+    bn_part_add(part, b, gridDim.x, rep, C, 1, c, a1);
   }
 }
 
@@ -227,7 +227,7 @@ void launch_head(const bf16_t *y, const float *s, const float *t, const float *W
                      loss, correct, train ? dlogits : nullptr);
   if (!train) return;
   hipLaunchKernelGGL(head_bwd_kernel, grid2, dim3(256), 0, st, y, s, t, Wl, dlogits, HW, C, NC, drop_p, seed,
-                     hyper, g_out, part);
+                     hyper, g_out, part, g_bn_rep);
   hipLaunchKernelGGL(head_wgrad_kernel, dim3((NC * C + NC + 255) / 256), dim3(256), 0, st, dlogits, pd, B, C,
                      NC, dW, db);
 }

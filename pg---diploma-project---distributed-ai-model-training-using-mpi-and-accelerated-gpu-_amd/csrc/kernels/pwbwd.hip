@@ -42,6 +42,7 @@ struct PwBwdArgs {
   float *part;                  // [gx][2][Ng]
   float *wpart;                 // [gx][Kg][Ng]
   int M, Kg, Ng;
+  int bn_rep;                   // BN-statistics replica rows (g_bn_rep)
 };
 template <int KP, int BN, int BM>
 struct BwdLds {
@@ -349,7 +350,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
       float a = 0.f;
 #pragma unroll
       for (int g = 0; g < BM / 4; ++g) a += Red[g * BN + c];
-      if (n0 + c < p.Ng) p.part[((size_t)blockIdx.x * 2 + s) * p.Ng + n0 + c] = a;
+      if (n0 + c < p.Ng) bn_part_add(p.part, blockIdx.x, gridDim.x, p.bn_rep, p.Ng, s, n0 + c, a);
     }
     __syncthreads();
   }
@@ -421,7 +422,7 @@ void launch_pw_bwd(int epi, const bf16_t *G, const bf16_t *Y, const float *ca, c
                    float *grad, int M, int Kg, int Ng, hipStream_t st) {
   const BwdGeom g = bwd_geom(M, Kg, Ng);
   if (!g.ok) return;
-  PwBwdArgs a{G, Y, ca, cb, cc, WT, out, Yt, es, et, R, X, part, wpart, M, Kg, Ng};
+  PwBwdArgs a{G, Y, ca, cb, cc, WT, out, Yt, es, et, R, X, part, wpart, M, Kg, Ng, g_bn_rep};
   if (epi == EPI_BWD_RELU6_) launch_bwd_epi<EPI_BWD_RELU6_>(a, g, st);
   else launch_bwd_epi<EPI_BWD_LIN_>(a, g, st);
   // grad == nullptr: the caller reduces wpart itself (e.g. on its weight-gradient stream)

@@ -67,6 +67,7 @@ struct PwArgs {
   const float *wsc;
   float asc;
   int ldw8;
+  int bn_rep;           // BN-statistics replica rows (g_bn_rep)
 };
 }  // namespace
 
@@ -386,7 +387,7 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
     for (int c = tid; c < BN; c += 256) {
       float a = 0.f;
       for (int g = 0; g < RSTEP; ++g) a += Red[g * BN + c];
-      if (n0 + c < p.N) p.part[((size_t)blockIdx.x * 2 + s) * p.N + n0 + c] = a;
+      if (n0 + c < p.N) bn_part_add(p.part, blockIdx.x, gridDim.x, p.bn_rep, p.N, s, n0 + c, a);
     }
     __syncthreads();
   }
@@ -705,6 +706,7 @@ void launch_pw_gemm(int pro, int epi, const bf16_t *A, const bf16_t *A2, const f
                     const bf16_t *Yt, const float *es, const float *et, const bf16_t *R, float *part,
                     int M, int N, int K, bf16_t *Aout, hipStream_t st) {
   PwArgs a{A, A2, pa, pb, pc, W, out, Yt, es, et, R, part, M, N, K, Aout};
+  a.bn_rep = g_bn_rep;
   const PwGeom g = pw_geom(M, N, K, pro);
   if (g.bdirect) {
     launch_pw_tile(pro, epi, A, A2, pa, pb, pc, W, out, Yt, es, et, R, part, M, N, K, Aout, st);
@@ -735,7 +737,7 @@ void launch_pw_gemm_f8(int pro, const bf16_t *A, const float *pa, const float *p
     return;
   }
   PwArgs a{A, nullptr, pa, pb, nullptr, nullptr, out, nullptr, nullptr, nullptr, nullptr, part, M, N, K, nullptr,
-           W8, wsc, asc, ldw8};
+           W8, wsc, asc, ldw8, g_bn_rep};
   const int Kp = (K + 63) / 64 * 64;
   g.lds -= (size_t)g.BN * (Kp + kBPad) * 2;
   g.lds += (size_t)g.BN * (Kp + 16);

@@ -36,6 +36,7 @@ struct PwTArgs {
   const float *wsc;
   float asc;            // F8: the prologue output is scaled by asc before its e4m3 conversion
   int ldw8;
+  int bn_rep;           // BN-statistics replica rows (g_bn_rep)
 };
 }  // namespace
 
@@ -320,7 +321,7 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
     for (int c = tid; c < BN; c += 256) {
       float a = 0.f;
       for (int g = 0; g < RSTEP; ++g) a += Red[g * BN + c];
-      if (n0 + c < p.N) p.part[((size_t)mt * 2 + s) * p.N + n0 + c] = a;
+      if (n0 + c < p.N) bn_part_add(p.part, mt, nmt, p.bn_rep, p.N, s, n0 + c, a);
     }
     __syncthreads();
   }
@@ -382,6 +383,7 @@ void launch_pw_tile(int pro, int epi, const bf16_t *A, const bf16_t *A2, const f
                     const float *et, const bf16_t *R, float *part, int M, int N, int K, bf16_t *Aout,
                     hipStream_t st) {
   PwTArgs a{A, A2, pa, pb, pc, W, out, Yt, es, et, R, part, M, N, K, Aout};
+  a.bn_rep = g_bn_rep;
   const TileGeom g = tile_geom(M, N, K, pro);
 #define PT_CASE(P, E) \
   if (pro == P && epi == E) { launch_tile_pe<P, E>(a, g, st); return; }
@@ -398,7 +400,7 @@ void launch_pw_tile_f8(int pro, const bf16_t *A, const float *pa, const float *p
                        const float *wsc, float asc, bf16_t *out, float *part, int M, int N, int K,
                        hipStream_t st) {
   PwTArgs a{A, nullptr, pa, pb, nullptr, nullptr, out, nullptr, nullptr, nullptr, nullptr, part, M, N, K,
-            nullptr, W8, wsc, asc, ldw8};
+            nullptr, W8, wsc, asc, ldw8, g_bn_rep};
   TileGeom g = tile_geom(M, N, K, pro);   // the bf16 LDS size bounds the e4m3 one
   if (pro == ACT_NONE) launch_tile_pe<ACT_NONE, EPI_FWD_T, true>(a, g, st);
   else if (pro == ACT_BN_RELU6) launch_tile_pe<ACT_BN_RELU6, EPI_FWD_T, true>(a, g, st);

@@ -23,7 +23,7 @@ template <int kPx>
 __global__ __launch_bounds__(256) void stem_fwd_kernel(const bf16_t *__restrict__ img,
                                                       const bf16_t *__restrict__ w,  // [32][3][3][3]
                                                       bf16_t *__restrict__ y, float *__restrict__ part,
-                                                      int B, int H, int W, int Ho, int Wo) {
+                                                      int B, int H, int W, int Ho, int Wo, int rep) {
   // thread = (group of kPx output pixels, group of 8 output channels): 4 threads per pixel
   // group; each pair of LDS weight reads (8 channels of one input channel x tap) feeds the
   // kPx pixels; each thread stores one 16-B vector per pixel.
@@ -104,7 +104,7 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(const bf16_t *__restrict_
     if (tid < kCo) {
       float a = 0.f;
       for (int r = 0; r < 64; ++r) a += red[r][tid];
-      part[((size_t)blockIdx.x * 2 + s) * kCo + tid] = a;
+      bn_part_add(part, blockIdx.x, gridDim.x, rep, kCo, s, tid, a);
     }
     __syncthreads();
   }
@@ -125,9 +125,9 @@ bool launch_stem_fwd(const bf16_t *img, const bf16_t *w, bf16_t *y, float *part,
                      int W, int px, hipStream_t st) {
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
   const int grid = stem_fwd_num_partials(B, H, W);
-  if (px == 1) hipLaunchKernelGGL(stem_fwd_kernel<1>, dim3(grid), dim3(256), 0, st, img, w, y, part, B, H, W, Ho, Wo);
-  else if (px == 2) hipLaunchKernelGGL(stem_fwd_kernel<2>, dim3(grid), dim3(256), 0, st, img, w, y, part, B, H, W, Ho, Wo);
-  else if (px == 4) hipLaunchKernelGGL(stem_fwd_kernel<4>, dim3(grid), dim3(256), 0, st, img, w, y, part, B, H, W, Ho, Wo);
+  if (px == 1) hipLaunchKernelGGL(stem_fwd_kernel<1>, dim3(grid), dim3(256), 0, st, img, w, y, part, B, H, W, Ho, Wo, g_bn_rep);
+  else if (px == 2) hipLaunchKernelGGL(stem_fwd_kernel<2>, dim3(grid), dim3(256), 0, st, img, w, y, part, B, H, W, Ho, Wo, g_bn_rep);
+  else if (px == 4) hipLaunchKernelGGL(stem_fwd_kernel<4>, dim3(grid), dim3(256), 0, st, img, w, y, part, B, H, W, Ho, Wo, g_bn_rep);
   else return false;
   return true;
 }

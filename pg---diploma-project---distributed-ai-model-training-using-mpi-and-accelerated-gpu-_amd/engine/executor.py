@@ -54,6 +54,10 @@ class BNState:
         self.y = torch.empty(M, C, dtype=torch.bfloat16, device=device)   # pre-BN activation
         self.g = torch.empty(M, C, dtype=torch.bfloat16, device=device) if need_g else None
         self.param_names = [prefix + ".weight", prefix + ".bias"]
+        # atomic statistics accumulators [rows][2][C] of this BN's forward / backward producer
+        # (views into the executor's arena, zeroed once per training step)
+        self.acc_f: Optional[torch.Tensor] = None
+        self.acc_b: Optional[torch.Tensor] = None
 
     def finalize_fwd(self, part, P):
         K.bn_fwd_finalize(part, P, self.C, self.M, self.gamma, self.beta, self.eps, self.momentum,
@@ -81,6 +85,24 @@ class BNState:
     @property
     def c(self):
         return self.coef[2]
+
+
+class AtomicBNState(BNState):
+    """BN of the MobileNetV2 executor: its producers accumulate the statistics atomically into
+    min(P, bn_rep) replica rows of ``acc_f`` / ``acc_b`` (P = the producer's partial rows), so a
+    finalize reduces those rows only (deterministic mode: bn_rep unbounded, one row per
+    producer workgroup).  ``rows_f`` / ``rows_b``: rows the accumulators were sized for."""
+    rows_f = rows_b = 0
+
+    def finalize_fwd(self, part, P):
+        r = K.bn_rows(P)
+        assert r <= self.rows_f, f"{self.prefix}: forward producer has {r} rows > {self.rows_f} allocated"
+        super().finalize_fwd(part, r)
+
+    def finalize_bwd(self, part, P):
+        r = K.bn_rows(P)
+        assert r <= self.rows_b, f"{self.prefix}: backward producer has {r} rows > {self.rows_b} allocated"
+        super().finalize_bwd(part, r)
 
 
 @dataclass
@@ -132,8 +154,7 @@ class MobileNetV2Executor:
         H = (img_size - 1) // 2 + 1
         self.H0 = H
         self.stem_w = "features.0.0.weight"
-        self.bn0 = BNState(self.flat, feats[0][1], "features.0.1", B * H * H, feats[0][0].out_channels, device)
-        parts = [(K.stem_num_partials(B, img_size, img_size), 32)]   # (partial rows, channels)
+        self.bn0 = AtomicBNState(self.flat, feats[0][1], "features.0.1", B * H * H, feats[0][0].out_channels, device)
         wg = [K.stem_wgrad_workspace(B, img_size, img_size, 32)]   # side-stream weight gradients
         wparts = {}   # fused dgrad+wgrad: one split-M partial buffer per layer, reduced on the side stream
         # ---------------- blocks
@@ -147,7 +168,7 @@ class MobileNetV2Executor:
             Min, Mout = B * Hin * Hin, B * Ho * Ho
             expand = blk.expand_ratio != 1
             if expand:
-                bn_e = BNState(self.flat, blk.conv[0][1], f"{pre}.0.1", Min, blk.hidden, device)
+                bn_e = AtomicBNState(self.flat, blk.conv[0][1], f"{pre}.0.1", Min, blk.hidden, device)
                 dwm, w_e = blk.conv[1], f"{pre}.0.0.weight"
                 w_d, bn_d_pre = f"{pre}.1.0.weight", f"{pre}.1.1"
                 w_p, bn_p_mod, bn_p_pre = f"{pre}.2.weight", blk.conv[3], f"{pre}.3"
@@ -155,31 +176,23 @@ class MobileNetV2Executor:
                 bn_e, w_e, dwm = None, None, blk.conv[0]
                 w_d, bn_d_pre = f"{pre}.0.0.weight", f"{pre}.0.1"
                 w_p, bn_p_mod, bn_p_pre = f"{pre}.1.weight", blk.conv[2], f"{pre}.2"
-            bn_d = BNState(self.flat, dwm[1], bn_d_pre, Mout, blk.hidden, device)
-            bn_p = BNState(self.flat, bn_p_mod, bn_p_pre, Mout, blk.oup, device, need_g=False)
+            bn_d = AtomicBNState(self.flat, dwm[1], bn_d_pre, Mout, blk.hidden, device)
+            bn_p = AtomicBNState(self.flat, bn_p_mod, bn_p_pre, Mout, blk.oup, device, need_g=False)
             bp = BlockPlan(i, pre, blk.inp, blk.oup, blk.hidden, blk.stride, expand, blk.use_res_connect,
                            Hin, Hin, Ho, Ho, w_e, w_d, w_p, bn_e, bn_d, bn_p)
             bp.o = torch.empty(Mout, blk.oup, dtype=torch.bfloat16, device=device)
             bp.G = torch.empty(Mout, blk.oup, dtype=torch.bfloat16, device=device)
             self.blocks.append(bp)
             if expand:
-                parts.append((K.pw_num_partials(Min, blk.hidden, blk.inp), blk.hidden))        # fwd expand
-                parts.append((K.pw_num_partials(Min, blk.inp, blk.hidden), blk.inp))               # bwd expand dgrad
                 wg.append(K.pw_wgrad_workspace(Min, blk.hidden, blk.inp))
                 if K.pw_bwd_supported(Min, blk.hidden, blk.inp):
-                    parts.append((K.pw_bwd_num_partials(Min, blk.hidden, blk.inp), blk.inp))
                     wparts[(i, "e")] = K.pw_bwd_wgrad_workspace(Min, blk.hidden, blk.inp)
-            parts.append((K.dw_num_partials("fwd", B, Hin, Hin, blk.hidden, blk.stride), blk.hidden))
-            parts.append((K.dw_num_partials("dgrad", B, Hin, Hin, blk.hidden, blk.stride), blk.hidden))
             if Hin >= self.DW_FUSE_MIN_H:
                 wparts[(i, "d")] = K.dw_dgrad_wgrad_workspace(B, Hin, Hin, blk.hidden, blk.stride)
             else:
                 wg.append(K.dw_wgrad_workspace(B, Hin, Hin, blk.hidden, blk.stride))
-            parts.append((K.pw_num_partials(Mout, blk.oup, blk.hidden), blk.oup))                 # fwd project
-            parts.append((K.pw_num_partials(Mout, blk.hidden, blk.oup), blk.hidden))           # bwd project dgrad
             wg.append(K.pw_wgrad_workspace(Mout, blk.oup, blk.hidden))
             if K.pw_bwd_supported(Mout, blk.oup, blk.hidden):
-                parts.append((K.pw_bwd_num_partials(Mout, blk.oup, blk.hidden), blk.hidden))
                 wparts[(i, "p")] = K.pw_bwd_wgrad_workspace(Mout, blk.oup, blk.hidden)
             cur_h = Ho
         # ---------------- final 1x1 conv + head
@@ -189,10 +202,7 @@ class MobileNetV2Executor:
         self.C_last_in = self.blocks[-1].cout
         self.C_last = last[0].out_channels
         self.w_last = f"features.{len(feats) - 1}.0.weight"
-        self.bn_last = BNState(self.flat, last[1], f"features.{len(feats) - 1}.1", Mf, self.C_last, device)
-        parts.append((K.pw_num_partials(Mf, self.C_last, self.C_last_in), self.C_last))
-        parts.append((K.pw_num_partials(Mf, self.C_last_in, self.C_last), self.C_last_in))
-        parts.append((B, self.C_last))
+        self.bn_last = AtomicBNState(self.flat, last[1], f"features.{len(feats) - 1}.1", Mf, self.C_last, device)
         wg.append(K.pw_wgrad_workspace(Mf, self.C_last, self.C_last_in))
         self.NC = model.classifier[1].out_features
         self.w_lin, self.b_lin = "classifier.1.weight", "classifier.1.bias"
@@ -203,7 +213,20 @@ class MobileNetV2Executor:
         self.dlogits = torch.zeros(B, self.NC, **f32)
         self.pd = torch.zeros(B, self.C_last, **f32)
         # ---------------- workspaces (stream-ordered reuse)
-        self.ws_part = torch.zeros(max(K.bn_part_floats(P, C) for P, C in parts) + 1024, **f32)
+        # BN statistics: one accumulator pair per BN ([rows][2][C] forward and backward, rows =
+        # min(producer partial rows, bn_rep)), all in one arena so a training step zeroes them
+        # with a single memset
+        o, spans = 0, []
+        self.bn_rep = K.bn_rep()   # the producers' replica rows the arena is sized for
+        for bn, (pf, pb) in self._bn_producer_rows().items():
+            bn.rows_f, bn.rows_b = K.bn_rows(pf), K.bn_rows(pb)
+            nf, nb = K.bn_part_floats(bn.rows_f, bn.C), K.bn_part_floats(bn.rows_b, bn.C)
+            spans.append((bn, o, nf, nb))
+            o += (nf + nb + 63) // 64 * 64
+        self.bn_arena = torch.zeros(o + 64, **f32)
+        for bn, o, nf, nb in spans:
+            bn.acc_f = self.bn_arena[o:o + nf]
+            bn.acc_b = self.bn_arena[o + nf:o + nf + nb]
         self.ws_wgrad = torch.zeros(max(wg) + 1024, **f32)
         # the stem weight gradient may run on the main stream concurrently with side-stream
         # weight gradients: its own split-M workspace
@@ -249,6 +272,41 @@ class MobileNetV2Executor:
                 self.w8[name] = (self.w8_buf[d0:d0 + n * K.fp8_pitch(k)], self.w8_scale[c0:c0 + n])
 
     # ------------------------------------------------------------------ helpers
+    def _bn_producer_rows(self):
+        """{bn: (forward P, backward P)}: partial rows of the kernels that produce each BN's
+        statistics, in the order forward()/backward() launch them (the finalize asserts the
+        launched P fits)."""
+        B, S = self.B, self.S
+        rows = {bn: [1, 1] for bn in self.all_bns()}
+        rows[self.bn0][0] = K.stem_num_partials(B, S, S)
+        for bi, bp in enumerate(self.blocks):
+            prev = self.blocks[bi - 1] if bi > 0 else None
+            Min, Mout = B * bp.H * bp.H, B * bp.Ho * bp.Wo
+            dw_in = bp.bn_e if bp.expand else self.bn0
+            if bp.expand:
+                rows[bp.bn_e][0] = K.pw_num_partials(Min, bp.hidden, bp.cin)
+                rows[prev.bn_p][1] = (K.pw_bwd_num_partials(Min, bp.hidden, bp.cin)
+                                      if K.pw_bwd_supported(Min, bp.hidden, bp.cin)
+                                      else K.pw_num_partials(Min, bp.cin, bp.hidden))
+            rows[bp.bn_d][0] = K.dw_num_partials("fwd", B, bp.H, bp.H, bp.hidden, bp.stride)
+            rows[dw_in][1] = K.dw_num_partials("dgrad", B, bp.H, bp.H, bp.hidden, bp.stride)
+            rows[bp.bn_p][0] = K.pw_num_partials(Mout, bp.cout, bp.hidden)
+            rows[bp.bn_d][1] = (K.pw_bwd_num_partials(Mout, bp.cout, bp.hidden)
+                                if K.pw_bwd_supported(Mout, bp.cout, bp.hidden)
+                                else K.pw_num_partials(Mout, bp.hidden, bp.cout))
+        Mf = B * self.Hf * self.Hf
+        rows[self.bn_last][0] = K.pw_num_partials(Mf, self.C_last, self.C_last_in)
+        rows[self.bn_last][1] = B
+        rows[self.blocks[-1].bn_p][1] = K.pw_num_partials(Mf, self.C_last_in, self.C_last)
+        return {bn: tuple(r) for bn, r in rows.items()}
+
+    def _check_bn_mode(self):
+        # the producers write min(P, bn_rep()) rows: a mode switch after construction would
+        # overrun the accumulators sized here
+        if K.bn_rep() != self.bn_rep:
+            raise RuntimeError(f"BN replica rows changed from {self.bn_rep} to {K.bn_rep()} after the executor "
+                               "was built (ops.kernels.set_deterministic before building it)")
+
     def _ready(self, names):
         """Gradients of ``names`` are final once the work enqueued so far completes.  With a
         side stream the callback (DDP bucket launch) runs on it after it has joined the main
@@ -291,17 +349,19 @@ class MobileNetV2Executor:
 
     def _fin_fwd(self, bn: BNState, P: int, train: bool):
         if train:
-            bn.finalize_fwd(self.ws_part, P)
+            bn.finalize_fwd(bn.acc_f, P)
 
     # ------------------------------------------------------------------ forward
     def forward(self, train: bool = True):
         """Runs the forward pass on ``self.img`` (and, when training, the head backward)."""
         f, B, S = self.flat, self.B, self.S
-        ws = self.ws_part
+        self._check_bn_mode()
+        if train:
+            self.bn_arena.zero_()   # every BN statistics accumulator of this step
         if self.fp8:
             K.w8_quant(f.master, self.w8_buf, self.w8_scale, self.w8_tab, self.w8_tab.shape[0])
         # stem
-        K.stem_fwd(self.img, f.b(self.stem_w), self.bn0.y, ws, B, S, S)
+        K.stem_fwd(self.img, f.b(self.stem_w), self.bn0.y, self.bn0.acc_f, B, S, S)
         self._fin_fwd(self.bn0, K.stem_num_partials(B, S, S), train)
         inp_bn, inp_t = self.bn0, None   # block input: virtual relu6(bn0(y0))
         # A block output o = BN_p(y_p) (+ residual) is not materialised by a separate pass: its
@@ -313,22 +373,22 @@ class MobileNetV2Executor:
             Min = B * Hin * Hin
             if bp.expand:
                 if pend is not None:
-                    self._consume_output(pend, f.b(bp.w_e), bp.bn_e.y, ws, Min, bp.hidden, bp.cin)
+                    self._consume_output(pend, f.b(bp.w_e), bp.bn_e.y, bp.bn_e.acc_f, Min, bp.hidden, bp.cin)
                 elif inp_t is None:
-                    self._pw_fwd(K.ACT_BN_RELU6, inp_bn.y, bp.w_e, bp.bn_e.y, ws, Min, bp.hidden, bp.cin,
+                    self._pw_fwd(K.ACT_BN_RELU6, inp_bn.y, bp.w_e, bp.bn_e.y, bp.bn_e.acc_f, Min, bp.hidden, bp.cin,
                                  pa=inp_bn.scale, pb=inp_bn.shift)
                 else:
-                    self._pw_fwd(K.ACT_NONE, inp_t, bp.w_e, bp.bn_e.y, ws, Min, bp.hidden, bp.cin)
+                    self._pw_fwd(K.ACT_NONE, inp_t, bp.w_e, bp.bn_e.y, bp.bn_e.acc_f, Min, bp.hidden, bp.cin)
                 self._fin_fwd(bp.bn_e, K.pw_num_partials(Min, bp.hidden, bp.cin), train)
                 dw_in = bp.bn_e
             else:
                 assert inp_t is None and pend is None, "t=1 block expects the (virtual) stem output"
                 dw_in = inp_bn
-            K.dw_fwd(dw_in.y, dw_in.scale, dw_in.shift, K.ACT_BN_RELU6, f.b(bp.w_d), bp.bn_d.y, ws, B, Hin, Hin,
+            K.dw_fwd(dw_in.y, dw_in.scale, dw_in.shift, K.ACT_BN_RELU6, f.b(bp.w_d), bp.bn_d.y, bp.bn_d.acc_f, B, Hin, Hin,
                      bp.hidden, bp.stride)
             self._fin_fwd(bp.bn_d, K.dw_num_partials("fwd", B, Hin, Hin, bp.hidden, bp.stride), train)
             Mout = B * bp.Ho * bp.Wo
-            self._pw_fwd(K.ACT_BN_RELU6, bp.bn_d.y, bp.w_p, bp.bn_p.y, ws, Mout, bp.cout, bp.hidden,
+            self._pw_fwd(K.ACT_BN_RELU6, bp.bn_d.y, bp.w_p, bp.bn_p.y, bp.bn_p.acc_f, Mout, bp.cout, bp.hidden,
                          pa=bp.bn_d.scale, pb=bp.bn_d.shift)
             self._fin_fwd(bp.bn_p, K.pw_num_partials(Mout, bp.cout, bp.hidden), train)
             if self.FUSE_BLOCK_OUTPUT and not self.fp8:
@@ -340,36 +400,40 @@ class MobileNetV2Executor:
         # final 1x1 conv (materialises the last block output o_17)
         Mf = B * self.Hf * self.Hf
         if pend is not None:
-            self._consume_output(pend, f.b(self.w_last), self.bn_last.y, ws, Mf, self.C_last, self.C_last_in)
+            self._consume_output(pend, f.b(self.w_last), self.bn_last.y, self.bn_last.acc_f, Mf, self.C_last,
+                                 self.C_last_in)
         else:
-            self._pw_fwd(K.ACT_NONE, inp_t, self.w_last, self.bn_last.y, ws, Mf, self.C_last, self.C_last_in)
+            self._pw_fwd(K.ACT_NONE, inp_t, self.w_last, self.bn_last.y, self.bn_last.acc_f, Mf, self.C_last,
+                         self.C_last_in)
         self._fin_fwd(self.bn_last, K.pw_num_partials(Mf, self.C_last, self.C_last_in), train)
         # head (+ its backward when training)
         K.head(self.bn_last.y, self.bn_last.scale, self.bn_last.shift, f.w(self.w_lin), f.w(self.b_lin),
                self.labels, B, self.Hf * self.Hf, self.C_last, self.NC, self.drop_p, self.dropout_seed,
                self.hyper, train, 1.0 / B, logits=self.logits, loss=self.loss, correct=self.correct,
                dlogits=self.dlogits if train else None, pd=self.pd,
-               g_out=self.bn_last.g if train else None, part=ws if train else None,
+               g_out=self.bn_last.g if train else None, part=self.bn_last.acc_b if train else None,
                dW=f.g(self.w_lin) if train else None, db=f.g(self.b_lin) if train else None)
 
     # ------------------------------------------------------------------ backward
     def backward(self):
         f, B, S = self.flat, self.B, self.S
-        ws, wg = self.ws_part, self.ws_wgrad
+        self._check_bn_mode()
+        wg = self.ws_wgrad
         # transposed 1x1 weights for the dgrad GEMMs (one batched launch)
         K.wt_transpose(f.shadow, f.shadow_t, self.wt_tab, self.wt_n)
         self._ready([self.w_lin, self.b_lin])
         # BN of the final conv (g produced by the head kernel)
         bnl = self.bn_last
-        bnl.finalize_bwd(ws, B)
+        bnl.finalize_bwd(bnl.acc_b, B)
         self._ready(bnl.param_names)
         Mf = B * self.Hf * self.Hf
         last_blk = self.blocks[-1]
         # dgrad of the final conv -> gradient w.r.t. o_17 (feeds BN_p of block 17, linear)
-        K.pw_gemm(K.PRO_BNBWD, K.EPI_BWD_LIN, bnl.g, f.bt(self.w_last), last_blk.G, ws, Mf, self.C_last_in,
+        K.pw_gemm(K.PRO_BNBWD, K.EPI_BWD_LIN, bnl.g, f.bt(self.w_last), last_blk.G, last_blk.bn_p.acc_b, Mf,
+                  self.C_last_in,
                   self.C_last, A2=bnl.y, pa=bnl.a, pb=bnl.b, pc=bnl.c, Yt=last_blk.bn_p.y, R=None)
         P_g = K.pw_num_partials(Mf, self.C_last_in, self.C_last)
-        last_blk.bn_p.finalize_bwd(ws, P_g)
+        last_blk.bn_p.finalize_bwd(last_blk.bn_p.acc_b, P_g)
         self._wgrad(lambda: K.pw_wgrad(bnl.g, bnl.y, bnl.a, bnl.b, bnl.c, last_blk.o, None, None, K.ACT_NONE,
                                        wg, f.g(self.w_last), Mf, self.C_last, self.C_last_in))
         self._ready([self.w_last] + last_blk.bn_p.param_names)
@@ -385,15 +449,15 @@ class MobileNetV2Executor:
             if K.pw_bwd_supported(Mout, bp.cout, bp.hidden):
                 # fused dgrad + wgrad (x = relu6(BN_d(y_d)) rebuilt from the mask operand)
                 wpm = self._wpart[(bp.idx, "p")]
-                K.pw_bwd(K.EPI_BWD_RELU6, bp.G, bnp.y, bnp.a, bnp.b, bnp.c, f.bt(bp.w_p), bnd.g, bnd.y, ws, wpm,
+                K.pw_bwd(K.EPI_BWD_RELU6, bp.G, bnp.y, bnp.a, bnp.b, bnp.c, f.bt(bp.w_p), bnd.g, bnd.y, bnd.acc_b, wpm,
                          None, Mout, bp.cout, bp.hidden, es=bnd.scale, et=bnd.shift)
                 self._wgrad(lambda: K.wgrad_reduce(wpm, K.pw_bwd_num_partials(Mout, bp.cout, bp.hidden),
                                                    bp.cout * bp.hidden, f.g(bp.w_p)))
-                bnd.finalize_bwd(ws, K.pw_bwd_num_partials(Mout, bp.cout, bp.hidden))
+                bnd.finalize_bwd(bnd.acc_b, K.pw_bwd_num_partials(Mout, bp.cout, bp.hidden))
             else:
-                K.pw_gemm(K.PRO_BNBWD, K.EPI_BWD_RELU6, bp.G, f.bt(bp.w_p), bnd.g, ws, Mout, bp.hidden, bp.cout,
+                K.pw_gemm(K.PRO_BNBWD, K.EPI_BWD_RELU6, bp.G, f.bt(bp.w_p), bnd.g, bnd.acc_b, Mout, bp.hidden, bp.cout,
                           A2=bnp.y, pa=bnp.a, pb=bnp.b, pc=bnp.c, Yt=bnd.y, es=bnd.scale, et=bnd.shift)
-                bnd.finalize_bwd(ws, K.pw_num_partials(Mout, bp.hidden, bp.cout))
+                bnd.finalize_bwd(bnd.acc_b, K.pw_num_partials(Mout, bp.hidden, bp.cout))
                 # project wgrad
                 self._wgrad(lambda: K.pw_wgrad(bp.G, bnp.y, bnp.a, bnp.b, bnp.c, bnd.y, bnd.scale, bnd.shift,
                                                K.ACT_BN_RELU6, wg, f.g(bp.w_p), Mout, bp.cout, bp.hidden))
@@ -405,15 +469,17 @@ class MobileNetV2Executor:
             if wpd is not None:
                 # large maps (bandwidth-bound): fused dgrad + wgrad, one pass over (g, y, yprev);
                 # the wgrad partials are reduced on the side stream
-                K.dw_dgrad(bnd.g, bnd.y, bnd.coef, f.b(bp.w_d), dw_in.y, dw_in.scale, dw_in.shift, dw_in.g, ws,
+                K.dw_dgrad(bnd.g, bnd.y, bnd.coef, f.b(bp.w_d), dw_in.y, dw_in.scale, dw_in.shift, dw_in.g,
+                           dw_in.acc_b,
                            B, Hin, Hin, bp.hidden, bp.stride, wpart=wpd)
-                dw_in.finalize_bwd(ws, Pd)
+                dw_in.finalize_bwd(dw_in.acc_b, Pd)
                 self._wgrad(lambda: K.wgrad_reduce(wpd, Pd, 9 * bp.hidden, f.g(bp.w_d)))
             else:
                 # small maps (latency-bound): lean dgrad on the critical path, wgrad on the side stream
-                K.dw_dgrad(bnd.g, bnd.y, bnd.coef, f.b(bp.w_d), dw_in.y, dw_in.scale, dw_in.shift, dw_in.g, ws,
+                K.dw_dgrad(bnd.g, bnd.y, bnd.coef, f.b(bp.w_d), dw_in.y, dw_in.scale, dw_in.shift, dw_in.g,
+                           dw_in.acc_b,
                            B, Hin, Hin, bp.hidden, bp.stride)
-                dw_in.finalize_bwd(ws, Pd)
+                dw_in.finalize_bwd(dw_in.acc_b, Pd)
                 self._wgrad(lambda: K.dw_wgrad(bnd.g, bnd.y, bnd.coef, dw_in.y, dw_in.scale, dw_in.shift, wg,
                                                f.g(bp.w_d), B, Hin, Hin, bp.hidden, bp.stride))
             self._ready([bp.w_d] + dw_in.param_names)
@@ -424,16 +490,17 @@ class MobileNetV2Executor:
                 if K.pw_bwd_supported(Min, bp.hidden, bp.cin):
                     wpe = self._wpart[(bp.idx, "e")]
                     K.pw_bwd(K.EPI_BWD_LIN, bne.g, bne.y, bne.a, bne.b, bne.c, f.bt(bp.w_e), prev.G, prev.bn_p.y,
-                             ws, wpe, None, Min, bp.hidden, bp.cin, R=bp.G if bp.residual else None,
+                             prev.bn_p.acc_b, wpe, None, Min, bp.hidden, bp.cin, R=bp.G if bp.residual else None,
                              X=prev.o)
                     self._wgrad(lambda: K.wgrad_reduce(wpe, K.pw_bwd_num_partials(Min, bp.hidden, bp.cin),
                                                        bp.hidden * bp.cin, f.g(bp.w_e)))
-                    prev.bn_p.finalize_bwd(ws, K.pw_bwd_num_partials(Min, bp.hidden, bp.cin))
+                    prev.bn_p.finalize_bwd(prev.bn_p.acc_b, K.pw_bwd_num_partials(Min, bp.hidden, bp.cin))
                 else:
-                    K.pw_gemm(K.PRO_BNBWD, K.EPI_BWD_LIN, bne.g, f.bt(bp.w_e), prev.G, ws, Min, bp.cin, bp.hidden,
+                    K.pw_gemm(K.PRO_BNBWD, K.EPI_BWD_LIN, bne.g, f.bt(bp.w_e), prev.G, prev.bn_p.acc_b, Min, bp.cin,
+                              bp.hidden,
                               A2=bne.y, pa=bne.a, pb=bne.b, pc=bne.c, Yt=prev.bn_p.y,
                               R=bp.G if bp.residual else None)
-                    prev.bn_p.finalize_bwd(ws, K.pw_num_partials(Min, bp.cin, bp.hidden))
+                    prev.bn_p.finalize_bwd(prev.bn_p.acc_b, K.pw_num_partials(Min, bp.cin, bp.hidden))
                     self._wgrad(lambda: K.pw_wgrad(bne.g, bne.y, bne.a, bne.b, bne.c, prev.o, None, None,
                                                    K.ACT_NONE, wg, f.g(bp.w_e), Min, bp.hidden, bp.cin))
                 self._ready([bp.w_e] + prev.bn_p.param_names)

@@ -29,6 +29,8 @@ def lib():
             raise RuntimeError(
                 "pgdist native library _pgdist_C is not built; run `python -m pgdist._build` "
                 "(or __graft_entry__.build())") from e
+    if os.environ.get("PGDIST_DETERMINISTIC", "0") == "1":
+        _LIB.bn_set_rep(1 << 30)   # ops.kernels.set_deterministic(True)
     return _LIB
 
 

@@ -54,6 +54,34 @@ def register_side_stream(stream):
     lib().register_side_stream(stream.cuda_stream)
 
 
+BN_REP_DETERMINISTIC = 1 << 30   # > any producer's partial rows: one row per workgroup
+
+
+def bn_rep():
+    """Replica rows of the atomic BN-statistics accumulators of the MobileNetV2 producers."""
+    return lib().bn_rep()
+
+
+def set_deterministic(on: bool = True):
+    """Bitwise run-to-run reproducible BN statistics.  By default the producers add their
+    per-workgroup partial sums into ``bn_rep()`` (8) replica rows with float atomics, whose
+    order varies between runs (a few ulp, which a deep net at a tiny batch can amplify);
+    deterministic mode gives every workgroup its own row and the finalize sums the rows in a
+    fixed order (slightly slower: more rows to reduce, larger accumulators).  Affects
+    executors built afterwards (their accumulators are sized for the mode)."""
+    lib().bn_set_rep(BN_REP_DETERMINISTIC if on else 8)
+
+
+def deterministic() -> bool:
+    return bn_rep() >= BN_REP_DETERMINISTIC
+
+
+def bn_rows(P):
+    """Rows a BN finalize reduces after a producer with P partial rows accumulated atomically
+    (rows = min(P, bn_rep()); the accumulator must be zeroed before the producer runs)."""
+    return min(int(P), bn_rep())
+
+
 def bn_part_floats(P, C):
     """Workspace a BN finalize over P partial rows needs ([P][2][C] + level-1 fold scratch)."""
     return lib().bn_part_floats(P, C)
@@ -135,7 +163,7 @@ def dw_fwd(x, in_s, in_t, act, w, y, part, B, H, W, C, stride):
     _chk(x, BF16, B * H * W * C, "x")
     _chk(w, BF16, C * 9, "w")
     _chk(y, BF16, B * Ho * Wo * C, "y")
-    _chk(part, F32, dw_num_partials("fwd", B, H, W, C, stride) * 2 * C, "part")
+    _chk(part, F32, bn_rows(dw_num_partials("fwd", B, H, W, C, stride)) * 2 * C, "part")
     lib().dw_fwd(_p(x), _p(in_s), _p(in_t), int(act), _p(w), _p(y), _p(part), B, H, W, C, stride, _s())
 
 
@@ -154,7 +182,7 @@ def dw_dgrad(g, yself, coef, w, yprev, ps, pt, gout, part, B, H, W, C, stride, w
     _chk(yself, BF16, B * Ho * Wo * C, "yself")
     _chk(yprev, BF16, B * H * W * C, "yprev")
     _chk(gout, BF16, B * H * W * C, "gout")
-    _chk(part, F32, dw_num_partials("dgrad", B, H, W, C, stride) * 2 * C, "part")
+    _chk(part, F32, bn_rows(dw_num_partials("dgrad", B, H, W, C, stride)) * 2 * C, "part")
     _chk(wpart, F32, dw_dgrad_wgrad_workspace(B, H, W, C, stride), "wpart")
     lib().dw_dgrad(_p(g), _p(yself), _p(coef), _p(w), _p(yprev), _p(ps), _p(pt), _p(gout), _p(part),
                    B, H, W, C, stride, _p(wpart), _s())
@@ -195,7 +223,7 @@ def pw_gemm(pro, epi, A, W, out, part, M, N, K, A2=None, pa=None, pb=None, pc=No
     _chk(out, BF16, M * N, "out")
     _chk(Yt, BF16, M * N, "Yt")
     _chk(R, BF16, M * N, "R")
-    _chk(part, F32, pw_num_partials(M, N, K) * 2 * N, "part")
+    _chk(part, F32, bn_rows(pw_num_partials(M, N, K)) * 2 * N, "part")
     if pro in (ACT_BN_RELU6, ACT_BN, PRO_BNBWD, PRO_BNRES):
         assert pa is not None and pb is not None and pa.numel() >= K
     if pro == PRO_BNBWD:
@@ -241,7 +269,7 @@ def pw_gemm_f8(pro, A, W8, wsc, out, part, M, N, K, pa=None, pb=None, asc=None):
     _chk(W8, FP8, N * ld, "W8")
     _chk(wsc, F32, N, "wsc")
     _chk(out, BF16, M * N, "out")
-    _chk(part, F32, pw_num_partials(M, N, K) * 2 * N, "part")
+    _chk(part, F32, bn_rows(pw_num_partials(M, N, K)) * 2 * N, "part")
     if pro != ACT_NONE:
         assert pa is not None and pb is not None and pa.numel() >= K
     a = float(FP8_ASC[pro] if asc is None else asc)
@@ -299,7 +327,7 @@ def pw_bwd(epi, G, Y, ca, cb, cc, WT, out, Yt, part, wpart, grad, M, Kg, Ng, es=
     _chk(Yt, BF16, M * Ng, "Yt")
     _chk(R, BF16, M * Ng, "R")
     _chk(X, BF16, M * Ng, "X")
-    _chk(part, F32, pw_bwd_num_partials(M, Kg, Ng) * 2 * Ng, "part")
+    _chk(part, F32, bn_rows(pw_bwd_num_partials(M, Kg, Ng)) * 2 * Ng, "part")
     _chk(wpart, F32, pw_bwd_wgrad_workspace(M, Kg, Ng), "wpart")
     _chk(grad, F32, Kg * Ng, "grad")   # grad=None: reduce wpart later with wgrad_reduce()
     for t, nm in ((ca, "ca"), (cb, "cb"), (cc, "cc")):
@@ -357,7 +385,7 @@ def stem_fwd(img, w, y, part, B, H, W, px=None):
     _chk(img, BF16, B * H * W * 4, "img")
     _chk(w, BF16, 32 * 27, "w")
     _chk(y, BF16, B * Ho * Wo * 32, "y")
-    _chk(part, F32, stem_num_partials(B, H, W) * 2 * 32, "part")
+    _chk(part, F32, bn_rows(stem_num_partials(B, H, W)) * 2 * 32, "part")
     lib().stem_fwd(_p(img), _p(w), _p(y), _p(part), B, H, W, px, _s())
 
 
@@ -392,7 +420,7 @@ def head(y, s, t, Wl, bl, labels, B, HW, C, NC, drop_p, seed, hyper, train, loss
             if t_ is None:
                 raise ValueError(f"head(train=True) needs {n}")
         _chk(g_out, BF16, B * HW * C, "g_out")
-        _chk(part, F32, B * 2 * C, "part")
+        _chk(part, F32, bn_rows(B) * 2 * C, "part")
     if labels is not None:
         _chk(labels, torch.int64, B, "labels")
     lib().head(_p(y), _p(s), _p(t), _p(Wl), _p(bl), _p(labels), B, HW, C, NC, float(drop_p),

@@ -60,6 +60,8 @@ def _grad_worker(rank, world, port, q):
     import pgdist  # noqa: F401
     from pgdist.models import build_model
     from pgdist.engine.native_step import NativeTrainStep
+    from pgdist.ops import kernels as K
+    K.set_deterministic(True)   # the shard-sum comparison needs bitwise-reproducible BN statistics
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)

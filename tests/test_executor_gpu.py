@@ -157,8 +157,48 @@ def test_native_train_step_fp8_loss_decreases(dev):
     assert losses[-1] < losses[0] * 0.5, losses
 
 
+@pytest.fixture
+def deterministic():
+    from pgdist.ops import kernels as K
+    K.set_deterministic(True)
+    yield
+    K.set_deterministic(False)
+
+
+def _one_step_grad(dev, B=8, S=64):
+    from pgdist.engine.native_step import NativeTrainStep
+    src = torch.randint(0, 256, (32, 32, 32, 3), dtype=torch.uint8, device=dev,
+                        generator=torch.Generator(device=dev).manual_seed(7))
+    labels = torch.randint(0, 10, (32,), device=dev, generator=torch.Generator(device=dev).manual_seed(8))
+    torch.manual_seed(100)
+    st = NativeTrainStep(mobilenet_v2(10), B, dev, img_size=S, lr=1e-3, use_graph=False)
+    st.set_data(src, labels)
+    st.run(torch.arange(B, device=dev))
+    torch.cuda.synchronize()
+    return st.flat.grad.clone()
+
+
+def test_deterministic_mode_is_bitwise_reproducible(dev, deterministic):
+    """Deterministic mode (one BN-statistics row per producer workgroup, fixed-order finalize):
+    two identical training steps give bitwise identical gradients."""
+    g0, g1 = _one_step_grad(dev), _one_step_grad(dev)
+    assert torch.equal(g0, g1)
+
+
+def test_bn_mode_switch_after_build_rejected(dev):
+    from pgdist.ops import kernels as K
+    from pgdist.engine.executor import MobileNetV2Executor
+    exe = MobileNetV2Executor(mobilenet_v2(10), 2, 32, dev)
+    K.set_deterministic(True)
+    try:
+        with pytest.raises(RuntimeError, match="replica rows"):
+            exe.forward(train=True)
+    finally:
+        K.set_deterministic(False)
+
+
 @pytest.mark.parametrize("mode", ["forward_graph", "full_graph"])
-def test_graph_modes_match_eager(dev, mode):
+def test_graph_modes_match_eager(dev, mode, deterministic):
     """The forward-only hipGraph (replayed forward + eager two-stream backward) and the
     whole-step graph give the same weights as eager launching after several steps."""
     from pgdist.engine.native_step import NativeTrainStep

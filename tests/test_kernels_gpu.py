@@ -191,7 +191,8 @@ def test_dw_dgrad_wgrad(dev, B, H, W, C, stride):
     part2 = torch.zeros(P * 2 * C, device=dev)
     wpart2 = torch.zeros(K.dw_dgrad_wgrad_workspace(B, H, W, C, stride), device=dev)
     K.dw_dgrad(g, yself, coef, tapmajor(w), yprev, s, t, gout2, part2, B, H, W, C, stride, wpart=wpart2)
-    assert torch.equal(gout2, gout) and torch.equal(part2, part)
+    # identical dgrad; the BN partials are float-atomic sums (order-dependent in the last bits)
+    assert torch.equal(gout2, gout) and torch.allclose(part2, part, rtol=1e-5, atol=1e-5)
     grad2 = torch.empty(C * 9, device=dev)
     K.wgrad_reduce(wpart2, P, 9 * C, grad2)
     assert rel(grad2.view(9, C).t().reshape(C, 1, 3, 3), wref) < 1e-3
