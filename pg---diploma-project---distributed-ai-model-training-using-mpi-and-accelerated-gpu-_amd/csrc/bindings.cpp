@@ -11,9 +11,11 @@
 #include <pybind11/numpy.h>
 
 #include <cstdint>
+#include <memory>
 #include <stdexcept>
 #include <string>
 
+#include "runtime/plan.h"
 #include "runtime/runtime.h"
 
 namespace py = pybind11;
@@ -33,6 +35,9 @@ void launch_adam_flat(float *, const float *, float *, float *, bf16_t *, long l
 void launch_f32_to_bf16(const float *, bf16_t *, long long, hipStream_t);
 int dw_fwd_num_partials(int, int, int, int, int);
 int bn_rep();
+void bn_fin_arm(const void *desc);
+std::string bn_fin_pack(float *, int *, int, int, float, int, const float *, const float *, float, float, float *,
+                        float *, long long *, float *, float *, float *, float *, float *, float *, float *);
 void bn_set_rep(int rep);
 int dw_dgrad_num_partials(int, int, int, int, int);
 int dw_wgrad_num_partials(int, int, int, int, int);
@@ -128,124 +133,176 @@ PYBIND11_MODULE(_pgdist_C, m) {
   // ---- BatchNorm ----
   m.def("bn_fwd_finalize", [](P part, int Pn, int C, float count, P gamma, P beta, float eps,
                               float mom, P rm, P rv, P nbt, P mean, P rstd, P scale, P shift, P s) {
-    launch_bn_fwd_finalize(ptr<float>(part), Pn, C, count, ptr<float>(gamma), ptr<float>(beta), eps,
-                           mom, ptr<float>(rm), ptr<float>(rv), ptr<long long>(nbt), ptr<float>(mean),
-                           ptr<float>(rstd), ptr<float>(scale), ptr<float>(shift), S(s));
+    pgdist_rt::run_op([=] {
+      launch_bn_fwd_finalize(ptr<float>(part), Pn, C, count, ptr<float>(gamma), ptr<float>(beta), eps,
+                             mom, ptr<float>(rm), ptr<float>(rv), ptr<long long>(nbt), ptr<float>(mean),
+                             ptr<float>(rstd), ptr<float>(scale), ptr<float>(shift), S(s));
+    });
   });
   m.def("bn_bwd_finalize", [](P part, int Pn, int C, float count, P mean, P rstd, P gamma, P coef,
                               P dgamma, P dbeta, P s) {
-    launch_bn_bwd_finalize(ptr<float>(part), Pn, C, count, ptr<float>(mean), ptr<float>(rstd),
-                           ptr<float>(gamma), ptr<float>(coef), ptr<float>(dgamma), ptr<float>(dbeta),
-                           S(s));
+    pgdist_rt::run_op([=] {
+      launch_bn_bwd_finalize(ptr<float>(part), Pn, C, count, ptr<float>(mean), ptr<float>(rstd),
+                             ptr<float>(gamma), ptr<float>(coef), ptr<float>(dgamma), ptr<float>(dbeta),
+                             S(s));
+    });
   });
   m.def("bn_apply", [](P y, P res, P scale, P shift, P out, long long M, int C, bool relu6, P s) {
-    launch_bn_apply(ptr<bf16_t>(y), ptr<bf16_t>(res), ptr<float>(scale), ptr<float>(shift),
-                    ptr<bf16_t>(out), M, C, relu6, S(s));
+    pgdist_rt::run_op([=] {
+      launch_bn_apply(ptr<bf16_t>(y), ptr<bf16_t>(res), ptr<float>(scale), ptr<float>(shift),
+                      ptr<bf16_t>(out), M, C, relu6, S(s));
+    });
   });
   // ---- optimizer ----
   m.def("adam_flat", [](P p, P g, P mm, P v, P pb, long long n, P hyper, float b1, float b2,
                         float eps, float wd, float gscale, P s) {
-    launch_adam_flat(ptr<float>(p), ptr<float>(g), ptr<float>(mm), ptr<float>(v), ptr<bf16_t>(pb),
-                     n, ptr<float>(hyper), b1, b2, eps, wd, gscale, S(s));
+    pgdist_rt::run_op([=] {
+      launch_adam_flat(ptr<float>(p), ptr<float>(g), ptr<float>(mm), ptr<float>(v), ptr<bf16_t>(pb),
+                       n, ptr<float>(hyper), b1, b2, eps, wd, gscale, S(s));
+    });
   });
   m.def("f32_to_bf16", [](P x, P y, long long n, P s) {
-    launch_f32_to_bf16(ptr<float>(x), ptr<bf16_t>(y), n, S(s));
+    pgdist_rt::run_op([=] {
+      launch_f32_to_bf16(ptr<float>(x), ptr<bf16_t>(y), n, S(s));
+    });
   });
-  m.def("step_begin", [](P hyper, P s) { launch_step_begin(ptr<float>(hyper), S(s)); });
+  m.def("step_begin", [](P hyper, P s) {
+    pgdist_rt::run_op([=] { launch_step_begin(ptr<float>(hyper), S(s)); });
+  });
   m.def("reduce_metrics", [](P loss, P correct, int B, P acc, P s) {
-    launch_reduce_metrics(ptr<float>(loss), ptr<float>(correct), B, ptr<double>(acc), S(s));
+    pgdist_rt::run_op([=] {
+      launch_reduce_metrics(ptr<float>(loss), ptr<float>(correct), B, ptr<double>(acc), S(s));
+    });
   });
   // ---- depthwise ----
   m.def("dw_fwd_num_partials", &dw_fwd_num_partials);
   m.def("bn_rep", &bn_rep, "replica rows of the atomic BN-statistics accumulators");
+  m.def("bn_fin_arm", [](P d) { pgdist_rt::run_op([=] { bn_fin_arm(reinterpret_cast<const void *>(d)); }); },
+        "arm a device BnFin descriptor for the next BN-statistics producer launch (finalize fused in its tail)");
+  m.def("bn_fin_pack", [](P acc, P ctr, int rows, int C, float count, int bwd, P gamma, P beta, float eps,
+                          float mom, P rm, P rv, P nbt, P mean, P rstd, P scale, P shift, P coef, P dgamma,
+                          P dbeta) {
+    return py::bytes(bn_fin_pack(ptr<float>(acc), ptr<int>(ctr), rows, C, count, bwd, ptr<float>(gamma),
+                                 ptr<float>(beta), eps, mom, ptr<float>(rm), ptr<float>(rv), ptr<long long>(nbt),
+                                 ptr<float>(mean), ptr<float>(rstd), ptr<float>(scale), ptr<float>(shift),
+                                 ptr<float>(coef), ptr<float>(dgamma), ptr<float>(dbeta)));
+  });
   m.def("bn_set_rep", &bn_set_rep, "set the replica rows (large = one row per workgroup: deterministic)");
   m.def("dw_dgrad_num_partials", &dw_dgrad_num_partials);
   m.def("dw_wgrad_num_partials", &dw_wgrad_num_partials);
   m.def("dw_fwd", [](P x, P is, P it, int act, P w, P y, P part, int B, int H, int W, int C,
                      int stride, P s) {
-    launch_dw_fwd(ptr<bf16_t>(x), ptr<float>(is), ptr<float>(it), act, ptr<bf16_t>(w), ptr<bf16_t>(y),
-                  ptr<float>(part), B, H, W, C, stride, S(s));
+    pgdist_rt::run_op([=] {
+      launch_dw_fwd(ptr<bf16_t>(x), ptr<float>(is), ptr<float>(it), act, ptr<bf16_t>(w), ptr<bf16_t>(y),
+                    ptr<float>(part), B, H, W, C, stride, S(s));
+    });
   });
   m.def("dw_dgrad", [](P g, P ys, P coef, P w, P yp, P ps, P pt, P gout, P part, int B, int H,
                        int W, int C, int stride, P wpart, P s) {
-    launch_dw_dgrad(ptr<bf16_t>(g), ptr<bf16_t>(ys), ptr<float>(coef), ptr<bf16_t>(w),
-                    ptr<bf16_t>(yp), ptr<float>(ps), ptr<float>(pt), ptr<bf16_t>(gout),
-                    ptr<float>(part), B, H, W, C, stride, ptr<float>(wpart), S(s));
+    pgdist_rt::run_op([=] {
+      launch_dw_dgrad(ptr<bf16_t>(g), ptr<bf16_t>(ys), ptr<float>(coef), ptr<bf16_t>(w),
+                      ptr<bf16_t>(yp), ptr<float>(ps), ptr<float>(pt), ptr<bf16_t>(gout),
+                      ptr<float>(part), B, H, W, C, stride, ptr<float>(wpart), S(s));
+    });
   });
   m.def("dw_dgrad_wgrad_workspace_floats", &dw_dgrad_wgrad_workspace_floats);
   m.def("dw_wgrad", [](P g, P ys, P coef, P yp, P ps, P pt, P part, P grad, int B, int H, int W,
                        int C, int stride, P s) {
-    launch_dw_wgrad(ptr<bf16_t>(g), ptr<bf16_t>(ys), ptr<float>(coef), ptr<bf16_t>(yp),
-                    ptr<float>(ps), ptr<float>(pt), ptr<float>(part), ptr<float>(grad), B, H, W, C,
-                    stride, S(s));
+    pgdist_rt::run_op([=] {
+      launch_dw_wgrad(ptr<bf16_t>(g), ptr<bf16_t>(ys), ptr<float>(coef), ptr<bf16_t>(yp),
+                      ptr<float>(ps), ptr<float>(pt), ptr<float>(part), ptr<float>(grad), B, H, W, C,
+                      stride, S(s));
+    });
   });
   // ---- pointwise ----
   m.def("pw_gemm_num_partials", &pw_gemm_num_partials);
   m.def("pw_gemm", [](int pro, int epi, P A, P A2, P pa, P pb, P pc, P W, P out, P Yt, P es, P et,
                       P R, P part, int M, int N, int K, P Aout, P s) {
-    launch_pw_gemm(pro, epi, ptr<bf16_t>(A), ptr<bf16_t>(A2), ptr<float>(pa), ptr<float>(pb),
-                   ptr<float>(pc), ptr<bf16_t>(W), ptr<bf16_t>(out), ptr<bf16_t>(Yt), ptr<float>(es),
-                   ptr<float>(et), ptr<bf16_t>(R), ptr<float>(part), M, N, K, ptr<bf16_t>(Aout), S(s));
+    pgdist_rt::run_op([=] {
+      launch_pw_gemm(pro, epi, ptr<bf16_t>(A), ptr<bf16_t>(A2), ptr<float>(pa), ptr<float>(pb),
+                     ptr<float>(pc), ptr<bf16_t>(W), ptr<bf16_t>(out), ptr<bf16_t>(Yt), ptr<float>(es),
+                     ptr<float>(et), ptr<bf16_t>(R), ptr<float>(part), M, N, K, ptr<bf16_t>(Aout), S(s));
+    });
   });
   m.def("pw_gemm_f8", [](int pro, P A, P pa, P pb, P W8, int ldw8, P wsc, float asc, P out, P part, int M,
                          int N, int K, P s) {
-    launch_pw_gemm_f8(pro, ptr<bf16_t>(A), ptr<float>(pa), ptr<float>(pb), ptr<uint8_t>(W8), ldw8,
-                      ptr<float>(wsc), asc, ptr<bf16_t>(out), ptr<float>(part), M, N, K, S(s));
+    pgdist_rt::run_op([=] {
+      launch_pw_gemm_f8(pro, ptr<bf16_t>(A), ptr<float>(pa), ptr<float>(pb), ptr<uint8_t>(W8), ldw8,
+                        ptr<float>(wsc), asc, ptr<bf16_t>(out), ptr<float>(part), M, N, K, S(s));
+    });
   });
   m.def("w8_quant", [](P src, P dst, P wsc, P tab, int n, P s) {
-    launch_w8_quant(ptr<float>(src), ptr<uint8_t>(dst), ptr<float>(wsc), ptr<int>(tab), n, S(s));
+    pgdist_rt::run_op([=] {
+      launch_w8_quant(ptr<float>(src), ptr<uint8_t>(dst), ptr<float>(wsc), ptr<int>(tab), n, S(s));
+    });
   });
   m.def("wt_transpose", [](P src, P dst, P tab, int n, P s) {
-    launch_wt_transpose(ptr<bf16_t>(src), ptr<bf16_t>(dst), ptr<int>(tab), n, S(s));
+    pgdist_rt::run_op([=] {
+      launch_wt_transpose(ptr<bf16_t>(src), ptr<bf16_t>(dst), ptr<int>(tab), n, S(s));
+    });
   });
   m.def("pw_bwd_supported", &pw_bwd_supported);
   m.def("pw_bwd_num_partials", &pw_bwd_num_partials);
   m.def("pw_bwd_wgrad_workspace_floats", &pw_bwd_wgrad_workspace_floats);
   m.def("pw_bwd", [](int epi, P G, P Y, P ca, P cb, P cc, P WT, P out, P Yt, P es, P et, P R, P X,
                      P part, P wpart, P grad, int M, int Kg, int Ng, P s) {
-    launch_pw_bwd(epi, ptr<bf16_t>(G), ptr<bf16_t>(Y), ptr<float>(ca), ptr<float>(cb), ptr<float>(cc),
-                  ptr<bf16_t>(WT), ptr<bf16_t>(out), ptr<bf16_t>(Yt), ptr<float>(es), ptr<float>(et),
-                  ptr<bf16_t>(R), ptr<bf16_t>(X), ptr<float>(part), ptr<float>(wpart), ptr<float>(grad),
-                  M, Kg, Ng, S(s));
+    pgdist_rt::run_op([=] {
+      launch_pw_bwd(epi, ptr<bf16_t>(G), ptr<bf16_t>(Y), ptr<float>(ca), ptr<float>(cb), ptr<float>(cc),
+                    ptr<bf16_t>(WT), ptr<bf16_t>(out), ptr<bf16_t>(Yt), ptr<float>(es), ptr<float>(et),
+                    ptr<bf16_t>(R), ptr<bf16_t>(X), ptr<float>(part), ptr<float>(wpart), ptr<float>(grad),
+                    M, Kg, Ng, S(s));
+    });
   });
   m.def("wgrad_reduce", [](P part, int nsplit, long long n, P grad, P s) {
-    launch_wgrad_reduce(ptr<float>(part), nsplit, n, ptr<float>(grad), S(s));
+    pgdist_rt::run_op([=] {
+      launch_wgrad_reduce(ptr<float>(part), nsplit, n, ptr<float>(grad), S(s));
+    });
   }, "grad[n] = sum of the S split rows of part[S][n] (deterministic, one launch)");
   m.def("pw_wgrad_workspace_floats", &pw_wgrad_workspace_floats);
   m.def("pw_wgrad", [](P G, P Y, P ga, P gb, P gc, P X, P xs, P xt, int xact, P part, P grad, int M,
                        int N, int K, P s) {
-    launch_pw_wgrad(ptr<bf16_t>(G), ptr<bf16_t>(Y), ptr<float>(ga), ptr<float>(gb), ptr<float>(gc),
-                    ptr<bf16_t>(X), ptr<float>(xs), ptr<float>(xt), xact, ptr<float>(part),
-                    ptr<float>(grad), M, N, K, S(s));
+    pgdist_rt::run_op([=] {
+      launch_pw_wgrad(ptr<bf16_t>(G), ptr<bf16_t>(Y), ptr<float>(ga), ptr<float>(gb), ptr<float>(gc),
+                      ptr<bf16_t>(X), ptr<float>(xs), ptr<float>(xt), xact, ptr<float>(part),
+                      ptr<float>(grad), M, N, K, S(s));
+    });
   });
   // ---- stem ----
   m.def("stem_fwd_num_partials", &stem_fwd_num_partials);
   m.def("stem_fwd", [](P img, P w, P y, P part, int B, int H, int W, int px, P s) {
-    if (!launch_stem_fwd(ptr<bf16_t>(img), ptr<bf16_t>(w), ptr<bf16_t>(y), ptr<float>(part), B, H, W, px, S(s)))
-      throw std::invalid_argument("stem_fwd: px must be 1, 2 or 4");
+    if (px != 1 && px != 2 && px != 4) throw std::invalid_argument("stem_fwd: px must be 1, 2 or 4");
+    pgdist_rt::run_op([=] {
+      (void)launch_stem_fwd(ptr<bf16_t>(img), ptr<bf16_t>(w), ptr<bf16_t>(y), ptr<float>(part), B, H, W, px, S(s));
+    });
   });
   m.def("stem_wgrad_workspace_floats", &stem_wgrad_workspace_floats);
   m.def("stem_wgrad", [](P G, P Y, P ga, P gb, P gc, P img, P part, P grad, int B, int H, int W,
                          int O, P s) {
-    launch_stem_wgrad(ptr<bf16_t>(G), ptr<bf16_t>(Y), ptr<float>(ga), ptr<float>(gb), ptr<float>(gc),
-                      ptr<bf16_t>(img), ptr<float>(part), ptr<float>(grad), B, H, W, O, S(s));
+    pgdist_rt::run_op([=] {
+      launch_stem_wgrad(ptr<bf16_t>(G), ptr<bf16_t>(Y), ptr<float>(ga), ptr<float>(gb), ptr<float>(gc),
+                        ptr<bf16_t>(img), ptr<float>(part), ptr<float>(grad), B, H, W, O, S(s));
+    });
   });
   // ---- head ----
   m.def("head", [](P y, P sc, P sh, P Wl, P bl, P labels, int B, int HW, int C, int NC, float p,
                    unsigned long long seed, P hyper, int train, float loss_scale, P logits, P loss,
                    P correct, P dlogits, P pd, P g, P part, P dW, P db, P s) {
-    launch_head(ptr<bf16_t>(y), ptr<float>(sc), ptr<float>(sh), ptr<float>(Wl), ptr<float>(bl),
-                ptr<long long>(labels), B, HW, C, NC, p, seed, ptr<float>(hyper), train, loss_scale,
-                ptr<float>(logits), ptr<float>(loss), ptr<float>(correct), ptr<float>(dlogits),
-                ptr<float>(pd), ptr<bf16_t>(g), ptr<float>(part), ptr<float>(dW), ptr<float>(db), S(s));
+    pgdist_rt::run_op([=] {
+      launch_head(ptr<bf16_t>(y), ptr<float>(sc), ptr<float>(sh), ptr<float>(Wl), ptr<float>(bl),
+                  ptr<long long>(labels), B, HW, C, NC, p, seed, ptr<float>(hyper), train, loss_scale,
+                  ptr<float>(logits), ptr<float>(loss), ptr<float>(correct), ptr<float>(dlogits),
+                  ptr<float>(pd), ptr<bf16_t>(g), ptr<float>(part), ptr<float>(dW), ptr<float>(db), S(s));
+    });
   });
   // ---- data ----
   m.def("augment", [](P src, P idx, P labels_src, int nsrc, int B, int out_hw, int train,
                       int double_resize, P params, unsigned long long seed, P hyper, int epoch_ctr,
                       P out, P labels_out, P params_out, P s) {
-    launch_augment(ptr<unsigned char>(src), ptr<long long>(idx), ptr<long long>(labels_src), nsrc, B,
-                   out_hw, train, double_resize, ptr<float>(params), seed, ptr<float>(hyper),
-                   epoch_ctr, ptr<bf16_t>(out), ptr<long long>(labels_out), ptr<float>(params_out), S(s));
+    pgdist_rt::run_op([=] {
+      launch_augment(ptr<unsigned char>(src), ptr<long long>(idx), ptr<long long>(labels_src), nsrc, B,
+                     out_hw, train, double_resize, ptr<float>(params), seed, ptr<float>(hyper),
+                     epoch_ctr, ptr<bf16_t>(out), ptr<long long>(labels_out), ptr<float>(params_out), S(s));
+    });
   });
 
   // ---- dense convolutions (ResNet-50) ----
@@ -253,55 +310,100 @@ PYBIND11_MODULE(_pgdist_C, m) {
   m.def("conv_dgrad_num_partials", &conv_dgrad_num_partials);
   m.def("conv_fwd", [](int pro, P x, P pa, P pb, P w, P y, P part, int Nb, int H, int W, int Ci, int N, int R,
                        int Sk, int st, int pad, P s) {
-    launch_conv_fwd(pro, ptr<bf16_t>(x), ptr<float>(pa), ptr<float>(pb), ptr<bf16_t>(w), ptr<bf16_t>(y),
-                    ptr<float>(part), Nb, H, W, Ci, N, R, Sk, st, pad, S(s));
+    pgdist_rt::run_op([=] {
+      launch_conv_fwd(pro, ptr<bf16_t>(x), ptr<float>(pa), ptr<float>(pb), ptr<bf16_t>(w), ptr<bf16_t>(y),
+                      ptr<float>(part), Nb, H, W, Ci, N, R, Sk, st, pad, S(s));
+    });
   });
   m.def("conv_dgrad", [](int epi, P G, P Y, P ga, P gb, P gc, P wt, P dx, P Yt, P es, P et, P Rg, P X, P Yt2,
                          P part, P part2, int Nb, int H, int W, int Cin, int Cout, int R, int Sk, int st, int pad,
                          P s) {
-    launch_conv_dgrad(epi, ptr<bf16_t>(G), ptr<bf16_t>(Y), ptr<float>(ga), ptr<float>(gb), ptr<float>(gc),
-                      ptr<bf16_t>(wt), ptr<bf16_t>(dx), ptr<bf16_t>(Yt), ptr<float>(es), ptr<float>(et),
-                      ptr<bf16_t>(Rg), ptr<bf16_t>(X), ptr<bf16_t>(Yt2), ptr<float>(part), ptr<float>(part2), Nb,
-                      H, W, Cin, Cout, R, Sk, st, pad, S(s));
+    pgdist_rt::run_op([=] {
+      launch_conv_dgrad(epi, ptr<bf16_t>(G), ptr<bf16_t>(Y), ptr<float>(ga), ptr<float>(gb), ptr<float>(gc),
+                        ptr<bf16_t>(wt), ptr<bf16_t>(dx), ptr<bf16_t>(Yt), ptr<float>(es), ptr<float>(et),
+                        ptr<bf16_t>(Rg), ptr<bf16_t>(X), ptr<bf16_t>(Yt2), ptr<float>(part), ptr<float>(part2), Nb,
+                        H, W, Cin, Cout, R, Sk, st, pad, S(s));
+    });
   });
   m.def("conv_wgrad_workspace_floats", &conv_wgrad_workspace_floats);
   m.def("conv_wgrad", [](P G, P Y, P ga, P gb, P gc, P x, P xs, P xt, int xpro, P ws, P grad, int Nb, int H,
                          int W, int Ci, int N, int R, int Sk, int st, int pad, P s) {
-    launch_conv_wgrad(ptr<bf16_t>(G), ptr<bf16_t>(Y), ptr<float>(ga), ptr<float>(gb), ptr<float>(gc),
-                      ptr<bf16_t>(x), ptr<float>(xs), ptr<float>(xt), xpro, ptr<float>(ws), ptr<float>(grad), Nb,
-                      H, W, Ci, N, R, Sk, st, pad, S(s));
+    pgdist_rt::run_op([=] {
+      launch_conv_wgrad(ptr<bf16_t>(G), ptr<bf16_t>(Y), ptr<float>(ga), ptr<float>(gb), ptr<float>(gc),
+                        ptr<bf16_t>(x), ptr<float>(xs), ptr<float>(xt), xpro, ptr<float>(ws), ptr<float>(grad), Nb,
+                        H, W, Ci, N, R, Sk, st, pad, S(s));
+    });
   });
   m.def("conv_wt", [](P src, P dst, P tab, int n, P s) {
-    launch_conv_wt(ptr<bf16_t>(src), ptr<bf16_t>(dst), ptr<int>(tab), n, S(s));
+    pgdist_rt::run_op([=] {
+      launch_conv_wt(ptr<bf16_t>(src), ptr<bf16_t>(dst), ptr<int>(tab), n, S(s));
+    });
   });
   m.def("res_out", [](P y, P sc, P sh, P r, P rs, P rt, P out, long long M, int C, P s) {
-    launch_res_out(ptr<bf16_t>(y), ptr<float>(sc), ptr<float>(sh), ptr<bf16_t>(r), ptr<float>(rs),
-                   ptr<float>(rt), ptr<bf16_t>(out), M, C, S(s));
+    pgdist_rt::run_op([=] {
+      launch_res_out(ptr<bf16_t>(y), ptr<float>(sc), ptr<float>(sh), ptr<bf16_t>(r), ptr<float>(rs),
+                     ptr<float>(rt), ptr<bf16_t>(out), M, C, S(s));
+    });
   });
   m.def("maxpool_fwd", [](P y, P sc, P sh, P out, P idx, int Nb, int H, int W, int C, P s) {
-    launch_maxpool_fwd(ptr<bf16_t>(y), ptr<float>(sc), ptr<float>(sh), ptr<bf16_t>(out), ptr<uint8_t>(idx), Nb,
-                       H, W, C, S(s));
+    pgdist_rt::run_op([=] {
+      launch_maxpool_fwd(ptr<bf16_t>(y), ptr<float>(sc), ptr<float>(sh), ptr<bf16_t>(out), ptr<uint8_t>(idx), Nb,
+                         H, W, C, S(s));
+    });
   });
   m.def("maxpool_bwd_num_partials", &maxpool_bwd_num_partials);
   m.def("maxpool_bwd", [](P gp, P idx, P y, P sc, P sh, P g, P part, int Nb, int H, int W, int C, P s) {
-    launch_maxpool_bwd(ptr<bf16_t>(gp), ptr<uint8_t>(idx), ptr<bf16_t>(y), ptr<float>(sc), ptr<float>(sh),
-                       ptr<bf16_t>(g), ptr<float>(part), Nb, H, W, C, S(s));
+    pgdist_rt::run_op([=] {
+      launch_maxpool_bwd(ptr<bf16_t>(gp), ptr<uint8_t>(idx), ptr<bf16_t>(y), ptr<float>(sc), ptr<float>(sh),
+                         ptr<bf16_t>(g), ptr<float>(part), Nb, H, W, C, S(s));
+    });
   });
   m.def("avgpool", [](P x, P out, int Nb, int HW, int C, P s) {
-    launch_avgpool(ptr<bf16_t>(x), ptr<float>(out), Nb, HW, C, S(s));
+    pgdist_rt::run_op([=] {
+      launch_avgpool(ptr<bf16_t>(x), ptr<float>(out), Nb, HW, C, S(s));
+    });
   });
   m.def("head_bwd", [](P dpool, P x, P y, P G, P part, int Nb, int HW, int C, P s) {
-    launch_head_bwd(ptr<float>(dpool), ptr<bf16_t>(x), ptr<bf16_t>(y), ptr<bf16_t>(G), ptr<float>(part), Nb,
-                    HW, C, S(s));
+    pgdist_rt::run_op([=] {
+      launch_head_bwd(ptr<float>(dpool), ptr<bf16_t>(x), ptr<bf16_t>(y), ptr<bf16_t>(G), ptr<float>(part), Nb,
+                      HW, C, S(s));
+    });
   });
   m.def("softmax_ce", [](P logits, P labels, int B, int NC, float scale, P loss, P correct, P dlogits, P s) {
-    launch_softmax_ce(ptr<float>(logits), ptr<long long>(labels), B, NC, scale, ptr<float>(loss),
-                      ptr<float>(correct), ptr<float>(dlogits), S(s));
+    pgdist_rt::run_op([=] {
+      launch_softmax_ce(ptr<float>(logits), ptr<long long>(labels), B, NC, scale, ptr<float>(loss),
+                        ptr<float>(correct), ptr<float>(dlogits), S(s));
+    });
   });
   m.def("image_prep", [](P src, P idx, P lab_src, int B, int H, int W, unsigned long long seed, P hyper, P out,
                          P lab_out, P s) {
-    launch_image_prep(ptr<uint8_t>(src), ptr<long long>(idx), ptr<long long>(lab_src), B, H, W, seed,
-                      ptr<float>(hyper), ptr<bf16_t>(out), ptr<long long>(lab_out), S(s));
+    pgdist_rt::run_op([=] {
+      launch_image_prep(ptr<uint8_t>(src), ptr<long long>(idx), ptr<long long>(lab_src), B, H, W, seed,
+                        ptr<float>(hyper), ptr<bf16_t>(out), ptr<long long>(lab_out), S(s));
+    });
+  });
+
+  // ---- launch plans (runtime/plan.h) ----
+  m.def("plan_record_begin", &pgdist_rt::plan_record_begin);
+  m.def("plan_record_end", &pgdist_rt::plan_record_end);
+  m.def("plan_record_abort", &pgdist_rt::plan_record_abort);
+  m.def("plan_recording", &pgdist_rt::plan_recording);
+  m.def("plan_replay", &pgdist_rt::plan_replay, "re-issue a recorded step (GIL held: Python ops run inline)");
+  m.def("plan_free", &pgdist_rt::plan_free);
+  m.def("plan_size", &pgdist_rt::plan_size);
+  m.def("plan_py", [](py::function fn) {
+    fn();
+    if (pgdist_rt::plan_recording()) {
+      // the Python callable is kept alive by the plan; plans are never destroyed after the
+      // interpreter finalises (plan.cpp), and plan_free runs with the GIL held
+      auto h = std::make_shared<py::object>(std::move(fn));
+      pgdist_rt::plan_append([h] { (*h)(); });
+    }
+  }, "run a Python callable now and, while recording, as a plan op (replayed with the GIL held)");
+  m.def("stream_wait", [](P waiter, P signaler) { pgdist_rt::stream_wait(S(waiter), S(signaler)); },
+        "waiter waits for the work enqueued so far on signaler (recordable)");
+  m.def("memset_async", [](P p, int value, long long bytes, P s) {
+    pgdist_rt::memset_async(ptr<void>(p), value, (size_t)bytes, S(s));
   });
 
   // ---- native runtime (host) ----

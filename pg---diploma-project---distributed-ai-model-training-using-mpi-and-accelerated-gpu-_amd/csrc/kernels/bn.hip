@@ -8,9 +8,10 @@
 // materialisation of block outputs (BN + residual) — reference semantics:
 // torchvision BatchNorm2d(eps=1e-5, momentum=0.1) inside MobileNetV2
 // (SURVEY.md §2.6 "BatchNorm2d (train)", §2.8).
-#include "../reduce.h"
+#include "../bnfin.h"
 
 #include <stdexcept>
+#include <string>
 
 // ---------------------------------------------------------------------------
 // Reduction of the [P][2][C] partials (one launch, reduce.h): grid (ceil(C/16) channel
@@ -82,23 +83,9 @@ __global__ __launch_bounds__(1024) void bn_fwd_finalize_kernel(
   __shared__ int flag;
   if (!bn_reduce(part, P, C, rch, nch, lvl1, ctr, sh, fin, flag)) return;
   const int tid = threadIdx.x, c = blockIdx.x * 16 + tid;
-  if (tid < 16 && c < C) {
-    const double n = (double)count;
-    const double mean = fin[tid] / n;
-    double var = fin[16 + tid] / n - mean * mean;
-    if (var < 0.0) var = 0.0;
-    const float rstd = (float)(1.0 / sqrt(var + (double)eps));
-    const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
-    mean_out[c] = (float)mean;
-    rstd_out[c] = rstd;
-    scale_out[c] = g * rstd;
-    shift_out[c] = b - (float)mean * g * rstd;
-    if (running_mean) {
-      const double unbiased = n > 1.0 ? var * n / (n - 1.0) : var;
-      running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
-      running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unbiased;
-    }
-  }
+  if (tid < 16 && c < C)
+    bn_fwd_channel(c, fin[tid], fin[16 + tid], (double)count, gamma, beta, eps, momentum, running_mean,
+                   running_var, mean_out, rstd_out, scale_out, shift_out);
   if (nbt && blockIdx.x == 0 && tid == 0) nbt[0] += 1;
 }
 
@@ -112,18 +99,40 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
   __shared__ int flag;
   if (!bn_reduce(part, P, C, rch, nch, lvl1, ctr, sh, fin, flag)) return;
   const int tid = threadIdx.x, c = blockIdx.x * 16 + tid;
-  if (tid < 16 && c < C) {
-    const double sg = fin[tid], sgy = fin[16 + tid];
-    const double n = (double)count, mu = mean[c], rs = rstd[c];
-    const double g = gamma ? gamma[c] : 1.0;
-    const double sgx = (sgy - mu * sg) * rs;  // sum g * xhat
-    if (dgamma) dgamma[c] = (float)sgx;
-    if (dbeta) dbeta[c] = (float)sg;
-    const double a = g * rs;
-    coef[c] = (float)a;
-    coef[C + c] = (float)(-a * rs * sgx / n);
-    coef[2 * C + c] = (float)(-a * sg / n + a * rs * mu * sgx / n);
+  if (tid < 16 && c < C)
+    bn_bwd_channel(c, C, fin[tid], fin[16 + tid], (double)count, mean, rstd, gamma, coef, dgamma, dbeta);
+}
+
+// Finalize of an accumulator with P <= kBnRep rows (the atomic replica rows of the MobileNetV2
+// producers): one thread per channel, all 2 x kBnRep row loads issued before the first use
+// (rows beyond P re-read row 0 and are weighted 0), 128-thread workgroups — a few workgroups
+// instead of C/16 1024-thread ones.
+template <bool BWD>
+__global__ __launch_bounds__(128) void bn_finalize_small_kernel(
+    const float *__restrict__ part, int P, int C, float count, const float *__restrict__ gamma,
+    const float *__restrict__ beta, float eps, float momentum, float *__restrict__ rmean, float *__restrict__ rvar,
+    long long *__restrict__ nbt, float *__restrict__ mean, float *__restrict__ rstd, float *__restrict__ scale,
+    float *__restrict__ shift, float *__restrict__ coef, float *__restrict__ dgamma, float *__restrict__ dbeta) {
+  const int c = blockIdx.x * 128 + threadIdx.x;
+  if (c < C) {
+    float v[2 * kBnRep];
+#pragma unroll
+    for (int r = 0; r < kBnRep; ++r) {
+      const int rr = r < P ? r : 0;
+      v[2 * r] = part[(size_t)(2 * rr) * C + c];
+      v[2 * r + 1] = part[(size_t)(2 * rr + 1) * C + c];
+    }
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int r = 0; r < kBnRep; ++r) {
+      const double m = r < P ? 1.0 : 0.0;
+      s0 += m * (double)v[2 * r];
+      s1 += m * (double)v[2 * r + 1];
+    }
+    if (BWD) bn_bwd_channel(c, C, s0, s1, (double)count, mean, rstd, gamma, coef, dgamma, dbeta);
+    else bn_fwd_channel(c, s0, s1, (double)count, gamma, beta, eps, momentum, rmean, rvar, mean, rstd, scale, shift);
   }
+  if (!BWD && nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -156,6 +165,27 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t *__restrict_
 // host launchers
 // ---------------------------------------------------------------------------
 int g_bn_rep = kBnRep;
+
+// fused finalize descriptor armed for the next producer launch (see bnfin.h)
+static const BnFin *g_bn_fin = nullptr;
+void bn_fin_arm(const void *desc) { g_bn_fin = static_cast<const BnFin *>(desc); }
+const BnFin *take_bn_fin() {
+  const BnFin *d = g_bn_fin;
+  g_bn_fin = nullptr;
+  return d;
+}
+// the descriptor as bytes (the caller copies them to device memory once)
+std::string bn_fin_pack(float *acc, int *ctr, int rows, int C, float count, int bwd, const float *gamma,
+                        const float *beta, float eps, float momentum, float *rmean, float *rvar, long long *nbt,
+                        float *mean, float *rstd, float *scale, float *shift, float *coef, float *dgamma,
+                        float *dbeta) {
+  if (rows < 1 || rows > kBnRep || C < 1) throw std::invalid_argument("bn_fin_pack: rows in [1, kBnRep], C >= 1");
+  if (!acc || !ctr || (bwd ? !(mean && rstd && coef) : !(mean && rstd && scale && shift)))
+    throw std::invalid_argument("bn_fin_pack: missing buffer");
+  const BnFin d{acc, ctr, rows, C, count, bwd, gamma, beta, eps, momentum, rmean, rvar, nbt,
+                mean, rstd, scale, shift, coef, dgamma, dbeta};
+  return std::string(reinterpret_cast<const char *>(&d), sizeof d);
+}
 int bn_rep() { return g_bn_rep; }
 void bn_set_rep(int rep) {
   if (rep < 1) throw std::invalid_argument("bn_set_rep: rep must be >= 1");
@@ -180,6 +210,12 @@ void launch_bn_fwd_finalize(const float *part, int P, int C, float count, const 
                             const float *beta, float eps, float momentum, float *rmean,
                             float *rvar, long long *nbt, float *mean, float *rstd, float *scale,
                             float *shift, hipStream_t st) {
+  if (P <= kBnRep) {
+    hipLaunchKernelGGL(bn_finalize_small_kernel<false>, dim3((C + 127) / 128), dim3(128), 0, st, part, P, C, count,
+                       gamma, beta, eps, momentum, rmean, rvar, nbt, mean, rstd, scale, shift, nullptr, nullptr,
+                       nullptr);
+    return;
+  }
   // P <= 1024: one 1024-thread workgroup per 16 channels reads all rows (no hand-off)
   const bool one = P <= kBnOneMax;
   const int rch = one ? P : red_rch(P, kBnMinRows), nch = one ? 1 : red_nch(P, kBnMinRows);
@@ -193,6 +229,12 @@ void launch_bn_fwd_finalize(const float *part, int P, int C, float count, const 
 void launch_bn_bwd_finalize(const float *part, int P, int C, float count, const float *mean,
                             const float *rstd, const float *gamma, float *coef, float *dgamma,
                             float *dbeta, hipStream_t st) {
+  if (P <= kBnRep) {
+    hipLaunchKernelGGL(bn_finalize_small_kernel<true>, dim3((C + 127) / 128), dim3(128), 0, st, part, P, C, count,
+                       gamma, nullptr, 0.f, 0.f, nullptr, nullptr, nullptr, const_cast<float *>(mean),
+                       const_cast<float *>(rstd), nullptr, nullptr, coef, dgamma, dbeta);
+    return;
+  }
   const bool one = P <= kBnOneMax;
   const int rch = one ? P : red_rch(P, kBnMinRows), nch = one ? 1 : red_nch(P, kBnMinRows);
   const int nb = (C + 15) / 16;

@@ -20,7 +20,7 @@
 //    layer's BN partial sums, the dgrad epilogue the producer-BN backward
 //    partials; the weight gradient is reduced per workgroup and then by a
 //    deterministic two-level column sum.
-#include "../common.h"
+#include "../bnfin.h"
 
 #include <cstdlib>
 
@@ -35,7 +35,8 @@ struct DwGeom {
   int TWc;    // columns per workgroup
   int R;      // rows per workgroup
   int tiles_w, tiles_h;
-  int bn_rep;  // BN-statistics replica rows (g_bn_rep)
+  int bn_rep;         // BN-statistics replica rows (g_bn_rep)
+  const BnFin *fin;   // fused BN finalize in the tail (nullptr: none)
 };
 
 PG_DEVICE void unpack4(const uint2 &u, float (&f)[CPT]) {
@@ -312,6 +313,7 @@ __global__ __launch_bounds__(256) void dw_fwd_lds_kernel(
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may still target the ring
   __syncthreads();
   block_channel_partials<2>(stats, part, g.C, g.CC, cbase, g.TWc, red, tl.idx, dw_tiles(g), g.bn_rep);
+  bn_fin_tail(g.fin);
 }
 
 // dgrad (stride 1): thread = one INPUT column, strip of input rows.  Streams per step k: the dy
@@ -455,6 +457,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_s1_lds_kernel(
   __syncthreads();
   block_channel_partials<2>(stats, part, g.C, g.CC, cbase, g.TWc, red, tl.idx, dw_tiles(g), g.bn_rep);
   if constexpr (WG) block_channel_partials<9>(accw, wpart, g.C, g.CC, cbase, g.TWc, red, tl.idx);
+  bn_fin_tail(g.fin);
 }
 
 // dgrad (stride 2): thread = one INPUT column iw; it needs dy columns owA (tap dw = 0 for odd
@@ -639,6 +642,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_s2_lds_kernel(
   __syncthreads();
   block_channel_partials<2>(stats, part, g.C, g.CC, cbase, g.TWc, red, tl.idx, dw_tiles(g), g.bn_rep);
   if constexpr (WG) block_channel_partials<9>(accw, wpart, g.C, g.CC, cbase, g.TWc, red, tl.idx);
+  bn_fin_tail(g.fin);
 }
 
 // wgrad: dW[tap][c] partials per workgroup [P][9][C]; thread = one output column.  Streams per
@@ -779,6 +783,7 @@ int dw_cc(int C) {
 DwGeom dw_geom(int kind, int B, int H, int W, int C, int stride) {
   DwGeom g;
   g.bn_rep = g_bn_rep;
+  g.fin = nullptr;
   g.B = B;
   g.H = H;
   g.W = W;
@@ -821,7 +826,8 @@ int dw_wgrad_num_partials(int B, int H, int W, int C, int stride) { return dw_gr
 
 void launch_dw_fwd(const bf16_t *x, const float *in_s, const float *in_t, int act, const bf16_t *w,
                    bf16_t *y, float *part, int B, int H, int W, int C, int stride, hipStream_t st) {
-  const DwGeom g = dw_geom(0, B, H, W, C, stride);
+  DwGeom g = dw_geom(0, B, H, W, C, stride);
+  g.fin = take_bn_fin();
   const dim3 grid(dw_grid_x(g) * (C / g.CC)), block(256);
   if (stride == 1) {
     if (act == ACT_BN_RELU6) hipLaunchKernelGGL((dw_fwd_lds_kernel<1, ACT_BN_RELU6>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
@@ -837,7 +843,8 @@ int colsum_rows(int R);
 void launch_dw_dgrad(const bf16_t *gin, const bf16_t *yself, const float *coef, const bf16_t *w,
                      const bf16_t *yprev, const float *ps, const float *pt, bf16_t *gout,
                      float *part, int B, int H, int W, int C, int stride, float *wpart, hipStream_t st) {
-  const DwGeom g = dw_geom(1, B, H, W, C, stride);
+  DwGeom g = dw_geom(1, B, H, W, C, stride);
+  g.fin = take_bn_fin();
   const dim3 grid(dw_grid_x(g) * (C / g.CC)), block(256);
   if (wpart) {
     if (stride == 1)

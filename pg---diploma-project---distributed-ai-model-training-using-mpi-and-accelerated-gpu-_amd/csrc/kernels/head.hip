@@ -7,7 +7,7 @@
 // Linear(1280, 10), CrossEntropyLoss, torch.max + .item() metrics
 // (cifar10_mpi_mobilenet_224.py:177-185).  Metrics stay on the device (per-image
 // loss / correct vectors), so the step needs no host synchronisation.
-#include "../common.h"
+#include "../bnfin.h"
 
 namespace {
 constexpr int kMaxNC = 16;
@@ -122,7 +122,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
     const bf16_t *__restrict__ y, const float *__restrict__ s, const float *__restrict__ t,
     const float *__restrict__ Wl, const float *__restrict__ dlogits, int HW, int C, int NC, float drop_p,
     unsigned long long seed, const float *__restrict__ hyper, bf16_t *__restrict__ g_out,
-    float *__restrict__ part, int rep) {
+    float *__restrict__ part, int rep, const BnFin *fin) {
   __shared__ float r0[kSlots][kChunk + 4];
   __shared__ float r1[kSlots][kChunk + 4];
   const int b = blockIdx.x, tid = threadIdx.x, cl = tid & 31, slot = tid >> 5;
@@ -190,6 +190,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
     bn_part_add(part, b, gridDim.x, rep, C, 0, c, a0);
     bn_part_add(part, b, gridDim.x, rep, C, 1, c, a1);
   }
+  bn_fin_tail(fin);
 }
 
 // dW[j][c] = sum_b dlogits[b][j] * pd[b][c];  db[j] = sum_b dlogits[b][j]
@@ -222,12 +223,13 @@ void launch_head(const bf16_t *y, const float *s, const float *t, const float *W
                  float *logits, float *loss, float *correct, float *dlogits, float *pd,
                  bf16_t *g_out, float *part, float *dW, float *db, hipStream_t st) {
   const dim3 grid2(B, (C + kChunk - 1) / kChunk);
+  const BnFin *fin = take_bn_fin();   // backward statistics of the final BN (train only)
   hipLaunchKernelGGL(head_pool_kernel, grid2, dim3(256), 0, st, y, s, t, HW, C, drop_p, seed, hyper, train, pd);
   hipLaunchKernelGGL(head_ce_kernel, dim3(B), dim3(256), 0, st, pd, Wl, bl, labels, C, NC, loss_scale, logits,
                      loss, correct, train ? dlogits : nullptr);
   if (!train) return;
   hipLaunchKernelGGL(head_bwd_kernel, grid2, dim3(256), 0, st, y, s, t, Wl, dlogits, HW, C, NC, drop_p, seed,
-                     hyper, g_out, part, g_bn_rep);
+                     hyper, g_out, part, g_bn_rep, fin);
   hipLaunchKernelGGL(head_wgrad_kernel, dim3((NC * C + NC + 255) / 256), dim3(256), 0, st, dlogits, pd, B, C,
                      NC, dW, db);
 }

@@ -23,7 +23,7 @@
 //   * wgrad:  dW[kg][ng] += sum_m dyT[kg][m] xT[ng][m], accumulated in registers
 //     across the workgroup's tiles and written once as a split-M partial
 //     [gridDim.x][Kg][Ng] (deterministic fixed-order reduction afterwards).
-#include "../common.h"
+#include "../bnfin.h"
 
 #include <cstdlib>
 
@@ -43,6 +43,7 @@ struct PwBwdArgs {
   float *wpart;                 // [gx][Kg][Ng]
   int M, Kg, Ng;
   int bn_rep;                   // BN-statistics replica rows (g_bn_rep)
+  const BnFin *fin;             // fused BN finalize in the tail (nullptr: none)
 };
 template <int KP, int BN, int BM>
 struct BwdLds {
@@ -354,6 +355,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
     }
     __syncthreads();
   }
+  bn_fin_tail(p.fin);
 }
 
 // ===========================================================================
@@ -421,8 +423,9 @@ void launch_pw_bwd(int epi, const bf16_t *G, const bf16_t *Y, const float *ca, c
                    const float *et, const bf16_t *R, const bf16_t *X, float *part, float *wpart,
                    float *grad, int M, int Kg, int Ng, hipStream_t st) {
   const BwdGeom g = bwd_geom(M, Kg, Ng);
+  const BnFin *fin = take_bn_fin();
   if (!g.ok) return;
-  PwBwdArgs a{G, Y, ca, cb, cc, WT, out, Yt, es, et, R, X, part, wpart, M, Kg, Ng, g_bn_rep};
+  PwBwdArgs a{G, Y, ca, cb, cc, WT, out, Yt, es, et, R, X, part, wpart, M, Kg, Ng, g_bn_rep, fin};
   if (epi == EPI_BWD_RELU6_) launch_bwd_epi<EPI_BWD_RELU6_>(a, g, st);
   else launch_bwd_epi<EPI_BWD_LIN_>(a, g, st);
   // grad == nullptr: the caller reduces wpart itself (e.g. on its weight-gradient stream)

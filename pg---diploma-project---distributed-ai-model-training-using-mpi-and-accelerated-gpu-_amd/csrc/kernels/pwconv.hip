@@ -33,7 +33,7 @@
 // The weight gradient dW[N][K] = sum_m dy[m][n] x[m][k] reduces over M; it is
 // a split-M MFMA kernel whose operands are staged TRANSPOSED in LDS (4 rows of
 // m packed per ds_write_b64) so both fragments are plain ds_read_b128.
-#include "../common.h"
+#include "../bnfin.h"
 
 #include <cstdlib>
 
@@ -68,6 +68,7 @@ struct PwArgs {
   float asc;
   int ldw8;
   int bn_rep;           // BN-statistics replica rows (g_bn_rep)
+  const BnFin *fin;     // fused BN finalize in the tail (nullptr: none)
 };
 }  // namespace
 
@@ -391,6 +392,7 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
     }
     __syncthreads();
   }
+  bn_fin_tail(p.fin);
 }
 
 // dgrad weights: W^T of every 1x1 conv, batched (one table entry per layer):
@@ -707,11 +709,13 @@ void launch_pw_gemm(int pro, int epi, const bf16_t *A, const bf16_t *A2, const f
                     int M, int N, int K, bf16_t *Aout, hipStream_t st) {
   PwArgs a{A, A2, pa, pb, pc, W, out, Yt, es, et, R, part, M, N, K, Aout};
   a.bn_rep = g_bn_rep;
+  a.fin = nullptr;
   const PwGeom g = pw_geom(M, N, K, pro);
   if (g.bdirect) {
     launch_pw_tile(pro, epi, A, A2, pa, pb, pc, W, out, Yt, es, et, R, part, M, N, K, Aout, st);
     return;
   }
+  a.fin = take_bn_fin();
 #define PW_CASE(P, E) \
   if (pro == P && epi == E) { launch_pw_geom<P, E>(a, g, st); return; }
   PW_CASE(ACT_NONE, EPI_FWD)
@@ -737,7 +741,7 @@ void launch_pw_gemm_f8(int pro, const bf16_t *A, const float *pa, const float *p
     return;
   }
   PwArgs a{A, nullptr, pa, pb, nullptr, nullptr, out, nullptr, nullptr, nullptr, nullptr, part, M, N, K, nullptr,
-           W8, wsc, asc, ldw8, g_bn_rep};
+           W8, wsc, asc, ldw8, g_bn_rep, take_bn_fin()};
   const int Kp = (K + 63) / 64 * 64;
   g.lds -= (size_t)g.BN * (Kp + kBPad) * 2;
   g.lds += (size_t)g.BN * (Kp + 16);

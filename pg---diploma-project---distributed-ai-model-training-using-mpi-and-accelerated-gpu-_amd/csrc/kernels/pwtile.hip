@@ -12,7 +12,7 @@
 // a*G + b*Y + c) is applied once per element while staging A.  Workgroup ids
 // put the N tiles of an M tile 8 ids apart (same XCD, dispatched together) so
 // the A tile is fetched from HBM once into that XCD's L2.
-#include "../common.h"
+#include "../bnfin.h"
 
 #include <cstdlib>
 
@@ -37,6 +37,7 @@ struct PwTArgs {
   float asc;            // F8: the prologue output is scaled by asc before its e4m3 conversion
   int ldw8;
   int bn_rep;           // BN-statistics replica rows (g_bn_rep)
+  const BnFin *fin;     // fused BN finalize in the tail (nullptr: none)
 };
 }  // namespace
 
@@ -325,6 +326,7 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
     }
     __syncthreads();
   }
+  bn_fin_tail(p.fin);
 }
 
 // ===========================================================================
@@ -384,6 +386,7 @@ void launch_pw_tile(int pro, int epi, const bf16_t *A, const bf16_t *A2, const f
                     hipStream_t st) {
   PwTArgs a{A, A2, pa, pb, pc, W, out, Yt, es, et, R, part, M, N, K, Aout};
   a.bn_rep = g_bn_rep;
+  a.fin = take_bn_fin();
   const TileGeom g = tile_geom(M, N, K, pro);
 #define PT_CASE(P, E) \
   if (pro == P && epi == E) { launch_tile_pe<P, E>(a, g, st); return; }
@@ -400,7 +403,7 @@ void launch_pw_tile_f8(int pro, const bf16_t *A, const float *pa, const float *p
                        const float *wsc, float asc, bf16_t *out, float *part, int M, int N, int K,
                        hipStream_t st) {
   PwTArgs a{A, nullptr, pa, pb, nullptr, nullptr, out, nullptr, nullptr, nullptr, nullptr, part, M, N, K,
-            nullptr, W8, wsc, asc, ldw8, g_bn_rep};
+            nullptr, W8, wsc, asc, ldw8, g_bn_rep, take_bn_fin()};
   TileGeom g = tile_geom(M, N, K, pro);   // the bf16 LDS size bounds the e4m3 one
   if (pro == ACT_NONE) launch_tile_pe<ACT_NONE, EPI_FWD_T, true>(a, g, st);
   else if (pro == ACT_BN_RELU6) launch_tile_pe<ACT_BN_RELU6, EPI_FWD_T, true>(a, g, st);

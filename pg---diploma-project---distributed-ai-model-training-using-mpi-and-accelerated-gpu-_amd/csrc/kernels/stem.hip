@@ -13,7 +13,7 @@
 // 4).  Each thread stores one 16-B vector per pixel and accumulates the BN0
 // partial sums.  The weight gradient is the im2col MFMA kernel in pwconv.hip
 // (launch_stem_wgrad).  No input gradient is needed.
-#include "../common.h"
+#include "../bnfin.h"
 
 namespace {
 constexpr int kCo = 32;
@@ -23,7 +23,8 @@ template <int kPx>
 __global__ __launch_bounds__(256) void stem_fwd_kernel(const bf16_t *__restrict__ img,
                                                       const bf16_t *__restrict__ w,  // [32][3][3][3]
                                                       bf16_t *__restrict__ y, float *__restrict__ part,
-                                                      int B, int H, int W, int Ho, int Wo, int rep) {
+                                                      int B, int H, int W, int Ho, int Wo, int rep,
+                                                      const BnFin *fin) {
   // thread = (group of kPx output pixels, group of 8 output channels): 4 threads per pixel
   // group; each pair of LDS weight reads (8 channels of one input channel x tap) feeds the
   // kPx pixels; each thread stores one 16-B vector per pixel.
@@ -108,6 +109,7 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(const bf16_t *__restrict_
     }
     __syncthreads();
   }
+  bn_fin_tail(fin);
 }
 
 int stem_fwd_num_partials(int B, int H, int W) {
@@ -125,9 +127,10 @@ bool launch_stem_fwd(const bf16_t *img, const bf16_t *w, bf16_t *y, float *part,
                      int W, int px, hipStream_t st) {
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
   const int grid = stem_fwd_num_partials(B, H, W);
-  if (px == 1) hipLaunchKernelGGL(stem_fwd_kernel<1>, dim3(grid), dim3(256), 0, st, img, w, y, part, B, H, W, Ho, Wo, g_bn_rep);
-  else if (px == 2) hipLaunchKernelGGL(stem_fwd_kernel<2>, dim3(grid), dim3(256), 0, st, img, w, y, part, B, H, W, Ho, Wo, g_bn_rep);
-  else if (px == 4) hipLaunchKernelGGL(stem_fwd_kernel<4>, dim3(grid), dim3(256), 0, st, img, w, y, part, B, H, W, Ho, Wo, g_bn_rep);
+  const BnFin *fin = take_bn_fin();
+  if (px == 1) hipLaunchKernelGGL(stem_fwd_kernel<1>, dim3(grid), dim3(256), 0, st, img, w, y, part, B, H, W, Ho, Wo, g_bn_rep, fin);
+  else if (px == 2) hipLaunchKernelGGL(stem_fwd_kernel<2>, dim3(grid), dim3(256), 0, st, img, w, y, part, B, H, W, Ho, Wo, g_bn_rep, fin);
+  else if (px == 4) hipLaunchKernelGGL(stem_fwd_kernel<4>, dim3(grid), dim3(256), 0, st, img, w, y, part, B, H, W, Ho, Wo, g_bn_rep, fin);
   else return false;
   return true;
 }

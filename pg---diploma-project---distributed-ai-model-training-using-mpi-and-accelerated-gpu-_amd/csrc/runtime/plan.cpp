@@ -1,0 +1,116 @@
+// Launch plans (plan.h).
+#include "plan.h"
+
+#include <hip/hip_runtime_api.h>
+
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace pgdist_rt {
+namespace {
+
+struct Plan {
+  std::vector<PlanOp> ops;
+};
+
+// heap-allocated and never destroyed: a plan may hold Python callbacks, which must not be
+// released after the interpreter has finalised
+std::map<int, Plan> &plans() {
+  static auto *m = new std::map<int, Plan>();
+  return *m;
+}
+Plan *g_rec = nullptr;
+int g_next_id = 1;
+
+void check(hipError_t e, const char *what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+struct Event {
+  hipEvent_t e = nullptr;
+  Event() { check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreateWithFlags"); }
+  ~Event() {
+    if (e) (void)hipEventDestroy(e);
+  }
+  Event(const Event &) = delete;
+  Event &operator=(const Event &) = delete;
+};
+
+// eager (unrecorded) waits: a ring of events; reusing one is safe because its record and the
+// wait on it are both enqueued before the next reuse (the wait binds the record at call time)
+hipEvent_t ring_event() {
+  static auto *ring = new std::vector<std::unique_ptr<Event>>();
+  static std::size_t next = 0;
+  if (ring->size() < 64) {
+    ring->push_back(std::make_unique<Event>());
+    return ring->back()->e;
+  }
+  hipEvent_t e = (*ring)[next]->e;
+  next = (next + 1) % ring->size();
+  return e;
+}
+
+}  // namespace
+
+void plan_record_begin() {
+  if (g_rec) throw std::runtime_error("plan_record_begin: a recording is already open");
+  g_rec = new Plan();
+}
+
+int plan_record_end() {
+  if (!g_rec) throw std::runtime_error("plan_record_end: no open recording");
+  const int id = g_next_id++;
+  plans()[id] = std::move(*g_rec);
+  delete g_rec;
+  g_rec = nullptr;
+  return id;
+}
+
+void plan_record_abort() {
+  delete g_rec;
+  g_rec = nullptr;
+}
+
+bool plan_recording() { return g_rec != nullptr; }
+
+void plan_append(PlanOp op) {
+  if (g_rec) g_rec->ops.push_back(std::move(op));
+}
+
+void plan_replay(int id) {
+  auto it = plans().find(id);
+  if (it == plans().end()) throw std::out_of_range("plan_replay: unknown plan " + std::to_string(id));
+  if (g_rec) throw std::runtime_error("plan_replay: not allowed while recording");
+  for (auto &op : it->second.ops) op();
+}
+
+void plan_free(int id) { plans().erase(id); }
+
+std::size_t plan_size(int id) {
+  auto it = plans().find(id);
+  return it == plans().end() ? 0 : it->second.ops.size();
+}
+
+void stream_wait(hipStream_t waiter, hipStream_t signaler) {
+  if (waiter == signaler) return;
+  if (!plan_recording()) {
+    hipEvent_t e = ring_event();
+    check(hipEventRecord(e, signaler), "hipEventRecord");
+    check(hipStreamWaitEvent(waiter, e, 0), "hipStreamWaitEvent");
+    return;
+  }
+  auto ev = std::make_shared<Event>();
+  run_op([ev, waiter, signaler] {
+    (void)hipEventRecord(ev->e, signaler);
+    (void)hipStreamWaitEvent(waiter, ev->e, 0);
+  });
+}
+
+void memset_async(void *ptr, int value, std::size_t bytes, hipStream_t st) {
+  run_op([=] { (void)hipMemsetAsync(ptr, value, bytes, st); });
+}
+
+}  // namespace pgdist_rt

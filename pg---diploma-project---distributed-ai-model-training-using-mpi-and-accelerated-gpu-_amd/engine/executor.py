@@ -91,18 +91,42 @@ class AtomicBNState(BNState):
     """BN of the MobileNetV2 executor: its producers accumulate the statistics atomically into
     min(P, bn_rep) replica rows of ``acc_f`` / ``acc_b`` (P = the producer's partial rows), so a
     finalize reduces those rows only (deterministic mode: bn_rep unbounded, one row per
-    producer workgroup).  ``rows_f`` / ``rows_b``: rows the accumulators were sized for."""
+    producer workgroup).  ``rows_f`` / ``rows_b``: rows the accumulators were sized for.
+
+    Fused finalize (default, not in deterministic mode): ``fin_f`` / ``fin_b`` are device
+    descriptors (ops.kernels.bn_fin_desc) the executor passes to the statistics producers,
+    whose last workgroup then finalizes this BN in the producer's tail (bnfin.h) instead of a
+    separate finalize launch; ``finalize_fwd`` / ``finalize_bwd`` are then no-ops."""
     rows_f = rows_b = 0
+    fin_f = fin_b = None
+
+    def build_fin(self, ctr_f, ctr_b):
+        """(Re)write the fused-finalize descriptors (in place once built, so captured graphs
+        keep valid pointers): call again after the module's running buffers were re-homed."""
+        m = self.module
+        df = K.bn_fin_desc(self.acc_f, ctr_f, self.rows_f, self.C, self.M, 0, gamma=self.gamma, beta=self.beta,
+                           eps=self.eps, momentum=self.momentum, rmean=m.running_mean, rvar=m.running_var,
+                           nbt=m.num_batches_tracked, mean=self.mean, rstd=self.rstd, scale=self.scale,
+                           shift=self.shift)
+        db = K.bn_fin_desc(self.acc_b, ctr_b, self.rows_b, self.C, self.M, 1, gamma=self.gamma, mean=self.mean,
+                           rstd=self.rstd, coef=self.coef, dgamma=self.dgamma, dbeta=self.dbeta)
+        if self.fin_f is None:
+            self.fin_f, self.fin_b = df, db
+        else:
+            self.fin_f.copy_(df)
+            self.fin_b.copy_(db)
 
     def finalize_fwd(self, part, P):
         r = K.bn_rows(P)
         assert r <= self.rows_f, f"{self.prefix}: forward producer has {r} rows > {self.rows_f} allocated"
-        super().finalize_fwd(part, r)
+        if self.fin_f is None:
+            super().finalize_fwd(part, r)
 
     def finalize_bwd(self, part, P):
         r = K.bn_rows(P)
         assert r <= self.rows_b, f"{self.prefix}: backward producer has {r} rows > {self.rows_b} allocated"
-        super().finalize_bwd(part, r)
+        if self.fin_b is None:
+            super().finalize_bwd(part, r)
 
 
 @dataclass
@@ -130,6 +154,9 @@ class BlockPlan:
 
 
 class MobileNetV2Executor:
+    # every host-side action of a training step goes through recordable native ops
+    # (ops.kernels: launches, stream_wait, memset, plan_py): the step can be a LaunchPlan
+    PLAN_SAFE = True
     DW_FUSE_MIN_H = 56   # depthwise dgrad+wgrad fused on maps >= this size (measured on MI355X)
     # block outputs materialised by the consumer GEMM instead of a BN-apply pass: measured neutral
     # on MI355X (the consumer reads y_p and the residual per N tile), so off by default
@@ -227,6 +254,14 @@ class MobileNetV2Executor:
         for bn, o, nf, nb in spans:
             bn.acc_f = self.bn_arena[o:o + nf]
             bn.acc_b = self.bn_arena[o + nf:o + nf + nb]
+        # finalize fused into the statistics producers (one arrival-counter pair per BN);
+        # opt-in (PGDIST_BN_FUSED=1): measured on MI355X at bs128 5.93 ms/step fused vs 5.60
+        # with the separate small finalize launches — every producer workgroup must wait for
+        # its statistics atomics to be acknowledged before arriving, which costs more than
+        # the kernel boundary it saves
+        self.fused_bn = not K.deterministic() and os.environ.get("PGDIST_BN_FUSED", "0") == "1"
+        self.bn_ctr = torch.zeros(8 * len(spans) + 16, dtype=torch.int32, device=device)   # 16-B apart
+        self.refresh_bn_fin()
         self.ws_wgrad = torch.zeros(max(wg) + 1024, **f32)
         # the stem weight gradient may run on the main stream concurrently with side-stream
         # weight gradients: its own split-M workspace
@@ -272,6 +307,14 @@ class MobileNetV2Executor:
                 self.w8[name] = (self.w8_buf[d0:d0 + n * K.fp8_pitch(k)], self.w8_scale[c0:c0 + n])
 
     # ------------------------------------------------------------------ helpers
+    def refresh_bn_fin(self):
+        """(Re)build the fused BN-finalize descriptors (after BN running buffers were re-homed,
+        e.g. coalesced for the per-step buffer broadcast)."""
+        if not self.fused_bn:
+            return
+        for i, bn in enumerate(self.all_bns()):
+            bn.build_fin(self.bn_ctr[8 * i:8 * i + 1], self.bn_ctr[8 * i + 4:8 * i + 5])
+
     def _bn_producer_rows(self):
         """{bn: (forward P, backward P)}: partial rows of the kernels that produce each BN's
         statistics, in the order forward()/backward() launch them (the finalize asserts the
@@ -310,9 +353,13 @@ class MobileNetV2Executor:
     def _ready(self, names):
         """Gradients of ``names`` are final once the work enqueued so far completes.  With a
         side stream the callback (DDP bucket launch) runs on it after it has joined the main
-        stream, so the collective is ordered after both streams' producers."""
+        stream, so the collective is ordered after both streams' producers.  Host-side Python
+        (the reducer's bookkeeping and collectives): a launch-plan op (ops.kernels.plan_py)."""
         if self.on_params_ready is None:
             return
+        K.plan_py(lambda: self._ready_now(names))
+
+    def _ready_now(self, names):
         if self.side is None or (self.ready_probe is not None and not self.ready_probe(names)):
             self.on_params_ready(names)
             return
@@ -326,26 +373,27 @@ class MobileNetV2Executor:
         if self.side is None:
             fn()
             return
-        self.side.wait_stream(torch.cuda.current_stream(self.device))
+        K.stream_wait(self.side, torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.side):
             fn()
 
-    def _consume_output(self, pend, W, out, ws, M, N, K_):
+    def _consume_output(self, pend, W, out, ws, M, N, K_, fin=None):
         """Forward 1x1 conv whose input is a pending block output: prologue BN_p (+ residual),
         side-writes the block output o."""
         bn, res, o = pend
         if res is not None:
-            K.pw_gemm(K.PRO_BNRES, K.EPI_FWD, bn.y, W, out, ws, M, N, K_, A2=res, pa=bn.scale, pb=bn.shift, Aout=o)
+            K.pw_gemm(K.PRO_BNRES, K.EPI_FWD, bn.y, W, out, ws, M, N, K_, A2=res, pa=bn.scale, pb=bn.shift, Aout=o,
+                      fin=fin)
         else:
-            K.pw_gemm(K.ACT_BN, K.EPI_FWD, bn.y, W, out, ws, M, N, K_, pa=bn.scale, pb=bn.shift, Aout=o)
+            K.pw_gemm(K.ACT_BN, K.EPI_FWD, bn.y, W, out, ws, M, N, K_, pa=bn.scale, pb=bn.shift, Aout=o, fin=fin)
 
-    def _pw_fwd(self, pro, A, wname, out, ws, M, N, K_, pa=None, pb=None):
+    def _pw_fwd(self, pro, A, wname, out, ws, M, N, K_, pa=None, pb=None, fin=None):
         """Forward 1x1 conv: bf16 MFMA GEMM, or the e4m3 one in fp8 mode."""
         if self.fp8:
             W8, wsc = self.w8[wname]
-            K.pw_gemm_f8(pro, A, W8, wsc, out, ws, M, N, K_, pa=pa, pb=pb)
+            K.pw_gemm_f8(pro, A, W8, wsc, out, ws, M, N, K_, pa=pa, pb=pb, fin=fin)
         else:
-            K.pw_gemm(pro, K.EPI_FWD, A, self.flat.b(wname), out, ws, M, N, K_, pa=pa, pb=pb)
+            K.pw_gemm(pro, K.EPI_FWD, A, self.flat.b(wname), out, ws, M, N, K_, pa=pa, pb=pb, fin=fin)
 
     def _fin_fwd(self, bn: BNState, P: int, train: bool):
         if train:
@@ -357,11 +405,12 @@ class MobileNetV2Executor:
         f, B, S = self.flat, self.B, self.S
         self._check_bn_mode()
         if train:
-            self.bn_arena.zero_()   # every BN statistics accumulator of this step
+            K.memset(self.bn_arena)   # every BN statistics accumulator of this step
         if self.fp8:
             K.w8_quant(f.master, self.w8_buf, self.w8_scale, self.w8_tab, self.w8_tab.shape[0])
         # stem
-        K.stem_fwd(self.img, f.b(self.stem_w), self.bn0.y, self.bn0.acc_f, B, S, S)
+        F = (lambda bn: bn.fin_f) if train else (lambda bn: None)   # fused forward finalize  # noqa: E731
+        K.stem_fwd(self.img, f.b(self.stem_w), self.bn0.y, self.bn0.acc_f, B, S, S, fin=F(self.bn0))
         self._fin_fwd(self.bn0, K.stem_num_partials(B, S, S), train)
         inp_bn, inp_t = self.bn0, None   # block input: virtual relu6(bn0(y0))
         # A block output o = BN_p(y_p) (+ residual) is not materialised by a separate pass: its
@@ -373,23 +422,25 @@ class MobileNetV2Executor:
             Min = B * Hin * Hin
             if bp.expand:
                 if pend is not None:
-                    self._consume_output(pend, f.b(bp.w_e), bp.bn_e.y, bp.bn_e.acc_f, Min, bp.hidden, bp.cin)
+                    self._consume_output(pend, f.b(bp.w_e), bp.bn_e.y, bp.bn_e.acc_f, Min, bp.hidden, bp.cin,
+                                         fin=F(bp.bn_e))
                 elif inp_t is None:
                     self._pw_fwd(K.ACT_BN_RELU6, inp_bn.y, bp.w_e, bp.bn_e.y, bp.bn_e.acc_f, Min, bp.hidden, bp.cin,
-                                 pa=inp_bn.scale, pb=inp_bn.shift)
+                                 pa=inp_bn.scale, pb=inp_bn.shift, fin=F(bp.bn_e))
                 else:
-                    self._pw_fwd(K.ACT_NONE, inp_t, bp.w_e, bp.bn_e.y, bp.bn_e.acc_f, Min, bp.hidden, bp.cin)
+                    self._pw_fwd(K.ACT_NONE, inp_t, bp.w_e, bp.bn_e.y, bp.bn_e.acc_f, Min, bp.hidden, bp.cin,
+                                 fin=F(bp.bn_e))
                 self._fin_fwd(bp.bn_e, K.pw_num_partials(Min, bp.hidden, bp.cin), train)
                 dw_in = bp.bn_e
             else:
                 assert inp_t is None and pend is None, "t=1 block expects the (virtual) stem output"
                 dw_in = inp_bn
             K.dw_fwd(dw_in.y, dw_in.scale, dw_in.shift, K.ACT_BN_RELU6, f.b(bp.w_d), bp.bn_d.y, bp.bn_d.acc_f, B, Hin, Hin,
-                     bp.hidden, bp.stride)
+                     bp.hidden, bp.stride, fin=F(bp.bn_d))
             self._fin_fwd(bp.bn_d, K.dw_num_partials("fwd", B, Hin, Hin, bp.hidden, bp.stride), train)
             Mout = B * bp.Ho * bp.Wo
             self._pw_fwd(K.ACT_BN_RELU6, bp.bn_d.y, bp.w_p, bp.bn_p.y, bp.bn_p.acc_f, Mout, bp.cout, bp.hidden,
-                         pa=bp.bn_d.scale, pb=bp.bn_d.shift)
+                         pa=bp.bn_d.scale, pb=bp.bn_d.shift, fin=F(bp.bn_p))
             self._fin_fwd(bp.bn_p, K.pw_num_partials(Mout, bp.cout, bp.hidden), train)
             if self.FUSE_BLOCK_OUTPUT and not self.fp8:
                 pend = (bp.bn_p, inp_t if bp.residual else None, bp.o)
@@ -401,10 +452,10 @@ class MobileNetV2Executor:
         Mf = B * self.Hf * self.Hf
         if pend is not None:
             self._consume_output(pend, f.b(self.w_last), self.bn_last.y, self.bn_last.acc_f, Mf, self.C_last,
-                                 self.C_last_in)
+                                 self.C_last_in, fin=F(self.bn_last))
         else:
             self._pw_fwd(K.ACT_NONE, inp_t, self.w_last, self.bn_last.y, self.bn_last.acc_f, Mf, self.C_last,
-                         self.C_last_in)
+                         self.C_last_in, fin=F(self.bn_last))
         self._fin_fwd(self.bn_last, K.pw_num_partials(Mf, self.C_last, self.C_last_in), train)
         # head (+ its backward when training)
         K.head(self.bn_last.y, self.bn_last.scale, self.bn_last.shift, f.w(self.w_lin), f.w(self.b_lin),
@@ -412,7 +463,8 @@ class MobileNetV2Executor:
                self.hyper, train, 1.0 / B, logits=self.logits, loss=self.loss, correct=self.correct,
                dlogits=self.dlogits if train else None, pd=self.pd,
                g_out=self.bn_last.g if train else None, part=self.bn_last.acc_b if train else None,
-               dW=f.g(self.w_lin) if train else None, db=f.g(self.b_lin) if train else None)
+               dW=f.g(self.w_lin) if train else None, db=f.g(self.b_lin) if train else None,
+               fin=self.bn_last.fin_b if train else None)
 
     # ------------------------------------------------------------------ backward
     def backward(self):
@@ -431,7 +483,8 @@ class MobileNetV2Executor:
         # dgrad of the final conv -> gradient w.r.t. o_17 (feeds BN_p of block 17, linear)
         K.pw_gemm(K.PRO_BNBWD, K.EPI_BWD_LIN, bnl.g, f.bt(self.w_last), last_blk.G, last_blk.bn_p.acc_b, Mf,
                   self.C_last_in,
-                  self.C_last, A2=bnl.y, pa=bnl.a, pb=bnl.b, pc=bnl.c, Yt=last_blk.bn_p.y, R=None)
+                  self.C_last, A2=bnl.y, pa=bnl.a, pb=bnl.b, pc=bnl.c, Yt=last_blk.bn_p.y, R=None,
+                  fin=last_blk.bn_p.fin_b)
         P_g = K.pw_num_partials(Mf, self.C_last_in, self.C_last)
         last_blk.bn_p.finalize_bwd(last_blk.bn_p.acc_b, P_g)
         self._wgrad(lambda: K.pw_wgrad(bnl.g, bnl.y, bnl.a, bnl.b, bnl.c, last_blk.o, None, None, K.ACT_NONE,
@@ -450,13 +503,14 @@ class MobileNetV2Executor:
                 # fused dgrad + wgrad (x = relu6(BN_d(y_d)) rebuilt from the mask operand)
                 wpm = self._wpart[(bp.idx, "p")]
                 K.pw_bwd(K.EPI_BWD_RELU6, bp.G, bnp.y, bnp.a, bnp.b, bnp.c, f.bt(bp.w_p), bnd.g, bnd.y, bnd.acc_b, wpm,
-                         None, Mout, bp.cout, bp.hidden, es=bnd.scale, et=bnd.shift)
+                         None, Mout, bp.cout, bp.hidden, es=bnd.scale, et=bnd.shift, fin=bnd.fin_b)
                 self._wgrad(lambda: K.wgrad_reduce(wpm, K.pw_bwd_num_partials(Mout, bp.cout, bp.hidden),
                                                    bp.cout * bp.hidden, f.g(bp.w_p)))
                 bnd.finalize_bwd(bnd.acc_b, K.pw_bwd_num_partials(Mout, bp.cout, bp.hidden))
             else:
                 K.pw_gemm(K.PRO_BNBWD, K.EPI_BWD_RELU6, bp.G, f.bt(bp.w_p), bnd.g, bnd.acc_b, Mout, bp.hidden, bp.cout,
-                          A2=bnp.y, pa=bnp.a, pb=bnp.b, pc=bnp.c, Yt=bnd.y, es=bnd.scale, et=bnd.shift)
+                          A2=bnp.y, pa=bnp.a, pb=bnp.b, pc=bnp.c, Yt=bnd.y, es=bnd.scale, et=bnd.shift,
+                          fin=bnd.fin_b)
                 bnd.finalize_bwd(bnd.acc_b, K.pw_num_partials(Mout, bp.hidden, bp.cout))
                 # project wgrad
                 self._wgrad(lambda: K.pw_wgrad(bp.G, bnp.y, bnp.a, bnp.b, bnp.c, bnd.y, bnd.scale, bnd.shift,
@@ -471,14 +525,14 @@ class MobileNetV2Executor:
                 # the wgrad partials are reduced on the side stream
                 K.dw_dgrad(bnd.g, bnd.y, bnd.coef, f.b(bp.w_d), dw_in.y, dw_in.scale, dw_in.shift, dw_in.g,
                            dw_in.acc_b,
-                           B, Hin, Hin, bp.hidden, bp.stride, wpart=wpd)
+                           B, Hin, Hin, bp.hidden, bp.stride, wpart=wpd, fin=dw_in.fin_b)
                 dw_in.finalize_bwd(dw_in.acc_b, Pd)
                 self._wgrad(lambda: K.wgrad_reduce(wpd, Pd, 9 * bp.hidden, f.g(bp.w_d)))
             else:
                 # small maps (latency-bound): lean dgrad on the critical path, wgrad on the side stream
                 K.dw_dgrad(bnd.g, bnd.y, bnd.coef, f.b(bp.w_d), dw_in.y, dw_in.scale, dw_in.shift, dw_in.g,
                            dw_in.acc_b,
-                           B, Hin, Hin, bp.hidden, bp.stride)
+                           B, Hin, Hin, bp.hidden, bp.stride, fin=dw_in.fin_b)
                 dw_in.finalize_bwd(dw_in.acc_b, Pd)
                 self._wgrad(lambda: K.dw_wgrad(bnd.g, bnd.y, bnd.coef, dw_in.y, dw_in.scale, dw_in.shift, wg,
                                                f.g(bp.w_d), B, Hin, Hin, bp.hidden, bp.stride))
@@ -491,7 +545,7 @@ class MobileNetV2Executor:
                     wpe = self._wpart[(bp.idx, "e")]
                     K.pw_bwd(K.EPI_BWD_LIN, bne.g, bne.y, bne.a, bne.b, bne.c, f.bt(bp.w_e), prev.G, prev.bn_p.y,
                              prev.bn_p.acc_b, wpe, None, Min, bp.hidden, bp.cin, R=bp.G if bp.residual else None,
-                             X=prev.o)
+                             X=prev.o, fin=prev.bn_p.fin_b)
                     self._wgrad(lambda: K.wgrad_reduce(wpe, K.pw_bwd_num_partials(Min, bp.hidden, bp.cin),
                                                        bp.hidden * bp.cin, f.g(bp.w_e)))
                     prev.bn_p.finalize_bwd(prev.bn_p.acc_b, K.pw_bwd_num_partials(Min, bp.hidden, bp.cin))
@@ -499,7 +553,7 @@ class MobileNetV2Executor:
                     K.pw_gemm(K.PRO_BNBWD, K.EPI_BWD_LIN, bne.g, f.bt(bp.w_e), prev.G, prev.bn_p.acc_b, Min, bp.cin,
                               bp.hidden,
                               A2=bne.y, pa=bne.a, pb=bne.b, pc=bne.c, Yt=prev.bn_p.y,
-                              R=bp.G if bp.residual else None)
+                              R=bp.G if bp.residual else None, fin=prev.bn_p.fin_b)
                     prev.bn_p.finalize_bwd(prev.bn_p.acc_b, K.pw_num_partials(Min, bp.cin, bp.hidden))
                     self._wgrad(lambda: K.pw_wgrad(bne.g, bne.y, bne.a, bne.b, bne.c, prev.o, None, None,
                                                    K.ACT_NONE, wg, f.g(bp.w_e), Min, bp.hidden, bp.cin))
@@ -517,7 +571,7 @@ class MobileNetV2Executor:
                     stem_wg()
                 self._ready([self.stem_w])
         if self.side is not None:   # join: the optimizer (main stream) needs every gradient
-            torch.cuda.current_stream(self.device).wait_stream(self.side)
+            K.stream_wait(torch.cuda.current_stream(self.device), self.side)
 
     # ------------------------------------------------------------------ eval
     def eval_prepare(self):

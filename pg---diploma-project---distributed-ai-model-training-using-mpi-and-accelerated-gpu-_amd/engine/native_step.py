@@ -8,6 +8,7 @@ loss.backward(); optimizer.step(); torch.max(...); loss.item(); (...).item()``
 — two host syncs per batch and a CPU/PIL data pipeline.  Here the only host
 work per step is one 1 KB index copy and a graph replay.
 """
+import os
 from typing import Optional
 
 import torch
@@ -90,6 +91,8 @@ class NativeTrainStep:
         self.bn_broadcast = bn_broadcast and world_size > 1
         if self.bn_broadcast:
             self.bn_flat, self.bn_nbt = coalesce_bn_buffers(self.exe.model)
+            if hasattr(self.exe, "refresh_bn_fin"):
+                self.exe.refresh_bn_fin()   # fused BN finalize: descriptors point at the re-homed buffers
         # RCCL collectives are issued eagerly between graph segments; a single-graph
         # capture is used on one GPU
         self.use_graph = use_graph and world_size == 1
@@ -102,6 +105,11 @@ class NativeTrainStep:
         # applies to data-parallel runs too (not with the per-step BN buffer broadcast).
         self.graph_forward = graph_forward and not self.use_graph and not self.bn_broadcast
         self.fwd_graph: Optional[torch.cuda.CUDAGraph] = None
+        # eager steps replayed from a native launch plan (csrc/runtime/plan.h): same two-stream
+        # schedule as eager launching, none of its Python host cost (PGDIST_PLAN=0: off)
+        self.use_plan = (not self.use_graph and not self.graph_forward
+                         and getattr(self.exe, "PLAN_SAFE", False) and os.environ.get("PGDIST_PLAN", "1") == "1")
+        self.plan: Optional[K.LaunchPlan] = None
 
     # ------------------------------------------------------------------ setup
     @classmethod
@@ -144,6 +152,7 @@ class NativeTrainStep:
         st.idx = torch.zeros(batch, dtype=torch.int64, device=self.device)
         st.aug_params = torch.zeros(batch, K.AUG_NPARAMS, dtype=torch.float32, device=self.device)
         st.use_graph, st.graph, st._eager_runs = False, None, 0
+        st.use_plan, st.plan = False, None
         st.graph_forward, st.fwd_graph = False, None
         return st
 
@@ -154,6 +163,9 @@ class NativeTrainStep:
         assert tuple(src_u8.shape[1:3]) in ((32, 32), (self.S, self.S)), "source images: 32x32 or SxS"
         self.src = src_u8.contiguous()
         self.src_labels = labels.to(self.device, torch.int64).contiguous()
+        if getattr(self, "plan", None) is not None:   # the recorded augment launch reads the old pool
+            self.plan.free()
+            self.plan, self._eager_runs = None, 0
 
     def sync_from_rank0(self):
         mods = [m for m in self.exe.model.modules() if isinstance(m, torch.nn.BatchNorm2d)]
@@ -183,17 +195,17 @@ class NativeTrainStep:
                       double_resize=self.double_resize, seed=self.seed + 17 * self.rank, hyper=self.hyper,
                       epoch_ctr=0, out_hw=self.S)
         if self.bn_broadcast:
-            broadcast_parameters([self.bn_flat, self.bn_nbt])
+            K.plan_py(lambda: broadcast_parameters([self.bn_flat, self.bn_nbt]))
         exe.forward(train=True)
 
     def _back(self):
         """Backward (+ bucketed all-reduce), Adam and metrics."""
         exe = self.exe
         if self.reducer is not None:
-            self.reducer.begin()
+            K.plan_py(self.reducer.begin)
         exe.backward()
         if self.reducer is not None:
-            self.reducer.finish()
+            K.plan_py(self.reducer.finish)
         K.adam_flat(self.flat.master, self.flat.grad, self.flat.exp_avg, self.flat.exp_avg_sq,
                     self.flat.shadow, self.hyper, self.betas[0], self.betas[1], self.eps, self.wd,
                     1.0 / self.world)
@@ -214,6 +226,17 @@ class NativeTrainStep:
                     self._front()
             self.fwd_graph.replay()
             self._back()
+            return
+        if self.use_plan:
+            if self.plan is None:
+                if self._eager_runs < 2:   # warm-up: module loading / first-touch outside recording
+                    self._eager_runs += 1
+                    self._body()
+                    return
+                self.plan = K.LaunchPlan()
+                self.plan.record(self._body)   # runs this step eagerly while recording it
+                return
+            self.plan.replay()
             return
         if not self.use_graph:
             self._body()

@@ -111,6 +111,9 @@ class Trainer:
         cfg = self.cfg
         if cfg.model not in ("mobilenet_v2", "resnet50"):
             raise NotImplementedError("native HIP executors: mobilenet_v2, resnet50")
+        if cfg.deterministic:
+            from ..ops import kernels as K
+            K.set_deterministic(True)   # fixed-order BN statistics (bitwise-reproducible runs)
         self.step = NativeTrainStep(self.model, cfg.batch_size, self.device, img_size=cfg.img_size,
                                     lr=self.base_lr, betas=cfg.betas, eps=cfg.eps,
                                     weight_decay=cfg.weight_decay, world_size=self.world, rank=self.rank,

@@ -76,6 +76,38 @@ def deterministic() -> bool:
     return bn_rep() >= BN_REP_DETERMINISTIC
 
 
+BN_FIN_BYTES = None
+
+
+def bn_fin_desc(acc, ctr, rows, C, count, bwd, gamma=None, beta=None, eps=1e-5, momentum=0.1, rmean=None,
+                rvar=None, nbt=None, mean=None, rstd=None, scale=None, shift=None, coef=None, dgamma=None,
+                dbeta=None):
+    """Device descriptor of a BN finalize fused into the tail of its statistics producer
+    (bnfin.h): ``acc`` the producer's [rows][2][C] atomic accumulator (rows <= bn_rep()),
+    ``ctr`` one int32 arrival counter (zero; re-armed by the kernel).  Forward (bwd=0) writes
+    mean / rstd / scale / shift and the running statistics; backward (bwd=1) reads mean / rstd
+    and writes coef [3][C], dgamma, dbeta.  Pass the returned tensor as ``fin=`` to the
+    producer wrapper (stem_fwd, pw_gemm, pw_gemm_f8, pw_bwd, dw_fwd, dw_dgrad, head)."""
+    _chk(acc, F32, 2 * rows * C, "acc")
+    _chk(ctr, torch.int32, 1, "ctr")
+    for t, n in ((gamma, C), (beta, C), (rmean, C), (rvar, C), (mean, C), (rstd, C), (scale, C), (shift, C),
+                 (coef, 3 * C), (dgamma, C), (dbeta, C)):
+        _chk(t, F32, n)
+    raw = lib().bn_fin_pack(_p(acc), _p(ctr), int(rows), int(C), float(count), int(bwd), _p(gamma), _p(beta),
+                            float(eps), float(momentum), _p(rmean), _p(rvar), _p(nbt), _p(mean), _p(rstd),
+                            _p(scale), _p(shift), _p(coef), _p(dgamma), _p(dbeta))
+    host = torch.frombuffer(bytearray(raw), dtype=torch.uint8)
+    return host.to(acc.device)
+
+
+def _arm(fin):
+    """Arm a fused-finalize descriptor for the launch that immediately follows."""
+    if fin is not None:
+        if not (fin.is_cuda and fin.dtype == torch.uint8):
+            raise TypeError("fin: a device descriptor from bn_fin_desc")
+        lib().bn_fin_arm(fin.data_ptr())
+
+
 def bn_rows(P):
     """Rows a BN finalize reduces after a producer with P partial rows accumulated atomically
     (rows = min(P, bn_rep()); the accumulator must be zeroed before the producer runs)."""
@@ -157,13 +189,14 @@ def _dw_check(B, H, W, C, stride):
         raise ValueError("depthwise: stride must be 1 or 2")
 
 
-def dw_fwd(x, in_s, in_t, act, w, y, part, B, H, W, C, stride):
+def dw_fwd(x, in_s, in_t, act, w, y, part, B, H, W, C, stride, fin=None):
     _dw_check(B, H, W, C, stride)
     Ho, Wo = dw_out_hw(H, W, stride)
     _chk(x, BF16, B * H * W * C, "x")
     _chk(w, BF16, C * 9, "w")
     _chk(y, BF16, B * Ho * Wo * C, "y")
     _chk(part, F32, bn_rows(dw_num_partials("fwd", B, H, W, C, stride)) * 2 * C, "part")
+    _arm(fin)
     lib().dw_fwd(_p(x), _p(in_s), _p(in_t), int(act), _p(w), _p(y), _p(part), B, H, W, C, stride, _s())
 
 
@@ -172,7 +205,7 @@ def dw_dgrad_wgrad_workspace(B, H, W, C, stride):
     return lib().dw_dgrad_wgrad_workspace_floats(B, H, W, C, stride)
 
 
-def dw_dgrad(g, yself, coef, w, yprev, ps, pt, gout, part, B, H, W, C, stride, wpart=None):
+def dw_dgrad(g, yself, coef, w, yprev, ps, pt, gout, part, B, H, W, C, stride, wpart=None, fin=None):
     """Depthwise dgrad (+ BN partials of gout).  With ``wpart`` the layer's weight gradient is
     accumulated in the same pass into split partials wpart[P][9][C] (P = dw_num_partials
     ("dgrad", ...)); reduce them with ``wgrad_reduce(wpart, P, 9 * C, grad)``."""
@@ -184,6 +217,7 @@ def dw_dgrad(g, yself, coef, w, yprev, ps, pt, gout, part, B, H, W, C, stride, w
     _chk(gout, BF16, B * H * W * C, "gout")
     _chk(part, F32, bn_rows(dw_num_partials("dgrad", B, H, W, C, stride)) * 2 * C, "part")
     _chk(wpart, F32, dw_dgrad_wgrad_workspace(B, H, W, C, stride), "wpart")
+    _arm(fin)
     lib().dw_dgrad(_p(g), _p(yself), _p(coef), _p(w), _p(yprev), _p(ps), _p(pt), _p(gout), _p(part),
                    B, H, W, C, stride, _p(wpart), _s())
 
@@ -210,7 +244,7 @@ def pw_num_partials(M, N, K):
 
 
 def pw_gemm(pro, epi, A, W, out, part, M, N, K, A2=None, pa=None, pb=None, pc=None, Yt=None,
-            es=None, et=None, R=None, Aout=None):
+            es=None, et=None, R=None, Aout=None, fin=None):
     """out[M,N] = prologue(A)[M,K] @ W^T with W [N,K] in GEMM terms for every mode.
 
     For the dgrad (pro == PRO_BNBWD) W is the TRANSPOSED conv weight ([Cin][Cout],
@@ -237,6 +271,7 @@ def pw_gemm(pro, epi, A, W, out, part, M, N, K, A2=None, pa=None, pb=None, pc=No
     if epi == EPI_BWD_RELU6:
         assert es is not None and et is not None
     _chk(Aout, BF16, M * K, "Aout")
+    _arm(fin)
     lib().pw_gemm(int(pro), int(epi), _p(A), _p(A2), _p(pa), _p(pb), _p(pc), _p(W), _p(out), _p(Yt),
                   _p(es), _p(et), _p(R), _p(part), M, N, K, _p(Aout), _s())
 
@@ -254,7 +289,7 @@ def fp8_pitch(K: int) -> int:
     return (K + 63) // 64 * 64
 
 
-def pw_gemm_f8(pro, A, W8, wsc, out, part, M, N, K, pa=None, pb=None, asc=None):
+def pw_gemm_f8(pro, A, W8, wsc, out, part, M, N, K, pa=None, pb=None, asc=None, fin=None):
     """fp8 forward 1x1 conv: out[M,N] = bf16( (e4m3(asc*prologue(A)) . W8^T) * wsc[n] / asc ).
 
     W8 is the per-output-channel e4m3 weight copy [N][fp8_pitch(K)] (see :func:`w8_quant`),
@@ -273,6 +308,7 @@ def pw_gemm_f8(pro, A, W8, wsc, out, part, M, N, K, pa=None, pb=None, asc=None):
     if pro != ACT_NONE:
         assert pa is not None and pb is not None and pa.numel() >= K
     a = float(FP8_ASC[pro] if asc is None else asc)
+    _arm(fin)
     lib().pw_gemm_f8(int(pro), _p(A), _p(pa), _p(pb), _p(W8), ld, _p(wsc), a, _p(out), _p(part), M, N, K, _s())
 
 
@@ -309,7 +345,7 @@ def pw_bwd_wgrad_workspace(M, Kg, Ng):
 
 
 def pw_bwd(epi, G, Y, ca, cb, cc, WT, out, Yt, part, wpart, grad, M, Kg, Ng, es=None, et=None, R=None,
-           X=None):
+           X=None, fin=None):
     """Fused 1x1-conv backward (one read of G, Y):
 
     dy = ca*G + cb*Y + cc                      [M, Kg]   (this conv's BN backward)
@@ -338,6 +374,7 @@ def pw_bwd(epi, G, Y, ca, cb, cc, WT, out, Yt, part, wpart, grad, M, Kg, Ng, es=
         assert X is not None
     else:
         raise ValueError(f"pw_bwd: bad epilogue {epi}")
+    _arm(fin)
     lib().pw_bwd(int(epi), _p(G), _p(Y), _p(ca), _p(cb), _p(cc), _p(WT), _p(out), _p(Yt), _p(es), _p(et),
                  _p(R), _p(X), _p(part), _p(wpart), _p(grad), M, Kg, Ng, _s())
 
@@ -375,7 +412,7 @@ def _stem_px_default():
     return int(v)
 
 
-def stem_fwd(img, w, y, part, B, H, W, px=None):
+def stem_fwd(img, w, y, part, B, H, W, px=None, fin=None):
     """Stem 3x3 s2 conv forward; ``px`` output pixels per thread (1, 2 or 4; default from
     PGDIST_STEM_PX, else 1 — the measured fastest)."""
     px = _stem_px_default() if px is None else int(px)
@@ -386,6 +423,7 @@ def stem_fwd(img, w, y, part, B, H, W, px=None):
     _chk(w, BF16, 32 * 27, "w")
     _chk(y, BF16, B * Ho * Wo * 32, "y")
     _chk(part, F32, bn_rows(stem_num_partials(B, H, W)) * 2 * 32, "part")
+    _arm(fin)
     lib().stem_fwd(_p(img), _p(w), _p(y), _p(part), B, H, W, px, _s())
 
 
@@ -406,7 +444,7 @@ def stem_wgrad(G, Y, ga, gb, gc, img, part, grad, B, H, W, O=32):
 # --------------------------------------------------------------------------- head
 def head(y, s, t, Wl, bl, labels, B, HW, C, NC, drop_p, seed, hyper, train, loss_scale,
          logits=None, loss=None, correct=None, dlogits=None, pd=None, g_out=None, part=None,
-         dW=None, db=None):
+         dW=None, db=None, fin=None):
     if NC > 16 or C % 8 or C // 8 > 256:
         raise ValueError("head kernel supports NC <= 16 and C <= 2048 (C % 8 == 0)")
     _chk(y, BF16, B * HW * C, "y")
@@ -423,6 +461,7 @@ def head(y, s, t, Wl, bl, labels, B, HW, C, NC, drop_p, seed, hyper, train, loss
         _chk(part, F32, bn_rows(B) * 2 * C, "part")
     if labels is not None:
         _chk(labels, torch.int64, B, "labels")
+    _arm(fin if train else None)
     lib().head(_p(y), _p(s), _p(t), _p(Wl), _p(bl), _p(labels), B, HW, C, NC, float(drop_p),
                int(seed) & ((1 << 64) - 1), _p(hyper), int(bool(train)), float(loss_scale), _p(logits),
                _p(loss), _p(correct), _p(dlogits), _p(pd), _p(g_out), _p(part), _p(dW), _p(db), _s())
@@ -642,3 +681,59 @@ def image_prep(src, idx, labels_src, out, labels_out, seed=0, hyper=None):
     _chk(labels_out, torch.int64, B, "labels_out")
     lib().image_prep(_p(src), _p(idx), _p(labels_src), B, H, W, int(seed) & ((1 << 64) - 1), _p(hyper), _p(out),
                      _p(labels_out), _s())
+
+
+# --------------------------------------------------------------------------- launch plans
+def stream_wait(waiter, signaler):
+    """``waiter`` waits for the work enqueued so far on ``signaler`` (torch streams); unlike
+    ``Stream.wait_stream`` it is recorded into an open launch plan."""
+    lib().stream_wait(waiter.cuda_stream, signaler.cuda_stream)
+
+
+def memset(t: torch.Tensor, value: int = 0):
+    """Byte-wise fill of a contiguous device tensor on the current stream (recordable)."""
+    if not (t.is_cuda and t.is_contiguous()):
+        raise ValueError("memset: contiguous device tensor expected")
+    lib().memset_async(t.data_ptr(), int(value), t.numel() * t.element_size(), _s())
+
+
+def plan_py(fn):
+    """Run ``fn()`` now and, while a launch plan is being recorded, again at this point of
+    every replay (host-side Python work of a step, e.g. the DDP bucket hand-off)."""
+    lib().plan_py(fn)
+
+
+def plan_recording() -> bool:
+    return lib().plan_recording()
+
+
+class LaunchPlan:
+    """One training step recorded as a native launch sequence (csrc/runtime/plan.h).
+
+    ``record(fn)`` runs ``fn()`` eagerly and records every native launch, stream wait,
+    memset and ``plan_py`` callback it issues; ``replay()`` re-issues them from C++ (no Python
+    wrapper or validation in between).  Everything ``fn`` passes to the kernels must stay
+    valid (fixed buffers; per-step values in device memory) — the hipGraph-capture contract."""
+
+    def __init__(self):
+        self.id = None
+
+    def record(self, fn):
+        lib().plan_record_begin()
+        try:
+            fn()
+        except BaseException:
+            lib().plan_record_abort()
+            raise
+        self.id = lib().plan_record_end()
+
+    def replay(self):
+        lib().plan_replay(self.id)
+
+    def __len__(self):
+        return 0 if self.id is None else lib().plan_size(self.id)
+
+    def free(self):
+        if self.id is not None:
+            lib().plan_free(self.id)
+            self.id = None

@@ -197,6 +197,31 @@ def test_bn_mode_switch_after_build_rejected(dev):
         K.set_deterministic(False)
 
 
+def test_launch_plan_matches_eager(dev, deterministic, monkeypatch):
+    """Steps replayed from a native launch plan (recorded on the 3rd step) give bitwise the
+    same weights and metrics as eager launching (deterministic BN statistics)."""
+    from pgdist.engine.native_step import NativeTrainStep
+    src = torch.randint(0, 256, (16, 32, 32, 3), dtype=torch.uint8, device=dev,
+                        generator=torch.Generator(device=dev).manual_seed(3))
+    labels = torch.arange(16, device=dev) % 10
+    out = {}
+    for plan in ("1", "0"):
+        monkeypatch.setenv("PGDIST_PLAN", plan)
+        torch.manual_seed(0)
+        st = NativeTrainStep(mobilenet_v2(10), 8, dev, img_size=64, lr=1e-3, use_graph=False)
+        assert st.use_plan == (plan == "1")
+        st.set_data(src, labels)
+        for i in range(6):
+            st.run((torch.arange(8, device=dev) + 3 * i) % 16)
+        torch.cuda.synchronize()
+        if plan == "1":
+            assert st.plan is not None and len(st.plan) > 200
+        out[plan] = (st.flat.master.clone(), st.flat.exp_avg.clone(), st.read_metrics())
+    assert torch.equal(out["1"][0], out["0"][0])
+    assert torch.equal(out["1"][1], out["0"][1])
+    assert out["1"][2] == out["0"][2]
+
+
 @pytest.mark.parametrize("mode", ["forward_graph", "full_graph"])
 def test_graph_modes_match_eager(dev, mode, deterministic):
     """The forward-only hipGraph (replayed forward + eager two-stream backward) and the
