@@ -115,6 +115,11 @@ __global__ __launch_bounds__(128) void bn_finalize_small_kernel(
     float *__restrict__ shift, float *__restrict__ coef, float *__restrict__ dgamma, float *__restrict__ dbeta) {
   const int c = blockIdx.x * 128 + threadIdx.x;
   if (c < C) {
+    // every load of the thread is issued up front (one memory latency, not a chain of them)
+    const float g = gamma ? gamma[c] : 1.f;
+    const float b = (!BWD && beta) ? beta[c] : 0.f;
+    const float rm0 = (!BWD && rmean) ? rmean[c] : 0.f, rv0 = (!BWD && rmean) ? rvar[c] : 0.f;
+    const float mu = BWD ? mean[c] : 0.f, rs = BWD ? rstd[c] : 0.f;
     float v[2 * kBnRep];
 #pragma unroll
     for (int r = 0; r < kBnRep; ++r) {
@@ -129,8 +134,30 @@ __global__ __launch_bounds__(128) void bn_finalize_small_kernel(
       s0 += m * (double)v[2 * r];
       s1 += m * (double)v[2 * r + 1];
     }
-    if (BWD) bn_bwd_channel(c, C, s0, s1, (double)count, mean, rstd, gamma, coef, dgamma, dbeta);
-    else bn_fwd_channel(c, s0, s1, (double)count, gamma, beta, eps, momentum, rmean, rvar, mean, rstd, scale, shift);
+    const double n = (double)count;
+    if (BWD) {
+      const double sgx = (s1 - (double)mu * s0) * rs;   // sum g * xhat
+      if (dgamma) dgamma[c] = (float)sgx;
+      if (dbeta) dbeta[c] = (float)s0;
+      const double a = (double)g * rs;
+      coef[c] = (float)a;
+      coef[C + c] = (float)(-a * rs * sgx / n);
+      coef[2 * C + c] = (float)(-a * s0 / n + a * rs * (double)mu * sgx / n);
+    } else {
+      const double m = s0 / n;
+      double var = s1 / n - m * m;
+      if (var < 0.0) var = 0.0;
+      const float r = (float)(1.0 / sqrt(var + (double)eps));
+      mean[c] = (float)m;
+      rstd[c] = r;
+      scale[c] = g * r;
+      shift[c] = b - (float)m * g * r;
+      if (rmean) {
+        const double unbiased = n > 1.0 ? var * n / (n - 1.0) : var;
+        rmean[c] = (1.f - momentum) * rm0 + momentum * (float)m;
+        rvar[c] = (1.f - momentum) * rv0 + momentum * (float)unbiased;
+      }
+    }
   }
   if (!BWD && nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
 }
