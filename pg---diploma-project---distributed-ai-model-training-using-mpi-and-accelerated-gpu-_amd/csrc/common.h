@@ -33,8 +33,13 @@ PG_DEVICE void unpack8(const uint4 &u, float (&f)[8]) {
   }
 }
 
+// two floats -> two round-to-nearest-even bf16 in one v_cvt_pk_bf16_f32 (converting them one
+// at a time costs two conversions and an OR; the ext_vector __builtin_convertvector form of the
+// same instruction kept some arrays of conv_wgrad_kernel out of registers -> scratch)
 PG_DEVICE uint32_t pack2(float a, float b) {
-  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+  uint32_t r;
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
 }
 
 PG_DEVICE uint4 pack8(const float (&f)[8]) {

@@ -11,10 +11,12 @@
 // Per 64-row tile (4 waves, grid-stride over M, ALL loads of a tile — G, Y and the
 // epilogue operands — prefetched one tile ahead; one N tile spans the whole Ng
 // of the project convs so G, Y are read exactly once):
-//   * dy is computed once from (G, Y) and written to LDS twice: row-major
-//     dyN[m][kg] (A operand of the dgrad MFMA) and transposed dyT[kg][m]
-//     (A operand of the wgrad MFMA, reduction over m);
-//   * the wgrad's second operand x (this conv's input) is staged transposed:
+//   * dy is computed once from (G, Y) and written to LDS once, row-major dyN[m][kg]: the
+//     dgrad MFMA reads it by rows (A operand), the wgrad MFMA (reduction over m) reads the
+//     same image column-wise with the gfx950 transposing read ds_read_b64_tr_b16;
+//   * the wgrad's second operand x (this conv's input) is staged row-major xN[m][ng], also
+//     read transposed (the former transposed copies dyT / xT cost 8 ds_write_b64 per item at
+//     8-10 bank-conflict cycles per LDS instruction, SQ_LDS_BANK_CONFLICT):
 //       EPI_BWD_RELU6 (project conv): x = relu6(Yt*s + t) — Yt is the tensor the
 //         dgrad epilogue reads anyway for the ReLU6 mask, so x costs no HBM bytes;
 //       EPI_BWD_LIN   (expand conv):  x = X, the materialised block input;
@@ -28,6 +30,8 @@
 #include <cstdlib>
 
 enum { EPI_BWD_RELU6_ = 1, EPI_BWD_LIN_ = 2 };   // same values as pwconv.hip
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
 
 namespace {
 struct PwBwdArgs {
@@ -47,13 +51,12 @@ struct PwBwdArgs {
 };
 template <int KP, int BN, int BM>
 struct BwdLds {
-  static constexpr int LDA = KP + 8, LDM = BM + 8, LDC = BN + 8;
+  static constexpr int LDA = KP + 8, LDX = BN + 8, LDC = BN + 8;
   static constexpr int WT = 0;                              // [BN][LDA] W^T tile (resident)
   static constexpr int STG = WT + BN * LDA * 2;             // per-tile staging:
   static constexpr int DYN = STG;                           //   dyN [BM][LDA]
-  static constexpr int DYT = DYN + BM * LDA * 2;            //   dyT [KP][LDM]
-  static constexpr int XT = DYT + KP * LDM * 2;             //   xT  [BN][LDM]
-  static constexpr int STG_END = XT + BN * LDM * 2;
+  static constexpr int XN = DYN + BM * LDA * 2;             //   xN  [BM][LDX]
+  static constexpr int STG_END = XN + BM * LDX * 2;
   static constexpr int CS = STG;                            // C tile [BM][LDC] aliases the staging
   static constexpr int RED = STG;                           // [BM/4][BN] floats at the very end
   static constexpr int CS_END = CS + BM * LDC * 2;
@@ -69,7 +72,7 @@ struct BwdLds {
 template <int EPI, int KP, int BN, int BM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void pw_bwd_fused_kernel(PwBwdArgs p) {
   using L = BwdLds<KP, BN, BM>;
-  constexpr int LDA = L::LDA, LDM = L::LDM, LDC = L::LDC;
+  constexpr int LDA = L::LDA, LDX = L::LDX, LDC = L::LDC;
   constexpr int CT = BN / 16;
   constexpr int RGS = BM / 16;                   // dgrad row groups of 16
   constexpr int RPW = RGS >= 4 ? RGS / 4 : 1;    // row groups per wave
@@ -88,8 +91,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t *WTs = reinterpret_cast<bf16_t *>(smem + L::WT);
   bf16_t *dyN = reinterpret_cast<bf16_t *>(smem + L::DYN);
-  bf16_t *dyT = reinterpret_cast<bf16_t *>(smem + L::DYT);
-  bf16_t *xT = reinterpret_cast<bf16_t *>(smem + L::XT);
+  bf16_t *xN = reinterpret_cast<bf16_t *>(smem + L::XN);
   bf16_t *Cs = reinterpret_cast<bf16_t *>(smem + L::CS);
   float *Red = reinterpret_cast<float *>(smem + L::RED);
   float *Ps = reinterpret_cast<float *>(smem + L::PS);
@@ -170,7 +172,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
   for (int mt = blockIdx.x; mt < nmt; mt += gridDim.x) {
     const int m0 = mt * BM;
     __syncthreads();                 // previous tile's epilogue is done with Cs (aliases the staging)
-    // ---- stage dy (row-major + transposed) and x (transposed) for this tile
+    // ---- stage dy and x (row-major) for this tile
 #pragma unroll
     for (int i = 0; i < IDY; ++i) {
       const int it = tid + i * 256;
@@ -192,13 +194,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[q][j] = valid ? bf2f(f2bf(fmaf(a[j], g[j], fmaf(b[j], y[j], c[j])))) : 0.f;
           *reinterpret_cast<uint4 *>(dyN + (m4 * 4 + q) * LDA + c8) = pack8(v[q]);
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          uint2 w;
-          w.x = pack2(v[0][j], v[1][j]);
-          w.y = pack2(v[2][j], v[3][j]);
-          *reinterpret_cast<uint2 *>(dyT + (c8 + j) * LDM + m4 * 4) = w;
         }
       }
     }
@@ -224,12 +219,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
       }
       if (it < NX) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          uint2 w;
-          w.x = pack2(v[0][j], v[1][j]);
-          w.y = pack2(v[2][j], v[3][j]);
-          *reinterpret_cast<uint2 *>(xT + (c8 + j) * LDM + m4 * 4) = w;
-        }
+        for (int q = 0; q < 4; ++q) *reinterpret_cast<uint4 *>(xN + (m4 * 4 + q) * LDX + c8) = pack8(v[q]);
       }
     }
     __syncthreads();
@@ -255,7 +245,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
                                                               __builtin_bit_cast(bf16x8_t, bf), acc[r][c], 0, 0, 0);
       }
     }
-    // ---- wgrad MFMA: dW[kg][ng] over this tile's 64 rows
+    // ---- wgrad MFMA: dW[kg][ng] over this tile's rows.  Both operands are transposed reads of
+    // the row-major images: lane 4q+p of each 16-lane group addresses row m0+q, columns 4p..4p+3
+    // of a 4 x 16 block and receives one column (4 rows); rows 8g..8g+3 and 8g+4..8g+7 of the
+    // 32-row step give lane (i, g) the 8 k-values of column i (EXEC is full: t is wave-uniform)
+    const int trow = 8 * (lane >> 4) + ((lane & 15) >> 2), tcol = 4 * (lane & 3);
 #pragma unroll
     for (int u = 0; u < WPW; ++u) {
       const int t = wave + 4 * u;
@@ -263,8 +257,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
         const int ti = t / (BN / 16), tj = t % (BN / 16);
 #pragma unroll
         for (int ms = 0; ms < BM / 32; ++ms) {
-          const s16x8_t af = *reinterpret_cast<const s16x8_t *>(dyT + (ti * 16 + (lane & 15)) * LDM + ms * 32 + 8 * (lane >> 4));
-          const s16x8_t bf = *reinterpret_cast<const s16x8_t *>(xT + (tj * 16 + (lane & 15)) * LDM + ms * 32 + 8 * (lane >> 4));
+          const bf16_t *pa = dyN + (ms * 32 + trow) * LDA + ti * 16 + tcol;
+          const bf16_t *pb = xN + (ms * 32 + trow) * LDX + tj * 16 + tcol;
+          const s16x4_t a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)pa);
+          const s16x4_t a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)(pa + 4 * LDA));
+          const s16x4_t b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)pb);
+          const s16x4_t b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)(pb + 4 * LDX));
+          const s16x8_t af = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
+          const s16x8_t bf = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
           accW[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af),
                                                             __builtin_bit_cast(bf16x8_t, bf), accW[u], 0, 0, 0);
         }
