@@ -39,6 +39,8 @@ void bn_fin_arm(const void *desc);
 std::string bn_fin_pack(float *, int *, int, int, float, int, const float *, const float *, float, float, float *,
                         float *, long long *, float *, float *, float *, float *, float *, float *, float *);
 void bn_set_rep(int rep);
+void conv_set_glds(int mode);
+int conv_get_glds();
 int dw_dgrad_num_partials(int, int, int, int, int);
 int dw_wgrad_num_partials(int, int, int, int, int);
 void launch_dw_fwd(const bf16_t *, const float *, const float *, int, const bf16_t *, bf16_t *,
@@ -99,6 +101,8 @@ void launch_conv_wgrad(const bf16_t *, const bf16_t *, const float *, const floa
                        const bf16_t *, const float *, const float *, int, float *, float *, int, int, int, int,
                        int, int, int, int, int, hipStream_t);
 void launch_conv_wt(const bf16_t *, bf16_t *, const int *, int, hipStream_t);
+void launch_bn_mat(int, const bf16_t *, const bf16_t *, const float *, const float *, const float *, bf16_t *, int, int,
+                   hipStream_t);
 void launch_res_out(const bf16_t *, const float *, const float *, const bf16_t *, const float *, const float *,
                     bf16_t *, long long, int, hipStream_t);
 void launch_maxpool_fwd(const bf16_t *, const float *, const float *, bf16_t *, uint8_t *, int, int, int, int,
@@ -187,6 +191,8 @@ PYBIND11_MODULE(_pgdist_C, m) {
                                  ptr<float>(mean), ptr<float>(rstd), ptr<float>(scale), ptr<float>(shift),
                                  ptr<float>(coef), ptr<float>(dgamma), ptr<float>(dbeta)));
   });
+  m.def("conv_set_glds", &conv_set_glds, "dense conv staging: 0 register-staged, 2/3 LDS-DMA buffers");
+  m.def("conv_get_glds", &conv_get_glds);
   m.def("bn_set_rep", &bn_set_rep, "set the replica rows (large = one row per workgroup: deterministic)");
   m.def("dw_dgrad_num_partials", &dw_dgrad_num_partials);
   m.def("dw_wgrad_num_partials", &dw_wgrad_num_partials);
@@ -332,6 +338,12 @@ PYBIND11_MODULE(_pgdist_C, m) {
       launch_conv_wgrad(ptr<bf16_t>(G), ptr<bf16_t>(Y), ptr<float>(ga), ptr<float>(gb), ptr<float>(gc),
                         ptr<bf16_t>(x), ptr<float>(xs), ptr<float>(xt), xpro, ptr<float>(ws), ptr<float>(grad), Nb,
                         H, W, Ci, N, R, Sk, st, pad, S(s));
+    });
+  });
+  m.def("bn_mat", [](int mode, P G, P Y, P a, P b, P c, P out, int M, int C, P s) {
+    pgdist_rt::run_op([=] {
+      launch_bn_mat(mode, ptr<bf16_t>(G), ptr<bf16_t>(Y), ptr<float>(a), ptr<float>(b), ptr<float>(c),
+                    ptr<bf16_t>(out), M, C, S(s));
     });
   });
   m.def("conv_wt", [](P src, P dst, P tab, int n, P s) {

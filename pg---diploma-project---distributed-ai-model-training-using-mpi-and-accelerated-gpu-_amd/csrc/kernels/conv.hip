@@ -58,6 +58,7 @@ struct ConvArgs {
   int Mc;               // GEMM rows per class
   int Hc, Wc;           // dgrad: class image (Ho / st, Wo / st); fwd: Ho, Wo
   int nmt;              // M tiles per class
+  int Nb;               // images (operand extents for the buffer descriptors)
   int ntap[4];
   signed char tr[4][9], ts[4][9], tdh[4][9], tdw[4][9];
 };
@@ -81,6 +82,148 @@ PG_DEVICE void ld8f(const float *p, float (&v)[8]) {
 // ===========================================================================
 // forward / dgrad implicit GEMM
 // ===========================================================================
+// Epilogue shared by the register-staged and the LDS-DMA implicit-GEMM kernels: the bf16 C
+// tile goes through LDS (smem, free after the K loop), then 16-B row chunks with the fused
+// backward operands and the BN partial sums of the tile's columns.
+template <int MODE, int EPI, int BM, int BN>
+PG_DEVICE void conv_epilogue(const ConvArgs &p, f32x4_t (&acc)[BM / 32][BN / 32], char *smem, int m0, int n0,
+                             int mt, int cls, int ph, int pw) {
+  constexpr int RT = BM / 32, CTW = BN / 32;
+  constexpr int LDC = BN + 8;
+  constexpr int CH = BN / 8, RSTEP = 256 / CH, NP = BM / RSTEP;
+  bf16_t *Cs = reinterpret_cast<bf16_t *>(smem);     // [BM][LDC]
+  float *Red = reinterpret_cast<float *>(smem);      // [RSTEP][BN] (end)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nmt = p.nmt;
+  const int HWc = p.Hc * p.Wc;
+  // bf16 C tile in LDS, then 16-B row chunks.  The epilogue operands of the
+  // first EB rows are loaded before the C tile is staged; rows past the end are clamped to
+  // a valid row (loads are unconditional, results discarded) so hipcc keeps them in flight.
+  constexpr bool E_R = EPI == CE_BWD_R || EPI == CE_BWD_RXY || EPI == CE_BWD_RXYY;
+  constexpr bool E_X = EPI == CE_BWD_RXY || EPI == CE_BWD_RXYY;
+  constexpr bool E_YT = EPI == CE_BWD_RELU || EPI == CE_BWD_RXY || EPI == CE_BWD_RXYY;
+  constexpr bool E_YT2 = EPI == CE_BWD_RXYY;
+  constexpr bool STATS = EPI == CE_FWD || E_YT;
+  constexpr int EB = NP < 4 ? NP : 4;
+  const int my_chunk = tid % CH;
+  const bool colok = n0 + my_chunk * 8 < p.N;
+  const int ncol0 = colok ? n0 + my_chunk * 8 : 0;
+  float s0[8], s1[8], s2[8], es[8], et[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s0[j] = s1[j] = s2[j] = 0.f;
+  if constexpr (EPI == CE_BWD_RELU) {
+    ld8f(p.es + ncol0, es);
+    ld8f(p.et + ncol0, et);
+  }
+  uint4 oy[EB], orr[EB], ox[EB], oy2[EB];
+  size_t offs[EB];
+  bool okr[EB];
+  auto issue = [&](int i0) {
+#pragma unroll
+    for (int e = 0; e < EB; ++e) {
+      const int rr = tid / CH + (i0 + e) * RSTEP;
+      int m = m0 + rr;
+      okr[e] = m < p.Mc && colok;
+      if (m >= p.Mc) m = p.Mc - 1;
+      size_t pix;
+      if constexpr (MODE == CM_FWD) {
+        pix = m;
+      } else {
+        const int b = m / HWc, rem = m % HWc, hh = rem / p.Wc, ww = rem % p.Wc;
+        pix = ((size_t)b * p.Ho + hh * p.stride + ph) * p.Wo + ww * p.stride + pw;
+      }
+      offs[e] = pix * p.N + ncol0;
+      if constexpr (E_YT) oy[e] = ldg16(p.Yt + offs[e]);
+      if constexpr (E_R) orr[e] = ldg16(p.Rg + offs[e]);
+      if constexpr (E_X) ox[e] = ldg16(p.X + offs[e]);
+      if constexpr (E_YT2) oy2[e] = ldg16(p.Yt2 + offs[e]);
+    }
+  };
+  issue(0);
+#pragma unroll
+  for (int c = 0; c < CTW; ++c) {
+    const int col = wn * (BN / 2) + c * 16 + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) Cs[(wm * (BM / 2) + r * 16 + 4 * (lane >> 4) + j) * LDC + col] = f2bf(acc[r][c][j]);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i0 = 0; i0 < NP; i0 += EB) {
+    if (i0 > 0) issue(i0);
+#pragma unroll
+    for (int e = 0; e < EB; ++e) {
+      const int rr = tid / CH + (i0 + e) * RSTEP;
+      float v[8];
+      unpack8(*reinterpret_cast<const uint4 *>(Cs + rr * LDC + my_chunk * 8), v);
+      if constexpr (EPI == CE_FWD) {
+        if (okr[e]) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { s0[j] += v[j]; s1[j] = fmaf(v[j], v[j], s1[j]); }
+        }
+      } else {
+        float yt[8];
+        if constexpr (E_YT) unpack8(oy[e], yt);
+        if constexpr (EPI == CE_BWD_RELU) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = fmaf(yt[j], es[j], et[j]) > 0.f ? v[j] : 0.f;
+        }
+        if constexpr (E_R) {
+          float rv[8];
+          unpack8(orr[e], rv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] += rv[j];
+        }
+        if constexpr (E_X) {
+          float xv[8];
+          unpack8(ox[e], xv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = xv[j] > 0.f ? v[j] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = bf2f(f2bf(v[j]));
+        if (okr[e]) {
+          if constexpr (E_YT) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { s0[j] += v[j]; s1[j] = fmaf(v[j], yt[j], s1[j]); }
+          }
+          if constexpr (E_YT2) {
+            float y2[8];
+            unpack8(oy2[e], y2);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s2[j] = fmaf(v[j], y2[j], s2[j]);
+          }
+        }
+      }
+      if (okr[e]) stg16(p.out + offs[e], pack8(v));
+    }
+  }
+  if constexpr (!STATS) return;
+  const bool has_yt2 = E_YT2;
+  __syncthreads();
+  // ---- BN partials of this tile's columns -> part[cls*nmt + mt][2][N] (and part2)
+  const int prow = cls * nmt + mt;
+  const int nstat = has_yt2 ? 3 : 2;
+  for (int s = 0; s < nstat; ++s) {
+    const int rgrp = tid / CH;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Red[rgrp * BN + my_chunk * 8 + j] = s == 0 ? s0[j] : (s == 1 ? s1[j] : s2[j]);
+    __syncthreads();
+    for (int c = tid; c < BN; c += 256) {
+      float a = 0.f;
+      for (int g = 0; g < RSTEP; ++g) a += Red[g * BN + c];
+      if (n0 + c < p.N) {
+        if (s < 2) p.part[((size_t)prow * 2 + s) * p.N + n0 + c] = a;
+        if (s == 0 && has_yt2) p.part2[((size_t)prow * 2) * p.N + n0 + c] = a;
+        if (s == 2) p.part2[((size_t)prow * 2 + 1) * p.N + n0 + c] = a;
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // CV: channels per gathered chunk (8 = one 16-B load; 4 = the 4-channel padded stem input,
 // one 8-B load per chunk).  UT: Ci % KSTEP == 0 (uniform tap per k-step).
 template <int MODE, int PRO, int EPI, int BM, int BN, int KSTEP, int CV, bool UT>
@@ -90,16 +233,12 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs p) {
   constexpr int KCH = KSTEP / CV;                    // chunks per staged row
   constexpr int RT = BM / 32, CTW = BN / 32;         // per-wave 16x16 tiles
   constexpr int ACH = BM * KCH / 256, BCH = BN * KCH / 256;
-  constexpr int LDC = BN + 8;
-  constexpr int CH = BN / 8, RSTEP = 256 / CH, NP = BM / RSTEP;
   constexpr bool HAS_A2 = PRO == CP_BNBWD;
-  static_assert(ACH >= 1 && BCH >= 1 && NP >= 1, "tile too small for 256 threads");
+  static_assert(ACH >= 1 && BCH >= 1 && BM >= 256 / (BN / 8), "tile too small for 256 threads");
   typedef typename std::conditional<CV == 8, uint4, uint2>::type chunk_t;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t *As = reinterpret_cast<bf16_t *>(smem);     // [2][BM][kLDK]
   bf16_t *Bs = As + 2 * BM * kLDK;                   // [2][BN][kLDK]
-  bf16_t *Cs = reinterpret_cast<bf16_t *>(smem);     // [BM][LDC] (after the K loop)
-  float *Red = reinterpret_cast<float *>(smem);      // [RSTEP][BN] (end)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -310,130 +449,219 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs p) {
     __syncthreads();
   }
 
-  // ---- epilogue: bf16 C tile in LDS, then 16-B row chunks.  The epilogue operands of the
-  // first EB rows are loaded before the C tile is staged; rows past the end are clamped to
-  // a valid row (loads are unconditional, results discarded) so hipcc keeps them in flight.
-  constexpr bool E_R = EPI == CE_BWD_R || EPI == CE_BWD_RXY || EPI == CE_BWD_RXYY;
-  constexpr bool E_X = EPI == CE_BWD_RXY || EPI == CE_BWD_RXYY;
-  constexpr bool E_YT = EPI == CE_BWD_RELU || EPI == CE_BWD_RXY || EPI == CE_BWD_RXYY;
-  constexpr bool E_YT2 = EPI == CE_BWD_RXYY;
-  constexpr bool STATS = EPI == CE_FWD || E_YT;
-  constexpr int EB = NP < 4 ? NP : 4;
-  const int my_chunk = tid % CH;
-  const bool colok = n0 + my_chunk * 8 < p.N;
-  const int ncol0 = colok ? n0 + my_chunk * 8 : 0;
-  float s0[8], s1[8], s2[8], es[8], et[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) s0[j] = s1[j] = s2[j] = 0.f;
-  if constexpr (EPI == CE_BWD_RELU) {
-    ld8f(p.es + ncol0, es);
-    ld8f(p.et + ncol0, et);
+  conv_epilogue<MODE, EPI, BM, BN>(p, acc, smem, m0, n0, mt, cls, ph, pw);
+}
+
+// ===========================================================================
+// LDS-DMA implicit GEMM (operands already materialised: no prologue).  Both operand tiles are
+// streamed global -> LDS by buffer_load_dwordx4 ... lds, so the staging costs no VGPRs, no
+// ds_write and no per-element VALU (the register-staged kernel above spends ~40 VALU per 16-B
+// chunk on its BN prologue and address math, and is issue-bound on MI355X).  Requires
+// Ci % 64 == 0: a 64-wide k-step lies inside one filter tap.
+//   * one wave-instruction fills a 1-KiB piece = 8 staged rows x 128 B, lane-linear in LDS;
+//     lane l loads k-chunk (l & 7) ^ (l >> 3) of row l >> 3 (XOR swizzle on the SOURCE
+//     address), so the ds_read_b128 fragment reads are bank-conflict free;
+//   * zero padding and rows past M / N come from the descriptor range check (offset kOOB);
+//   * NBUF = 2: two barriers per k-step (wait for this step's DMAs, then for every wave's reads
+//     before the buffer is refilled); NBUF = 3: one barrier per k-step, the DMA two steps ahead
+//     stays in flight across it (counted vmcnt + raw s_barrier, never __syncthreads()).
+// ===========================================================================
+template <int N>
+PG_DEVICE void glds_wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+template <int MODE, int EPI, int BM, int BN, int NBUF>
+__global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs p) {
+  constexpr int KS = 64, ROWB = KS * 2;              // 128-B staged rows
+  constexpr int APW = BM / 32, BPW = BN / 32;         // 1-KiB pieces per wave per k-step
+  constexpr int PW = APW + BPW;
+  constexpr int RT = BM / 32, CTW = BN / 32;
+  constexpr int ABYTES = BM * ROWB, BUFB = (BM + BN) * ROWB;
+  static_assert(NBUF == 2 || NBUF == 3, "2 or 3 LDS buffers");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int NT = (p.N + BN - 1) / BN;
+  const int nmt = p.nmt;
+  const int cls = MODE == CM_DGRAD ? blockIdx.y : 0;
+  int mt, nt;
+  {
+    const int L = blockIdx.x, full = (nmt / 8) * 8 * NT;
+    if (L < full) {
+      mt = (L / (8 * NT)) * 8 + L % 8;
+      nt = (L / 8) % NT;
+    } else {
+      const int rem = nmt % 8, Lr = L - full;
+      mt = (nmt / 8) * 8 + Lr % rem;
+      nt = Lr / rem;
+    }
   }
-  uint4 oy[EB], orr[EB], ox[EB], oy2[EB];
-  size_t offs[EB];
-  bool okr[EB];
-  auto issue = [&](int i0) {
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int ph = MODE == CM_DGRAD ? cls / p.stride : 0, pw = MODE == CM_DGRAD ? cls % p.stride : 0;
+  const int Kc = MODE == CM_DGRAD ? p.ntap[cls] * p.Ci : p.K;
+  const int nk = Kc / KS;
+  const int HWc = p.Hc * p.Wc;
+  const int lrow = lane >> 3;                 // row of this lane inside a 1-KiB piece
+  const int lch = (lane & 7) ^ lrow;          // k-chunk this lane fetches (source swizzle)
+  const rsrc_t ra = make_rsrc(p.A, (uint32_t)p.Nb * p.Hi * p.Wi * p.Ci * 2);
+  const rsrc_t rw = make_rsrc(p.W, (uint32_t)p.N * p.Kw * 2);
+
+  // A rows of this wave's pieces (fixed across k-steps): image, base h / w; rb < 0: past M
+  int rb[APW], rh[APW], rwc[APW];
 #pragma unroll
-    for (int e = 0; e < EB; ++e) {
-      const int rr = tid / CH + (i0 + e) * RSTEP;
-      int m = m0 + rr;
-      okr[e] = m < p.Mc && colok;
-      if (m >= p.Mc) m = p.Mc - 1;
-      size_t pix;
-      if constexpr (MODE == CM_FWD) {
-        pix = m;
-      } else {
-        const int b = m / HWc, rem = m % HWc, hh = rem / p.Wc, ww = rem % p.Wc;
-        pix = ((size_t)b * p.Ho + hh * p.stride + ph) * p.Wo + ww * p.stride + pw;
-      }
-      offs[e] = pix * p.N + ncol0;
-      if constexpr (E_YT) oy[e] = ldg16(p.Yt + offs[e]);
-      if constexpr (E_R) orr[e] = ldg16(p.Rg + offs[e]);
-      if constexpr (E_X) ox[e] = ldg16(p.X + offs[e]);
-      if constexpr (E_YT2) oy2[e] = ldg16(p.Yt2 + offs[e]);
+  for (int i = 0; i < APW; ++i) {
+    const int m = m0 + (wave * APW + i) * 8 + lrow;
+    if (m < p.Mc) {
+      const int b = m / HWc, rem = m % HWc, hh = rem / p.Wc, ww = rem % p.Wc;
+      rb[i] = b;
+      rh[i] = MODE == CM_FWD ? hh * p.stride - p.pad : hh;
+      rwc[i] = MODE == CM_FWD ? ww * p.stride - p.pad : ww;
+    } else {
+      rb[i] = -1; rh[i] = 0; rwc[i] = 0;
+    }
+  }
+  uint32_t wrow[BPW];   // weight row byte offsets (kOOB past N)
+#pragma unroll
+  for (int i = 0; i < BPW; ++i) {
+    const int n = n0 + (wave * BPW + i) * 8 + lrow;
+    wrow[i] = n < p.N ? (uint32_t)n * p.Kw * 2 : kOOB;
+  }
+
+  auto issue = [&](int ks, int buf) {
+    const int k0 = ks * KS;
+    const int j = k0 / p.Ci;
+    const int ci = k0 - j * p.Ci + lch * 8;
+    int dh, dw, wt;
+    if constexpr (MODE == CM_FWD) {
+      dh = j / p.S; dw = j - dh * p.S; wt = j;
+    } else {
+      dh = p.tdh[cls][j]; dw = p.tdw[cls][j];
+      wt = p.tr[cls][j] * p.S + p.ts[cls][j];
+    }
+    char *abase = smem + buf * BUFB;
+    char *bbase = abase + ABYTES;
+#pragma unroll
+    for (int i = 0; i < APW; ++i) {
+      const int ih = rh[i] + dh, iw = rwc[i] + dw;
+      const bool ok = rb[i] >= 0 && ih >= 0 && ih < p.Hi && iw >= 0 && iw < p.Wi;
+      const uint32_t off = ok ? (uint32_t)((((rb[i] * p.Hi + ih) * p.Wi + iw) * p.Ci + ci) * 2) : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (__attribute__((address_space(3))) void *)(abase + (wave * APW + i) * 1024),
+                                               16, off, 0, 0, 0);
+    }
+    const uint32_t kb = (uint32_t)(wt * p.Ci + ci) * 2;
+#pragma unroll
+    for (int i = 0; i < BPW; ++i) {
+      const uint32_t off = wrow[i] == kOOB ? kOOB : wrow[i] + kb;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void *)(bbase + (wave * BPW + i) * 1024),
+                                               16, off, 0, 0, 0);
     }
   };
-  issue(0);
+
+  f32x4_t acc[RT][CTW];
 #pragma unroll
-  for (int c = 0; c < CTW; ++c) {
-    const int col = wn * (BN / 2) + c * 16 + (lane & 15);
+  for (int r = 0; r < RT; ++r)
 #pragma unroll
-    for (int r = 0; r < RT; ++r)
+    for (int c = 0; c < CTW; ++c) acc[r][c] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  // fragment reads: row (lane & 15) of a 16-row block, k-chunk kc = 4*sub + (lane >> 4) stored at
+  // position kc ^ (row & 7) = kc ^ (lane & 7)
+  auto mma = [&](int buf) {
+    const char *Ab = smem + buf * BUFB;
+    const char *Bb = Ab + ABYTES;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) Cs[(wm * (BM / 2) + r * 16 + 4 * (lane >> 4) + j) * LDC + col] = f2bf(acc[r][c][j]);
-  }
-  __syncthreads();
+    for (int sub = 0; sub < KS / 32; ++sub) {
+      const int pos = ((4 * sub + (lane >> 4)) ^ (lane & 7)) * 16;
+      s16x8_t af[RT];
 #pragma unroll
-  for (int i0 = 0; i0 < NP; i0 += EB) {
-    if (i0 > 0) issue(i0);
+      for (int r = 0; r < RT; ++r)
+        af[r] = *reinterpret_cast<const s16x8_t *>(Ab + (wm * (BM / 2) + r * 16 + (lane & 15)) * ROWB + pos);
 #pragma unroll
-    for (int e = 0; e < EB; ++e) {
-      const int rr = tid / CH + (i0 + e) * RSTEP;
-      float v[8];
-      unpack8(*reinterpret_cast<const uint4 *>(Cs + rr * LDC + my_chunk * 8), v);
-      if constexpr (EPI == CE_FWD) {
-        if (okr[e]) {
+      for (int c = 0; c < CTW; ++c) {
+        const s16x8_t bf =
+            *reinterpret_cast<const s16x8_t *>(Bb + (wn * (BN / 2) + c * 16 + (lane & 15)) * ROWB + pos);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) { s0[j] += v[j]; s1[j] = fmaf(v[j], v[j], s1[j]); }
-        }
+        for (int r = 0; r < RT; ++r) acc[r][c] = mfma16(af[r], bf, acc[r][c]);
+      }
+    }
+  };
+
+  if constexpr (NBUF == 2) {
+    if (nk > 0) issue(0, 0);
+    for (int ks = 0; ks < nk; ++ks) {
+      const int buf = ks & 1;
+      if (ks + 1 < nk) {
+        issue(ks + 1, buf ^ 1);
+        glds_wait_barrier<PW>();        // this step's pieces landed (every wave)
       } else {
-        float yt[8];
-        if constexpr (E_YT) unpack8(oy[e], yt);
-        if constexpr (EPI == CE_BWD_RELU) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = fmaf(yt[j], es[j], et[j]) > 0.f ? v[j] : 0.f;
-        }
-        if constexpr (E_R) {
-          float rv[8];
-          unpack8(orr[e], rv);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] += rv[j];
-        }
-        if constexpr (E_X) {
-          float xv[8];
-          unpack8(ox[e], xv);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = xv[j] > 0.f ? v[j] : 0.f;
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = bf2f(f2bf(v[j]));
-        if (okr[e]) {
-          if constexpr (E_YT) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) { s0[j] += v[j]; s1[j] = fmaf(v[j], yt[j], s1[j]); }
-          }
-          if constexpr (E_YT2) {
-            float y2[8];
-            unpack8(oy2[e], y2);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) s2[j] = fmaf(v[j], y2[j], s2[j]);
-          }
-        }
+        glds_wait_barrier<0>();
       }
-      if (okr[e]) stg16(p.out + offs[e], pack8(v));
+      mma(buf);
+      glds_wait_barrier<PW>();          // every wave done reading buf before it is refilled
     }
+  } else {
+    if (nk > 0) issue(0, 0);
+    if (nk > 1) issue(1, 1);
+    int buf = 0, nbuf = 2;
+    for (int ks = 0; ks < nk; ++ks) {
+      if (ks + 1 < nk) glds_wait_barrier<PW>();
+      else glds_wait_barrier<0>();
+      if (ks + 2 < nk) issue(ks + 2, nbuf);
+      mma(buf);
+      buf = buf == 2 ? 0 : buf + 1;
+      nbuf = nbuf == 2 ? 0 : nbuf + 1;
+    }
+    glds_wait_barrier<0>();             // every wave done reading before the C tile reuses LDS
   }
-  if constexpr (!STATS) return;
-  const bool has_yt2 = E_YT2;
-  __syncthreads();
-  // ---- BN partials of this tile's columns -> part[cls*nmt + mt][2][N] (and part2)
-  const int prow = cls * nmt + mt;
-  const int nstat = has_yt2 ? 3 : 2;
-  for (int s = 0; s < nstat; ++s) {
-    const int rgrp = tid / CH;
+  conv_epilogue<MODE, EPI, BM, BN>(p, acc, smem, m0, n0, mt, cls, ph, pw);
+}
+
+// ===========================================================================
+// BN materialisation for the LDS-DMA convs (operands without a prologue), [M][C] bf16:
+//   MODE 0: act = relu(Y*a + b)        (forward: the producer BN + ReLU, consumer input)
+//   MODE 1: dy  = a*G + b*Y + c        (backward: this layer's BN backward, dgrad + wgrad input)
+// Thread t owns channel chunk t % C8 (coefficients in registers), rows t / C8 + i*(256/C8);
+// UR rows in flight per thread.  C8 = C/8 must divide 256 (checked by the launcher).
+// ===========================================================================
+template <int MODE>
+__global__ __launch_bounds__(256) void bn_mat_kernel(const bf16_t *__restrict__ G, const bf16_t *__restrict__ Y,
+                                                    const float *__restrict__ a, const float *__restrict__ b,
+                                                    const float *__restrict__ c, bf16_t *__restrict__ out, int M,
+                                                    int C) {
+  constexpr int UR = 4;
+  const int C8 = C >> 3, rpi = 256 / C8;
+  const int cc = threadIdx.x % C8, r0 = threadIdx.x / C8;
+  float a8[8], b8[8], c8[8];
+  ld8f(a + cc * 8, a8);
+  ld8f(b + cc * 8, b8);
+  if constexpr (MODE == 1) ld8f(c + cc * 8, c8);
+  const rsrc_t ry = make_rsrc(Y, (uint32_t)M * C * 2), ro = make_rsrc(out, (uint32_t)M * C * 2);
+  const rsrc_t rg = make_rsrc(MODE == 1 ? G : Y, (uint32_t)M * C * 2);
+  const int stride = gridDim.x * rpi * UR;
+  for (int m = blockIdx.x * rpi * UR + r0; m < M; m += stride) {
+    uint4 yv[UR], gv[UR];
+    uint32_t off[UR];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) Red[rgrp * BN + my_chunk * 8 + j] = s == 0 ? s0[j] : (s == 1 ? s1[j] : s2[j]);
-    __syncthreads();
-    for (int c = tid; c < BN; c += 256) {
-      float a = 0.f;
-      for (int g = 0; g < RSTEP; ++g) a += Red[g * BN + c];
-      if (n0 + c < p.N) {
-        if (s < 2) p.part[((size_t)prow * 2 + s) * p.N + n0 + c] = a;
-        if (s == 0 && has_yt2) p.part2[((size_t)prow * 2) * p.N + n0 + c] = a;
-        if (s == 2) p.part2[((size_t)prow * 2 + 1) * p.N + n0 + c] = a;
-      }
+    for (int u = 0; u < UR; ++u) {
+      const int row = m + u * rpi;
+      off[u] = row < M ? (uint32_t)(row * C + cc * 8) * 2 : kOOB;
+      yv[u] = bld16(ry, off[u]);
+      if constexpr (MODE == 1) gv[u] = bld16(rg, off[u]);
     }
-    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < UR; ++u) {
+      float y[8], v[8];
+      unpack8(yv[u], y);
+      if constexpr (MODE == 1) {
+        float g[8];
+        unpack8(gv[u], g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = fmaf(a8[j], g[j], fmaf(b8[j], y[j], c8[j]));
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = reluf(fmaf(y[j], a8[j], b8[j]));
+      }
+      bst16(ro, off[u], pack8(v));
+    }
   }
 }
 
@@ -461,7 +689,7 @@ constexpr int kWgMK = 64;             // m rows per step
 constexpr int kWgLD = kWgMK + 8;      // transposed row pitch (bf16)
 }  // namespace
 
-template <int XPRO, int TN, int TK, int CV>
+template <int XPRO, int TN, int TK, int CV, bool DM>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs p) {
   constexpr int QN = TN / 2, QK = TK / 2, RN = QN / 16, RK = QK / 16;
   constexpr int M4 = kWgMK / 4;
@@ -492,7 +720,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs p) {
     const bool ok = d_on[i] && d_col[i] < p.N;
 #pragma unroll
     for (int j = 0; j < 8; ++j) ga8[i][j] = gb8[i][j] = gc8[i][j] = 0.f;
-    if (ok) {
+    if (ok && !DM) {
       ld8f(p.ga + d_col[i], ga8[i]);
       ld8f(p.gb + d_col[i], gb8[i]);
       ld8f(p.gc + d_col[i], gc8[i]);
@@ -550,7 +778,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs p) {
         dvm[i] |= ok ? 1u << q : 0u;
         const size_t off = (size_t)(mr + q) * p.N + d_col[i];
         dg[i][q] = ok ? ldg16(p.G + off) : make_uint4(0, 0, 0, 0);
-        dyv[i][q] = ok ? ldg16(p.Y + off) : make_uint4(0, 0, 0, 0);
+        if constexpr (!DM) dyv[i][q] = ok ? ldg16(p.Y + off) : make_uint4(0, 0, 0, 0);
       }
     }
 #pragma unroll
@@ -604,10 +832,15 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs p) {
       for (int q = 0; q < 4; ++q) {
         float g[8], y[8];
         unpack8(dg[i][q], g);
-        unpack8(dyv[i][q], y);
-        const bool ok = (dvm[i] >> q) & 1u;   // a*0 + b*0 + c != 0: invalid rows must be zeroed
+        if constexpr (DM) {   // materialised dy (invalid rows were loaded as zeros)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[q][j] = ok ? fmaf(ga8[i][j], g[j], fmaf(gb8[i][j], y[j], gc8[i][j])) : 0.f;
+          for (int j = 0; j < 8; ++j) v[q][j] = g[j];
+        } else {
+          unpack8(dyv[i][q], y);
+          const bool ok = (dvm[i] >> q) & 1u;   // a*0 + b*0 + c != 0: invalid rows must be zeroed
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[q][j] = ok ? fmaf(ga8[i][j], g[j], fmaf(gb8[i][j], y[j], gc8[i][j])) : 0.f;
+        }
       }
       put(Tdy[buf], d_col[i] - n0, d_m4[i] * 4, v);
     }
@@ -1013,6 +1246,42 @@ void launch_geom(const ConvArgs &a, const Geom &g, hipStream_t st) {
   }
 }
 
+// LDS-DMA kernel (conv_glds_kernel) for operands without a prologue: g_conv_glds = 0 off (the
+// register-staged kernel), 2 or 3 LDS buffers.  Default 2; PGDIST_CONV_GLDS / conv_set_glds().
+int conv_glds_default() {
+  const char *e = getenv("PGDIST_CONV_GLDS");
+  const int v = e ? atoi(e) : 2;
+  return v == 0 || v == 3 ? v : 2;
+}
+int g_conv_glds = conv_glds_default();
+bool glds_ok(int Ci) { return g_conv_glds != 0 && Ci % 64 == 0; }
+int glds_nbuf() { return g_conv_glds; }
+
+template <int MODE, int EPI, int BM, int BN, int NBUF>
+void launch_glds_t(const ConvArgs &a, const Geom &g, hipStream_t st) {
+  size_t lds = (size_t)NBUF * (BM + BN) * 128;
+  const size_t ctile = (size_t)BM * (BN + 8) * 2, red = (size_t)(256 / (BN / 8)) * BN * 4;
+  if (ctile > lds) lds = ctile;
+  if (red > lds) lds = red;
+  hipLaunchKernelGGL((conv_glds_kernel<MODE, EPI, BM, BN, NBUF>), dim3(g.nmt * g.nt, g.ncls), dim3(256), lds, st, a);
+}
+
+template <int MODE, int EPI>
+void launch_glds(const ConvArgs &a, const Geom &g, hipStream_t st) {
+  const bool three = glds_nbuf() == 3;
+#define LG_GLDS(BM_, BN_)                                                                               \
+  if (g.BM == BM_ && g.BN == BN_) {                                                                     \
+    if (three) launch_glds_t<MODE, EPI, BM_, BN_, 3>(a, g, st);                                          \
+    else launch_glds_t<MODE, EPI, BM_, BN_, 2>(a, g, st);                                                \
+    return;                                                                                             \
+  }
+  LG_GLDS(128, 128)
+  LG_GLDS(128, 64)
+  LG_GLDS(64, 128)
+  LG_GLDS(64, 64)
+#undef LG_GLDS
+}
+
 // dgrad parity classes of a (R, S, stride, pad) convolution
 void dgrad_classes(ConvArgs &a, int R, int S, int st, int pad) {
   for (int cls = 0; cls < st * st; ++cls) {
@@ -1033,6 +1302,9 @@ void dgrad_classes(ConvArgs &a, int R, int S, int st, int pad) {
   }
 }
 }  // namespace
+
+void conv_set_glds(int mode) { g_conv_glds = mode == 0 || mode == 3 ? mode : 2; }
+int conv_get_glds() { return g_conv_glds; }
 
 // BN partial rows a forward conv writes (per M tile)
 int conv_fwd_num_partials(int Nb, int Ho, int Wo, int N, int K, int Ci) {
@@ -1060,9 +1332,11 @@ void launch_conv_fwd(int pro, const bf16_t *x, const float *pa, const float *pb,
   a.K = Ci == 4 ? (a.Kw + 31) / 32 * 32 : a.Kw;
   a.Mc = Nb * a.Ho * a.Wo;
   a.Hc = a.Ho; a.Wc = a.Wo;
+  a.Nb = Nb;
   const Geom g = igemm_geom(a.Mc, N, a.Kw, Ci, 1);
   a.nmt = g.nmt;
   if (Ci == 4) { launch_geom<CM_FWD, CP_NONE, CE_FWD, 4>(a, g, stream); return; }
+  if (pro == CP_NONE && glds_ok(Ci)) { launch_glds<CM_FWD, CE_FWD>(a, g, stream); return; }
   if (pro == CP_BN_RELU) launch_geom<CM_FWD, CP_BN_RELU, CE_FWD, 8>(a, g, stream);
   else launch_geom<CM_FWD, CP_NONE, CE_FWD, 8>(a, g, stream);
 }
@@ -1093,6 +1367,15 @@ void launch_conv_dgrad(int epi, const bf16_t *G, const bf16_t *Y, const float *g
   a.K = kmax;
   const Geom g = igemm_geom(a.Mc, Cin, kmax, Cout, st * st);
   a.nmt = g.nmt;
+  a.Nb = Nb;
+  if (Y == nullptr) {   // G is the materialised dy (launch_bn_mat): LDS-DMA kernel, no prologue
+    if (epi == CE_BWD_RELU) { launch_glds<CM_DGRAD, CE_BWD_RELU>(a, g, stream); return; }
+    if (!Rg && !X && !Yt && !Yt2) launch_glds<CM_DGRAD, CE_BWD_PLAIN>(a, g, stream);
+    else if (Rg && !X && !Yt && !Yt2) launch_glds<CM_DGRAD, CE_BWD_R>(a, g, stream);
+    else if (Rg && X && Yt && !Yt2) launch_glds<CM_DGRAD, CE_BWD_RXY>(a, g, stream);
+    else if (Rg && X && Yt && Yt2) launch_glds<CM_DGRAD, CE_BWD_RXYY>(a, g, stream);
+    return;
+  }
   if (epi == CE_BWD_RELU) { launch_geom<CM_DGRAD, CP_BNBWD, CE_BWD_RELU, 8>(a, g, stream); return; }
   // (dx + Rg) * 1[X > 0] with statistics against Yt (, Yt2): supported operand sets
   if (!Rg && !X && !Yt && !Yt2) launch_geom<CM_DGRAD, CP_BNBWD, CE_BWD_PLAIN, 8>(a, g, stream);
@@ -1149,7 +1432,12 @@ void launch_conv_wgrad(const bf16_t *G, const bf16_t *Y, const float *ga, const 
   a.rows_per_split = g.rows;
   a.out = g.nsplit == 1 ? grad : ws;
   const dim3 grid((N + g.TN - 1) / g.TN, (a.Kw + g.TK - 1) / g.TK, g.nsplit);
-#define WG_L(XP, TN_, TK_, CV_) hipLaunchKernelGGL((conv_wgrad_kernel<XP, TN_, TK_, CV_>), grid, dim3(256), 0, stream, a)
+  const bool dm = Y == nullptr;   // G is the materialised dy (launch_bn_mat)
+#define WG_L(XP, TN_, TK_, CV_)                                                                                  \
+  do {                                                                                                          \
+    if (dm) hipLaunchKernelGGL((conv_wgrad_kernel<XP, TN_, TK_, CV_, true>), grid, dim3(256), 0, stream, a);     \
+    else hipLaunchKernelGGL((conv_wgrad_kernel<XP, TN_, TK_, CV_, false>), grid, dim3(256), 0, stream, a);       \
+  } while (0)
   if (Ci == 4) {
     if (g.TN == 128) WG_L(CP_NONE, 128, 128, 4); else WG_L(CP_NONE, 64, 128, 4);
   } else if (xpro == CP_BN_RELU) {
@@ -1221,4 +1509,15 @@ void launch_image_prep(const uint8_t *src, const long long *idx, const long long
   const int HW = H * W;
   hipLaunchKernelGGL(image_prep_kernel, dim3((HW + 255) / 256 < 64 ? (HW + 255) / 256 : 64, B), dim3(256), 0, st, src,
                      idx, lab_src, HW, W, seed, hyper, out, lab_out);
+}
+
+// BN materialisation (bn_mat_kernel): mode 0 act = relu(Y*a + b); mode 1 dy = a*G + b*Y + c
+void launch_bn_mat(int mode, const bf16_t *G, const bf16_t *Y, const float *a, const float *b, const float *c,
+                   bf16_t *out, int M, int C, hipStream_t stream) {
+  const int C8 = C / 8, rpi = 256 / C8;
+  long long blocks = ((long long)M + rpi * 4 - 1) / (rpi * 4);
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  if (mode == 1) hipLaunchKernelGGL(bn_mat_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, stream, G, Y, a, b, c, out, M, C);
+  else hipLaunchKernelGGL(bn_mat_kernel<0>, dim3((unsigned)blocks), dim3(256), 0, stream, G, Y, a, b, c, out, M, C);
 }

@@ -53,6 +53,7 @@ class BNState:
         self.coef = torch.zeros(3, C, **f32)
         self.y = torch.empty(M, C, dtype=torch.bfloat16, device=device)   # pre-BN activation
         self.g = torch.empty(M, C, dtype=torch.bfloat16, device=device) if need_g else None
+        self.act: Optional[torch.Tensor] = None   # relu(BN(y)) when a consumer wants it materialised
         self.param_names = [prefix + ".weight", prefix + ".bias"]
         # atomic statistics accumulators [rows][2][C] of this BN's forward / backward producer
         # (views into the executor's arena, zeroed once per training step)

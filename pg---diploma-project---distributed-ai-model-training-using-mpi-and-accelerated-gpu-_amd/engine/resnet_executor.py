@@ -22,9 +22,18 @@ layer's BN backward (a*G + b*Y + c) while staging dy and the producer's ReLU mas
 epilogue, and weight gradients (split-M, BN-backward / BN+ReLU fused in the staging)
 run on a side stream, reporting finished parameters to the DDP bucket reducer.
 
+LDS-DMA convs (default, ``ops.kernels.conv_set_glds``): the operand tiles of a conv are
+streamed global -> LDS by buffer_load ... lds, which needs operands without a prologue.  So
+every backward conv first materialises its dy = a*G + b*Y + c once (``bn_mat``; read by both
+the dgrad and the side-stream wgrad, which then skip the BN-backward prologue), and the
+forward materialises relu(BN(y)) for the convs where the prologue costs more than the extra
+pass (``mat_dy_pays`` / ``mat_act_pays``, measured per layer with scripts/conv_bench.py;
+PGDIST_RN_DY / PGDIST_RN_ACT = all|none|auto override).
+
 Reference call stack for the model forward: SURVEY.md §3.3 (cuDNN conv / BN / ReLU
 launches per layer); this executor replaces all of them.
 """
+import os
 from dataclasses import dataclass
 from typing import Callable, List, Optional
 
@@ -45,6 +54,8 @@ class ConvSpec:
     stride: int
     pad: int
     H: int          # input spatial size (square)
+    dy: Optional[torch.Tensor] = None   # materialised BN-backward output gradient (bn_mat)
+    act: bool = False                   # input relu(BN(y)) materialised for this conv (bn_mat)
 
     @property
     def Ho(self) -> int:
@@ -138,6 +149,19 @@ class ResNet50Executor:
                     dgrad_parts(c)
                 self.blocks.append(bp)
                 H, x_in = Ho, bp.out
+        # ---------------- materialised operands of the LDS-DMA convs
+        self.mat = K.conv_get_glds() != 0 and os.environ.get("PGDIST_RN_MAT", "1") != "0"
+        act_mode = os.environ.get("PGDIST_RN_ACT", "auto")
+        dy_mode = os.environ.get("PGDIST_RN_DY", "auto")
+        if self.mat:
+            for bp in self.blocks:
+                for c in (bp.c1, bp.c2, bp.c3) + ((bp.cd,) if bp.cd else ()):
+                    if dy_mode == "all" or (dy_mode == "auto" and self.mat_dy_pays(c, B)):
+                        c.dy = torch.empty(B * c.Ho * c.Ho, c.cout, **bf16)
+                for c, bn in ((bp.c2, bp.bn1), (bp.c3, bp.bn2)):
+                    c.act = act_mode == "all" or (act_mode == "auto" and self.mat_act_pays(c, B))
+                    if c.act:
+                        bn.act = torch.empty(B * c.H * c.H, c.cin, **bf16)
         # ---------------- head
         self.Hf = H
         self.C_last = self.blocks[-1].cout
@@ -178,6 +202,21 @@ class ResNet50Executor:
         self.wt_tab = torch.tensor(tab, dtype=torch.int32, device=device).contiguous()
 
     # ------------------------------------------------------------------ helpers
+    # Materialisation policy, from per-layer timings of every ResNet-50 conv on MI355X at bs 128
+    # (scripts/conv_bench.py: dgrad vs bn_mat + dgrad on the materialised dy, fwdbn vs bn_mat +
+    # fwd).  A 3x3 conv re-stages each operand element up to 9x per N tile, so its BN prologue is
+    # expensive and one materialising pass pays; a 1x1 conv stages each element once per N tile,
+    # so the extra pass pays only while the tensor is small (launch-bound maps).
+    MAT_ELEMS = 16 * 2 ** 20
+
+    @classmethod
+    def mat_dy_pays(cls, c: ConvSpec, B: int) -> bool:
+        return c.k == 3 or B * c.Ho * c.Ho * c.cout <= cls.MAT_ELEMS
+
+    @classmethod
+    def mat_act_pays(cls, c: ConvSpec, B: int) -> bool:
+        n = B * c.H * c.H * c.cin
+        return n <= 2 * cls.MAT_ELEMS if c.k == 3 else n <= cls.MAT_ELEMS // 2
     def _ready(self, names):
         if self.on_params_ready is None:
             return
@@ -203,10 +242,30 @@ class ResNet50Executor:
     def _conv(self, c: ConvSpec, pro, x, y, train, bn_out: BNState, bn_in: Optional[BNState] = None):
         B = self.B
         ci = 4 if c.cin == 3 else c.cin
+        if c.act and pro == K.CP_BN_RELU:   # relu(BN(x)) materialised once: plain LDS-DMA conv
+            K.bn_mat(K.BN_MAT_ACT, x, bn_in.scale, bn_in.shift, bn_in.act)
+            pro, x, bn_in = K.CP_NONE, bn_in.act, None
         K.conv_fwd(pro, x, self.flat.b(c.name), y, self.ws_part, B, c.H, c.H, ci, c.cout, c.k, c.k, c.stride,
                    c.pad, pa=bn_in.scale if bn_in is not None else None,
                    pb=bn_in.shift if bn_in is not None else None)
         self._fin(bn_out, K.conv_fwd_num_partials(B, c.Ho, c.Ho, c.cout, c.k * c.k * ci, ci), train)
+
+    def _dy(self, c: ConvSpec, G, bn: BNState):
+        """(G, Y) operands of conv ``c``'s dgrad / wgrad: dy = a*G + b*Y + c materialised once
+        into c.dy (LDS-DMA kernels, Y = None), or the pair for the fused BN-backward prologue."""
+        if c.dy is None:
+            return G, bn.y
+        K.bn_mat(K.BN_MAT_BWD, bn.y, bn.a, bn.b, c.dy, G=G, c=bn.c)
+        return c.dy, None
+
+    @staticmethod
+    def _wx(c: ConvSpec, x, bn_in: Optional[BNState]):
+        """wgrad input operand: the materialised relu(BN(x)) when the forward made one"""
+        if bn_in is None:
+            return dict(x=x, xpro=K.CP_NONE)
+        if c.act:
+            return dict(x=bn_in.act, xpro=K.CP_NONE)
+        return dict(x=x, xpro=K.CP_BN_RELU, xs=bn_in.scale, xt=bn_in.shift)
 
     # ------------------------------------------------------------------ forward
     def forward(self, train: bool = True):
@@ -250,49 +309,52 @@ class ResNet50Executor:
             H, Ho = bp.H, bp.Ho
             c1, c2, c3, cd = bp.c1, bp.c2, bp.c3, bp.cd
             # conv3 dgrad -> G2 (ReLU mask of BN2) + BN2 partials
-            K.conv_dgrad(K.CE_BWD_RELU, bn3.g, bn3.y, bn3.a, bn3.b, bn3.c, f.bt(c3.name), bn2.g, ws, B, Ho, Ho,
+            g3, y3 = self._dy(c3, bn3.g, bn3)
+            K.conv_dgrad(K.CE_BWD_RELU, g3, y3, bn3.a, bn3.b, bn3.c, f.bt(c3.name), bn2.g, ws, B, Ho, Ho,
                          c3.cin, c3.cout, 1, 1, 1, 0, Yt=bn2.y, es=bn2.scale, et=bn2.shift)
             bn2.finalize_bwd(ws, K.conv_dgrad_num_partials(B, Ho, Ho, c3.cin, c3.cout, 1, 1, 1))
-            self._wgrad(lambda bp=bp: K.conv_wgrad(bp.bn3.g, bp.bn3.y, bp.bn3.a, bp.bn3.b, bp.bn3.c, bp.bn2.y, wg,
-                                                   f.g(bp.c3.name), B, bp.Ho, bp.Ho, bp.c3.cin, bp.c3.cout, 1, 1, 1,
-                                                   0, xpro=K.CP_BN_RELU, xs=bp.bn2.scale, xt=bp.bn2.shift))
+            self._wgrad(lambda bp=bp, g3=g3, y3=y3: K.conv_wgrad(
+                g3, y3, bp.bn3.a, bp.bn3.b, bp.bn3.c, ws=wg, grad=f.g(bp.c3.name), B=B, H=bp.Ho, W=bp.Ho,
+                Ci=bp.c3.cin, N=bp.c3.cout, R=1, S=1, stride=1, pad=0, **self._wx(bp.c3, bp.bn2.y, bp.bn2)))
             self._ready([c3.name] + bn2.param_names)
             # projection shortcut: data gradient (summed in conv1's dgrad epilogue) + weight gradient
             if cd is not None:
-                K.conv_dgrad(K.CE_BWD_RES, bn3.g, bnd.y, bnd.a, bnd.b, bnd.c, f.bt(cd.name), bp.Rd, None, B, H, H,
+                gd, yd = self._dy(cd, bn3.g, bnd)
+                K.conv_dgrad(K.CE_BWD_RES, gd, yd, bnd.a, bnd.b, bnd.c, f.bt(cd.name), bp.Rd, None, B, H, H,
                              cd.cin, cd.cout, 1, 1, cd.stride, 0)
-                self._wgrad(lambda bp=bp: K.conv_wgrad(bp.bn3.g, bp.bnd.y, bp.bnd.a, bp.bnd.b, bp.bnd.c, bp.x_in,
-                                                       wg, f.g(bp.cd.name), B, bp.H, bp.H, bp.cd.cin, bp.cd.cout,
-                                                       1, 1, bp.cd.stride, 0))
+                self._wgrad(lambda bp=bp, gd=gd, yd=yd: K.conv_wgrad(
+                    gd, yd, bp.bnd.a, bp.bnd.b, bp.bnd.c, ws=wg, grad=f.g(bp.cd.name), B=B, H=bp.H, W=bp.H,
+                    Ci=bp.cd.cin, N=bp.cd.cout, R=1, S=1, stride=bp.cd.stride, pad=0, **self._wx(bp.cd, bp.x_in, None)))
                 self._ready([cd.name])
             # conv2 dgrad -> G1 (ReLU mask of BN1) + BN1 partials
-            K.conv_dgrad(K.CE_BWD_RELU, bn2.g, bn2.y, bn2.a, bn2.b, bn2.c, f.bt(c2.name), bn1.g, ws, B, H, H,
+            g2, y2 = self._dy(c2, bn2.g, bn2)
+            K.conv_dgrad(K.CE_BWD_RELU, g2, y2, bn2.a, bn2.b, bn2.c, f.bt(c2.name), bn1.g, ws, B, H, H,
                          c2.cin, c2.cout, 3, 3, c2.stride, 1, Yt=bn1.y, es=bn1.scale, et=bn1.shift)
             bn1.finalize_bwd(ws, K.conv_dgrad_num_partials(B, H, H, c2.cin, c2.cout, 3, 3, c2.stride))
-            self._wgrad(lambda bp=bp: K.conv_wgrad(bp.bn2.g, bp.bn2.y, bp.bn2.a, bp.bn2.b, bp.bn2.c, bp.bn1.y, wg,
-                                                   f.g(bp.c2.name), B, bp.H, bp.H, bp.c2.cin, bp.c2.cout, 3, 3,
-                                                   bp.c2.stride, 1, xpro=K.CP_BN_RELU, xs=bp.bn1.scale,
-                                                   xt=bp.bn1.shift))
+            self._wgrad(lambda bp=bp, g2=g2, y2=y2: K.conv_wgrad(
+                g2, y2, bp.bn2.a, bp.bn2.b, bp.bn2.c, ws=wg, grad=f.g(bp.c2.name), B=B, H=bp.H, W=bp.H,
+                Ci=bp.c2.cin, N=bp.c2.cout, R=3, S=3, stride=bp.c2.stride, pad=1, **self._wx(bp.c2, bp.bn1.y, bp.bn1)))
             self._ready([c2.name] + bn1.param_names)
             # conv1 dgrad + shortcut gradient -> gradient of the block input:
             #   previous block: Gz_prev = (dx + sc) * 1[o_prev > 0], BN3 (+BNd) partials of that block
             #   first block: gradient of the max-pool output (no ReLU in between)
             sc = bp.Rd if cd is not None else bn3.g
             P1 = K.conv_dgrad_num_partials(B, H, H, c1.cin, c1.cout, 1, 1, 1)
+            g1, y1 = self._dy(c1, bn1.g, bn1)
             if prev is not None:
                 pds = prev.bnd is not None
-                K.conv_dgrad(K.CE_BWD_RES, bn1.g, bn1.y, bn1.a, bn1.b, bn1.c, f.bt(c1.name), prev.bn3.g, ws, B, H,
+                K.conv_dgrad(K.CE_BWD_RES, g1, y1, bn1.a, bn1.b, bn1.c, f.bt(c1.name), prev.bn3.g, ws, B, H,
                              H, c1.cin, c1.cout, 1, 1, 1, 0, Yt=prev.bn3.y, Rg=sc, X=prev.out,
                              Yt2=prev.bnd.y if pds else None, part2=ws2 if pds else None)
                 prev.bn3.finalize_bwd(ws, P1)
                 if pds:
                     prev.bnd.finalize_bwd(ws2, P1)
             else:
-                K.conv_dgrad(K.CE_BWD_RES, bn1.g, bn1.y, bn1.a, bn1.b, bn1.c, f.bt(c1.name), self.Gpool, None, B,
+                K.conv_dgrad(K.CE_BWD_RES, g1, y1, bn1.a, bn1.b, bn1.c, f.bt(c1.name), self.Gpool, None, B,
                              H, H, c1.cin, c1.cout, 1, 1, 1, 0, Rg=sc)
-            self._wgrad(lambda bp=bp: K.conv_wgrad(bp.bn1.g, bp.bn1.y, bp.bn1.a, bp.bn1.b, bp.bn1.c, bp.x_in, wg,
-                                                   f.g(bp.c1.name), B, bp.H, bp.H, bp.c1.cin, bp.c1.cout, 1, 1, 1,
-                                                   0))
+            self._wgrad(lambda bp=bp, g1=g1, y1=y1: K.conv_wgrad(
+                g1, y1, bp.bn1.a, bp.bn1.b, bp.bn1.c, ws=wg, grad=f.g(bp.c1.name), B=B, H=bp.H, W=bp.H,
+                Ci=bp.c1.cin, N=bp.c1.cout, R=1, S=1, stride=1, pad=0, **self._wx(bp.c1, bp.x_in, None)))
             names = [c1.name]
             if prev is not None:
                 names += prev.bn3.param_names + (prev.bnd.param_names if prev.bnd is not None else [])

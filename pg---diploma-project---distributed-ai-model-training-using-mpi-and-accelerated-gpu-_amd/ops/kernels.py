@@ -488,6 +488,16 @@ CP_NONE, CP_BN_RELU, CP_BNBWD = 0, 1, 3
 CE_BWD_RELU, CE_BWD_RES = 1, 2
 
 
+def conv_set_glds(mode):
+    """Operand staging of the dense convs without a prologue: 0 = register-staged kernel,
+    2 / 3 = LDS-DMA kernel with that many LDS buffers (default 2, env PGDIST_CONV_GLDS)."""
+    lib().conv_set_glds(int(mode))
+
+
+def conv_get_glds():
+    return lib().conv_get_glds()
+
+
 def conv_out_hw(H, W, R, S, stride, pad):
     return (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
 
@@ -529,21 +539,30 @@ def conv_fwd(pro, x, w, y, part, B, H, W, Ci, N, R, S, stride, pad, pa=None, pb=
 def conv_dgrad(epi, G, Y, ga, gb, gc, wt, dx, part, B, H, W, Cin, Cout, R, S, stride, pad, Yt=None, es=None,
                et=None, Rg=None, X=None, Yt2=None, part2=None):
     """Data gradient of y = conv(x, w) with this layer's BN backward fused on the way in:
-    dy = ga*G + gb*Y + gc  ([B,Ho,Wo,Cout]),  dx = conv^T(dy, wt)  ([B,H,W,Cin]), where
+    dy = ga*G + gb*Y + gc  ([B,Ho,Wo,Cout]),  dx = conv^T(dy, wt)  ([B,H,W,Cin]), or with
+    Y = None: G is dy itself, materialised by :func:`bn_mat` (LDS-DMA kernel, no prologue), where
     wt = w transposed to [Cin,R,S,Cout] (:func:`conv_wt`).  Epilogues:
       CE_BWD_RELU  dx *= 1[Yt*es + et > 0];  part <- (sum dx, sum dx*Yt)
       CE_BWD_RES   dx = (dx + Rg) * 1[X > 0]  (null operands skipped);
                    part <- (sum dx, sum dx*Yt), part2 <- (sum dx, sum dx*Yt2) when given."""
     _conv_check(Cout, Cin, "conv_dgrad")
+    if Y is None and (Cout % 64 or conv_get_glds() == 0):
+        raise ValueError("conv_dgrad: a materialised dy (Y=None) needs Cout % 64 == 0 and the LDS-DMA kernel "
+                         "(conv_set_glds != 0)")
     if H % stride or W % stride:
         raise ValueError("conv_dgrad: H and W must be multiples of the stride")
     if R > 3 or S > 3:
         raise ValueError("conv_dgrad: filters up to 3x3")
     Ho, Wo = conv_out_hw(H, W, R, S, stride, pad)
+    if G is None:
+        raise ValueError("conv_dgrad: G is required")
     for t, nm in ((G, "G"), (Y, "Y")):
         _chk(t, BF16, B * Ho * Wo * Cout, nm)
-    for t, nm in ((ga, "ga"), (gb, "gb"), (gc, "gc")):
-        _chk(t, F32, Cout, nm)
+    if Y is not None:
+        for t, nm in ((ga, "ga"), (gb, "gb"), (gc, "gc")):
+            if t is None:
+                raise ValueError(f"conv_dgrad: {nm} is required with Y")
+            _chk(t, F32, Cout, nm)
     _chk(wt, BF16, Cin * R * S * Cout, "wt")
     for t, nm in ((dx, "dx"), (Yt, "Yt"), (Rg, "Rg"), (X, "X"), (Yt2, "Yt2")):
         _chk(t, BF16, B * H * W * Cin, nm)
@@ -575,13 +594,19 @@ def conv_wgrad_workspace(B, H, W, Ci, N, R, S, stride, pad):
 
 def conv_wgrad(G, Y, ga, gb, gc, x, ws, grad, B, H, W, Ci, N, R, S, stride, pad, xpro=CP_NONE, xs=None, xt=None):
     """grad [N,R,S,Ci] (fp32, overwritten) = sum_m dy[m] (x) im2col(x')[m] with
-    dy = ga*G + gb*Y + gc and x' = relu(x*xs + xt) (xpro = CP_BN_RELU) or x."""
+    dy = ga*G + gb*Y + gc (or G itself when Y is None: materialised by :func:`bn_mat`) and
+    x' = relu(x*xs + xt) (xpro = CP_BN_RELU) or x."""
     _conv_check(Ci, N, "conv_wgrad")
     Ho, Wo = conv_out_hw(H, W, R, S, stride, pad)
+    if G is None:
+        raise ValueError("conv_wgrad: G is required")
     _chk(G, BF16, B * Ho * Wo * N, "G")
     _chk(Y, BF16, B * Ho * Wo * N, "Y")
-    for t, nm in ((ga, "ga"), (gb, "gb"), (gc, "gc")):
-        _chk(t, F32, N, nm)
+    if Y is not None:
+        for t, nm in ((ga, "ga"), (gb, "gb"), (gc, "gc")):
+            if t is None:
+                raise ValueError(f"conv_wgrad: {nm} is required with Y")
+            _chk(t, F32, N, nm)
     _chk(x, BF16, B * H * W * Ci, "x")
     if xpro == CP_BN_RELU:
         _chk(xs, F32, Ci, "xs")
@@ -590,6 +615,31 @@ def conv_wgrad(G, Y, ga, gb, gc, x, ws, grad, B, H, W, Ci, N, R, S, stride, pad,
     _chk(grad, F32, N * R * S * Ci, "grad")
     lib().conv_wgrad(_p(G), _p(Y), _p(ga), _p(gb), _p(gc), _p(x), _p(xs), _p(xt), int(xpro), _p(ws), _p(grad),
                      B, H, W, Ci, N, R, S, stride, pad, _s())
+
+
+BN_MAT_ACT, BN_MAT_BWD = 0, 1
+
+
+def bn_mat(mode, Y, a, b, out, G=None, c=None):
+    """Materialise a BN-transformed [M, C] bf16 operand for the LDS-DMA convs:
+    BN_MAT_ACT  out = relu(Y*a + b)        (producer BN + ReLU: the next conv's input)
+    BN_MAT_BWD  out = a*G + b*Y + c        (this layer's BN backward: dgrad / wgrad dy)
+    C/8 must divide 256 (C in 8, 16, ..., 2048 powers of two)."""
+    M, C = Y.shape
+    if C % 8 or 256 % (C // 8):
+        raise ValueError(f"bn_mat: C={C} (C/8 must divide 256)")
+    _chk(Y, BF16, M * C, "Y")
+    _chk(out, BF16, M * C, "out")
+    _chk(a, F32, C, "a")
+    _chk(b, F32, C, "b")
+    if mode == BN_MAT_BWD:
+        if G is None or c is None:
+            raise ValueError("bn_mat(BN_MAT_BWD) needs G and c")
+        _chk(G, BF16, M * C, "G")
+        _chk(c, F32, C, "c")
+    elif mode != BN_MAT_ACT:
+        raise ValueError(f"bn_mat: bad mode {mode}")
+    lib().bn_mat(int(mode), _p(G), _p(Y), _p(a), _p(b), _p(c), _p(out), M, C, _s())
 
 
 def conv_wt(src, dst, tab, n):

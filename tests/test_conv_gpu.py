@@ -58,12 +58,24 @@ FWD_SHAPES = [
     (2, 8, 64, 256, 1, 2, 0),
     (3, 14, 128, 128, 3, 1, 1),
     (2, 6, 512, 2048, 1, 1, 0),
+    (8, 64, 64, 128, 3, 1, 1),     # 128 x 128 tiles (>= 256 workgroups)
+    (4, 30, 128, 200, 3, 2, 1),    # N not a multiple of the N tile, M tail
 ]
 
 
+@pytest.fixture
+def glds_mode():
+    """restores the dense-conv staging mode a test selects (ops.kernels.conv_set_glds)"""
+    old = K.conv_get_glds()
+    yield K.conv_set_glds
+    K.conv_set_glds(old)
+
+
 @pytest.mark.parametrize("shape", FWD_SHAPES)
-@pytest.mark.parametrize("pro", [K.CP_NONE, K.CP_BN_RELU])
-def test_conv_fwd(dev, shape, pro):
+@pytest.mark.parametrize("pro,glds", [(K.CP_NONE, 0), (K.CP_NONE, 2), (K.CP_NONE, 3), (K.CP_BN_RELU, 2)])
+def test_conv_fwd(dev, shape, pro, glds, glds_mode):
+    """CP_NONE with Ci % 64 == 0 runs on the LDS-DMA kernel (2 or 3 LDS buffers) unless glds=0."""
+    glds_mode(glds)
     B, H, Ci, N, R, st, pad = shape
     x = bfr(rnd(B, H, H, Ci, dev=dev, seed=1))
     w = bfr(rnd(N, Ci, R, R, dev=dev, scale=(Ci * R * R) ** -0.5, seed=2))
@@ -110,6 +122,8 @@ DGRAD_SHAPES = [
     (2, 8, 64, 256, 1, 2, 0),
     (2, 14, 256, 256, 3, 2, 1),
     (2, 7, 2048, 512, 1, 1, 0),
+    (8, 64, 128, 64, 3, 1, 1),     # 128 x 128 tiles
+    (8, 64, 64, 128, 3, 2, 1),     # 128 x 64 tiles over 4 parity classes
 ]
 
 
@@ -120,9 +134,23 @@ def _dgrad_ref(dy, w, H, st, pad, B, Cin):
     return nhwc(gx)
 
 
+def _mat_dy(G, Y, ga, gb, gc):
+    """dy = ga*G + gb*Y + gc materialised by the bn_mat kernel (checked against fp32)"""
+    C = G.shape[-1]
+    bf = lambda t: t.to(torch.bfloat16).contiguous().view(-1, C)  # noqa: E731
+    out = torch.empty_like(bf(G))
+    K.bn_mat(K.BN_MAT_BWD, bf(Y), ga, gb, out, G=bf(G), c=gc)
+    torch.cuda.synchronize()
+    ref = ga * G.reshape(-1, C) + gb * Y.reshape(-1, C) + gc
+    assert rel(out, ref) < 5e-3
+    return out.view(G.shape)
+
+
 @pytest.mark.parametrize("shape", DGRAD_SHAPES)
 @pytest.mark.parametrize("epi", ["relu", "res", "plain"])
-def test_conv_dgrad(dev, shape, epi):
+@pytest.mark.parametrize("mat", [False, True])
+def test_conv_dgrad(dev, shape, epi, mat):
+    """mat: dy materialised by bn_mat and consumed by the LDS-DMA dgrad kernel (Y=None)"""
     B, H, Cin, Cout, R, st, pad = shape
     Ho, Wo = K.conv_out_hw(H, H, R, R, st, pad)
     G = bfr(rnd(B, Ho, Wo, Cout, dev=dev, seed=5))
@@ -139,6 +167,10 @@ def test_conv_dgrad(dev, shape, epi):
     K.conv_wt(ws, wt, tab, 1)
     assert torch.equal(wt.view(Cin, R, R, Cout), w.permute(1, 2, 3, 0).to(torch.bfloat16))
     bf = lambda t: t.to(torch.bfloat16).contiguous()  # noqa: E731
+    if mat:
+        Gk, Yk = _mat_dy(G, Y, ga, gb, gc), None
+    else:
+        Gk, Yk = bf(G), bf(Y)
     dx = torch.empty(B, H, H, Cin, dtype=torch.bfloat16, device=dev)
     P = K.conv_dgrad_num_partials(B, H, H, Cin, Cout, R, R, st)
     part = torch.zeros(P, 2, Cin, device=dev)
@@ -146,7 +178,7 @@ def test_conv_dgrad(dev, shape, epi):
     Yt = bfr(rnd(B, H, H, Cin, dev=dev, seed=10))
     if epi == "relu":
         es, et = bn_params(Cin, dev, 11)
-        K.conv_dgrad(K.CE_BWD_RELU, bf(G), bf(Y), ga, gb, gc, wt, dx, part, B, H, H, Cin, Cout, R, R, st, pad,
+        K.conv_dgrad(K.CE_BWD_RELU, Gk, Yk, ga, gb, gc, wt, dx, part, B, H, H, Cin, Cout, R, R, st, pad,
                      Yt=bf(Yt), es=es, et=et)
         ref = dx_ref * ((Yt * es + et) > 0)
         ref_b = bfr(ref)
@@ -155,14 +187,14 @@ def test_conv_dgrad(dev, shape, epi):
         Rg = bfr(rnd(B, H, H, Cin, dev=dev, seed=12))
         X = bfr(rnd(B, H, H, Cin, dev=dev, seed=13))
         Yt2 = bfr(rnd(B, H, H, Cin, dev=dev, seed=14))
-        K.conv_dgrad(K.CE_BWD_RES, bf(G), bf(Y), ga, gb, gc, wt, dx, part, B, H, H, Cin, Cout, R, R, st, pad,
+        K.conv_dgrad(K.CE_BWD_RES, Gk, Yk, ga, gb, gc, wt, dx, part, B, H, H, Cin, Cout, R, R, st, pad,
                      Yt=bf(Yt), Rg=bf(Rg), X=bf(X), Yt2=bf(Yt2), part2=part2)
         ref = (dx_ref + Rg) * (X > 0)
         ref_b = bfr(ref)
         s_ref = [ref_b.reshape(-1, Cin).sum(0), (ref_b * Yt).reshape(-1, Cin).sum(0),
                  (ref_b * Yt2).reshape(-1, Cin).sum(0)]
     else:
-        K.conv_dgrad(K.CE_BWD_RES, bf(G), bf(Y), ga, gb, gc, wt, dx, None, B, H, H, Cin, Cout, R, R, st, pad)
+        K.conv_dgrad(K.CE_BWD_RES, Gk, Yk, ga, gb, gc, wt, dx, None, B, H, H, Cin, Cout, R, R, st, pad)
         ref, s_ref = dx_ref, None
     torch.cuda.synchronize()
     assert rel(dx, ref) < 1.5e-2, rel(dx, ref)
@@ -197,7 +229,9 @@ def _wgrad_ref(x_in, dy, w_shape, st, pad):
 
 @pytest.mark.parametrize("shape", WGRAD_SHAPES)
 @pytest.mark.parametrize("xpro", [K.CP_NONE, K.CP_BN_RELU])
-def test_conv_wgrad(dev, shape, xpro):
+@pytest.mark.parametrize("mat", [False, True])
+def test_conv_wgrad(dev, shape, xpro, mat):
+    """mat: dy materialised by bn_mat (G = dy, Y = None)"""
     B, H, Ci, N, R, st, pad = shape
     Ho, Wo = K.conv_out_hw(H, H, R, R, st, pad)
     x = bfr(rnd(B, H, H, Ci, dev=dev, seed=21))
@@ -212,7 +246,8 @@ def test_conv_wgrad(dev, shape, xpro):
     ws = torch.zeros(max(K.conv_wgrad_workspace(B, H, H, Ci, N, R, R, st, pad), 1), device=dev)
     grad = torch.full((N, R, R, Ci), float("nan"), device=dev)
     bf = lambda t: t.to(torch.bfloat16).contiguous()  # noqa: E731
-    K.conv_wgrad(bf(G), bf(Y), ga, gb, gc, bf(x), ws, grad, B, H, H, Ci, N, R, R, st, pad, xpro=xpro,
+    Gk, Yk = (_mat_dy(G, Y, ga, gb, gc), None) if mat else (bf(G), bf(Y))
+    K.conv_wgrad(Gk, Yk, ga, gb, gc, bf(x), ws, grad, B, H, H, Ci, N, R, R, st, pad, xpro=xpro,
                  xs=xs if xpro else None, xt=xt if xpro else None)
     torch.cuda.synchronize()
     assert rel(grad, ref) < 1e-2, rel(grad, ref)
@@ -341,3 +376,14 @@ def test_wgrad_reduce(dev, S, n):
         ref = vals.double().sum(0)
         assert torch.allclose(grad.double(), ref, rtol=1e-4, atol=1e-3 * (S ** 0.5))
         assert torch.equal(grad, g2)
+
+
+@pytest.mark.parametrize("M,C", [(1000, 64), (333, 2048), (4096, 256), (7, 8)])
+def test_bn_mat_act(dev, M, C):
+    """BN_MAT_ACT: relu(y*s + t) materialised for the LDS-DMA forward conv"""
+    y = bfr(rnd(M, C, dev=dev, seed=41))
+    s, t = bn_params(C, dev, 42)
+    out = torch.empty(M, C, dtype=torch.bfloat16, device=dev)
+    K.bn_mat(K.BN_MAT_ACT, y.to(torch.bfloat16), s, t, out)
+    torch.cuda.synchronize()
+    assert rel(out, torch.relu(y * s + t)) < 5e-3
