@@ -36,6 +36,8 @@ void launch_f32_to_bf16(const float *, bf16_t *, long long, hipStream_t);
 int dw_fwd_num_partials(int, int, int, int, int);
 int bn_rep();
 void bn_fin_arm(const void *desc);
+void bn_lz_arm(const void *desc);
+void launch_bn_finalize_batch(const void *tab, int n, int maxC, hipStream_t st);
 std::string bn_fin_pack(float *, int *, int, int, float, int, const float *, const float *, float, float, float *,
                         float *, long long *, float *, float *, float *, float *, float *, float *, float *);
 void bn_set_rep(int rep);
@@ -183,6 +185,11 @@ PYBIND11_MODULE(_pgdist_C, m) {
   m.def("bn_rep", &bn_rep, "replica rows of the atomic BN-statistics accumulators");
   m.def("bn_fin_arm", [](P d) { pgdist_rt::run_op([=] { bn_fin_arm(reinterpret_cast<const void *>(d)); }); },
         "arm a device BnFin descriptor for the next BN-statistics producer launch (finalize fused in its tail)");
+  m.def("bn_lz_arm", [](P d) { pgdist_rt::run_op([=] { bn_lz_arm(reinterpret_cast<const void *>(d)); }); },
+        "arm a device BnFin descriptor for the next BN-parameter consumer launch (lazy finalize in its prologue)");
+  m.def("bn_finalize_batch", [](P tab, int n, int maxC, P s) {
+    pgdist_rt::run_op([=] { launch_bn_finalize_batch(reinterpret_cast<const void *>(tab), n, maxC, S(s)); });
+  }, "finalize every BN of a device table of BnFin descriptor pointers in one launch");
   m.def("bn_fin_pack", [](P acc, P ctr, int rows, int C, float count, int bwd, P gamma, P beta, float eps,
                           float mom, P rm, P rv, P nbt, P mean, P rstd, P scale, P shift, P coef, P dgamma,
                           P dbeta) {

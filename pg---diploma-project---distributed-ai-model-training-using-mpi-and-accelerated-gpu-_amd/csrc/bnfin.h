@@ -122,3 +122,58 @@ PG_DEVICE void bn_fin_tail(const BnFin *fin) {
 // host: the descriptor armed for the next producer launch (bn_fin_arm), taken (and cleared)
 // by that launcher; nullptr when none is armed
 const BnFin *take_bn_fin();
+
+// ---------------------------------------------------------------------------
+// Lazy (consumer-side) finalize.  A kernel that consumes a BN's per-channel parameters
+// (forward: scale / shift of the BN-apply prologue; backward: the dgrad coefficients a, b, c)
+// computes the ones it needs itself from the producer's replica rows instead of waiting for
+// a separate finalize launch between the two kernels: the rows were written by an EARLIER
+// kernel, so plain loads see them (kernel-boundary visibility, no hand-off inside the grid).
+// Redundant work per workgroup: 2 x kBnRep (+2..4) loads per needed channel, issued together.
+// The side outputs (mean / rstd / running statistics; dgamma / dbeta) are written off the
+// critical path by the regular finalize kernels (a batched forward finalize at the end of
+// the forward, the backward ones on the weight-gradient side stream); the backward form
+// reads mean / rstd, which that forward finalize wrote.  Bitwise the values of
+// bn_finalize_small_kernel (same accumulation order and rounding).
+// ---------------------------------------------------------------------------
+PG_DEVICE void bn_lazy(const BnFin *d, int c, float &o0, float &o1, float &o2) {
+  const int C = d->C, rows = d->rows;
+  const float *acc = d->acc;
+  const float g = d->gamma ? d->gamma[c] : 1.f;
+  const float b = (!d->bwd && d->beta) ? d->beta[c] : 0.f;
+  const float mu = d->bwd ? d->mean[c] : 0.f, rs = d->bwd ? d->rstd[c] : 0.f;
+  float v[2 * kBnRep];
+#pragma unroll
+  for (int r = 0; r < kBnRep; ++r) {
+    const int rr = r < rows ? r : 0;
+    v[2 * r] = acc[(size_t)(2 * rr) * C + c];
+    v[2 * r + 1] = acc[(size_t)(2 * rr + 1) * C + c];
+  }
+  double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+  for (int r = 0; r < kBnRep; ++r) {
+    const double m = r < rows ? 1.0 : 0.0;
+    s0 += m * (double)v[2 * r];
+    s1 += m * (double)v[2 * r + 1];
+  }
+  const double n = (double)d->count;
+  if (d->bwd) {
+    const double sgx = (s1 - (double)mu * s0) * rs;
+    const double a = (double)g * rs;
+    o0 = (float)a;
+    o1 = (float)(-a * rs * sgx / n);
+    o2 = (float)(-a * s0 / n + a * rs * (double)mu * sgx / n);
+  } else {
+    const double m = s0 / n;
+    double var = s1 / n - m * m;
+    if (var < 0.0) var = 0.0;
+    const float r = (float)(1.0 / sqrt(var + (double)d->eps));
+    o0 = g * r;
+    o1 = b - (float)m * g * r;
+    o2 = 0.f;
+  }
+}
+
+// host: the lazy descriptor armed for the next consumer launch (bn_lz_arm); nullptr: the
+// consumer reads materialised parameters
+const BnFin *take_bn_lz();

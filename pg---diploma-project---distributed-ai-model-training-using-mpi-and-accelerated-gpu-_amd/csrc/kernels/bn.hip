@@ -164,13 +164,26 @@ __global__ __launch_bounds__(128) void bn_finalize_small_kernel(
 
 // ---------------------------------------------------------------------------
 // materialise out = act(y*scale+shift) (+ res)    [M][C] bf16, C % 8 == 0
+// LZ: scale / shift computed per workgroup from the producer's replica rows (bn_lazy) into LDS
 // ---------------------------------------------------------------------------
-template <bool RELU6, bool RES>
+template <bool RELU6, bool RES, bool LZ>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t *__restrict__ y,
                                                       const bf16_t *__restrict__ res,
                                                       const float *__restrict__ scale,
                                                       const float *__restrict__ shift,
-                                                      bf16_t *__restrict__ out, long long n8, int C8) {
+                                                      bf16_t *__restrict__ out, long long n8, int C8,
+                                                      const BnFin *lz) {
+  extern __shared__ float sp[];   // LZ: [2][C]
+  if constexpr (LZ) {
+    const int C = C8 * 8;
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      float a, b, unused;
+      bn_lazy(lz, c, a, b, unused);
+      sp[c] = a;
+      sp[C + c] = b;
+    }
+    __syncthreads();
+  }
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8;
        i += (long long)gridDim.x * blockDim.x) {
     const int c0 = (int)(i % C8) * 8;
@@ -179,13 +192,47 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t *__restrict_
     if constexpr (RES) unpack8(ldg16(res + i * 8), r);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      float a = fmaf(v[k], scale[c0 + k], shift[c0 + k]);
+      float a;
+      if constexpr (LZ) a = fmaf(v[k], sp[c0 + k], sp[C8 * 8 + c0 + k]);
+      else a = fmaf(v[k], scale[c0 + k], shift[c0 + k]);
       if constexpr (RELU6) a = relu6f(a);
       if constexpr (RES) a += r[k];
       v[k] = a;
     }
     stg16(out + i * 8, pack8(v));
   }
+}
+
+// Batched finalize over a table of descriptors (grid: channel blocks x BNs): the side outputs
+// of BNs whose consumers finalized lazily (forward: mean / rstd / scale / shift / running
+// statistics of every BN of the forward in ONE launch at its end; backward: coef / dgamma /
+// dbeta), same values as bn_finalize_small_kernel.
+__global__ __launch_bounds__(128) void bn_finalize_batch_kernel(const BnFin *const *__restrict__ tab) {
+  const BnFin *d = tab[blockIdx.y];
+  const int c = blockIdx.x * 128 + threadIdx.x;
+  if (c < d->C) {
+    const int C = d->C, rows = d->rows;
+    float v[2 * kBnRep];
+#pragma unroll
+    for (int r = 0; r < kBnRep; ++r) {
+      const int rr = r < rows ? r : 0;
+      v[2 * r] = d->acc[(size_t)(2 * rr) * C + c];
+      v[2 * r + 1] = d->acc[(size_t)(2 * rr + 1) * C + c];
+    }
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int r = 0; r < kBnRep; ++r) {
+      const double m = r < rows ? 1.0 : 0.0;
+      s0 += m * (double)v[2 * r];
+      s1 += m * (double)v[2 * r + 1];
+    }
+    if (d->bwd)
+      bn_bwd_channel(c, C, s0, s1, (double)d->count, d->mean, d->rstd, d->gamma, d->coef, d->dgamma, d->dbeta);
+    else
+      bn_fwd_channel(c, s0, s1, (double)d->count, d->gamma, d->beta, d->eps, d->momentum, d->rmean, d->rvar,
+                     d->mean, d->rstd, d->scale, d->shift);
+  }
+  if (!d->bwd && d->nbt && blockIdx.x == 0 && threadIdx.x == 0) d->nbt[0] += 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -200,6 +247,19 @@ const BnFin *take_bn_fin() {
   const BnFin *d = g_bn_fin;
   g_bn_fin = nullptr;
   return d;
+}
+// lazy-finalize descriptor armed for the next consumer launch (see bnfin.h bn_lazy)
+static const BnFin *g_bn_lz = nullptr;
+void bn_lz_arm(const void *desc) { g_bn_lz = static_cast<const BnFin *>(desc); }
+const BnFin *take_bn_lz() {
+  const BnFin *d = g_bn_lz;
+  g_bn_lz = nullptr;
+  return d;
+}
+void launch_bn_finalize_batch(const void *tab, int n, int maxC, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(bn_finalize_batch_kernel, dim3((maxC + 127) / 128, n), dim3(128), 0, st,
+                     static_cast<const BnFin *const *>(tab));
 }
 // the descriptor as bytes (the caller copies them to device memory once)
 std::string bn_fin_pack(float *acc, int *ctr, int rows, int C, float count, int bwd, const float *gamma,
@@ -272,15 +332,23 @@ void launch_bn_bwd_finalize(const float *part, int P, int C, float count, const 
 
 void launch_bn_apply(const bf16_t *y, const bf16_t *res, const float *scale, const float *shift,
                      bf16_t *out, long long M, int C, bool relu6, hipStream_t st) {
+  const BnFin *lz = take_bn_lz();
   const long long n8 = M * (C / 8);
   int grid = (int)((n8 + 255) / 256);
-  if (grid > 8192) grid = 8192;
+  // lazy: every workgroup finalizes all C channels, so fewer (grid-stride) workgroups
+  const int cap = lz ? 2048 : 8192;
+  if (grid > cap) grid = cap;
   const int C8 = C / 8;
+  const size_t lds = lz ? (size_t)2 * C * sizeof(float) : 0;
+#define BNA(R6, RS)                                                                                            \
+  if (lz) hipLaunchKernelGGL((bn_apply_kernel<R6, RS, true>), dim3(grid), dim3(256), lds, st, y, res, scale,    \
+                             shift, out, n8, C8, lz);                                                           \
+  else hipLaunchKernelGGL((bn_apply_kernel<R6, RS, false>), dim3(grid), dim3(256), 0, st, y, res, scale, shift, \
+                          out, n8, C8, lz);
   if (relu6) {
-    if (res) hipLaunchKernelGGL((bn_apply_kernel<true, true>), dim3(grid), dim3(256), 0, st, y, res, scale, shift, out, n8, C8);
-    else hipLaunchKernelGGL((bn_apply_kernel<true, false>), dim3(grid), dim3(256), 0, st, y, res, scale, shift, out, n8, C8);
+    if (res) { BNA(true, true) } else { BNA(true, false) }
   } else {
-    if (res) hipLaunchKernelGGL((bn_apply_kernel<false, true>), dim3(grid), dim3(256), 0, st, y, res, scale, shift, out, n8, C8);
-    else hipLaunchKernelGGL((bn_apply_kernel<false, false>), dim3(grid), dim3(256), 0, st, y, res, scale, shift, out, n8, C8);
+    if (res) { BNA(false, true) } else { BNA(false, false) }
   }
+#undef BNA
 }

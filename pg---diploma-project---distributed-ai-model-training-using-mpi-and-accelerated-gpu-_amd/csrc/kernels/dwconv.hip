@@ -37,7 +37,24 @@ struct DwGeom {
   int tiles_w, tiles_h;
   int bn_rep;         // BN-statistics replica rows (g_bn_rep)
   const BnFin *fin;   // fused BN finalize in the tail (nullptr: none)
+  const BnFin *lz;    // lazy finalize (fwd: the input BN's scale / shift; dgrad: this layer's coef)
 };
+
+// Lazy BN finalize of this workgroup's channel slab [cbase, cbase + CC) into LDS (one
+// channel per thread, CC <= 64), then a barrier: every thread reads its CPT channels from
+// LDS instead of each computing them (the slab is shared by C4 = CC/4 threads per column).
+// npar = 2: forward scale / shift; 3: backward coefficients.
+__shared__ float lzp[3][64];
+PG_DEVICE void lazy_stage(const DwGeom &g, int cbase, int npar) {
+  if ((int)threadIdx.x < g.CC) {
+    float a, b, c;
+    bn_lazy(g.lz, cbase + threadIdx.x, a, b, c);
+    lzp[0][threadIdx.x] = a;
+    lzp[1][threadIdx.x] = b;
+    if (npar == 3) lzp[2][threadIdx.x] = c;
+  }
+  __syncthreads();
+}
 
 PG_DEVICE void unpack4(const uint2 &u, float (&f)[CPT]) {
   f[0] = __uint_as_float(u.x << 16);
@@ -227,10 +244,17 @@ __global__ __launch_bounds__(256) void dw_fwd_lds_kernel(
   const rsrc_t ry = make_rsrc(y, (uint32_t)g.B * g.Ho * g.Wo * g.C * 2);
 
   float s[CPT], t[CPT], stats[2][CPT], wt[9][CPT];
+  const bool lazy = ACT != ACT_NONE && g.lz != nullptr;
+  if (lazy) lazy_stage(g, cbase, 2);
 #pragma unroll
   for (int k = 0; k < CPT; ++k) {
-    s[k] = (ACT != ACT_NONE) ? in_s[c0 + k] : 1.f;
-    t[k] = (ACT != ACT_NONE) ? in_t[c0 + k] : 0.f;
+    if (lazy) {
+      s[k] = lzp[0][c4 * CPT + k];
+      t[k] = lzp[1][c4 * CPT + k];
+    } else {
+      s[k] = (ACT != ACT_NONE) ? in_s[c0 + k] : 1.f;
+      t[k] = (ACT != ACT_NONE) ? in_t[c0 + k] : 0.f;
+    }
     stats[0][k] = stats[1][k] = 0.f;
   }
 #pragma unroll
@@ -344,11 +368,18 @@ __global__ __launch_bounds__(256) void dw_dgrad_s1_lds_kernel(
 
   float al[CPT], be[CPT], ga[CPT], s[CPT], t[CPT], stats[2][CPT], wt[9][CPT];
   float accw[WG ? 9 : 1][CPT];
+  if (g.lz) lazy_stage(g, cbase, 3);
 #pragma unroll
   for (int k = 0; k < CPT; ++k) {
-    al[k] = coef[c0 + k];
-    be[k] = coef[g.C + c0 + k];
-    ga[k] = coef[2 * g.C + c0 + k];
+    if (g.lz) {
+      al[k] = lzp[0][c4 * CPT + k];
+      be[k] = lzp[1][c4 * CPT + k];
+      ga[k] = lzp[2][c4 * CPT + k];
+    } else {
+      al[k] = coef[c0 + k];
+      be[k] = coef[g.C + c0 + k];
+      ga[k] = coef[2 * g.C + c0 + k];
+    }
     s[k] = ps[c0 + k];
     t[k] = pt[c0 + k];
     stats[0][k] = stats[1][k] = 0.f;
@@ -495,11 +526,18 @@ __global__ __launch_bounds__(256) void dw_dgrad_s2_lds_kernel(
   const rsrc_t ro = make_rsrc(gout, nin);
 
   float al[CPT], be[CPT], ga[CPT], s[CPT], t[CPT], stats[2][CPT];
+  if (g.lz) lazy_stage(g, cbase, 3);
 #pragma unroll
   for (int k = 0; k < CPT; ++k) {
-    al[k] = coef[c0 + k];
-    be[k] = coef[g.C + c0 + k];
-    ga[k] = coef[2 * g.C + c0 + k];
+    if (g.lz) {
+      al[k] = lzp[0][c4 * CPT + k];
+      be[k] = lzp[1][c4 * CPT + k];
+      ga[k] = lzp[2][c4 * CPT + k];
+    } else {
+      al[k] = coef[c0 + k];
+      be[k] = coef[g.C + c0 + k];
+      ga[k] = coef[2 * g.C + c0 + k];
+    }
     s[k] = ps[c0 + k];
     t[k] = pt[c0 + k];
     stats[0][k] = stats[1][k] = 0.f;
@@ -784,6 +822,7 @@ DwGeom dw_geom(int kind, int B, int H, int W, int C, int stride) {
   DwGeom g;
   g.bn_rep = g_bn_rep;
   g.fin = nullptr;
+  g.lz = nullptr;
   g.B = B;
   g.H = H;
   g.W = W;
@@ -828,6 +867,7 @@ void launch_dw_fwd(const bf16_t *x, const float *in_s, const float *in_t, int ac
                    bf16_t *y, float *part, int B, int H, int W, int C, int stride, hipStream_t st) {
   DwGeom g = dw_geom(0, B, H, W, C, stride);
   g.fin = take_bn_fin();
+  g.lz = take_bn_lz();
   const dim3 grid(dw_grid_x(g) * (C / g.CC)), block(256);
   if (stride == 1) {
     if (act == ACT_BN_RELU6) hipLaunchKernelGGL((dw_fwd_lds_kernel<1, ACT_BN_RELU6>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
@@ -845,6 +885,7 @@ void launch_dw_dgrad(const bf16_t *gin, const bf16_t *yself, const float *coef, 
                      float *part, int B, int H, int W, int C, int stride, float *wpart, hipStream_t st) {
   DwGeom g = dw_geom(1, B, H, W, C, stride);
   g.fin = take_bn_fin();
+  g.lz = take_bn_lz();
   const dim3 grid(dw_grid_x(g) * (C / g.CC)), block(256);
   if (wpart) {
     if (stride == 1)

@@ -48,6 +48,7 @@ struct PwBwdArgs {
   int M, Kg, Ng;
   int bn_rep;                   // BN-statistics replica rows (g_bn_rep)
   const BnFin *fin;             // fused BN finalize in the tail (nullptr: none)
+  const BnFin *lz;              // lazy finalize of ca / cb / cc (nullptr: materialised)
 };
 template <int KP, int BN, int BM>
 struct BwdLds {
@@ -110,9 +111,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
   }
   for (int i = tid; i < KP; i += 256) {
     const bool ok = i < p.Kg;
-    Ps[i] = ok ? p.ca[i] : 0.f;
-    Ps[KP + i] = ok ? p.cb[i] : 0.f;
-    Ps[2 * KP + i] = ok ? p.cc[i] : 0.f;
+    if (p.lz) {
+      float a = 0.f, b = 0.f, c = 0.f;
+      if (ok) bn_lazy(p.lz, i, a, b, c);
+      Ps[i] = a;
+      Ps[KP + i] = b;
+      Ps[2 * KP + i] = c;
+    } else {
+      Ps[i] = ok ? p.ca[i] : 0.f;
+      Ps[KP + i] = ok ? p.cb[i] : 0.f;
+      Ps[2 * KP + i] = ok ? p.cc[i] : 0.f;
+    }
   }
   for (int i = tid; i < BN; i += 256) {
     const bool ok = !LIN && n0 + i < p.Ng;
@@ -424,8 +433,9 @@ void launch_pw_bwd(int epi, const bf16_t *G, const bf16_t *Y, const float *ca, c
                    float *grad, int M, int Kg, int Ng, hipStream_t st) {
   const BwdGeom g = bwd_geom(M, Kg, Ng);
   const BnFin *fin = take_bn_fin();
+  const BnFin *lz = take_bn_lz();
   if (!g.ok) return;
-  PwBwdArgs a{G, Y, ca, cb, cc, WT, out, Yt, es, et, R, X, part, wpart, M, Kg, Ng, g_bn_rep, fin};
+  PwBwdArgs a{G, Y, ca, cb, cc, WT, out, Yt, es, et, R, X, part, wpart, M, Kg, Ng, g_bn_rep, fin, lz};
   if (epi == EPI_BWD_RELU6_) launch_bwd_epi<EPI_BWD_RELU6_>(a, g, st);
   else launch_bwd_epi<EPI_BWD_LIN_>(a, g, st);
   // grad == nullptr: the caller reduces wpart itself (e.g. on its weight-gradient stream)

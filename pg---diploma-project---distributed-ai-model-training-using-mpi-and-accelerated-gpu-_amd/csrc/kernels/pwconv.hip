@@ -69,6 +69,7 @@ struct PwArgs {
   int ldw8;
   int bn_rep;           // BN-statistics replica rows (g_bn_rep)
   const BnFin *fin;     // fused BN finalize in the tail (nullptr: none)
+  const BnFin *lz;      // lazy finalize of the prologue parameters pa/pb(/pc) (nullptr: materialised)
 };
 }  // namespace
 
@@ -182,9 +183,17 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
   if constexpr (NPAR > 0) {
     for (int i = tid; i < Kp; i += 256) {
       const bool ok = i < p.K;
-      Ps[i] = ok ? p.pa[i] : 0.f;
-      Ps[Kp + i] = ok ? p.pb[i] : 0.f;
-      if constexpr (NPAR == 3) Ps[2 * Kp + i] = ok ? p.pc[i] : 0.f;
+      if (p.lz) {
+        float a = 0.f, b = 0.f, c = 0.f;
+        if (ok) bn_lazy(p.lz, i, a, b, c);
+        Ps[i] = a;
+        Ps[Kp + i] = b;
+        if constexpr (NPAR == 3) Ps[2 * Kp + i] = c;
+      } else {
+        Ps[i] = ok ? p.pa[i] : 0.f;
+        Ps[Kp + i] = ok ? p.pb[i] : 0.f;
+        if constexpr (NPAR == 3) Ps[2 * Kp + i] = ok ? p.pc[i] : 0.f;
+      }
     }
   }
   __syncthreads();
@@ -716,6 +725,7 @@ void launch_pw_gemm(int pro, int epi, const bf16_t *A, const bf16_t *A2, const f
     return;
   }
   a.fin = take_bn_fin();
+  a.lz = take_bn_lz();
 #define PW_CASE(P, E) \
   if (pro == P && epi == E) { launch_pw_geom<P, E>(a, g, st); return; }
   PW_CASE(ACT_NONE, EPI_FWD)
@@ -741,7 +751,7 @@ void launch_pw_gemm_f8(int pro, const bf16_t *A, const float *pa, const float *p
     return;
   }
   PwArgs a{A, nullptr, pa, pb, nullptr, nullptr, out, nullptr, nullptr, nullptr, nullptr, part, M, N, K, nullptr,
-           W8, wsc, asc, ldw8, g_bn_rep, take_bn_fin()};
+           W8, wsc, asc, ldw8, g_bn_rep, take_bn_fin(), take_bn_lz()};
   const int Kp = (K + 63) / 64 * 64;
   g.lds -= (size_t)g.BN * (Kp + kBPad) * 2;
   g.lds += (size_t)g.BN * (Kp + 16);

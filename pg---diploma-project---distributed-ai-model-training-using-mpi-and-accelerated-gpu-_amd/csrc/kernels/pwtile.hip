@@ -38,6 +38,7 @@ struct PwTArgs {
   int ldw8;
   int bn_rep;           // BN-statistics replica rows (g_bn_rep)
   const BnFin *fin;     // fused BN finalize in the tail (nullptr: none)
+  const BnFin *lz;      // lazy finalize of the prologue parameters (nullptr: materialised pa/pb/pc)
 };
 }  // namespace
 
@@ -94,9 +95,17 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
   if constexpr (NPAR > 0) {
     for (int i = tid; i < Kp; i += 256) {
       const bool ok = i < p.K;
-      Ps[i] = ok ? p.pa[i] : 0.f;
-      Ps[Kp + i] = ok ? p.pb[i] : 0.f;
-      if constexpr (NPAR == 3) Ps[2 * Kp + i] = ok ? p.pc[i] : 0.f;
+      if (p.lz) {
+        float a = 0.f, b = 0.f, c = 0.f;
+        if (ok) bn_lazy(p.lz, i, a, b, c);
+        Ps[i] = a;
+        Ps[Kp + i] = b;
+        if constexpr (NPAR == 3) Ps[2 * Kp + i] = c;
+      } else {
+        Ps[i] = ok ? p.pa[i] : 0.f;
+        Ps[Kp + i] = ok ? p.pb[i] : 0.f;
+        if constexpr (NPAR == 3) Ps[2 * Kp + i] = ok ? p.pc[i] : 0.f;
+      }
     }
   }
 
@@ -387,6 +396,7 @@ void launch_pw_tile(int pro, int epi, const bf16_t *A, const bf16_t *A2, const f
   PwTArgs a{A, A2, pa, pb, pc, W, out, Yt, es, et, R, part, M, N, K, Aout};
   a.bn_rep = g_bn_rep;
   a.fin = take_bn_fin();
+  a.lz = take_bn_lz();
   const TileGeom g = tile_geom(M, N, K, pro);
 #define PT_CASE(P, E) \
   if (pro == P && epi == E) { launch_tile_pe<P, E>(a, g, st); return; }
@@ -403,7 +413,7 @@ void launch_pw_tile_f8(int pro, const bf16_t *A, const float *pa, const float *p
                        const float *wsc, float asc, bf16_t *out, float *part, int M, int N, int K,
                        hipStream_t st) {
   PwTArgs a{A, nullptr, pa, pb, nullptr, nullptr, out, nullptr, nullptr, nullptr, nullptr, part, M, N, K,
-            nullptr, W8, wsc, asc, ldw8, g_bn_rep, take_bn_fin()};
+            nullptr, W8, wsc, asc, ldw8, g_bn_rep, take_bn_fin(), take_bn_lz()};
   TileGeom g = tile_geom(M, N, K, pro);   // the bf16 LDS size bounds the e4m3 one
   if (pro == ACT_NONE) launch_tile_pe<ACT_NONE, EPI_FWD_T, true>(a, g, st);
   else if (pro == ACT_BN_RELU6) launch_tile_pe<ACT_BN_RELU6, EPI_FWD_T, true>(a, g, st);

@@ -94,14 +94,24 @@ class AtomicBNState(BNState):
     finalize reduces those rows only (deterministic mode: bn_rep unbounded, one row per
     producer workgroup).  ``rows_f`` / ``rows_b``: rows the accumulators were sized for.
 
-    Fused finalize (default, not in deterministic mode): ``fin_f`` / ``fin_b`` are device
-    descriptors (ops.kernels.bn_fin_desc) the executor passes to the statistics producers,
-    whose last workgroup then finalizes this BN in the producer's tail (bnfin.h) instead of a
-    separate finalize launch; ``finalize_fwd`` / ``finalize_bwd`` are then no-ops."""
+    The finalize itself has three modes (``MobileNetV2Executor.bn_mode``):
+
+    * ``lazy`` (default): ``lz_f`` / ``lz_b`` are device descriptors (ops.kernels.bn_fin_desc)
+      passed to the CONSUMERS of this BN's parameters, which compute the scale / shift (or
+      the backward coefficients) they need from the accumulator rows in their prologue
+      (bnfin.h bn_lazy) -- no finalize launch between producer and consumer.  The side
+      outputs are written off the critical path: every forward BN by one batched finalize at
+      the end of the forward, the backward ones on the weight-gradient side stream.
+    * ``fused`` (PGDIST_BN_FUSED=1): ``fin_f`` / ``fin_b`` go to the statistics PRODUCERS,
+      whose last workgroup finalizes in the producer's tail; measured slower.
+    * ``launch`` (deterministic mode, or PGDIST_BN_LAZY=0): a separate finalize launch on
+      the main stream after every producer."""
     rows_f = rows_b = 0
     fin_f = fin_b = None
+    lz_f = lz_b = None
+    desc_f = desc_b = None
 
-    def build_fin(self, ctr_f, ctr_b):
+    def build_desc(self, ctr_f, ctr_b):
         """(Re)write the fused-finalize descriptors (in place once built, so captured graphs
         keep valid pointers): call again after the module's running buffers were re-homed."""
         m = self.module
@@ -111,22 +121,25 @@ class AtomicBNState(BNState):
                            shift=self.shift)
         db = K.bn_fin_desc(self.acc_b, ctr_b, self.rows_b, self.C, self.M, 1, gamma=self.gamma, mean=self.mean,
                            rstd=self.rstd, coef=self.coef, dgamma=self.dgamma, dbeta=self.dbeta)
-        if self.fin_f is None:
-            self.fin_f, self.fin_b = df, db
+        if self.desc_f is None:
+            self.desc_f, self.desc_b = df, db
         else:
-            self.fin_f.copy_(df)
-            self.fin_b.copy_(db)
+            self.desc_f.copy_(df)
+            self.desc_b.copy_(db)
 
     def finalize_fwd(self, part, P):
         r = K.bn_rows(P)
         assert r <= self.rows_f, f"{self.prefix}: forward producer has {r} rows > {self.rows_f} allocated"
-        if self.fin_f is None:
+        if self.fin_f is None and self.lz_f is None:
             super().finalize_fwd(part, r)
 
-    def finalize_bwd(self, part, P):
+    def finalize_bwd(self, part, P, force=False):
+        """Backward finalize launch; skipped when fused into the producer, and in lazy mode
+        unless ``force`` (the executor forces it where the side outputs are needed: on the
+        side stream, or for a main-stream consumer without a lazy prologue)."""
         r = K.bn_rows(P)
         assert r <= self.rows_b, f"{self.prefix}: backward producer has {r} rows > {self.rows_b} allocated"
-        if self.fin_b is None:
+        if self.fin_b is None and (self.lz_b is None or force):
             super().finalize_bwd(part, r)
 
 
@@ -261,8 +274,17 @@ class MobileNetV2Executor:
         # its statistics atomics to be acknowledged before arriving, which costs more than
         # the kernel boundary it saves
         self.fused_bn = not K.deterministic() and os.environ.get("PGDIST_BN_FUSED", "0") == "1"
+        # lazy finalize (default): the consumers compute the BN parameters from the accumulator
+        # rows (bnfin.h bn_lazy); one batched forward finalize, backward finalizes on the side
+        self.lazy_bn = (not K.deterministic() and not self.fused_bn
+                        and os.environ.get("PGDIST_BN_LAZY", "1") == "1")
+        self.bn_mode = "lazy" if self.lazy_bn else ("fused" if self.fused_bn else "launch")
         self.bn_ctr = torch.zeros(8 * len(spans) + 16, dtype=torch.int32, device=device)   # 16-B apart
         self.refresh_bn_fin()
+        if self.lazy_bn:
+            bns = self.all_bns()
+            self.fwd_fin_tab = K.bn_desc_table([bn.desc_f for bn in bns])
+            self.fwd_fin_n, self.fwd_fin_maxc = len(bns), max(bn.C for bn in bns)
         self.ws_wgrad = torch.zeros(max(wg) + 1024, **f32)
         # the stem weight gradient may run on the main stream concurrently with side-stream
         # weight gradients: its own split-M workspace
@@ -271,6 +293,8 @@ class MobileNetV2Executor:
         # weight gradients that are not fused into a dgrad run on a side stream, overlapping
         # the dgrad -> BN-finalize chain (the backward's critical path)
         self.side = None
+        self._side_pending: List[Callable[[], None]] = []
+        self.side_batch = max(1, int(os.environ.get("PGDIST_SIDE_BATCH", "3")))
         if device.type == "cuda" and side_stream:
             self.side = torch.cuda.Stream(device)
             K.register_side_stream(self.side)
@@ -309,12 +333,17 @@ class MobileNetV2Executor:
 
     # ------------------------------------------------------------------ helpers
     def refresh_bn_fin(self):
-        """(Re)build the fused BN-finalize descriptors (after BN running buffers were re-homed,
-        e.g. coalesced for the per-step buffer broadcast)."""
-        if not self.fused_bn:
+        """(Re)build the BN-finalize descriptors of the fused / lazy modes (after BN running
+        buffers were re-homed, e.g. coalesced for the per-step buffer broadcast): in place, so
+        recorded plans, captured graphs and the batched-finalize table stay valid."""
+        if not (self.fused_bn or self.lazy_bn):
             return
         for i, bn in enumerate(self.all_bns()):
-            bn.build_fin(self.bn_ctr[8 * i:8 * i + 1], self.bn_ctr[8 * i + 4:8 * i + 5])
+            bn.build_desc(self.bn_ctr[8 * i:8 * i + 1], self.bn_ctr[8 * i + 4:8 * i + 5])
+            if self.fused_bn:
+                bn.fin_f, bn.fin_b = bn.desc_f, bn.desc_b
+            else:
+                bn.lz_f, bn.lz_b = bn.desc_f, bn.desc_b
 
     def _bn_producer_rows(self):
         """{bn: (forward P, backward P)}: partial rows of the kernels that produce each BN's
@@ -355,9 +384,13 @@ class MobileNetV2Executor:
         """Gradients of ``names`` are final once the work enqueued so far completes.  With a
         side stream the callback (DDP bucket launch) runs on it after it has joined the main
         stream, so the collective is ordered after both streams' producers.  Host-side Python
-        (the reducer's bookkeeping and collectives): a launch-plan op (ops.kernels.plan_py)."""
+        (the reducer's bookkeeping and collectives): a launch-plan op (ops.kernels.plan_py).
+        A call that launches a bucket first flushes the deferred side-stream work (the probe
+        is a pure function of this step's reducer state, identical at record and replay)."""
         if self.on_params_ready is None:
             return
+        if self.side is not None and (self.ready_probe is None or self.ready_probe(names)):
+            self._flush_side()
         K.plan_py(lambda: self._ready_now(names))
 
     def _ready_now(self, names):
@@ -370,31 +403,56 @@ class MobileNetV2Executor:
 
     def _wgrad(self, fn):
         """Enqueue a weight-gradient launch on the side stream (after the main stream's
-        work so far, which produced its inputs)."""
+        work so far, which produced its inputs).  Deferred in groups of ``side_batch``: every
+        side-stream join is an event record on the main stream, whose barrier packet keeps the
+        next main kernel from overlapping the previous one's completion (~5-6 us of main-stream
+        idle per join on MI355X); one join per group instead of one per layer."""
         if self.side is None:
             fn()
             return
+        self._side_pending.append(fn)
+        if len(self._side_pending) >= self.side_batch:
+            self._flush_side()
+
+    def _flush_side(self):
+        """Join the side stream to the main stream's work so far and enqueue the deferred
+        weight-gradient work on it."""
+        if self.side is None or not self._side_pending:
+            return
         K.stream_wait(self.side, torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.side):
-            fn()
+            for fn in self._side_pending:
+                fn()
+        self._side_pending.clear()
 
-    def _consume_output(self, pend, W, out, ws, M, N, K_, fin=None):
+    def _consume_output(self, pend, W, out, ws, M, N, K_, fin=None, lz=None):
         """Forward 1x1 conv whose input is a pending block output: prologue BN_p (+ residual),
         side-writes the block output o."""
         bn, res, o = pend
         if res is not None:
             K.pw_gemm(K.PRO_BNRES, K.EPI_FWD, bn.y, W, out, ws, M, N, K_, A2=res, pa=bn.scale, pb=bn.shift, Aout=o,
-                      fin=fin)
+                      fin=fin, lz=lz)
         else:
-            K.pw_gemm(K.ACT_BN, K.EPI_FWD, bn.y, W, out, ws, M, N, K_, pa=bn.scale, pb=bn.shift, Aout=o, fin=fin)
+            K.pw_gemm(K.ACT_BN, K.EPI_FWD, bn.y, W, out, ws, M, N, K_, pa=bn.scale, pb=bn.shift, Aout=o, fin=fin,
+                      lz=lz)
 
-    def _pw_fwd(self, pro, A, wname, out, ws, M, N, K_, pa=None, pb=None, fin=None):
+    def _pw_fwd(self, pro, A, wname, out, ws, M, N, K_, pa=None, pb=None, fin=None, lz=None):
         """Forward 1x1 conv: bf16 MFMA GEMM, or the e4m3 one in fp8 mode."""
         if self.fp8:
             W8, wsc = self.w8[wname]
-            K.pw_gemm_f8(pro, A, W8, wsc, out, ws, M, N, K_, pa=pa, pb=pb, fin=fin)
+            K.pw_gemm_f8(pro, A, W8, wsc, out, ws, M, N, K_, pa=pa, pb=pb, fin=fin, lz=lz)
         else:
-            K.pw_gemm(pro, K.EPI_FWD, A, self.flat.b(wname), out, ws, M, N, K_, pa=pa, pb=pb, fin=fin)
+            K.pw_gemm(pro, K.EPI_FWD, A, self.flat.b(wname), out, ws, M, N, K_, pa=pa, pb=pb, fin=fin, lz=lz)
+
+    def _side_fin(self, *bn_p):
+        """Lazy mode: the backward finalizes of (bn, P) pairs whose statistics the main stream
+        just produced -- coef for the side-stream weight gradients, dgamma / dbeta for the
+        gradient buckets and the optimizer.  Called inside a ``_wgrad`` callable, so they run
+        on the side stream ahead of that weight gradient (main-stream consumers computed the
+        coefficients themselves)."""
+        if self.lazy_bn:
+            for bn, P in zip(bn_p[0::2], bn_p[1::2]):
+                bn.finalize_bwd(bn.acc_b, P, force=True)
 
     def _fin_fwd(self, bn: BNState, P: int, train: bool):
         if train:
@@ -411,6 +469,7 @@ class MobileNetV2Executor:
             K.w8_quant(f.master, self.w8_buf, self.w8_scale, self.w8_tab, self.w8_tab.shape[0])
         # stem
         F = (lambda bn: bn.fin_f) if train else (lambda bn: None)   # fused forward finalize  # noqa: E731
+        L = (lambda bn: bn.lz_f) if train else (lambda bn: None)    # lazy: consumer-side  # noqa: E731
         K.stem_fwd(self.img, f.b(self.stem_w), self.bn0.y, self.bn0.acc_f, B, S, S, fin=F(self.bn0))
         self._fin_fwd(self.bn0, K.stem_num_partials(B, S, S), train)
         inp_bn, inp_t = self.bn0, None   # block input: virtual relu6(bn0(y0))
@@ -424,10 +483,10 @@ class MobileNetV2Executor:
             if bp.expand:
                 if pend is not None:
                     self._consume_output(pend, f.b(bp.w_e), bp.bn_e.y, bp.bn_e.acc_f, Min, bp.hidden, bp.cin,
-                                         fin=F(bp.bn_e))
+                                         fin=F(bp.bn_e), lz=L(pend[0]))
                 elif inp_t is None:
                     self._pw_fwd(K.ACT_BN_RELU6, inp_bn.y, bp.w_e, bp.bn_e.y, bp.bn_e.acc_f, Min, bp.hidden, bp.cin,
-                                 pa=inp_bn.scale, pb=inp_bn.shift, fin=F(bp.bn_e))
+                                 pa=inp_bn.scale, pb=inp_bn.shift, fin=F(bp.bn_e), lz=L(inp_bn))
                 else:
                     self._pw_fwd(K.ACT_NONE, inp_t, bp.w_e, bp.bn_e.y, bp.bn_e.acc_f, Min, bp.hidden, bp.cin,
                                  fin=F(bp.bn_e))
@@ -437,27 +496,31 @@ class MobileNetV2Executor:
                 assert inp_t is None and pend is None, "t=1 block expects the (virtual) stem output"
                 dw_in = inp_bn
             K.dw_fwd(dw_in.y, dw_in.scale, dw_in.shift, K.ACT_BN_RELU6, f.b(bp.w_d), bp.bn_d.y, bp.bn_d.acc_f, B, Hin, Hin,
-                     bp.hidden, bp.stride, fin=F(bp.bn_d))
+                     bp.hidden, bp.stride, fin=F(bp.bn_d), lz=L(dw_in))
             self._fin_fwd(bp.bn_d, K.dw_num_partials("fwd", B, Hin, Hin, bp.hidden, bp.stride), train)
             Mout = B * bp.Ho * bp.Wo
             self._pw_fwd(K.ACT_BN_RELU6, bp.bn_d.y, bp.w_p, bp.bn_p.y, bp.bn_p.acc_f, Mout, bp.cout, bp.hidden,
-                         pa=bp.bn_d.scale, pb=bp.bn_d.shift, fin=F(bp.bn_p))
+                         pa=bp.bn_d.scale, pb=bp.bn_d.shift, fin=F(bp.bn_p), lz=L(bp.bn_d))
             self._fin_fwd(bp.bn_p, K.pw_num_partials(Mout, bp.cout, bp.hidden), train)
             if self.FUSE_BLOCK_OUTPUT and not self.fp8:
                 pend = (bp.bn_p, inp_t if bp.residual else None, bp.o)
             else:
                 K.bn_apply(bp.bn_p.y, bp.bn_p.scale, bp.bn_p.shift, bp.o, relu6=False,
-                           res=inp_t if bp.residual else None)
+                           res=inp_t if bp.residual else None, lz=L(bp.bn_p))
             inp_bn, inp_t = bp.bn_p, bp.o
         # final 1x1 conv (materialises the last block output o_17)
         Mf = B * self.Hf * self.Hf
         if pend is not None:
             self._consume_output(pend, f.b(self.w_last), self.bn_last.y, self.bn_last.acc_f, Mf, self.C_last,
-                                 self.C_last_in, fin=F(self.bn_last))
+                                 self.C_last_in, fin=F(self.bn_last), lz=L(pend[0]))
         else:
             self._pw_fwd(K.ACT_NONE, inp_t, self.w_last, self.bn_last.y, self.bn_last.acc_f, Mf, self.C_last,
                          self.C_last_in, fin=F(self.bn_last))
         self._fin_fwd(self.bn_last, K.pw_num_partials(Mf, self.C_last, self.C_last_in), train)
+        if train and self.lazy_bn:
+            # side outputs of every forward BN (mean / rstd / scale / shift for the backward
+            # and the head, running statistics) in one launch
+            K.bn_finalize_batch(self.fwd_fin_tab, self.fwd_fin_n, self.fwd_fin_maxc)
         # head (+ its backward when training)
         K.head(self.bn_last.y, self.bn_last.scale, self.bn_last.shift, f.w(self.w_lin), f.w(self.b_lin),
                self.labels, B, self.Hf * self.Hf, self.C_last, self.NC, self.drop_p, self.dropout_seed,
@@ -478,19 +541,24 @@ class MobileNetV2Executor:
         # BN of the final conv (g produced by the head kernel)
         bnl = self.bn_last
         bnl.finalize_bwd(bnl.acc_b, B)
-        self._ready(bnl.param_names)
+        if not self.lazy_bn:
+            self._ready(bnl.param_names)
         Mf = B * self.Hf * self.Hf
         last_blk = self.blocks[-1]
         # dgrad of the final conv -> gradient w.r.t. o_17 (feeds BN_p of block 17, linear)
         K.pw_gemm(K.PRO_BNBWD, K.EPI_BWD_LIN, bnl.g, f.bt(self.w_last), last_blk.G, last_blk.bn_p.acc_b, Mf,
                   self.C_last_in,
                   self.C_last, A2=bnl.y, pa=bnl.a, pb=bnl.b, pc=bnl.c, Yt=last_blk.bn_p.y, R=None,
-                  fin=last_blk.bn_p.fin_b)
+                  fin=last_blk.bn_p.fin_b, lz=bnl.lz_b)
         P_g = K.pw_num_partials(Mf, self.C_last_in, self.C_last)
         last_blk.bn_p.finalize_bwd(last_blk.bn_p.acc_b, P_g)
-        self._wgrad(lambda: K.pw_wgrad(bnl.g, bnl.y, bnl.a, bnl.b, bnl.c, last_blk.o, None, None, K.ACT_NONE,
-                                       wg, f.g(self.w_last), Mf, self.C_last, self.C_last_in))
-        self._ready([self.w_last] + last_blk.bn_p.param_names)
+
+        def last_wgrad():
+            self._side_fin(bnl, B, last_blk.bn_p, P_g)
+            K.pw_wgrad(bnl.g, bnl.y, bnl.a, bnl.b, bnl.c, last_blk.o, None, None, K.ACT_NONE,
+                       wg, f.g(self.w_last), Mf, self.C_last, self.C_last_in)
+        self._wgrad(last_wgrad)
+        self._ready((bnl.param_names if self.lazy_bn else []) + [self.w_last] + last_blk.bn_p.param_names)
 
         for bi in range(len(self.blocks) - 1, -1, -1):
             bp = self.blocks[bi]
@@ -504,39 +572,59 @@ class MobileNetV2Executor:
                 # fused dgrad + wgrad (x = relu6(BN_d(y_d)) rebuilt from the mask operand)
                 wpm = self._wpart[(bp.idx, "p")]
                 K.pw_bwd(K.EPI_BWD_RELU6, bp.G, bnp.y, bnp.a, bnp.b, bnp.c, f.bt(bp.w_p), bnd.g, bnd.y, bnd.acc_b, wpm,
-                         None, Mout, bp.cout, bp.hidden, es=bnd.scale, et=bnd.shift, fin=bnd.fin_b)
-                self._wgrad(lambda: K.wgrad_reduce(wpm, K.pw_bwd_num_partials(Mout, bp.cout, bp.hidden),
-                                                   bp.cout * bp.hidden, f.g(bp.w_p)))
-                bnd.finalize_bwd(bnd.acc_b, K.pw_bwd_num_partials(Mout, bp.cout, bp.hidden))
+                         None, Mout, bp.cout, bp.hidden, es=bnd.scale, et=bnd.shift, fin=bnd.fin_b, lz=bnp.lz_b)
+                Pb = K.pw_bwd_num_partials(Mout, bp.cout, bp.hidden)
+
+                def prj_wgrad(bnd=bnd, Pb=Pb, wpm=wpm, bp=bp):   # deferred: bind this layer's values
+                    self._side_fin(bnd, Pb)
+                    K.wgrad_reduce(wpm, Pb, bp.cout * bp.hidden, f.g(bp.w_p))
+                self._wgrad(prj_wgrad)
+                bnd.finalize_bwd(bnd.acc_b, Pb)
             else:
                 K.pw_gemm(K.PRO_BNBWD, K.EPI_BWD_RELU6, bp.G, f.bt(bp.w_p), bnd.g, bnd.acc_b, Mout, bp.hidden, bp.cout,
                           A2=bnp.y, pa=bnp.a, pb=bnp.b, pc=bnp.c, Yt=bnd.y, es=bnd.scale, et=bnd.shift,
-                          fin=bnd.fin_b)
-                bnd.finalize_bwd(bnd.acc_b, K.pw_num_partials(Mout, bp.hidden, bp.cout))
-                # project wgrad
-                self._wgrad(lambda: K.pw_wgrad(bp.G, bnp.y, bnp.a, bnp.b, bnp.c, bnd.y, bnd.scale, bnd.shift,
-                                               K.ACT_BN_RELU6, wg, f.g(bp.w_p), Mout, bp.cout, bp.hidden))
+                          fin=bnd.fin_b, lz=bnp.lz_b)
+                Pb = K.pw_num_partials(Mout, bp.hidden, bp.cout)
+                bnd.finalize_bwd(bnd.acc_b, Pb)
+
+                def prj_wgrad(bnd=bnd, bnp=bnp, Pb=Pb, bp=bp, Mout=Mout):   # project wgrad (deferred)
+                    self._side_fin(bnd, Pb)
+                    K.pw_wgrad(bp.G, bnp.y, bnp.a, bnp.b, bnp.c, bnd.y, bnd.scale, bnd.shift,
+                               K.ACT_BN_RELU6, wg, f.g(bp.w_p), Mout, bp.cout, bp.hidden)
+                self._wgrad(prj_wgrad)
             self._ready([bp.w_p] + bnd.param_names)
             # depthwise: input BN is BN_e (expand) or the stem BN0 (t=1 block)
             dw_in = bp.bn_e if bp.expand else self.bn0
             Pd = K.dw_num_partials("dgrad", B, Hin, Hin, bp.hidden, bp.stride)
             wpd = self._wpart.get((bp.idx, "d"))
+            # the stem BN0's coefficients feed the stem weight gradient on the MAIN stream: its
+            # finalize stays there; every other input BN is finalized on the side stream (lazy)
+            main_fin = dw_in is self.bn0
+            side_fin = (lambda: None) if main_fin else (lambda dw_in=dw_in, Pd=Pd: self._side_fin(dw_in, Pd))  # noqa: E731
             if wpd is not None:
                 # large maps (bandwidth-bound): fused dgrad + wgrad, one pass over (g, y, yprev);
                 # the wgrad partials are reduced on the side stream
                 K.dw_dgrad(bnd.g, bnd.y, bnd.coef, f.b(bp.w_d), dw_in.y, dw_in.scale, dw_in.shift, dw_in.g,
                            dw_in.acc_b,
-                           B, Hin, Hin, bp.hidden, bp.stride, wpart=wpd, fin=dw_in.fin_b)
-                dw_in.finalize_bwd(dw_in.acc_b, Pd)
-                self._wgrad(lambda: K.wgrad_reduce(wpd, Pd, 9 * bp.hidden, f.g(bp.w_d)))
+                           B, Hin, Hin, bp.hidden, bp.stride, wpart=wpd, fin=dw_in.fin_b, lz=bnd.lz_b)
+                dw_in.finalize_bwd(dw_in.acc_b, Pd, force=main_fin)
+
+                def dw_wg(side_fin=side_fin, wpd=wpd, Pd=Pd, bp=bp):   # deferred: bind this layer's values
+                    side_fin()
+                    K.wgrad_reduce(wpd, Pd, 9 * bp.hidden, f.g(bp.w_d))
+                self._wgrad(dw_wg)
             else:
                 # small maps (latency-bound): lean dgrad on the critical path, wgrad on the side stream
                 K.dw_dgrad(bnd.g, bnd.y, bnd.coef, f.b(bp.w_d), dw_in.y, dw_in.scale, dw_in.shift, dw_in.g,
                            dw_in.acc_b,
-                           B, Hin, Hin, bp.hidden, bp.stride, fin=dw_in.fin_b)
-                dw_in.finalize_bwd(dw_in.acc_b, Pd)
-                self._wgrad(lambda: K.dw_wgrad(bnd.g, bnd.y, bnd.coef, dw_in.y, dw_in.scale, dw_in.shift, wg,
-                                               f.g(bp.w_d), B, Hin, Hin, bp.hidden, bp.stride))
+                           B, Hin, Hin, bp.hidden, bp.stride, fin=dw_in.fin_b, lz=bnd.lz_b)
+                dw_in.finalize_bwd(dw_in.acc_b, Pd, force=main_fin)
+
+                def dw_wg(side_fin=side_fin, bnd=bnd, dw_in=dw_in, bp=bp, Hin=Hin):   # deferred
+                    side_fin()
+                    K.dw_wgrad(bnd.g, bnd.y, bnd.coef, dw_in.y, dw_in.scale, dw_in.shift, wg,
+                               f.g(bp.w_d), B, Hin, Hin, bp.hidden, bp.stride)
+                self._wgrad(dw_wg)
             self._ready([bp.w_d] + dw_in.param_names)
             if bp.expand:
                 bne = bp.bn_e
@@ -546,18 +634,27 @@ class MobileNetV2Executor:
                     wpe = self._wpart[(bp.idx, "e")]
                     K.pw_bwd(K.EPI_BWD_LIN, bne.g, bne.y, bne.a, bne.b, bne.c, f.bt(bp.w_e), prev.G, prev.bn_p.y,
                              prev.bn_p.acc_b, wpe, None, Min, bp.hidden, bp.cin, R=bp.G if bp.residual else None,
-                             X=prev.o, fin=prev.bn_p.fin_b)
-                    self._wgrad(lambda: K.wgrad_reduce(wpe, K.pw_bwd_num_partials(Min, bp.hidden, bp.cin),
-                                                       bp.hidden * bp.cin, f.g(bp.w_e)))
-                    prev.bn_p.finalize_bwd(prev.bn_p.acc_b, K.pw_bwd_num_partials(Min, bp.hidden, bp.cin))
+                             X=prev.o, fin=prev.bn_p.fin_b, lz=bne.lz_b)
+                    Pe = K.pw_bwd_num_partials(Min, bp.hidden, bp.cin)
+
+                    def exp_wgrad(prev=prev, Pe=Pe, wpe=wpe, bp=bp):   # deferred: bind this layer's values
+                        self._side_fin(prev.bn_p, Pe)
+                        K.wgrad_reduce(wpe, Pe, bp.hidden * bp.cin, f.g(bp.w_e))
+                    self._wgrad(exp_wgrad)
+                    prev.bn_p.finalize_bwd(prev.bn_p.acc_b, Pe)
                 else:
                     K.pw_gemm(K.PRO_BNBWD, K.EPI_BWD_LIN, bne.g, f.bt(bp.w_e), prev.G, prev.bn_p.acc_b, Min, bp.cin,
                               bp.hidden,
                               A2=bne.y, pa=bne.a, pb=bne.b, pc=bne.c, Yt=prev.bn_p.y,
-                              R=bp.G if bp.residual else None, fin=prev.bn_p.fin_b)
-                    prev.bn_p.finalize_bwd(prev.bn_p.acc_b, K.pw_num_partials(Min, bp.cin, bp.hidden))
-                    self._wgrad(lambda: K.pw_wgrad(bne.g, bne.y, bne.a, bne.b, bne.c, prev.o, None, None,
-                                                   K.ACT_NONE, wg, f.g(bp.w_e), Min, bp.hidden, bp.cin))
+                              R=bp.G if bp.residual else None, fin=prev.bn_p.fin_b, lz=bne.lz_b)
+                    Pe = K.pw_num_partials(Min, bp.cin, bp.hidden)
+                    prev.bn_p.finalize_bwd(prev.bn_p.acc_b, Pe)
+
+                    def exp_wgrad(prev=prev, Pe=Pe, bne=bne, bp=bp, Min=Min):   # deferred
+                        self._side_fin(prev.bn_p, Pe)
+                        K.pw_wgrad(bne.g, bne.y, bne.a, bne.b, bne.c, prev.o, None, None,
+                                   K.ACT_NONE, wg, f.g(bp.w_e), Min, bp.hidden, bp.cin)
+                    self._wgrad(exp_wgrad)
                 self._ready([bp.w_e] + prev.bn_p.param_names)
             else:
                 # t=1 block: its input is relu6(BN0(stem)) -> stem weight gradient.  It is the last
@@ -571,6 +668,7 @@ class MobileNetV2Executor:
                 else:
                     stem_wg()
                 self._ready([self.stem_w])
+        self._flush_side()
         if self.side is not None:   # join: the optimizer (main stream) needs every gradient
             K.stream_wait(torch.cuda.current_stream(self.device), self.side)
 

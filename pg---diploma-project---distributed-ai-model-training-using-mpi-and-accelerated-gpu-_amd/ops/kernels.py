@@ -108,6 +108,28 @@ def _arm(fin):
         lib().bn_fin_arm(fin.data_ptr())
 
 
+def _arm_lz(lz):
+    """Arm a lazy-finalize descriptor (bn_fin_desc of the BN whose parameters the next launch
+    consumes): the consumer computes them from the accumulator rows in its prologue
+    (bnfin.h bn_lazy) instead of reading materialised scale / shift / coef."""
+    if lz is not None:
+        if not (lz.is_cuda and lz.dtype == torch.uint8):
+            raise TypeError("lz: a device descriptor from bn_fin_desc")
+        lib().bn_lz_arm(lz.data_ptr())
+
+
+def bn_desc_table(descs):
+    """Device table (int64 pointers) of bn_fin_desc descriptors for :func:`bn_finalize_batch`."""
+    return torch.tensor([d.data_ptr() for d in descs], dtype=torch.int64, device=descs[0].device)
+
+
+def bn_finalize_batch(tab, n, max_c):
+    """Finalize the n BNs of a descriptor table in one launch (forward descriptors: mean /
+    rstd / scale / shift / running statistics; backward: coef / dgamma / dbeta)."""
+    assert tab.dtype == torch.int64 and tab.is_contiguous() and tab.numel() >= n
+    lib().bn_finalize_batch(_p(tab), int(n), int(max_c), _s())
+
+
 def bn_rows(P):
     """Rows a BN finalize reduces after a producer with P partial rows accumulated atomically
     (rows = min(P, bn_rep()); the accumulator must be zeroed before the producer runs)."""
@@ -137,12 +159,15 @@ def bn_bwd_finalize(part, P, C, count, mean, rstd, gamma, coef, dgamma=None, dbe
                           _p(dgamma), _p(dbeta), _s())
 
 
-def bn_apply(y, scale, shift, out, relu6=False, res=None):
+def bn_apply(y, scale, shift, out, relu6=False, res=None, lz=None):
     M, C = y.shape
     assert C % 8 == 0
     _chk(y, BF16, M * C, "y")
     _chk(out, BF16, M * C, "out")
     _chk(res, BF16, M * C, "res")
+    if lz is not None and C > 8192:
+        raise ValueError("bn_apply: lazy finalize stages 2*C floats in LDS (C <= 8192)")
+    _arm_lz(lz)
     lib().bn_apply(_p(y), _p(res), _p(scale), _p(shift), _p(out), M, C, bool(relu6), _s())
 
 
@@ -189,7 +214,7 @@ def _dw_check(B, H, W, C, stride):
         raise ValueError("depthwise: stride must be 1 or 2")
 
 
-def dw_fwd(x, in_s, in_t, act, w, y, part, B, H, W, C, stride, fin=None):
+def dw_fwd(x, in_s, in_t, act, w, y, part, B, H, W, C, stride, fin=None, lz=None):
     _dw_check(B, H, W, C, stride)
     Ho, Wo = dw_out_hw(H, W, stride)
     _chk(x, BF16, B * H * W * C, "x")
@@ -197,6 +222,7 @@ def dw_fwd(x, in_s, in_t, act, w, y, part, B, H, W, C, stride, fin=None):
     _chk(y, BF16, B * Ho * Wo * C, "y")
     _chk(part, F32, bn_rows(dw_num_partials("fwd", B, H, W, C, stride)) * 2 * C, "part")
     _arm(fin)
+    _arm_lz(lz)
     lib().dw_fwd(_p(x), _p(in_s), _p(in_t), int(act), _p(w), _p(y), _p(part), B, H, W, C, stride, _s())
 
 
@@ -205,7 +231,7 @@ def dw_dgrad_wgrad_workspace(B, H, W, C, stride):
     return lib().dw_dgrad_wgrad_workspace_floats(B, H, W, C, stride)
 
 
-def dw_dgrad(g, yself, coef, w, yprev, ps, pt, gout, part, B, H, W, C, stride, wpart=None, fin=None):
+def dw_dgrad(g, yself, coef, w, yprev, ps, pt, gout, part, B, H, W, C, stride, wpart=None, fin=None, lz=None):
     """Depthwise dgrad (+ BN partials of gout).  With ``wpart`` the layer's weight gradient is
     accumulated in the same pass into split partials wpart[P][9][C] (P = dw_num_partials
     ("dgrad", ...)); reduce them with ``wgrad_reduce(wpart, P, 9 * C, grad)``."""
@@ -218,6 +244,7 @@ def dw_dgrad(g, yself, coef, w, yprev, ps, pt, gout, part, B, H, W, C, stride, w
     _chk(part, F32, bn_rows(dw_num_partials("dgrad", B, H, W, C, stride)) * 2 * C, "part")
     _chk(wpart, F32, dw_dgrad_wgrad_workspace(B, H, W, C, stride), "wpart")
     _arm(fin)
+    _arm_lz(lz)
     lib().dw_dgrad(_p(g), _p(yself), _p(coef), _p(w), _p(yprev), _p(ps), _p(pt), _p(gout), _p(part),
                    B, H, W, C, stride, _p(wpart), _s())
 
@@ -244,7 +271,7 @@ def pw_num_partials(M, N, K):
 
 
 def pw_gemm(pro, epi, A, W, out, part, M, N, K, A2=None, pa=None, pb=None, pc=None, Yt=None,
-            es=None, et=None, R=None, Aout=None, fin=None):
+            es=None, et=None, R=None, Aout=None, fin=None, lz=None):
     """out[M,N] = prologue(A)[M,K] @ W^T with W [N,K] in GEMM terms for every mode.
 
     For the dgrad (pro == PRO_BNBWD) W is the TRANSPOSED conv weight ([Cin][Cout],
@@ -272,6 +299,7 @@ def pw_gemm(pro, epi, A, W, out, part, M, N, K, A2=None, pa=None, pb=None, pc=No
         assert es is not None and et is not None
     _chk(Aout, BF16, M * K, "Aout")
     _arm(fin)
+    _arm_lz(lz)
     lib().pw_gemm(int(pro), int(epi), _p(A), _p(A2), _p(pa), _p(pb), _p(pc), _p(W), _p(out), _p(Yt),
                   _p(es), _p(et), _p(R), _p(part), M, N, K, _p(Aout), _s())
 
@@ -289,7 +317,7 @@ def fp8_pitch(K: int) -> int:
     return (K + 63) // 64 * 64
 
 
-def pw_gemm_f8(pro, A, W8, wsc, out, part, M, N, K, pa=None, pb=None, asc=None, fin=None):
+def pw_gemm_f8(pro, A, W8, wsc, out, part, M, N, K, pa=None, pb=None, asc=None, fin=None, lz=None):
     """fp8 forward 1x1 conv: out[M,N] = bf16( (e4m3(asc*prologue(A)) . W8^T) * wsc[n] / asc ).
 
     W8 is the per-output-channel e4m3 weight copy [N][fp8_pitch(K)] (see :func:`w8_quant`),
@@ -309,6 +337,7 @@ def pw_gemm_f8(pro, A, W8, wsc, out, part, M, N, K, pa=None, pb=None, asc=None, 
         assert pa is not None and pb is not None and pa.numel() >= K
     a = float(FP8_ASC[pro] if asc is None else asc)
     _arm(fin)
+    _arm_lz(lz)
     lib().pw_gemm_f8(int(pro), _p(A), _p(pa), _p(pb), _p(W8), ld, _p(wsc), a, _p(out), _p(part), M, N, K, _s())
 
 
@@ -345,7 +374,7 @@ def pw_bwd_wgrad_workspace(M, Kg, Ng):
 
 
 def pw_bwd(epi, G, Y, ca, cb, cc, WT, out, Yt, part, wpart, grad, M, Kg, Ng, es=None, et=None, R=None,
-           X=None, fin=None):
+           X=None, fin=None, lz=None):
     """Fused 1x1-conv backward (one read of G, Y):
 
     dy = ca*G + cb*Y + cc                      [M, Kg]   (this conv's BN backward)
@@ -375,6 +404,7 @@ def pw_bwd(epi, G, Y, ca, cb, cc, WT, out, Yt, part, wpart, grad, M, Kg, Ng, es=
     else:
         raise ValueError(f"pw_bwd: bad epilogue {epi}")
     _arm(fin)
+    _arm_lz(lz)
     lib().pw_bwd(int(epi), _p(G), _p(Y), _p(ca), _p(cb), _p(cc), _p(WT), _p(out), _p(Yt), _p(es), _p(et),
                  _p(R), _p(X), _p(part), _p(wpart), _p(grad), M, Kg, Ng, _s())
 
