@@ -8,7 +8,8 @@
 // memory system:
 //
 //  * a workgroup = a tile of TWc columns x R rows of one image and a slab of
-//    CC <= 64 channels (a multiple of 8: 16-B chunks); a thread owns 4 channels of ONE
+//    CC <= 64 channels (a multiple of 8: 16-B chunks; up to 128 on narrow 7x7 / 14x14 maps,
+//    see dw_geom); a thread owns 4 channels of ONE
 //    column (output column for fwd / wgrad, input column for dgrad) and walks the R rows,
 //    keeping a rolling 3-row x 3-column window in registers;
 //  * every row the tile needs is streamed once into an LDS ring by LDS-DMA
@@ -41,10 +42,10 @@ struct DwGeom {
 };
 
 // Lazy BN finalize of this workgroup's channel slab [cbase, cbase + CC) into LDS (one
-// channel per thread, CC <= 64), then a barrier: every thread reads its CPT channels from
+// channel per thread, CC <= 128), then a barrier: every thread reads its CPT channels from
 // LDS instead of each computing them (the slab is shared by C4 = CC/4 threads per column).
 // npar = 2: forward scale / shift; 3: backward coefficients.
-__shared__ float lzp[3][64];
+__shared__ float lzp[3][128];
 PG_DEVICE void lazy_stage(const DwGeom &g, int cbase, int npar) {
   if ((int)threadIdx.x < g.CC) {
     float a, b, c;
@@ -817,6 +818,41 @@ int dw_cc(int C) {
   return 8;
 }
 
+// Widest tile (columns) a CC-channel slab supports: 256 threads of CPT channels, and the
+// LDS-DMA row segments of every kernel kind within their ring slots (whole 64-chunk wave
+// pieces: halo rows kSlotHalo = 192 chunks, own-column rows kSlotOwn = 128, stride-2 input
+// rows kSlotS2 = 256; the dgrad s2 dy segment spans ~TWc/2 + 2 columns in an own slot).
+static int dw_twc_max(int cc, int kind, int stride) {
+  const int c4 = cc / CPT, cc8 = cc / 8;
+  auto fits = [&](int t) {
+    if (t * cc8 > 128) return false;
+    if (stride == 1) return (t + 2) * cc8 <= 192;
+    if (kind != 1) return (2 * t + 1) * cc8 <= 256;
+    return (t / 2 + 2) * cc8 <= 128;
+  };
+  int t = 256 / c4;
+  while (t > 0 && !fits(t)) --t;
+  return t;
+}
+
+// Channel slab of a narrow map: with the default CC (<= 64) a 7-column map leaves half of
+// the 256 threads without a column (C4 = 16 threads x 7 columns); a wider slab (a multiple
+// of 8 dividing C, <= 128) gives every column more channel lanes: 7x7x960 -> CC = 120,
+// 210 active threads instead of 112 (PGDIST_DW_WIDE=0: off).
+static int dw_cc_narrow(int C, int gw, int kind, int stride, int cc0) {
+  static const bool on = [] { const char *e = getenv("PGDIST_DW_WIDE"); return !(e && atoi(e) == 0); }();
+  if (!on || dw_twc_max(cc0, kind, stride) <= gw) return cc0;
+  int best = cc0, best_act = (cc0 / CPT) * gw;
+  for (int cc = 8; cc <= 128; cc += 8) {
+    if (C % cc) continue;
+    const int t = dw_twc_max(cc, kind, stride);
+    if (t < 1) continue;
+    const int act = (cc / CPT) * (t < gw ? t : gw);
+    if (act > best_act) best = cc, best_act = act;
+  }
+  return best;
+}
+
 // kind 0 = fwd (tiles over the output grid), 1 = dgrad (input grid), 2 = wgrad (output grid)
 DwGeom dw_geom(int kind, int B, int H, int W, int C, int stride) {
   DwGeom g;
@@ -829,12 +865,9 @@ DwGeom dw_geom(int kind, int B, int H, int W, int C, int stride) {
   g.C = C;
   g.Ho = (H - 1) / stride + 1;
   g.Wo = (W - 1) / stride + 1;
-  g.CC = dw_cc(C);
-  const int C4 = g.CC / CPT;
   const int gw = kind == 1 ? W : g.Wo, gh = kind == 1 ? H : g.Ho;
-  int twc = 256 / C4;
-  // LDS-DMA stride-2 input rows over the output grid: (2 TWc + 1) x CC8 <= 256 chunks
-  if (kind != 1 && stride == 2 && twc > (256 / (g.CC / 8) - 1) / 2) twc = (256 / (g.CC / 8) - 1) / 2;
+  g.CC = dw_cc_narrow(C, gw, kind, stride, dw_cc(C));
+  int twc = dw_twc_max(g.CC, kind, stride);
   if (twc > gw) twc = gw;
   g.TWc = twc;
   static const int env_rows = [] {

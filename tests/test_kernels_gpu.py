@@ -134,7 +134,10 @@ DW_CASES = [(2, 14, 14, 32, 1), (2, 14, 14, 96, 2), (3, 28, 28, 144, 1), (2, 7, 
             (2, 56, 56, 96, 2), (1, 28, 28, 576, 2), (2, 9, 9, 24, 1), (2, 10, 10, 16, 2),
             # partial last column tile (W not a multiple of the tile width), odd sizes, full-size rows
             (1, 57, 57, 64, 2), (1, 45, 45, 192, 1), (1, 112, 112, 32, 1), (1, 112, 112, 96, 2),
-            (1, 29, 31, 48, 2), (1, 13, 33, 40, 1)]
+            (1, 29, 31, 48, 2), (1, 13, 33, 40, 1),
+            # narrow maps: widened channel slabs (dw_geom: CC up to 128, e.g. 120 for C = 960)
+            (2, 14, 14, 576, 2), (2, 7, 7, 576, 1), (1, 5, 5, 120, 1), (2, 14, 14, 960, 2), (1, 7, 9, 480, 1),
+            (2, 8, 8, 384, 2)]
 
 
 @pytest.mark.parametrize("B,H,W,C,stride", DW_CASES)
