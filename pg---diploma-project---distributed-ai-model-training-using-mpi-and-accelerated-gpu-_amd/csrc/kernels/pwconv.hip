@@ -814,7 +814,11 @@ static void wgrad_geom(int M, int N, int K, int &TN, int &TK, int &S, int &rps) 
   TN = N <= 32 ? 32 : (N <= 64 ? 64 : 128);
   TK = K <= 32 ? 32 : (K <= 64 ? 64 : 128);
   const int tiles = ((N + TN - 1) / TN) * ((K + TK - 1) / TK);
-  S = (1024 + tiles - 1) / tiles;
+  static const int target = [] {   // PGDIST_PWWG_WGS: split-M grid-size target (tuning experiments)
+    const char *e = getenv("PGDIST_PWWG_WGS");
+    return e && atoi(e) > 0 ? atoi(e) : 1024;
+  }();
+  S = (target + tiles - 1) / tiles;
   const int max_s = (M + kMinRowsPerSplit - 1) / kMinRowsPerSplit;
   if (S > max_s) S = max_s;
   if (S < 1) S = 1;

@@ -3,6 +3,7 @@
 // per-device arrival counters of the last-workgroup hand-off.
 #include "../reduce.h"
 
+#include <cstdlib>
 #include <mutex>
 #include <vector>
 
@@ -44,6 +45,14 @@ int *reduce_counters(int n, hipStream_t st) {
 // nch level-1 rows (<= kWredMaxChunks) the same way.
 constexpr int kWredMaxChunks = 128;
 constexpr int kWredTargetWgs = 2048;
+constexpr int kWredSideWgs = 384;
+
+bool is_side_stream(hipStream_t st) {
+  std::lock_guard<std::mutex> lock(g_mu);
+  for (auto s : g_side)
+    if (s == st) return true;
+  return false;
+}
 
 // level-1 rows the wgrad reduction of R partial rows may need after the partials
 int colsum_rows(int R) {
@@ -130,7 +139,15 @@ void launch_wgrad_reduce(float *part, int S, long long n, float *grad, hipStream
   const bool vec = (n % 4 == 0) && ((uintptr_t)part % 16 == 0) && ((uintptr_t)grad % 16 == 0);
   const int V = vec ? 4 : 1;
   const long long nb = (n + 16 * V - 1) / (16 * V);
-  long long want = kWredTargetWgs / (nb > 0 ? nb : 1);
+  // on a weight-gradient side stream a smaller grid: the reduction is off the critical path,
+  // and a 2k-workgroup launch there holds up the dispatch of the main stream's next kernel
+  // (MobileNetV2 bs128 on MI355X: 5.07 ms/step at 2048, 5.00 at 512, 4.98-5.00 at 256)
+  static const int env_t = [] {   // PGDIST_WRED_WGS: grid-size target of every reduction
+    const char *e = getenv("PGDIST_WRED_WGS");
+    return e && atoi(e) > 0 ? atoi(e) : 0;
+  }();
+  const int target = env_t > 0 ? env_t : (is_side_stream(st) ? kWredSideWgs : kWredTargetWgs);
+  long long want = target / (nb > 0 ? nb : 1);
   int nch = (int)(want < 1 ? 1 : want);
   const int cap = colsum_rows(S);
   if (nch > cap) nch = cap;
