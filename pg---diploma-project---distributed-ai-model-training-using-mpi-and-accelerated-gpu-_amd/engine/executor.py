@@ -293,7 +293,8 @@ class MobileNetV2Executor:
         # weight gradients that are not fused into a dgrad run on a side stream, overlapping
         # the dgrad -> BN-finalize chain (the backward's critical path)
         self.side = None
-        self._side_pending: List[Callable[[], None]] = []
+        self._side_pending = []   # deferred (BN finalizes, weight-gradient callable) pairs
+        self._fin_tabs = {}       # batched backward-finalize descriptor tables by BN group
         self.side_batch = max(1, int(os.environ.get("PGDIST_SIDE_BATCH", "3")))
         if device.type == "cuda" and side_stream:
             self.side = torch.cuda.Stream(device)
@@ -401,16 +402,17 @@ class MobileNetV2Executor:
         with torch.cuda.stream(self.side):
             self.on_params_ready(names)
 
-    def _wgrad(self, fn):
+    def _wgrad(self, fn, fins=()):
         """Enqueue a weight-gradient launch on the side stream (after the main stream's
         work so far, which produced its inputs).  Deferred in groups of ``side_batch``: every
         side-stream join is an event record on the main stream, whose barrier packet keeps the
         next main kernel from overlapping the previous one's completion (~5-6 us of main-stream
         idle per join on MI355X); one join per group instead of one per layer."""
         if self.side is None:
+            self._side_fins(fins)
             fn()
             return
-        self._side_pending.append(fn)
+        self._side_pending.append((fins, fn))
         if len(self._side_pending) >= self.side_batch:
             self._flush_side()
 
@@ -421,7 +423,8 @@ class MobileNetV2Executor:
             return
         K.stream_wait(self.side, torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.side):
-            for fn in self._side_pending:
+            self._side_fins([f for fins, _ in self._side_pending for f in fins])
+            for _, fn in self._side_pending:
                 fn()
         self._side_pending.clear()
 
@@ -444,15 +447,24 @@ class MobileNetV2Executor:
         else:
             K.pw_gemm(pro, K.EPI_FWD, A, self.flat.b(wname), out, ws, M, N, K_, pa=pa, pb=pb, fin=fin, lz=lz)
 
-    def _side_fin(self, *bn_p):
-        """Lazy mode: the backward finalizes of (bn, P) pairs whose statistics the main stream
-        just produced -- coef for the side-stream weight gradients, dgamma / dbeta for the
-        gradient buckets and the optimizer.  Called inside a ``_wgrad`` callable, so they run
-        on the side stream ahead of that weight gradient (main-stream consumers computed the
-        coefficients themselves)."""
-        if self.lazy_bn:
-            for bn, P in zip(bn_p[0::2], bn_p[1::2]):
-                bn.finalize_bwd(bn.acc_b, P, force=True)
+    def _side_fins(self, fins):
+        """Lazy mode: the backward finalizes of the (bn, P) pairs of a flushed group of weight
+        gradients -- coef for the side-stream weight gradients, dgamma / dbeta for the gradient
+        buckets and the optimizer -- as ONE batched launch ahead of the group's weight
+        gradients (main-stream consumers computed the coefficients themselves)."""
+        if not self.lazy_bn or not fins:
+            return
+        for bn, P in fins:
+            assert K.bn_rows(P) <= bn.rows_b, f"{bn.prefix}: backward producer rows exceed the accumulator"
+        if len(fins) == 1:
+            bn, P = fins[0]
+            bn.finalize_bwd(bn.acc_b, P, force=True)
+            return
+        key = tuple(id(bn) for bn, _ in fins)
+        tab = self._fin_tabs.get(key)
+        if tab is None:
+            tab = self._fin_tabs[key] = K.bn_desc_table([bn.desc_b for bn, _ in fins])
+        K.bn_finalize_batch(tab, len(fins), max(bn.C for bn, _ in fins))
 
     def _fin_fwd(self, bn: BNState, P: int, train: bool):
         if train:
@@ -554,10 +566,9 @@ class MobileNetV2Executor:
         last_blk.bn_p.finalize_bwd(last_blk.bn_p.acc_b, P_g)
 
         def last_wgrad():
-            self._side_fin(bnl, B, last_blk.bn_p, P_g)
             K.pw_wgrad(bnl.g, bnl.y, bnl.a, bnl.b, bnl.c, last_blk.o, None, None, K.ACT_NONE,
                        wg, f.g(self.w_last), Mf, self.C_last, self.C_last_in)
-        self._wgrad(last_wgrad)
+        self._wgrad(last_wgrad, fins=((bnl, B), (last_blk.bn_p, P_g)))
         self._ready((bnl.param_names if self.lazy_bn else []) + [self.w_last] + last_blk.bn_p.param_names)
 
         for bi in range(len(self.blocks) - 1, -1, -1):
@@ -575,10 +586,9 @@ class MobileNetV2Executor:
                          None, Mout, bp.cout, bp.hidden, es=bnd.scale, et=bnd.shift, fin=bnd.fin_b, lz=bnp.lz_b)
                 Pb = K.pw_bwd_num_partials(Mout, bp.cout, bp.hidden)
 
-                def prj_wgrad(bnd=bnd, Pb=Pb, wpm=wpm, bp=bp):   # deferred: bind this layer's values
-                    self._side_fin(bnd, Pb)
+                def prj_wgrad(Pb=Pb, wpm=wpm, bp=bp):   # deferred: bind this layer's values
                     K.wgrad_reduce(wpm, Pb, bp.cout * bp.hidden, f.g(bp.w_p))
-                self._wgrad(prj_wgrad)
+                self._wgrad(prj_wgrad, fins=((bnd, Pb),))
                 bnd.finalize_bwd(bnd.acc_b, Pb)
             else:
                 K.pw_gemm(K.PRO_BNBWD, K.EPI_BWD_RELU6, bp.G, f.bt(bp.w_p), bnd.g, bnd.acc_b, Mout, bp.hidden, bp.cout,
@@ -587,11 +597,10 @@ class MobileNetV2Executor:
                 Pb = K.pw_num_partials(Mout, bp.hidden, bp.cout)
                 bnd.finalize_bwd(bnd.acc_b, Pb)
 
-                def prj_wgrad(bnd=bnd, bnp=bnp, Pb=Pb, bp=bp, Mout=Mout):   # project wgrad (deferred)
-                    self._side_fin(bnd, Pb)
+                def prj_wgrad(bnd=bnd, bnp=bnp, bp=bp, Mout=Mout):   # project wgrad (deferred)
                     K.pw_wgrad(bp.G, bnp.y, bnp.a, bnp.b, bnp.c, bnd.y, bnd.scale, bnd.shift,
                                K.ACT_BN_RELU6, wg, f.g(bp.w_p), Mout, bp.cout, bp.hidden)
-                self._wgrad(prj_wgrad)
+                self._wgrad(prj_wgrad, fins=((bnd, Pb),))
             self._ready([bp.w_p] + bnd.param_names)
             # depthwise: input BN is BN_e (expand) or the stem BN0 (t=1 block)
             dw_in = bp.bn_e if bp.expand else self.bn0
@@ -600,7 +609,7 @@ class MobileNetV2Executor:
             # the stem BN0's coefficients feed the stem weight gradient on the MAIN stream: its
             # finalize stays there; every other input BN is finalized on the side stream (lazy)
             main_fin = dw_in is self.bn0
-            side_fin = (lambda: None) if main_fin else (lambda dw_in=dw_in, Pd=Pd: self._side_fin(dw_in, Pd))  # noqa: E731
+            side_fins = () if main_fin else ((dw_in, Pd),)
             if wpd is not None:
                 # large maps (bandwidth-bound): fused dgrad + wgrad, one pass over (g, y, yprev);
                 # the wgrad partials are reduced on the side stream
@@ -609,10 +618,9 @@ class MobileNetV2Executor:
                            B, Hin, Hin, bp.hidden, bp.stride, wpart=wpd, fin=dw_in.fin_b, lz=bnd.lz_b)
                 dw_in.finalize_bwd(dw_in.acc_b, Pd, force=main_fin)
 
-                def dw_wg(side_fin=side_fin, wpd=wpd, Pd=Pd, bp=bp):   # deferred: bind this layer's values
-                    side_fin()
+                def dw_wg(wpd=wpd, Pd=Pd, bp=bp):   # deferred: bind this layer's values
                     K.wgrad_reduce(wpd, Pd, 9 * bp.hidden, f.g(bp.w_d))
-                self._wgrad(dw_wg)
+                self._wgrad(dw_wg, fins=side_fins)
             else:
                 # small maps (latency-bound): lean dgrad on the critical path, wgrad on the side stream
                 K.dw_dgrad(bnd.g, bnd.y, bnd.coef, f.b(bp.w_d), dw_in.y, dw_in.scale, dw_in.shift, dw_in.g,
@@ -620,11 +628,10 @@ class MobileNetV2Executor:
                            B, Hin, Hin, bp.hidden, bp.stride, fin=dw_in.fin_b, lz=bnd.lz_b)
                 dw_in.finalize_bwd(dw_in.acc_b, Pd, force=main_fin)
 
-                def dw_wg(side_fin=side_fin, bnd=bnd, dw_in=dw_in, bp=bp, Hin=Hin):   # deferred
-                    side_fin()
+                def dw_wg(bnd=bnd, dw_in=dw_in, bp=bp, Hin=Hin):   # deferred
                     K.dw_wgrad(bnd.g, bnd.y, bnd.coef, dw_in.y, dw_in.scale, dw_in.shift, wg,
                                f.g(bp.w_d), B, Hin, Hin, bp.hidden, bp.stride)
-                self._wgrad(dw_wg)
+                self._wgrad(dw_wg, fins=side_fins)
             self._ready([bp.w_d] + dw_in.param_names)
             if bp.expand:
                 bne = bp.bn_e
@@ -637,10 +644,9 @@ class MobileNetV2Executor:
                              X=prev.o, fin=prev.bn_p.fin_b, lz=bne.lz_b)
                     Pe = K.pw_bwd_num_partials(Min, bp.hidden, bp.cin)
 
-                    def exp_wgrad(prev=prev, Pe=Pe, wpe=wpe, bp=bp):   # deferred: bind this layer's values
-                        self._side_fin(prev.bn_p, Pe)
+                    def exp_wgrad(Pe=Pe, wpe=wpe, bp=bp):   # deferred: bind this layer's values
                         K.wgrad_reduce(wpe, Pe, bp.hidden * bp.cin, f.g(bp.w_e))
-                    self._wgrad(exp_wgrad)
+                    self._wgrad(exp_wgrad, fins=((prev.bn_p, Pe),))
                     prev.bn_p.finalize_bwd(prev.bn_p.acc_b, Pe)
                 else:
                     K.pw_gemm(K.PRO_BNBWD, K.EPI_BWD_LIN, bne.g, f.bt(bp.w_e), prev.G, prev.bn_p.acc_b, Min, bp.cin,
@@ -650,11 +656,10 @@ class MobileNetV2Executor:
                     Pe = K.pw_num_partials(Min, bp.cin, bp.hidden)
                     prev.bn_p.finalize_bwd(prev.bn_p.acc_b, Pe)
 
-                    def exp_wgrad(prev=prev, Pe=Pe, bne=bne, bp=bp, Min=Min):   # deferred
-                        self._side_fin(prev.bn_p, Pe)
+                    def exp_wgrad(prev=prev, bne=bne, bp=bp, Min=Min):   # deferred
                         K.pw_wgrad(bne.g, bne.y, bne.a, bne.b, bne.c, prev.o, None, None,
                                    K.ACT_NONE, wg, f.g(bp.w_e), Min, bp.hidden, bp.cin)
-                    self._wgrad(exp_wgrad)
+                    self._wgrad(exp_wgrad, fins=((prev.bn_p, Pe),))
                 self._ready([bp.w_e] + prev.bn_p.param_names)
             else:
                 # t=1 block: its input is relu6(BN0(stem)) -> stem weight gradient.  It is the last
