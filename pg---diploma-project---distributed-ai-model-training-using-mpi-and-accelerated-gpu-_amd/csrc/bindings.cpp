@@ -86,6 +86,8 @@ void launch_augment(const unsigned char *, const long long *, const long long *,
 void launch_step_begin(float *, hipStream_t);
 int colsum_rows(int);
 void launch_wgrad_reduce(float *, int, long long, float *, hipStream_t);
+void wgrad_reduce_defer(bool on);
+void wgrad_reduce_flush(hipStream_t st);
 long long bn_part_floats(int, int);
 void register_side_stream(hipStream_t);
 void launch_reduce_metrics(const float *, const float *, int, double *, hipStream_t);
@@ -266,6 +268,10 @@ PYBIND11_MODULE(_pgdist_C, m) {
                     M, Kg, Ng, S(s));
     });
   });
+  m.def("wgrad_reduce_defer", [](bool on) { pgdist_rt::run_op([=] { wgrad_reduce_defer(on); }); },
+        "while on, weight-gradient split reductions are recorded instead of launched");
+  m.def("wgrad_reduce_flush", [](P s) { pgdist_rt::run_op([=] { wgrad_reduce_flush(S(s)); }); },
+        "launch every recorded weight-gradient reduction (multi-segment launches) on the stream");
   m.def("wgrad_reduce", [](P part, int nsplit, long long n, P grad, P s) {
     pgdist_rt::run_op([=] {
       launch_wgrad_reduce(ptr<float>(part), nsplit, n, ptr<float>(grad), S(s));

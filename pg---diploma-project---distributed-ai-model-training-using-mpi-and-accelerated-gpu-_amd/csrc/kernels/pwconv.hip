@@ -807,6 +807,8 @@ void launch_wt_transpose(const bf16_t *src, bf16_t *dst, const int *tab, int n, 
 
 int colsum_rows(int R);
 void launch_wgrad_reduce(float *part, int S, long long n, float *grad, hipStream_t st);
+void wgrad_reduce_defer(bool on);
+bool wgrad_reduce_deferring();
 
 // split-M geometry: tiles of TN x TK outputs, S splits of >= kMinRowsPerSplit rows each
 static constexpr int kMinRowsPerSplit = 512;
@@ -874,7 +876,10 @@ void launch_stem_wgrad(const bf16_t *G, const bf16_t *Y, const float *ga, const 
   launch_wg_x<IM2COL_STEM>(a, TN, TK, S, st);
   const long long n = (long long)O * 36;
   float *tmp = part + (size_t)(S + colsum_rows(S)) * n;
+  const bool deferring = wgrad_reduce_deferring();   // the permute below reads tmp right away
+  wgrad_reduce_defer(false);
   launch_wgrad_reduce(part, S, n, tmp, st);
+  wgrad_reduce_defer(deferring);
   hipLaunchKernelGGL(stem_wgrad_permute_kernel, dim3((O * 27 + 255) / 256), dim3(256), 0, st, tmp, grad, O);
 }
 

@@ -3,6 +3,7 @@
 // per-device arrival counters of the last-workgroup hand-off.
 #include "../reduce.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <mutex>
 #include <vector>
@@ -60,14 +61,16 @@ int colsum_rows(int R) {
   return c < 1 ? 1 : (c > kWredMaxChunks ? kWredMaxChunks : c);
 }
 
+// One workgroup's share of a column reduction: column block bx, row chunk by (ctr: the
+// arrival counter of column block bx).
 template <int V>
-__global__ __launch_bounds__(256) void col_reduce_kernel(const float *__restrict__ part, int R, long long n, int rch,
-                                                         int nch, float *__restrict__ lvl1, int *__restrict__ ctr,
-                                                         float *__restrict__ out) {
+PG_DEVICE void col_reduce_body(const float *__restrict__ part, int R, long long n, int rch, int nch,
+                               float *__restrict__ lvl1, int *__restrict__ ctr, float *__restrict__ out, int bx,
+                               int by) {
   __shared__ float sh[16][16 * V + 1];
   __shared__ int flag;
   const int cg = threadIdx.x & 15, stripe = threadIdx.x >> 4;
-  const long long c0 = ((long long)blockIdx.x * 16 + cg) * V;
+  const long long c0 = ((long long)bx * 16 + cg) * V;
   const bool cok = c0 < n;
   float acc[V], acc2[V];
 #pragma unroll
@@ -80,7 +83,7 @@ __global__ __launch_bounds__(256) void col_reduce_kernel(const float *__restrict
       v[0] = *p;
     }
   };
-  const int r0 = blockIdx.y * rch, r1 = min(R, r0 + rch);
+  const int r0 = by * rch, r1 = min(R, r0 + rch);
   if (cok) {
     int r = r0 + stripe;
     for (; r + 16 < r1; r += 32) {   // two rows in flight per thread, fixed order
@@ -101,7 +104,7 @@ __global__ __launch_bounds__(256) void col_reduce_kernel(const float *__restrict
   for (int j = 0; j < V; ++j) sh[stripe][cg * V + j] = acc[j] + acc2[j];
   __syncthreads();
   const int col = threadIdx.x;   // < 16 * V: one output column per thread
-  const long long oc = (long long)blockIdx.x * 16 * V + col;
+  const long long oc = (long long)bx * 16 * V + col;
   float s1 = 0.f;
   if (col < 16 * V) {
 #pragma unroll
@@ -111,8 +114,8 @@ __global__ __launch_bounds__(256) void col_reduce_kernel(const float *__restrict
     if (col < 16 * V && oc < n) out[oc] = s1;
     return;
   }
-  if (col < 16 * V && oc < n) st_sc1(lvl1 + (size_t)blockIdx.y * n + oc, s1);
-  if (!arrive_last(ctr, nch, &flag)) return;
+  if (col < 16 * V && oc < n) st_sc1(lvl1 + (size_t)by * n + oc, s1);
+  if (!arrive_last_at(ctr, nch, &flag)) return;
   float b[V];
 #pragma unroll
   for (int j = 0; j < V; ++j) b[j] = 0.f;
@@ -134,8 +137,105 @@ __global__ __launch_bounds__(256) void col_reduce_kernel(const float *__restrict
   }
 }
 
+template <int V>
+__global__ __launch_bounds__(256) void col_reduce_kernel(const float *__restrict__ part, int R, long long n, int rch,
+                                                         int nch, float *__restrict__ lvl1, int *__restrict__ ctr,
+                                                         float *__restrict__ out) {
+  col_reduce_body<V>(part, R, n, rch, nch, lvl1, ctr ? ctr + blockIdx.x : nullptr, out, blockIdx.x, blockIdx.y);
+}
+
+// Several independent reductions in ONE launch (the weight gradients of a group of layers
+// flushed together to the side stream): workgroups [wg0, wg0 + nb * nch) belong to segment k.
+namespace {
+constexpr int kRedMaxSeg = 8;
+struct RedSeg {
+  const float *part;
+  float *grad;
+  long long n;
+  int S, rch, nch, nb, wg0, ctr0;
+};
+struct RedSegs {
+  RedSeg s[kRedMaxSeg];
+  int nseg;
+  int *ctr;
+};
+}  // namespace
+
+template <int V>
+__global__ __launch_bounds__(256) void col_reduce_multi_kernel(RedSegs a) {
+  const int id = blockIdx.x;
+  int k = 0;
+  while (k + 1 < a.nseg && id >= a.s[k + 1].wg0) ++k;
+  const RedSeg &g = a.s[k];
+  const int local = id - g.wg0, bx = local % g.nb, by = local / g.nb;
+  col_reduce_body<V>(g.part, g.S, g.n, g.rch, g.nch, const_cast<float *>(g.part) + (size_t)g.S * g.n,
+                     g.nch > 1 ? a.ctr + g.ctr0 + bx : nullptr, g.grad, bx, by);
+}
+
+// Deferred mode (wgrad_reduce_defer): launch_wgrad_reduce records the reduction instead of
+// launching it; wgrad_reduce_flush launches every recorded one in col_reduce_multi launches.
+namespace {
+struct PendingRed {
+  float *part;
+  int S;
+  long long n;
+  float *grad;
+};
+bool g_red_defer = false;
+std::vector<PendingRed> g_red_pending;
+}  // namespace
+
+void wgrad_reduce_defer(bool on) { g_red_defer = on; }
+bool wgrad_reduce_deferring() { return g_red_defer; }
+
+static void red_geom(int S, long long n, int target, int V, int &nb, int &rch, int &nch) {
+  const long long nbl = (n + 16 * V - 1) / (16 * V);
+  long long want = target / (nbl > 0 ? nbl : 1);
+  nch = (int)(want < 1 ? 1 : want);
+  const int cap = colsum_rows(S);
+  if (nch > cap) nch = cap;
+  rch = (S + nch - 1) / nch;
+  nch = (S + rch - 1) / rch;
+  nb = (int)nbl;
+}
+
+void wgrad_reduce_flush(hipStream_t st) {
+  std::vector<PendingRed> segs;
+  segs.swap(g_red_pending);
+  bool vec = true;
+  for (const auto &r : segs)
+    vec &= (r.n % 4 == 0) && ((uintptr_t)r.part % 16 == 0) && ((uintptr_t)r.grad % 16 == 0);
+  const int V = vec ? 4 : 1;
+  for (size_t b = 0; b < segs.size(); b += kRedMaxSeg) {
+    RedSegs a{};
+    a.nseg = (int)std::min<size_t>(kRedMaxSeg, segs.size() - b);
+    const int target = std::max(64, (is_side_stream(st) ? kWredSideWgs : kWredTargetWgs) / a.nseg);
+    int wg = 0, ctrs = 0;
+    for (int k = 0; k < a.nseg; ++k) {
+      const PendingRed &r = segs[b + k];
+      RedSeg &g = a.s[k];
+      g.part = r.part;
+      g.grad = r.grad;
+      g.n = r.n;
+      g.S = r.S;
+      red_geom(r.S, r.n, target, V, g.nb, g.rch, g.nch);
+      g.wg0 = wg;
+      g.ctr0 = ctrs;
+      wg += g.nb * g.nch;
+      ctrs += g.nb;
+    }
+    a.ctr = reduce_counters(ctrs, st);
+    if (vec) hipLaunchKernelGGL(col_reduce_multi_kernel<4>, dim3(wg), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(col_reduce_multi_kernel<1>, dim3(wg), dim3(256), 0, st, a);
+  }
+}
+
 // grad[n] = sum over S split rows of part[S][n] (fixed order); part needs S + colsum_rows(S) rows
 void launch_wgrad_reduce(float *part, int S, long long n, float *grad, hipStream_t st) {
+  if (g_red_defer) {
+    g_red_pending.push_back(PendingRed{part, S, n, grad});
+    return;
+  }
   const bool vec = (n % 4 == 0) && ((uintptr_t)part % 16 == 0) && ((uintptr_t)grad % 16 == 0);
   const int V = vec ? 4 : 1;
   const long long nb = (n + 16 * V - 1) / (16 * V);

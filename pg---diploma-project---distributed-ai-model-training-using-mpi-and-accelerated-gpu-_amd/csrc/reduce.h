@@ -38,6 +38,20 @@ PG_DEVICE float ld_sc1(const float *p) {
                                            __HIP_MEMORY_SCOPE_AGENT));
 }
 
+// arrive_last with an explicit counter (the caller picked its column block's entry)
+PG_DEVICE bool arrive_last_at(int *c, int nch, int *lds_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int old = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == nch - 1;
+    if (last) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *lds_flag = last;
+  }
+  __syncthreads();
+  return *lds_flag != 0;
+}
+
 // Call with every thread of the workgroup after the level-1 values were stored with
 // st_sc1 (by any subset of threads).  Returns true (uniformly) in the last-arriving
 // workgroup of column block blockIdx.x; that workgroup also re-arms the counter.

@@ -286,6 +286,10 @@ class MobileNetV2Executor:
             self.fwd_fin_tab = K.bn_desc_table([bn.desc_f for bn in bns])
             self.fwd_fin_n, self.fwd_fin_maxc = len(bns), max(bn.C for bn in bns)
         self.ws_wgrad = torch.zeros(max(wg) + 1024, **f32)
+        # one split-partial workspace per weight gradient of a flushed side-stream group (their
+        # reductions are launched together after the group); ws_wgrad is the first
+        nws = max(1, int(os.environ.get("PGDIST_SIDE_BATCH", "3")))
+        self.ws_wgrad_pool = [self.ws_wgrad] + [torch.zeros_like(self.ws_wgrad) for _ in range(nws - 1)]
         # the stem weight gradient may run on the main stream concurrently with side-stream
         # weight gradients: its own split-M workspace
         self.ws_stem = torch.zeros(K.stem_wgrad_workspace(B, img_size, img_size, 32) + 1024, **f32)
@@ -296,6 +300,7 @@ class MobileNetV2Executor:
         self._side_pending = []   # deferred (BN finalizes, weight-gradient callable) pairs
         self._fin_tabs = {}       # batched backward-finalize descriptor tables by BN group
         self.side_batch = max(1, int(os.environ.get("PGDIST_SIDE_BATCH", "3")))
+        self.batch_reductions = os.environ.get("PGDIST_RED_BATCH", "1") == "1"
         if device.type == "cuda" and side_stream:
             self.side = torch.cuda.Stream(device)
             K.register_side_stream(self.side)
@@ -410,10 +415,10 @@ class MobileNetV2Executor:
         idle per join on MI355X); one join per group instead of one per layer."""
         if self.side is None:
             self._side_fins(fins)
-            fn()
+            fn(self.ws_wgrad)
             return
         self._side_pending.append((fins, fn))
-        if len(self._side_pending) >= self.side_batch:
+        if len(self._side_pending) >= min(self.side_batch, len(self.ws_wgrad_pool)):
             self._flush_side()
 
     def _flush_side(self):
@@ -424,8 +429,16 @@ class MobileNetV2Executor:
         K.stream_wait(self.side, torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.side):
             self._side_fins([f for fins, _ in self._side_pending for f in fins])
-            for _, fn in self._side_pending:
-                fn()
+            # the group's split-M reductions in one multi-segment launch: each weight gradient
+            # of the group writes its split partials into its own workspace
+            K.wgrad_reduce_defer(self.batch_reductions)
+            try:
+                for j, (_, fn) in enumerate(self._side_pending):
+                    fn(self.ws_wgrad_pool[j])
+            finally:
+                K.wgrad_reduce_defer(False)
+            if self.batch_reductions:
+                K.wgrad_reduce_flush()
         self._side_pending.clear()
 
     def _consume_output(self, pend, W, out, ws, M, N, K_, fin=None, lz=None):
@@ -546,7 +559,6 @@ class MobileNetV2Executor:
     def backward(self):
         f, B, S = self.flat, self.B, self.S
         self._check_bn_mode()
-        wg = self.ws_wgrad
         # transposed 1x1 weights for the dgrad GEMMs (one batched launch)
         K.wt_transpose(f.shadow, f.shadow_t, self.wt_tab, self.wt_n)
         self._ready([self.w_lin, self.b_lin])
@@ -565,9 +577,9 @@ class MobileNetV2Executor:
         P_g = K.pw_num_partials(Mf, self.C_last_in, self.C_last)
         last_blk.bn_p.finalize_bwd(last_blk.bn_p.acc_b, P_g)
 
-        def last_wgrad():
+        def last_wgrad(ws):
             K.pw_wgrad(bnl.g, bnl.y, bnl.a, bnl.b, bnl.c, last_blk.o, None, None, K.ACT_NONE,
-                       wg, f.g(self.w_last), Mf, self.C_last, self.C_last_in)
+                       ws, f.g(self.w_last), Mf, self.C_last, self.C_last_in)
         self._wgrad(last_wgrad, fins=((bnl, B), (last_blk.bn_p, P_g)))
         self._ready((bnl.param_names if self.lazy_bn else []) + [self.w_last] + last_blk.bn_p.param_names)
 
@@ -586,7 +598,7 @@ class MobileNetV2Executor:
                          None, Mout, bp.cout, bp.hidden, es=bnd.scale, et=bnd.shift, fin=bnd.fin_b, lz=bnp.lz_b)
                 Pb = K.pw_bwd_num_partials(Mout, bp.cout, bp.hidden)
 
-                def prj_wgrad(Pb=Pb, wpm=wpm, bp=bp):   # deferred: bind this layer's values
+                def prj_wgrad(ws, Pb=Pb, wpm=wpm, bp=bp):   # deferred: bind this layer's values
                     K.wgrad_reduce(wpm, Pb, bp.cout * bp.hidden, f.g(bp.w_p))
                 self._wgrad(prj_wgrad, fins=((bnd, Pb),))
                 bnd.finalize_bwd(bnd.acc_b, Pb)
@@ -597,9 +609,9 @@ class MobileNetV2Executor:
                 Pb = K.pw_num_partials(Mout, bp.hidden, bp.cout)
                 bnd.finalize_bwd(bnd.acc_b, Pb)
 
-                def prj_wgrad(bnd=bnd, bnp=bnp, bp=bp, Mout=Mout):   # project wgrad (deferred)
+                def prj_wgrad(ws, bnd=bnd, bnp=bnp, bp=bp, Mout=Mout):   # project wgrad (deferred)
                     K.pw_wgrad(bp.G, bnp.y, bnp.a, bnp.b, bnp.c, bnd.y, bnd.scale, bnd.shift,
-                               K.ACT_BN_RELU6, wg, f.g(bp.w_p), Mout, bp.cout, bp.hidden)
+                               K.ACT_BN_RELU6, ws, f.g(bp.w_p), Mout, bp.cout, bp.hidden)
                 self._wgrad(prj_wgrad, fins=((bnd, Pb),))
             self._ready([bp.w_p] + bnd.param_names)
             # depthwise: input BN is BN_e (expand) or the stem BN0 (t=1 block)
@@ -618,7 +630,7 @@ class MobileNetV2Executor:
                            B, Hin, Hin, bp.hidden, bp.stride, wpart=wpd, fin=dw_in.fin_b, lz=bnd.lz_b)
                 dw_in.finalize_bwd(dw_in.acc_b, Pd, force=main_fin)
 
-                def dw_wg(wpd=wpd, Pd=Pd, bp=bp):   # deferred: bind this layer's values
+                def dw_wg(ws, wpd=wpd, Pd=Pd, bp=bp):   # deferred: bind this layer's values
                     K.wgrad_reduce(wpd, Pd, 9 * bp.hidden, f.g(bp.w_d))
                 self._wgrad(dw_wg, fins=side_fins)
             else:
@@ -628,8 +640,8 @@ class MobileNetV2Executor:
                            B, Hin, Hin, bp.hidden, bp.stride, fin=dw_in.fin_b, lz=bnd.lz_b)
                 dw_in.finalize_bwd(dw_in.acc_b, Pd, force=main_fin)
 
-                def dw_wg(bnd=bnd, dw_in=dw_in, bp=bp, Hin=Hin):   # deferred
-                    K.dw_wgrad(bnd.g, bnd.y, bnd.coef, dw_in.y, dw_in.scale, dw_in.shift, wg,
+                def dw_wg(ws, bnd=bnd, dw_in=dw_in, bp=bp, Hin=Hin):   # deferred
+                    K.dw_wgrad(bnd.g, bnd.y, bnd.coef, dw_in.y, dw_in.scale, dw_in.shift, ws,
                                f.g(bp.w_d), B, Hin, Hin, bp.hidden, bp.stride)
                 self._wgrad(dw_wg, fins=side_fins)
             self._ready([bp.w_d] + dw_in.param_names)
@@ -644,7 +656,7 @@ class MobileNetV2Executor:
                              X=prev.o, fin=prev.bn_p.fin_b, lz=bne.lz_b)
                     Pe = K.pw_bwd_num_partials(Min, bp.hidden, bp.cin)
 
-                    def exp_wgrad(Pe=Pe, wpe=wpe, bp=bp):   # deferred: bind this layer's values
+                    def exp_wgrad(ws, Pe=Pe, wpe=wpe, bp=bp):   # deferred: bind this layer's values
                         K.wgrad_reduce(wpe, Pe, bp.hidden * bp.cin, f.g(bp.w_e))
                     self._wgrad(exp_wgrad, fins=((prev.bn_p, Pe),))
                     prev.bn_p.finalize_bwd(prev.bn_p.acc_b, Pe)
@@ -656,9 +668,9 @@ class MobileNetV2Executor:
                     Pe = K.pw_num_partials(Min, bp.cin, bp.hidden)
                     prev.bn_p.finalize_bwd(prev.bn_p.acc_b, Pe)
 
-                    def exp_wgrad(prev=prev, bne=bne, bp=bp, Min=Min):   # deferred
+                    def exp_wgrad(ws, prev=prev, bne=bne, bp=bp, Min=Min):   # deferred
                         K.pw_wgrad(bne.g, bne.y, bne.a, bne.b, bne.c, prev.o, None, None,
-                                   K.ACT_NONE, wg, f.g(bp.w_e), Min, bp.hidden, bp.cin)
+                                   K.ACT_NONE, ws, f.g(bp.w_e), Min, bp.hidden, bp.cin)
                     self._wgrad(exp_wgrad, fins=((prev.bn_p, Pe),))
                 self._ready([bp.w_e] + prev.bn_p.param_names)
             else:
@@ -669,7 +681,7 @@ class MobileNetV2Executor:
                 stem_wg = lambda: K.stem_wgrad(bn0.g, bn0.y, bn0.a, bn0.b, bn0.c, self.img, self.ws_stem,  # noqa: E731
                                                f.g(self.stem_w), B, S, S, 32)
                 if self.STEM_WGRAD_SIDE:
-                    self._wgrad(stem_wg)
+                    self._wgrad(lambda ws: stem_wg())
                 else:
                     stem_wg()
                 self._ready([self.stem_w])

@@ -416,6 +416,18 @@ def wgrad_reduce(part, S, n, grad):
     lib().wgrad_reduce(_p(part), int(S), int(n), _p(grad), _s())
 
 
+def wgrad_reduce_defer(on: bool):
+    """While on, every weight-gradient split reduction (wgrad_reduce and the reductions inside
+    pw_wgrad / dw_wgrad) is recorded instead of launched; :func:`wgrad_reduce_flush` then
+    launches them together (one multi-segment launch per up to 8).  Their partial buffers
+    must stay untouched until the flush."""
+    lib().wgrad_reduce_defer(bool(on))
+
+
+def wgrad_reduce_flush():
+    lib().wgrad_reduce_flush(_s())
+
+
 def pw_wgrad_workspace(M, N, K):
     return lib().pw_wgrad_workspace_floats(M, N, K)
 

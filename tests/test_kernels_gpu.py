@@ -610,3 +610,40 @@ def test_head_dropout_consistent(dev):
     dpool = ((torch.softmax(lg, 1) - F.one_hot(labels, NC)) / B) @ Wl * keepm
     gref = dpool[:, None, :] / HW * mask
     assert rel(g, gref) < 8e-3
+
+
+# ----------------------------------------------------------------------------- split-M reductions
+@pytest.mark.parametrize("segs", [
+    [(40, 64), (700, 96 * 9), (3, 16)],                      # vectorised (n % 4 == 0)
+    [(1024, 1296), (17, 30), (2000, 8)],                     # one odd n: scalar path for all
+    [(i * 37 % 900 + 1, 64 * (i + 1)) for i in range(11)],   # > 8 segments: two multi launches
+])
+def test_wgrad_reduce_deferred_multi(dev, segs):
+    """Deferred reductions flushed as multi-segment launches == one launch each == fp64 sums
+    (row chunking differs: a multi launch splits its grid target over the segments);
+    repeated to check the per-segment arrival counters are re-armed."""
+    for it in range(3):
+        parts, grads, refs = [], [], []
+        for k, (S, n) in enumerate(segs):
+            ws = torch.zeros((S + K.lib().colsum_rows(S)) * n + 64, device=dev)
+            src = rnd(S, n, dev=dev, seed=100 * it + k)
+            ws[:S * n] = src.reshape(-1)
+            parts.append(ws)
+            grads.append(torch.full((n,), float("nan"), device=dev))
+            refs.append(src.double().sum(0))
+        K.wgrad_reduce_defer(True)
+        try:
+            for (S, n), ws, g in zip(segs, parts, grads):
+                K.wgrad_reduce(ws, S, n, g)
+        finally:
+            K.wgrad_reduce_defer(False)
+        torch.cuda.synchronize()
+        assert all(torch.isnan(g).all() for g in grads), "a deferred reduction ran before the flush"
+        K.wgrad_reduce_flush()
+        torch.cuda.synchronize()
+        for (S, n), ws, g, r in zip(segs, parts, grads, refs):
+            assert torch.allclose(g.double(), r, rtol=1e-5, atol=1e-3), (S, n)
+            g1 = torch.empty(n, device=dev)
+            K.wgrad_reduce(ws, S, n, g1)
+            torch.cuda.synchronize()
+            assert torch.allclose(g1, g, rtol=1e-5, atol=1e-3), "multi-segment and single reductions differ"
