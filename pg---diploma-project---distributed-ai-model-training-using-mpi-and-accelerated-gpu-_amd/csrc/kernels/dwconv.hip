@@ -224,10 +224,11 @@ PG_DEVICE uint32_t nhwc_off(int b, int H, int W, int C, int h, int w, int c) {
 // Per step (one input row): 1 DMA + 1 store (out of range when no output row completes).
 // The row loop is unrolled over the window period (3 rows for stride 1, 4 for stride 2) so
 // the window rows rotate by register renaming instead of copies; weights stay unpacked.
-template <int S, int ACT>
+template <int S, int ACT, int D = kDepth>
 __global__ __launch_bounds__(256) void dw_fwd_lds_kernel(
     const bf16_t *__restrict__ x, const float *__restrict__ in_s, const float *__restrict__ in_t,
     const bf16_t *__restrict__ w, bf16_t *__restrict__ y, float *__restrict__ part, DwGeom g) {
+  constexpr int kDepth = D, kRing = D + 1;
   constexpr int kSlot = S == 1 ? kSlotHalo : kSlotS2;
   constexpr int U = S == 1 ? 3 : 4;                 // window period in input rows
   __shared__ __attribute__((aligned(16))) char ring[kRing * kSlot + 1024];
@@ -345,12 +346,14 @@ __global__ __launch_bounds__(256) void dw_fwd_lds_kernel(
 // rows (g, y of this layer's BN backward, halo columns) of dy row r0-1+k and yprev (the
 // producer's pre-BN activation, own columns: ReLU6 mask + fused weight gradient) of input row
 // r0+k-2; step k >= 2 emits input row r0+k-2.  Per step: 3 DMA + 1 store.
-template <bool WG>
+template <bool WG, int D = kDepth>
 __global__ __launch_bounds__(256) void dw_dgrad_s1_lds_kernel(
     const bf16_t *__restrict__ gin, const bf16_t *__restrict__ yself, const float *__restrict__ coef,
     const bf16_t *__restrict__ w, const bf16_t *__restrict__ yprev, const float *__restrict__ ps,
     const float *__restrict__ pt, bf16_t *__restrict__ gout, float *__restrict__ part, DwGeom g,
     float *__restrict__ wpart) {
+  // D rows in flight: 3 gives 39 KB of LDS per workgroup (4 per CU) instead of 48 KB (3 per CU)
+  constexpr int kDepth = D, kRing = D + 1;
   constexpr int kStep = 2 * kSlotHalo + kSlotOwn;   // g, y, yprev pieces of one ring slot
   __shared__ __attribute__((aligned(16))) char ring[kRing * kStep + 1024];
   __shared__ __attribute__((aligned(16))) float red[1024];
@@ -497,12 +500,13 @@ __global__ __launch_bounds__(256) void dw_dgrad_s1_lds_kernel(
 // row o = o0 + k (g, y over the dy columns the tile touches) and yprev input rows 2(o-1),
 // 2(o-1)+1 (own columns); step k >= 1 emits those two input rows (tap dh = 1 with dy row o-1;
 // dh = 2 with row o-1 and dh = 0 with row o).  Per step: 4 DMA + 2 stores.
-template <bool WG>
+template <bool WG, int D = kDepth>
 __global__ __launch_bounds__(256) void dw_dgrad_s2_lds_kernel(
     const bf16_t *__restrict__ gin, const bf16_t *__restrict__ yself, const float *__restrict__ coef,
     const bf16_t *__restrict__ w, const bf16_t *__restrict__ yprev, const float *__restrict__ ps,
     const float *__restrict__ pt, bf16_t *__restrict__ gout, float *__restrict__ part, DwGeom g,
     float *__restrict__ wpart) {
+  constexpr int kDepth = D, kRing = D + 1;
   constexpr int kStep = 4 * kSlotOwn;   // g, y (<= TWc/2 + 2 dy columns), yprev x 2
   __shared__ __attribute__((aligned(16))) char ring[kRing * kStep + 1024];
   __shared__ __attribute__((aligned(16))) float red[1024];
@@ -902,12 +906,18 @@ void launch_dw_fwd(const bf16_t *x, const float *in_s, const float *in_t, int ac
   g.fin = take_bn_fin();
   g.lz = take_bn_lz();
   const dim3 grid(dw_grid_x(g) * (C / g.CC)), block(256);
+  // PGDIST_DW_FDEPTH=3: forward ring depth 3 (tuning experiment; default 4)
+  static const bool fd3 = [] { const char *e = getenv("PGDIST_DW_FDEPTH"); return e && atoi(e) == 3; }();
   if (stride == 1) {
-    if (act == ACT_BN_RELU6) hipLaunchKernelGGL((dw_fwd_lds_kernel<1, ACT_BN_RELU6>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
-    else hipLaunchKernelGGL((dw_fwd_lds_kernel<1, ACT_NONE>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
+    if (act == ACT_BN_RELU6) {
+      if (fd3) hipLaunchKernelGGL((dw_fwd_lds_kernel<1, ACT_BN_RELU6, 3>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
+      else hipLaunchKernelGGL((dw_fwd_lds_kernel<1, ACT_BN_RELU6>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
+    } else hipLaunchKernelGGL((dw_fwd_lds_kernel<1, ACT_NONE>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
   } else {
-    if (act == ACT_BN_RELU6) hipLaunchKernelGGL((dw_fwd_lds_kernel<2, ACT_BN_RELU6>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
-    else hipLaunchKernelGGL((dw_fwd_lds_kernel<2, ACT_NONE>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
+    if (act == ACT_BN_RELU6) {
+      if (fd3) hipLaunchKernelGGL((dw_fwd_lds_kernel<2, ACT_BN_RELU6, 3>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
+      else hipLaunchKernelGGL((dw_fwd_lds_kernel<2, ACT_BN_RELU6>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
+    } else hipLaunchKernelGGL((dw_fwd_lds_kernel<2, ACT_NONE>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
   }
 }
 
@@ -920,17 +930,21 @@ void launch_dw_dgrad(const bf16_t *gin, const bf16_t *yself, const float *coef, 
   g.fin = take_bn_fin();
   g.lz = take_bn_lz();
   const dim3 grid(dw_grid_x(g) * (C / g.CC)), block(256);
+  // ring depth (rows in flight): 3 by default -- 39 KB of LDS per workgroup, 4 workgroups per CU
+  // instead of 3 at depth 4 (MobileNetV2 bs128: 5.02 -> 4.94 ms/step); PGDIST_DW_DDEPTH=2|3|4
+  static const int env_d = [] { const char *e = getenv("PGDIST_DW_DDEPTH"); return e ? atoi(e) : 3; }();
+#define DWD(KER, WGF)                                                                                     \
+  if (env_d == 2) hipLaunchKernelGGL((KER<WGF, 2>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g, wpart); \
+  else if (env_d == 4) hipLaunchKernelGGL((KER<WGF, 4>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g, wpart); \
+  else hipLaunchKernelGGL((KER<WGF, 3>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g, wpart);
   if (wpart) {
-    if (stride == 1)
-      hipLaunchKernelGGL((dw_dgrad_s1_lds_kernel<true>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g, wpart);
-    else
-      hipLaunchKernelGGL((dw_dgrad_s2_lds_kernel<true>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g, wpart);
+    if (stride == 1) { DWD(dw_dgrad_s1_lds_kernel, true) }
+    else { DWD(dw_dgrad_s2_lds_kernel, true) }
   } else {
-    if (stride == 1)
-      hipLaunchKernelGGL((dw_dgrad_s1_lds_kernel<false>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g, wpart);
-    else
-      hipLaunchKernelGGL((dw_dgrad_s2_lds_kernel<false>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g, wpart);
+    if (stride == 1) { DWD(dw_dgrad_s1_lds_kernel, false) }
+    else { DWD(dw_dgrad_s2_lds_kernel, false) }
   }
+#undef DWD
 }
 
 // wpart of the fused dgrad + wgrad: [P][9][C] with P = dgrad tiles, + level-1 rows of the reduction
