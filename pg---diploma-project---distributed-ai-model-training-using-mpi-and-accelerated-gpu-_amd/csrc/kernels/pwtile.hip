@@ -349,11 +349,12 @@ struct TileGeom {
 TileGeom tile_geom(int M, int N, int K, int pro) {
   TileGeom g{};
   // largest tile that still gives >= 384 workgroups (~1.5 per CU), else the smallest
+  static const int min_wgs = [] { const char *e = getenv("PGDIST_TILE_MINWG"); return e && atoi(e) > 0 ? atoi(e) : 384; }();
   const int cand[4][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}};
   int pick = 3;
   for (int i = 0; i < 4; ++i) {
     const long long wgs = (long long)((M + cand[i][0] - 1) / cand[i][0]) * ((N + cand[i][1] - 1) / cand[i][1]);
-    if (wgs >= 384) { pick = i; break; }
+    if (wgs >= min_wgs) { pick = i; break; }
   }
   g.BM = cand[pick][0];
   g.BN = cand[pick][1];

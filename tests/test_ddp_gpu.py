@@ -114,3 +114,52 @@ def test_native_ddp_reduced_gradient_equals_sum_of_shards():
     for bi, first, last, scale, err in per:
         assert scale > 0, f"bucket {bi} ({first} .. {last}) has an all-zero gradient"
         assert err < 1e-5, f"bucket {bi} ({first} .. {last}): rel err {err}"
+
+
+def _lazy_bn_grad_worker(rank, world, port, q):
+    """Lazy BN finalize (default mode) under data parallelism: the BN weight / bias gradients
+    are written by the side-stream batched finalizes, and every gradient bucket holding them
+    must be all-reduced only after those ran.  After one step each rank recomputes its LOCAL
+    dgamma / dbeta from the backward accumulators (still intact until the next forward) and
+    all-reduces them itself: the reducer's buckets must hold exactly that sum."""
+    import pgdist  # noqa: F401
+    from pgdist.models import build_model
+    from pgdist.engine.native_step import NativeTrainStep
+    from pgdist.ops import kernels as K
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(7)
+    src = torch.randint(0, 256, (32, 32, 32, 3), dtype=torch.uint8, device=dev, generator=g)
+    labels = torch.randint(0, 10, (32,), device=dev, generator=g)
+    torch.manual_seed(100)
+    st = NativeTrainStep(build_model("mobilenet_v2", num_classes=10), 8, dev, img_size=64, lr=1e-3,
+                         world_size=world, rank=rank, bucket_mb=0.5, first_bucket_mb=0.1)
+    assert st.exe.bn_mode == "lazy"
+    st.set_data(src, labels)
+    st.run(torch.arange(8, device=dev) + 8 * rank)
+    torch.cuda.synchronize()
+    bns = st.exe.all_bns()
+    local = []
+    for bn in bns:
+        coef = torch.zeros(3, bn.C, device=dev)
+        dg, db = torch.zeros(bn.C, device=dev), torch.zeros(bn.C, device=dev)
+        K.bn_bwd_finalize(bn.acc_b, bn.rows_b, bn.C, bn.M, bn.mean, bn.rstd, bn.gamma, coef, dg, db)
+        local += [dg, db]
+    torch.cuda.synchronize()
+    mine = torch.cat(local).cpu()
+    dist.all_reduce(mine)
+    got = torch.cat([st.flat.grad[slice(*st.flat.range_of(n))] for bn in bns for n in bn.param_names]).cpu()
+    err = ((got - mine).abs().max() / (mine.abs().max() + 1e-12)).item()
+    q.put(("ok", rank, err, mine.abs().max().item()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_native_ddp_lazy_bn_gradients_reduced_after_side_finalize():
+    world, port = 2, _free_port()
+    res = _run_ranks(_lazy_bn_grad_worker, world, (world, port), expect=world)
+    for _, rank, err, scale in res:
+        assert scale > 0
+        assert err < 1e-6, f"rank {rank}: BN gradients in the buckets differ from the summed local ones ({err})"
