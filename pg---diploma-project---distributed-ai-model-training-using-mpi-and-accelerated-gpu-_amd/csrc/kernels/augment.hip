@@ -24,7 +24,11 @@
 namespace {
 constexpr int kNP = 16;  // params per image
 // param slots
-enum { P_I = 0, P_J, P_H, P_W, P_FLIP, P_B, P_C, P_S, P_HUE, P_ORDER, P_ANGLE, P_MEAN, P_SRC_HW };
+enum { P_I = 0, P_J, P_H, P_W, P_FLIP, P_B, P_C, P_S, P_HUE, P_ORDER, P_ANGLE, P_MEAN, P_SRC_HW, P_MEAN1, P_MEAN2, P_MEAN3 };
+// The contrast mean is computed by kMeanSplit workgroups per image; each leaves the partial SUM
+// of its share of the 56x56 grey samples in one slot, the render kernel adds them up.
+constexpr int kMeanSplit = 4;
+__device__ constexpr int kMeanSlot[kMeanSplit] = {P_MEAN, P_MEAN1, P_MEAN2, P_MEAN3};
 constexpr float kMean[3] = {0.485f, 0.456f, 0.406f};
 constexpr float kStd[3] = {0.229f, 0.224f, 0.225f};
 
@@ -147,7 +151,8 @@ PG_DEVICE void jitter(float (&x)[3], const float *prm, float mean, bool stop_bef
 }  // namespace
 
 // ---------------------------------------------------------------------------
-// kernel 1: per-image parameters (+ contrast mean), one workgroup per image
+// kernel 1: per-image parameters (+ contrast mean partials): grid (B, kMeanSplit); every
+// workgroup of an image draws the same parameters (same counter-based RNG stream)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void augment_params_kernel(
     const unsigned char *__restrict__ src, const long long *__restrict__ idx, int B, int S,
@@ -156,7 +161,7 @@ __global__ __launch_bounds__(256) void augment_params_kernel(
   __shared__ float img[32 * 32 * 3];
   __shared__ float prm[kNP];
   __shared__ float red[4];
-  const int b = blockIdx.x, tid = threadIdx.x;
+  const int b = blockIdx.x, split = blockIdx.y, tid = threadIdx.x;
   const long long si = idx[b];
   for (int i = tid; i < 32 * 32 * 3; i += 256) img[i] = src[si * 3072 + i] * (1.f / 255.f);
   const int RH = dbl ? S : 32, RW = dbl ? S : 32;  // image the crop is taken from
@@ -212,8 +217,9 @@ __global__ __launch_bounds__(256) void augment_params_kernel(
   float acc = 0.f;
   const bool need_mean = prm[P_C] != 1.f;
   if (need_mean) {
-    const int G = 56;
-    for (int i = tid; i < G * G; i += 256) {
+    const int G = 56, per = (G * G + kMeanSplit - 1) / kMeanSplit;
+    const int i1 = min(G * G, (split + 1) * per);
+    for (int i = split * per + tid; i < i1; i += 256) {
       const int v = (i / G) * S / G + S / (2 * G), u = (i % G) * S / G + S / (2 * G);
       float x[3];
       f_pixel(img, 32, 32, RH, RW, prm, S, u, v, dbl != 0, x);
@@ -224,12 +230,13 @@ __global__ __launch_bounds__(256) void augment_params_kernel(
     if ((tid & 63) == 0) red[tid >> 6] = acc;
   }
   __syncthreads();
-  if (tid < kNP) {
+  const float psum = need_mean ? (red[0] + red[1] + red[2] + red[3]) : 0.f;
+  if (split == 0 && tid < kNP) {
     float val = prm[tid];
-    if (tid == P_MEAN) val = need_mean ? (red[0] + red[1] + red[2] + red[3]) / (56.f * 56.f) : 0.f;
     if (tid == P_SRC_HW) val = (float)RH;
-    params[b * kNP + tid] = val;
+    if (!(tid == P_MEAN || tid == P_MEAN1 || tid == P_MEAN2 || tid == P_MEAN3)) params[b * kNP + tid] = val;
   }
+  if (tid == 0) params[b * kNP + kMeanSlot[split]] = psum;
 }
 
 // ---------------------------------------------------------------------------
@@ -245,6 +252,9 @@ __global__ __launch_bounds__(256) void augment_render_kernel(
   const long long si = idx[b];
   for (int i = tid; i < 32 * 32 * 3; i += 256) img[i] = src[si * 3072 + i] * (1.f / 255.f);
   if (tid < kNP) prm[tid] = params[b * kNP + tid];
+  __syncthreads();
+  if (tid == 0)   // contrast mean = sum of the kMeanSplit partial sums, fixed order
+    prm[P_MEAN] = (((prm[P_MEAN] + prm[P_MEAN1]) + prm[P_MEAN2]) + prm[P_MEAN3]) * (1.f / (56.f * 56.f));
   if (labels_out && blockIdx.y == 0 && tid == 0) labels_out[b] = labels_src[si];
   __syncthreads();
   const int RH = (int)prm[P_SRC_HW], RW = RH;
@@ -288,7 +298,7 @@ void launch_augment(const unsigned char *src, const long long *idx, const long l
                     unsigned long long seed, const float *hyper, int epoch_ctr, bf16_t *out,
                     long long *labels_out, float *params, hipStream_t st) {
   (void)nsrc;
-  hipLaunchKernelGGL(augment_params_kernel, dim3(B), dim3(256), 0, st, src, idx, B, S, train, dbl,
+  hipLaunchKernelGGL(augment_params_kernel, dim3(B, kMeanSplit), dim3(256), 0, st, src, idx, B, S, train, dbl,
                      given, seed, hyper, epoch_ctr, params);
   const int rows_per_block = (256 * 8 + S - 1) / S;
   dim3 grid(B, (S + rows_per_block - 1) / rows_per_block);
