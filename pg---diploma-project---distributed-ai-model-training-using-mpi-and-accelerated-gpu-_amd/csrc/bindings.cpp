@@ -289,7 +289,7 @@ PYBIND11_MODULE(_pgdist_C, m) {
   // ---- stem ----
   m.def("stem_fwd_num_partials", &stem_fwd_num_partials);
   m.def("stem_fwd", [](P img, P w, P y, P part, int B, int H, int W, int px, P s) {
-    if (px != 1 && px != 2 && px != 4) throw std::invalid_argument("stem_fwd: px must be 1, 2 or 4");
+    if (px != 0 && px != 1 && px != 2 && px != 4) throw std::invalid_argument("stem_fwd: px must be 0, 1, 2 or 4");
     pgdist_rt::run_op([=] {
       (void)launch_stem_fwd(ptr<bf16_t>(img), ptr<bf16_t>(w), ptr<bf16_t>(y), ptr<float>(part), B, H, W, px, S(s));
     });

@@ -448,18 +448,20 @@ def stem_num_partials(B, H, W):
 
 
 def _stem_px_default():
-    v = os.environ.get("PGDIST_STEM_PX", "1")
-    if v not in ("1", "2", "4"):
-        raise ValueError(f"PGDIST_STEM_PX={v!r}: must be 1, 2 or 4")
+    # 0: the MFMA implicit GEMM (MobileNetV2 bs128 on MI355X: 4.81 vs 4.88 ms/step with the
+    # best VALU variant, px = 1)
+    v = os.environ.get("PGDIST_STEM_PX", "0")
+    if v not in ("0", "1", "2", "4"):
+        raise ValueError(f"PGDIST_STEM_PX={v!r}: must be 0 (MFMA), 1, 2 or 4")
     return int(v)
 
 
 def stem_fwd(img, w, y, part, B, H, W, px=None, fin=None):
-    """Stem 3x3 s2 conv forward; ``px`` output pixels per thread (1, 2 or 4; default from
-    PGDIST_STEM_PX, else 1 — the measured fastest)."""
+    """Stem 3x3 s2 conv forward; ``px``: 0 = MFMA implicit GEMM, else output pixels per thread
+    of the VALU kernel (1, 2 or 4); default from PGDIST_STEM_PX."""
     px = _stem_px_default() if px is None else int(px)
-    if px not in (1, 2, 4):
-        raise ValueError(f"stem_fwd: px={px} must be 1, 2 or 4")
+    if px not in (0, 1, 2, 4):
+        raise ValueError(f"stem_fwd: px={px} must be 0, 1, 2 or 4")
     Ho, Wo = dw_out_hw(H, W, 2)
     _chk(img, BF16, B * H * W * 4, "img")
     _chk(w, BF16, 32 * 27, "w")

@@ -409,11 +409,12 @@ def test_pw_bwd_fused(dev, M, Kg, Ng, mode, res):
 
 
 # ----------------------------------------------------------------------------- stem
-@pytest.mark.parametrize("px", [1, 2, 4])
+@pytest.mark.parametrize("px", [0, 1, 2, 4])
 @pytest.mark.parametrize("B,S", [(2, 32), (3, 64), (2, 224), (3, 30), (1, 50)])
 def test_stem(dev, B, S, px):
-    """Every register-blocking variant (px pixels per thread); (3, 30) / (1, 50) give
-    B*Ho*Wo = 675 / 625, not a multiple of 64*px, so the tail pixels are exercised."""
+    """The MFMA implicit-GEMM kernel (px = 0) and every register-blocking VALU variant (px
+    pixels per thread); (3, 30) / (1, 50) give B*Ho*Wo = 675 / 625, not a multiple of 16 or
+    64*px, so the tail pixels are exercised."""
     img = torch.zeros(B, S, S, 4, dtype=torch.bfloat16, device=dev)
     img[..., :3] = bf(rnd(B, S, S, 3, dev=dev, seed=1))
     w = bf(rnd(32, 3, 3, 3, dev=dev, seed=2) * 0.2)

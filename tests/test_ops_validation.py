@@ -7,7 +7,7 @@ import pgdist  # noqa: F401
 from pgdist.ops import kernels as K
 
 
-@pytest.mark.parametrize("px", [0, 3, 8])
+@pytest.mark.parametrize("px", [-1, 3, 8])
 def test_stem_px_rejected(px):
     t = torch.zeros(1)
     with pytest.raises(ValueError, match="px"):
