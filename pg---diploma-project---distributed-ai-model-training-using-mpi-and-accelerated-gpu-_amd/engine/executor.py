@@ -171,7 +171,10 @@ class MobileNetV2Executor:
     # every host-side action of a training step goes through recordable native ops
     # (ops.kernels: launches, stream_wait, memset, plan_py): the step can be a LaunchPlan
     PLAN_SAFE = True
-    DW_FUSE_MIN_H = 56   # depthwise dgrad+wgrad fused on maps >= this size (measured on MI355X)
+    # depthwise dgrad+wgrad fused on maps >= this size (measured on MI355X; PGDIST_DW_FUSE_MIN_H)
+    DW_FUSE_MIN_H = int(os.environ.get("PGDIST_DW_FUSE_MIN_H", "56"))
+    # fused 1x1 dgrad+wgrad (pw_bwd) where supported; PGDIST_PW_BWD_FUSE_MIN_M raises the M threshold
+    PW_BWD_FUSE_MIN_M = int(os.environ.get("PGDIST_PW_BWD_FUSE_MIN_M", "0"))
     # block outputs materialised by the consumer GEMM instead of a BN-apply pass: measured neutral
     # on MI355X (the consumer reads y_p and the residual per N tile), so off by default
     FUSE_BLOCK_OUTPUT = os.environ.get("PGDIST_FUSE_BLOCK_OUT", "0") == "1"
@@ -226,14 +229,14 @@ class MobileNetV2Executor:
             self.blocks.append(bp)
             if expand:
                 wg.append(K.pw_wgrad_workspace(Min, blk.hidden, blk.inp))
-                if K.pw_bwd_supported(Min, blk.hidden, blk.inp):
+                if self._pw_bwd_ok(Min, blk.hidden, blk.inp):
                     wparts[(i, "e")] = K.pw_bwd_wgrad_workspace(Min, blk.hidden, blk.inp)
             if Hin >= self.DW_FUSE_MIN_H:
                 wparts[(i, "d")] = K.dw_dgrad_wgrad_workspace(B, Hin, Hin, blk.hidden, blk.stride)
             else:
                 wg.append(K.dw_wgrad_workspace(B, Hin, Hin, blk.hidden, blk.stride))
             wg.append(K.pw_wgrad_workspace(Mout, blk.oup, blk.hidden))
-            if K.pw_bwd_supported(Mout, blk.oup, blk.hidden):
+            if self._pw_bwd_ok(Mout, blk.oup, blk.hidden):
                 wparts[(i, "p")] = K.pw_bwd_wgrad_workspace(Mout, blk.oup, blk.hidden)
             cur_h = Ho
         # ---------------- final 1x1 conv + head
@@ -365,19 +368,24 @@ class MobileNetV2Executor:
             if bp.expand:
                 rows[bp.bn_e][0] = K.pw_num_partials(Min, bp.hidden, bp.cin)
                 rows[prev.bn_p][1] = (K.pw_bwd_num_partials(Min, bp.hidden, bp.cin)
-                                      if K.pw_bwd_supported(Min, bp.hidden, bp.cin)
+                                      if self._pw_bwd_ok(Min, bp.hidden, bp.cin)
                                       else K.pw_num_partials(Min, bp.cin, bp.hidden))
             rows[bp.bn_d][0] = K.dw_num_partials("fwd", B, bp.H, bp.H, bp.hidden, bp.stride)
             rows[dw_in][1] = K.dw_num_partials("dgrad", B, bp.H, bp.H, bp.hidden, bp.stride)
             rows[bp.bn_p][0] = K.pw_num_partials(Mout, bp.cout, bp.hidden)
             rows[bp.bn_d][1] = (K.pw_bwd_num_partials(Mout, bp.cout, bp.hidden)
-                                if K.pw_bwd_supported(Mout, bp.cout, bp.hidden)
+                                if self._pw_bwd_ok(Mout, bp.cout, bp.hidden)
                                 else K.pw_num_partials(Mout, bp.hidden, bp.cout))
         Mf = B * self.Hf * self.Hf
         rows[self.bn_last][0] = K.pw_num_partials(Mf, self.C_last, self.C_last_in)
         rows[self.bn_last][1] = B
         rows[self.blocks[-1].bn_p][1] = K.pw_num_partials(Mf, self.C_last_in, self.C_last)
         return {bn: tuple(r) for bn, r in rows.items()}
+
+    def _pw_bwd_ok(self, M, Kg, Ng):
+        """Use the fused 1x1 dgrad+wgrad kernel for this backward (else dgrad on the main
+        stream, weight gradient on the side stream)."""
+        return M >= self.PW_BWD_FUSE_MIN_M and K.pw_bwd_supported(M, Kg, Ng)
 
     def _check_bn_mode(self):
         # the producers write min(P, bn_rep()) rows: a mode switch after construction would
@@ -591,7 +599,7 @@ class MobileNetV2Executor:
             bnp, bnd = bp.bn_p, bp.bn_d
             # bn_p backward coefficients were finalised by whoever produced bp.G
             # project dgrad -> g_d (relu6 mask of BN_d) + BN_d partials
-            if K.pw_bwd_supported(Mout, bp.cout, bp.hidden):
+            if self._pw_bwd_ok(Mout, bp.cout, bp.hidden):
                 # fused dgrad + wgrad (x = relu6(BN_d(y_d)) rebuilt from the mask operand)
                 wpm = self._wpart[(bp.idx, "p")]
                 K.pw_bwd(K.EPI_BWD_RELU6, bp.G, bnp.y, bnp.a, bnp.b, bnp.c, f.bt(bp.w_p), bnd.g, bnd.y, bnd.acc_b, wpm,
@@ -649,7 +657,7 @@ class MobileNetV2Executor:
                 bne = bp.bn_e
                 assert prev is not None
                 # expand dgrad -> gradient w.r.t. the block input o_prev (+ skip gradient)
-                if K.pw_bwd_supported(Min, bp.hidden, bp.cin):
+                if self._pw_bwd_ok(Min, bp.hidden, bp.cin):
                     wpe = self._wpart[(bp.idx, "e")]
                     K.pw_bwd(K.EPI_BWD_LIN, bne.g, bne.y, bne.a, bne.b, bne.c, f.bt(bp.w_e), prev.G, prev.bn_p.y,
                              prev.bn_p.acc_b, wpe, None, Min, bp.hidden, bp.cin, R=bp.G if bp.residual else None,
