@@ -906,19 +906,25 @@ void launch_dw_fwd(const bf16_t *x, const float *in_s, const float *in_t, int ac
   g.fin = take_bn_fin();
   g.lz = take_bn_lz();
   const dim3 grid(dw_grid_x(g) * (C / g.CC)), block(256);
-  // PGDIST_DW_FDEPTH=3: forward ring depth 3 (tuning experiment; default 4)
-  static const bool fd3 = [] { const char *e = getenv("PGDIST_DW_FDEPTH"); return e && atoi(e) == 3; }();
+  // ring depth: 4 rows in flight; on small maps (<= 14 rows) PGDIST_DW_FDEPTH_SMALL (6 / 8) rows so
+  // the whole strip is requested up front (one exposed DMA latency instead of ~3); PGDIST_DW_FDEPTH=3
+  // everywhere (tuning experiments)
+  static const int fd_all = [] { const char *e = getenv("PGDIST_DW_FDEPTH"); return e ? atoi(e) : 4; }();
+  static const int fd_small = [] { const char *e = getenv("PGDIST_DW_FDEPTH_SMALL"); return e ? atoi(e) : 0; }();
+  const int D = (fd_small > 0 && H <= 14) ? fd_small : fd_all;
+#define DWF(S_, A_)                                                                                           \
+  if (D == 3) hipLaunchKernelGGL((dw_fwd_lds_kernel<S_, A_, 3>), grid, block, 0, st, x, in_s, in_t, w, y, part, g); \
+  else if (D == 6) hipLaunchKernelGGL((dw_fwd_lds_kernel<S_, A_, 6>), grid, block, 0, st, x, in_s, in_t, w, y, part, g); \
+  else if (D == 8) hipLaunchKernelGGL((dw_fwd_lds_kernel<S_, A_, 8>), grid, block, 0, st, x, in_s, in_t, w, y, part, g); \
+  else hipLaunchKernelGGL((dw_fwd_lds_kernel<S_, A_, 4>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
   if (stride == 1) {
-    if (act == ACT_BN_RELU6) {
-      if (fd3) hipLaunchKernelGGL((dw_fwd_lds_kernel<1, ACT_BN_RELU6, 3>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
-      else hipLaunchKernelGGL((dw_fwd_lds_kernel<1, ACT_BN_RELU6>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
-    } else hipLaunchKernelGGL((dw_fwd_lds_kernel<1, ACT_NONE>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
+    if (act == ACT_BN_RELU6) { DWF(1, ACT_BN_RELU6) }
+    else { DWF(1, ACT_NONE) }
   } else {
-    if (act == ACT_BN_RELU6) {
-      if (fd3) hipLaunchKernelGGL((dw_fwd_lds_kernel<2, ACT_BN_RELU6, 3>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
-      else hipLaunchKernelGGL((dw_fwd_lds_kernel<2, ACT_BN_RELU6>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
-    } else hipLaunchKernelGGL((dw_fwd_lds_kernel<2, ACT_NONE>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
+    if (act == ACT_BN_RELU6) { DWF(2, ACT_BN_RELU6) }
+    else { DWF(2, ACT_NONE) }
   }
+#undef DWF
 }
 
 int colsum_rows(int R);
