@@ -28,7 +28,12 @@
 namespace {
 
 constexpr int CPT = 4;        // channels per thread
-constexpr int kRows = 28;     // rows per strip (swept 4..112 on MI355X: 28 fastest end to end)
+// rows per strip of the forward / dgrad tiles and of the weight-gradient tiles: round 1 swept
+// 4..112 (28 fastest then); with the LDS-DMA kernels, the lazy BN prologue and depth-3 dgrad
+// rings 56 is fastest for forward / dgrad (MobileNetV2 bs128: 4.84 -> 4.80 ms/step; 112 equal,
+// 40 and 14 slower), the side-stream weight gradients keep 28
+constexpr int kRows = 56;
+constexpr int kWRows = 28;
 
 struct DwGeom {
   int B, H, W, C, Ho, Wo;
@@ -883,7 +888,7 @@ DwGeom dw_geom(int kind, int B, int H, int W, int C, int stride) {
     return e ? atoi(e) : 0;
   }();
   int R = env_rows > 0 ? env_rows : kRows;
-  if (kind == 2) R = env_wrows > 0 ? env_wrows : kRows;
+  if (kind == 2) R = env_wrows > 0 ? env_wrows : kWRows;
   // (PGDIST_DW_ROWS / PGDIST_DW_WROWS override the strip length for tuning experiments)
   if (kind == 1 && stride == 2 && (R & 1)) ++R;  // dgrad s2 tiles start on even input rows
   if (R > gh) R = (kind == 1 && stride == 2) ? ((gh + 1) & ~1) : gh;
