@@ -672,7 +672,7 @@ static PwGeom pw_geom(int M, int N, int K, int pro) {
   g.nmt = (M + BM - 1) / BM;
   static const int env_lds = [] { const char *e = getenv("PGDIST_PW_WGS"); return e ? atoi(e) : 0; }();
   static const int env_bd = [] { const char *e = getenv("PGDIST_PW_WGS_BD"); return e ? atoi(e) : 0; }();
-  int gx = (g.bdirect ? (env_bd > 0 ? env_bd : 1024) : (env_lds > 0 ? env_lds : 1024)) / g.nt;
+  int gx = (g.bdirect ? (env_bd > 0 ? env_bd : 1024) : (env_lds > 0 ? env_lds : 2048)) / g.nt;   // LDS-resident path: 2048 (1024: +0.2-0.5 % step time)
   if (gx > g.nmt) gx = g.nmt;
   gx = (gx + 7) & ~7;                  // multiple of 8: the N tiles of one M tile share an XCD L2
   if (gx < 8) gx = 8;
