@@ -51,6 +51,14 @@ def coalesce_bn_buffers(model: torch.nn.Module):
     return flat, nbt
 
 
+def _dist_backend() -> str:
+    import torch.distributed as dist
+    try:
+        return str(dist.get_backend()) if dist.is_available() and dist.is_initialized() else ""
+    except Exception:   # no default group
+        return ""
+
+
 class NativeTrainStep:
     def __init__(self, model, batch: int, device: torch.device, img_size: int = 224, lr: float = 1e-4,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, world_size: int = 1,
@@ -107,8 +115,14 @@ class NativeTrainStep:
         self.fwd_graph: Optional[torch.cuda.CUDAGraph] = None
         # eager steps replayed from a native launch plan (csrc/runtime/plan.h): same two-stream
         # schedule as eager launching, none of its Python host cost (PGDIST_PLAN=0: off)
-        self.use_plan = (not self.use_graph and not self.graph_forward
-                         and getattr(self.exe, "PLAN_SAFE", False) and os.environ.get("PGDIST_PLAN", "1") == "1")
+        # Not with host-side (gloo) collectives on GPU tensors: their bucket launches and the
+        # step-end wait block the host inside the replay (2 ranks on one MI355X over gloo: 560 ms
+        # per step replayed vs 117 ms eager); RCCL collectives are stream-ordered and replay fine.
+        # PGDIST_PLAN=force: replay with gloo too (tests of the replayed data-parallel step)
+        plan_env = os.environ.get("PGDIST_PLAN", "1")
+        gloo = self.world > 1 and _dist_backend() == "gloo" and plan_env != "force"
+        self.use_plan = (not self.use_graph and not self.graph_forward and not gloo
+                         and getattr(self.exe, "PLAN_SAFE", False) and plan_env in ("1", "force"))
         self.plan: Optional[K.LaunchPlan] = None
 
     # ------------------------------------------------------------------ setup

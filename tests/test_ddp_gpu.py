@@ -18,6 +18,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _worker(rank, world, port, model_name, q):
+    os.environ["PGDIST_PLAN"] = "force"   # the replayed (launch-plan) step, as with RCCL
     import pgdist  # noqa: F401
     from pgdist.models import build_model
     from pgdist.engine.native_step import NativeTrainStep
@@ -47,6 +48,7 @@ def _worker(rank, world, port, model_name, q):
 
 @pytest.mark.parametrize("model_name", ["mobilenet_v2", "resnet50"])
 def test_native_ddp_two_ranks_one_gpu(model_name):
+    """4 data-parallel steps, launch-plan replay forced (MobileNetV2): replicas stay identical."""
     world, port = 2, _free_port()
     res = _run_ranks(_worker, world, (world, port, model_name), expect=world)
     for _, rank, diff, n, nb, finite in res:
