@@ -15,6 +15,9 @@
 #include <stdexcept>
 #include <string>
 
+#include <pybind11/stl.h>
+
+#include "runtime/comm.h"
 #include "runtime/plan.h"
 #include "runtime/runtime.h"
 
@@ -430,6 +433,33 @@ PYBIND11_MODULE(_pgdist_C, m) {
   m.def("memset_async", [](P p, int value, long long bytes, P s) {
     pgdist_rt::memset_async(ptr<void>(p), value, (size_t)bytes, S(s));
   });
+
+  // ---- native communicator (runtime/comm.h): RCCL + P2P xGMI collectives ----
+  m.def("rccl_available", &pgdist_rt::rccl_available);
+  m.def("rccl_version", &pgdist_rt::rccl_version);
+  m.def("comm_unique_id", []() { return py::bytes(pgdist_rt::comm_unique_id()); });
+  m.def("comm_create", [](int rank, int world, int device, py::bytes uid, long long region, int blocks, int nlocal,
+                          double timeout_s) {
+    std::string u = uid;
+    py::gil_scoped_release nogil;   // ncclCommInitRank blocks until every rank has joined
+    return pgdist_rt::comm_create(rank, world, device, u, region, blocks, nlocal, timeout_s);
+  });
+  m.def("comm_p2p_handle", [](int id) { return py::bytes(pgdist_rt::comm_p2p_handle(id)); });
+  m.def("comm_p2p_open", [](int id, std::vector<py::bytes> hs) {
+    std::vector<std::string> v(hs.begin(), hs.end());
+    pgdist_rt::comm_p2p_open(id, v);
+  });
+  m.def("comm_p2p_ready", &pgdist_rt::comm_p2p_ready);
+  m.def("comm_stream", &pgdist_rt::comm_stream);
+  m.def("comm_blocks", &pgdist_rt::comm_blocks);
+  m.def("comm_region_bytes", &pgdist_rt::comm_region_bytes);
+  m.def("comm_allreduce", &pgdist_rt::comm_allreduce, "in-place fp32 sum over ranks (recordable)");
+  m.def("comm_broadcast", &pgdist_rt::comm_broadcast, "fp32 broadcast from root (recordable)");
+  m.def("comm_allreduce_f64", &pgdist_rt::comm_allreduce_f64, "RCCL fp64 all-reduce (recordable)");
+  m.def("comm_join", &pgdist_rt::comm_join, "waiter stream waits for the collectives issued so far");
+  m.def("comm_time_allreduce", &pgdist_rt::comm_time_allreduce, py::call_guard<py::gil_scoped_release>());
+  m.def("comm_error", &pgdist_rt::comm_error, py::call_guard<py::gil_scoped_release>());
+  m.def("comm_destroy", &pgdist_rt::comm_destroy, py::call_guard<py::gil_scoped_release>());
 
   // ---- native runtime (host) ----
   m.def("read_cifar10_bin", &pgdist_rt::read_cifar10_bin, py::arg("paths"), py::arg("num_threads") = 4,

@@ -171,6 +171,8 @@ class MobileNetV2Executor:
     # every host-side action of a training step goes through recordable native ops
     # (ops.kernels: launches, stream_wait, memset, plan_py): the step can be a LaunchPlan
     PLAN_SAFE = True
+    # on_params_ready issues only recordable native ops (NativeBucketReducer): called directly
+    ready_native = False
     # depthwise dgrad+wgrad fused on maps >= this size (measured on MI355X; PGDIST_DW_FUSE_MIN_H)
     DW_FUSE_MIN_H = int(os.environ.get("PGDIST_DW_FUSE_MIN_H", "56"))
     # fused 1x1 dgrad+wgrad (pw_bwd) where supported; PGDIST_PW_BWD_FUSE_MIN_M raises the M threshold
@@ -405,6 +407,11 @@ class MobileNetV2Executor:
             return
         if self.side is not None and (self.ready_probe is None or self.ready_probe(names)):
             self._flush_side()
+        if self.ready_native:
+            # native reducer: the bucket launch is a native op that waits for both streams
+            # itself; its bookkeeping runs at record time only
+            self.on_params_ready(names)
+            return
         K.plan_py(lambda: self._ready_now(names))
 
     def _ready_now(self, names):

@@ -16,7 +16,8 @@ import torch.distributed as dist
 
 from ..models import build_model
 from ..ops import kernels as K
-from ..parallel.ddp import BucketedGradReducer, broadcast_parameters
+from ..parallel.comm import NativeComm
+from ..parallel.ddp import BucketedGradReducer, NativeBucketReducer, broadcast_parameters
 from .executor import MobileNetV2Executor
 
 
@@ -36,8 +37,9 @@ def coalesce_bn_buffers(model: torch.nn.Module):
     mods = [m for m in model.modules() if isinstance(m, torch.nn.BatchNorm2d)]
     dev = mods[0].running_mean.device
     n = sum(m.running_mean.numel() + m.running_var.numel() for m in mods)
-    flat = torch.empty(n, dtype=torch.float32, device=dev)
-    nbt = torch.empty(len(mods), dtype=torch.int64, device=dev)
+    # padded (zeros) so either buffer is a whole number of 16-B vectors (P2P broadcast)
+    flat = torch.zeros((n + 63) // 64 * 64, dtype=torch.float32, device=dev)
+    nbt = torch.zeros((len(mods) + 1) // 2 * 2, dtype=torch.int64, device=dev)
     o = 0
     for i, m in enumerate(mods):
         for name in ("running_mean", "running_var"):
@@ -51,10 +53,9 @@ def coalesce_bn_buffers(model: torch.nn.Module):
     return flat, nbt
 
 
-def _dist_backend() -> str:
-    import torch.distributed as dist
+def _dist_backend(group=None) -> str:
     try:
-        return str(dist.get_backend()) if dist.is_available() and dist.is_initialized() else ""
+        return str(dist.get_backend(group)) if dist.is_available() and dist.is_initialized() else ""
     except Exception:   # no default group
         return ""
 
@@ -66,7 +67,8 @@ class NativeTrainStep:
                  first_bucket_mb: float = 1.0, reduce_dtype: torch.dtype = torch.float32,
                  double_resize: bool = True, augment: bool = True, train_augment: bool = True,
                  side_stream: bool = True, bn_broadcast: bool = False, fp8: bool = False,
-                 graph_forward: bool = False):
+                 graph_forward: bool = False, comm: Optional[str] = None, force_ddp: bool = False,
+                 allreduce_algo: Optional[str] = None):
         self.device, self.B, self.S = device, batch, img_size
         self.world, self.rank = world_size, rank
         self.exe = executor_class(model)(model, batch, img_size, device, dropout_seed=(seed * 7919) ^ rank,
@@ -86,17 +88,34 @@ class NativeTrainStep:
         self.src_labels = None
         self.epoch_ctr = 0
         # ---- data parallel
+        # PGDIST_COMM: auto (native communicator when the process group is RCCL's, c10d with gloo)
+        # | rccl | p2p (IPC xGMI kernels only; also over a gloo default group) | native (both) | c10d
         self.reducer = None
-        if world_size > 1:
+        self.comm = None
+        self.comm_mode = comm or os.environ.get("PGDIST_COMM", "auto")
+        force_ddp = force_ddp or os.environ.get("PGDIST_FORCE_DDP", "0") == "1"
+        if world_size > 1 or force_ddp:
             ranges = [(n,) + self.flat.range_of(n) for n in self.flat.order]
-            self.reducer = BucketedGradReducer(self.flat.grad, ranges, bucket_mb, first_bucket_mb, reduce_dtype)
+            backend = _dist_backend()
+            mode = self.comm_mode
+            if mode == "auto":
+                mode = "native" if (backend == "nccl" or world_size == 1) else "c10d"
+            if mode == "c10d":
+                self.reducer = BucketedGradReducer(self.flat.grad, ranges, bucket_mb, first_bucket_mb, reduce_dtype)
+            else:
+                self.comm = self._make_comm(mode, world_size)
+                algo = allreduce_algo or os.environ.get("PGDIST_AR_ALGO", "auto")
+                self.reducer = NativeBucketReducer(self.comm, self.flat.grad, ranges, bucket_mb, first_bucket_mb,
+                                                   algo=algo, bf16_wire=reduce_dtype == torch.bfloat16,
+                                                   force=force_ddp)
+                self.exe.ready_native = True
             self.exe.on_params_ready = self.reducer.mark_ready
             self.exe.ready_probe = self.reducer.would_launch
             self.sync_from_rank0()
         # reference DDP default (broadcast_buffers=True): rank 0's BN running statistics are
         # broadcast before every training forward; the buffers are coalesced into one flat
         # fp32 tensor (+ one int64 tensor of num_batches_tracked) so that is two collectives
-        self.bn_broadcast = bn_broadcast and world_size > 1
+        self.bn_broadcast = bn_broadcast and (world_size > 1 or (self.reducer is not None and self.comm is not None))
         if self.bn_broadcast:
             self.bn_flat, self.bn_nbt = coalesce_bn_buffers(self.exe.model)
             if hasattr(self.exe, "refresh_bn_fin"):
@@ -120,10 +139,24 @@ class NativeTrainStep:
         # per step replayed vs 117 ms eager); RCCL collectives are stream-ordered and replay fine.
         # PGDIST_PLAN=force: replay with gloo too (tests of the replayed data-parallel step)
         plan_env = os.environ.get("PGDIST_PLAN", "1")
-        gloo = self.world > 1 and _dist_backend() == "gloo" and plan_env != "force"
+        gloo = (isinstance(self.reducer, BucketedGradReducer) and not getattr(self.reducer, "native", False)
+                and self.reducer.enabled and _dist_backend(self.reducer.group) == "gloo" and plan_env != "force")
         self.use_plan = (not self.use_graph and not self.graph_forward and not gloo
                          and getattr(self.exe, "PLAN_SAFE", False) and plan_env in ("1", "force"))
         self.plan: Optional[K.LaunchPlan] = None
+
+    def _make_comm(self, mode: str, world_size: int) -> NativeComm:
+        """Native communicator of this data-parallel step: RCCL (modes rccl / native) and the P2P
+        xGMI path (modes p2p / native, when every rank is on this node)."""
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world_size))
+        use_p2p = mode in ("p2p", "native") and local_world == world_size and world_size <= 8
+        if mode == "p2p" and not use_p2p:
+            raise RuntimeError("PGDIST_COMM=p2p needs every rank on this node (at most 8)")
+        grad_bytes = self.flat.grad.numel() * 4
+        return NativeComm.for_process_group(self.device, use_rccl=mode in ("rccl", "native"),
+                                            p2p_bytes=grad_bytes if use_p2p else 0) \
+            if world_size > 1 else NativeComm(0, 1, self.device, use_rccl=mode in ("rccl", "native"),
+                                              p2p_bytes=grad_bytes if use_p2p else 0)
 
     # ------------------------------------------------------------------ setup
     @classmethod
@@ -163,6 +196,7 @@ class NativeTrainStep:
                                 dropout_seed=self.exe.dropout_seed, hyper=self.hyper)
         st.exe.on_params_ready = self.exe.on_params_ready
         st.exe.ready_probe = self.exe.ready_probe
+        st.exe.ready_native = getattr(self.exe, "ready_native", False)
         st.idx = torch.zeros(batch, dtype=torch.int64, device=self.device)
         st.aug_params = torch.zeros(batch, K.AUG_NPARAMS, dtype=torch.float32, device=self.device)
         st.use_graph, st.graph, st._eager_runs = False, None, 0
@@ -209,16 +243,29 @@ class NativeTrainStep:
                       double_resize=self.double_resize, seed=self.seed + 17 * self.rank, hyper=self.hyper,
                       epoch_ctr=0, out_hw=self.S)
         if self.bn_broadcast:
-            K.plan_py(lambda: broadcast_parameters([self.bn_flat, self.bn_nbt]))
+            if self.comm is not None:   # native: recorded collectives, no Python at replay
+                algo = "rccl" if self.comm.has_rccl else "oneshot"
+                cur = torch.cuda.current_stream(self.device)
+                self.comm.broadcast(self.bn_flat, 0, algo, wait=[cur])
+                self.comm.broadcast(self.bn_nbt.view(torch.float32), 0, algo, wait=[cur])
+                self.comm.join(cur)
+            else:
+                K.plan_py(lambda: broadcast_parameters([self.bn_flat, self.bn_nbt]))
         exe.forward(train=True)
 
     def _back(self):
         """Backward (+ bucketed all-reduce), Adam and metrics."""
         exe = self.exe
-        if self.reducer is not None:
+        native = getattr(self.reducer, "native", False)
+        if native:   # host bookkeeping at record time only; the collectives are native plan ops
+            self.reducer.side = exe.side
+            self.reducer.begin()
+        elif self.reducer is not None:
             K.plan_py(self.reducer.begin)
         exe.backward()
-        if self.reducer is not None:
+        if native:
+            self.reducer.finish()
+        elif self.reducer is not None:
             K.plan_py(self.reducer.finish)
         K.adam_flat(self.flat.master, self.flat.grad, self.flat.exp_avg, self.flat.exp_avg_sq,
                     self.flat.shadow, self.hyper, self.betas[0], self.betas[1], self.eps, self.wd,

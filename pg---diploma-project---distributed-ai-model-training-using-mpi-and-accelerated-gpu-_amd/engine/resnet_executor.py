@@ -85,6 +85,9 @@ class BlockPlan:
 
 
 class ResNet50Executor:
+    # on_params_ready issues only recordable native ops (NativeBucketReducer): called directly
+    ready_native = False
+
     def __init__(self, model: ResNet, batch: int, img_size: int, device: torch.device,
                  flat: Optional[FlatParams] = None, hyper: Optional[torch.Tensor] = None,
                  side_stream: bool = True, dropout_seed: int = 0, fp8: bool = False):
@@ -219,8 +222,14 @@ class ResNet50Executor:
     def mat_act_pays(cls, c: ConvSpec, B: int) -> bool:
         n = B * c.H * c.H * c.cin
         return n <= 2 * cls.MAT_ELEMS if c.k == 3 else n <= cls.MAT_ELEMS // 2
+
     def _ready(self, names):
         if self.on_params_ready is None:
+            return
+        if self.ready_native:   # native reducer: waits for the main and side streams itself
+            if self.ready_probe is None or self.ready_probe(names):
+                self._flush_side()
+            self.on_params_ready(names)
             return
         if self.side is None or (self.ready_probe is not None and not self.ready_probe(names)):
             self.on_params_ready(names)

@@ -1,0 +1,226 @@
+"""Native data-parallel communicator: RCCL and peer-to-peer xGMI collectives driven from C++
+(``csrc/runtime/comm.cpp``, ``csrc/kernels/allreduce.hip``) on a dedicated HIP stream.
+
+Reference: the NCCL collectives behind ``DistributedDataParallel`` and the explicit metric
+all-reduces (``cifar10_mpi_mobilenet_224.py:34-35,142-145,187-196,215-224``; SURVEY.md §2.4,
+§2.7 N4-N8).  There they are issued by c10d's Python-visible work objects; here every
+collective of a training step is a native launch-plan op (the replayed step contains no
+Python), ordered after its producer streams by events and joined back by the consumer.
+
+Bootstrap: the RCCL unique id and the P2P staging buffers' IPC handles travel through the
+c10d TCPStore of the default process group (whatever its backend: the gloo default group of
+a one-GPU multi-process rehearsal can bootstrap a P2P-only communicator).
+
+Algorithms (``CommAlgo``): ``rccl`` (ncclAllReduce), ``oneshot`` and ``twoshot`` (P2P
+kernels reading all peers over xGMI at once).  :meth:`NativeComm.autotune` times every
+available algorithm on the real buckets at start-up, takes the MAX over ranks (so every rank
+picks the same one) and validates the P2P result against an exact integer pattern first
+(a P2P path that times out or miscomputes is dropped on every rank).
+"""
+import itertools
+import os
+from typing import Dict, List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+from ..ops._lib import lib
+
+ALGOS = {"rccl": 0, "oneshot": 1, "twoshot": 2}
+ALGO_NAMES = {v: k for k, v in ALGOS.items()}
+_SEQ = itertools.count()
+
+
+def _stream_handle(s) -> int:
+    return s.cuda_stream if hasattr(s, "cuda_stream") else int(s)
+
+
+def _ptrs(ts) -> List[int]:
+    ts = ts if isinstance(ts, (list, tuple)) else [ts]
+    for t in ts:
+        if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()):
+            raise TypeError("native collectives take contiguous fp32 device tensors")
+    return [t.data_ptr() for t in ts]
+
+
+def host_allreduce(t: torch.Tensor, op=None) -> torch.Tensor:
+    """All-reduce of a small host tensor over the default process group (through the device
+    when the group is RCCL's)."""
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+        return t
+    op = op or dist.ReduceOp.SUM
+    if dist.get_backend() == "nccl":
+        d = t.to(torch.device("cuda", torch.cuda.current_device()))
+        dist.all_reduce(d, op=op)
+        return d.cpu()
+    dist.all_reduce(t, op=op)
+    return t
+
+
+def default_store():
+    if not (dist.is_available() and dist.is_initialized()):
+        return None
+    from torch.distributed.distributed_c10d import _get_default_store
+    return _get_default_store()
+
+
+class NativeComm:
+    """One communicator of ``world`` ranks (this process is ``rank``) on ``device``.
+
+    ``use_rccl``: create an RCCL communicator (ids through ``store``).  ``p2p_bytes`` > 0:
+    allocate an uncached staging buffer of that region size and map every peer's (all ranks
+    must be on this node).  ``nlocal == world`` builds the single-process emulation of
+    ``world`` ranks on one GPU (P2P only)."""
+
+    def __init__(self, rank: int, world: int, device: torch.device, store=None, use_rccl: bool = True,
+                 p2p_bytes: int = 0, blocks: Optional[int] = None, timeout_s: float = 20.0,
+                 emulate: bool = False, tag: Optional[str] = None):
+        self.rank, self.world, self.device = rank, world, device
+        self.emulated = emulate
+        self.nlocal = world if emulate else 1
+        blocks = blocks or int(os.environ.get("PGDIST_P2P_BLOCKS", "32"))
+        region = (int(p2p_bytes) + 255) // 256 * 256
+        tag = tag or f"pgdist/comm/{next(_SEQ)}"
+        uid = b""
+        if use_rccl and not emulate:
+            if world > 1:
+                if store is None:
+                    raise RuntimeError("NativeComm: a store is needed to exchange the RCCL unique id")
+                if rank == 0:
+                    uid = lib().comm_unique_id()
+                    store.set(tag + "/nccl_id", uid)
+                else:
+                    uid = store.get(tag + "/nccl_id")
+            else:
+                uid = lib().comm_unique_id()
+        self.has_rccl = bool(uid)
+        self.id = lib().comm_create(0 if emulate else rank, world, device.index or 0, uid, region, blocks,
+                                    self.nlocal, float(timeout_s))
+        self.region = region
+        self.blocks = blocks
+        self.has_p2p = False
+        if region > 0:
+            if emulate or world == 1:
+                self.has_p2p = True
+            else:
+                if store is None:
+                    raise RuntimeError("NativeComm: a store is needed to exchange the P2P IPC handles")
+                store.set(f"{tag}/ipc/{rank}", lib().comm_p2p_handle(self.id))
+                handles = [store.get(f"{tag}/ipc/{r}") for r in range(world)]
+                lib().comm_p2p_open(self.id, handles)
+                self.has_p2p = True
+        self.stream = torch.cuda.ExternalStream(lib().comm_stream(self.id), device=device)
+
+    # ------------------------------------------------------------------ factory
+    @classmethod
+    def for_process_group(cls, device: torch.device, use_rccl: bool = True, p2p_bytes: int = 0, **kw):
+        """Communicator over the default process group's ranks (store = its TCPStore)."""
+        world = dist.get_world_size() if dist.is_initialized() else 1
+        rank = dist.get_rank() if dist.is_initialized() else 0
+        return cls(rank, world, device, store=default_store(), use_rccl=use_rccl, p2p_bytes=p2p_bytes, **kw)
+
+    # ------------------------------------------------------------------ collectives
+    def allreduce(self, bufs, algo="rccl", bf16_wire: bool = False, wait: Sequence = ()):
+        """In-place fp32 sum of ``bufs`` (one tensor; one per emulated rank) over the ranks, on the
+        comm stream after every stream in ``wait`` (default: the current stream)."""
+        a = ALGOS[algo] if isinstance(algo, str) else int(algo)
+        ptrs = _ptrs(bufs)
+        n = (bufs[0] if isinstance(bufs, (list, tuple)) else bufs).numel()
+        ws = [_stream_handle(s) for s in (wait or [torch.cuda.current_stream(self.device)])]
+        lib().comm_allreduce(self.id, ptrs, n, a, bool(bf16_wire), ws)
+
+    def broadcast(self, bufs, root: int = 0, algo="rccl", wait: Sequence = ()):
+        a = ALGOS[algo] if isinstance(algo, str) else int(algo)
+        if a == ALGOS["twoshot"]:
+            a = ALGOS["oneshot"]   # the P2P broadcast has one form
+        ptrs = _ptrs(bufs)
+        n = (bufs[0] if isinstance(bufs, (list, tuple)) else bufs).numel()
+        ws = [_stream_handle(s) for s in (wait or [torch.cuda.current_stream(self.device)])]
+        lib().comm_broadcast(self.id, ptrs, n, int(root), a, ws)
+
+    def allreduce_f64(self, t: torch.Tensor, op: str = "sum", wait: Sequence = ()):
+        assert t.is_cuda and t.dtype == torch.float64 and t.is_contiguous()
+        ws = [_stream_handle(s) for s in (wait or [torch.cuda.current_stream(self.device)])]
+        lib().comm_allreduce_f64(self.id, t.data_ptr(), t.numel(), 0 if op == "sum" else 2, ws)
+
+    def join(self, stream=None):
+        """``stream`` (default: current) waits for every collective issued so far."""
+        s = stream or torch.cuda.current_stream(self.device)
+        lib().comm_join(self.id, _stream_handle(s))
+
+    def time_allreduce(self, bufs, algo, bf16_wire=False, iters=20) -> float:
+        """Microseconds per all-reduce of ``bufs`` back to back on the comm stream (collective:
+        every rank must call it with the same arguments)."""
+        a = ALGOS[algo] if isinstance(algo, str) else int(algo)
+        n = (bufs[0] if isinstance(bufs, (list, tuple)) else bufs).numel()
+        return lib().comm_time_allreduce(self.id, _ptrs(bufs), n, a, bool(bf16_wire), int(iters))
+
+    def error(self) -> int:
+        """0, or P2P barrier-timeout bits | RCCL async error << 8 (synchronises the comm stream)."""
+        return lib().comm_error(self.id)
+
+    def check(self):
+        e = self.error()
+        if e:
+            raise RuntimeError(f"native communicator error 0x{e:x} (P2P barrier timeout bits | RCCL error << 8)")
+
+    def close(self):
+        if self.id is not None:
+            lib().comm_destroy(self.id)
+            self.id = None
+
+    # ------------------------------------------------------------------ algorithm choice
+    def available_algos(self) -> List[str]:
+        out = []
+        if self.has_rccl:
+            out.append("rccl")
+        if self.has_p2p:
+            out += ["oneshot", "twoshot"]
+        return out
+
+    def validate_p2p(self) -> bool:
+        """Exact-integer P2P all-reduce check (every rank contributes rank+1+i%7): True on every
+        rank iff it succeeded on every rank (agreement through the default process group)."""
+        if not self.has_p2p or self.emulated:
+            return self.has_p2p
+        n = 1 << 16
+        ok = 1.0
+        try:
+            base = torch.arange(n, device=self.device, dtype=torch.float32).remainder_(7)
+            expect = base * self.world + self.world * (self.world + 1) / 2
+            for algo in ("oneshot", "twoshot"):
+                for bf in (False, True):
+                    t = base + (self.rank + 1)
+                    self.allreduce(t, algo, bf)
+                    self.join()
+                    torch.cuda.synchronize(self.device)
+                    if self.error() or not torch.equal(t, expect):
+                        ok = 0.0
+        except Exception:
+            ok = 0.0
+        if self.world > 1:
+            ok = host_allreduce(torch.tensor([ok], dtype=torch.float64), dist.ReduceOp.MIN).item()
+        self.has_p2p = ok > 0
+        return self.has_p2p
+
+    def autotune(self, sizes: Sequence[int], candidates: Optional[Sequence[str]] = None, bf16_wire=False,
+                 iters: int = 10) -> Dict[int, str]:
+        """Fastest algorithm per all-reduce size (elements), by the MAX over ranks of the measured
+        time, identical on every rank."""
+        cands = [c for c in (candidates or self.available_algos()) if c in self.available_algos()]
+        if bf16_wire:
+            cands = [c for c in cands if c != "rccl"]
+        if not cands:
+            raise RuntimeError("autotune: no algorithm available")
+        if len(cands) == 1:
+            return {int(s): cands[0] for s in sizes}
+        uniq = sorted({int(s) for s in sizes})
+        scratch = torch.zeros(max(uniq), dtype=torch.float32, device=self.device)
+        times = torch.zeros(len(uniq), len(cands), dtype=torch.float64)
+        for i, s in enumerate(uniq):
+            for j, c in enumerate(cands):
+                times[i, j] = self.time_allreduce(scratch[:s], c, bf16_wire, iters)
+        if self.world > 1 and not self.emulated:
+            times = host_allreduce(times, dist.ReduceOp.MAX)
+        self.tuning = {s: {c: float(times[i, j]) for j, c in enumerate(cands)} for i, s in enumerate(uniq)}
+        return {s: cands[int(times[i].argmin())] for i, s in enumerate(uniq)}

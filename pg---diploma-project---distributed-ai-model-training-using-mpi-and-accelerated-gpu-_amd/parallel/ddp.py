@@ -148,6 +148,67 @@ class BucketedGradReducer:
         self._works = []
 
 
+class NativeBucketReducer(BucketedGradReducer):
+    """The same bucket schedule as :class:`BucketedGradReducer`, issued through a
+    :class:`~pgdist.parallel.comm.NativeComm`: every bucket launch is a native op (the comm
+    stream waits for the current stream and the executor's side stream, then RCCL or a P2P
+    xGMI kernel reduces the bucket in place) and ``finish`` makes the current stream wait for
+    the comm stream.  Nothing here needs Python at replay time: the bookkeeping runs once while
+    a launch plan records the step, and the recorded ops are the whole data-parallel part of
+    every replayed step (``native = True`` tells the executor to call the hooks directly
+    instead of wrapping them in ``plan_py``).
+
+    ``algo``: ``rccl`` | ``oneshot`` | ``twoshot`` | ``auto`` (per bucket: validated P2P
+    kernels and RCCL timed on this node at construction, fastest on the slowest rank)."""
+    native = True
+
+    def __init__(self, comm, flat_grad: torch.Tensor, ranges: Sequence[Tuple[str, int, int]],
+                 bucket_cap_mb: Optional[float] = None, first_bucket_mb: float = 1.0, algo: str = "auto",
+                 bf16_wire: bool = False, force: bool = False):
+        super().__init__(flat_grad, ranges, bucket_cap_mb, first_bucket_mb)
+        self.comm = comm
+        self.world = comm.world
+        self.force = force   # run the bucket collectives even at world size 1 (tests)
+        self.side = None     # the executor's side stream (weight-gradient producers)
+        self.bf16_wire = bf16_wire
+        # P2P kernels take multiples of 8 elements: bucket ends move to the next 64-element
+        # boundary (flat-buffer alignment padding, zero on every rank), the last to the end
+        n = flat_grad.numel()
+        b2 = []
+        for i, (s, e, names) in enumerate(self.buckets):
+            e = n if i == len(self.buckets) - 1 else min(n, (e + 63) // 64 * 64)
+            b2.append((s, e, names))
+        self.buckets = b2
+        sizes = [e - s for s, e, _ in self.buckets]
+        if algo == "auto":
+            if comm.has_p2p and comm.world > 1 and not comm.validate_p2p():
+                print("[pgdist] P2P all-reduce failed validation: RCCL only", flush=True)
+            choice = comm.autotune(sizes, bf16_wire=bf16_wire) if comm.world > 1 else {}
+            self.algos = [choice.get(sz, "rccl" if comm.has_rccl else "oneshot") for sz in sizes]
+        else:
+            self.algos = [algo] * len(sizes)
+        if bf16_wire and "rccl" in self.algos:
+            raise ValueError("bf16 wire format: P2P algorithms only")
+
+    @property
+    def enabled(self) -> bool:
+        return self.world > 1 or self.force
+
+    def _launch(self, bi: int):
+        s, e, _ = self.buckets[bi]
+        cur = torch.cuda.current_stream(self.grad.device)
+        wait = [cur] if self.side is None or self.side.cuda_stream == cur.cuda_stream else [cur, self.side]
+        self.comm.allreduce(self.grad[s:e], self.algos[bi], self.bf16_wire, wait=wait)
+
+    def finish(self):
+        if not self.enabled:
+            return
+        while self._next < len(self.buckets):
+            self._launch(self._next)
+            self._next += 1
+        self.comm.join(torch.cuda.current_stream(self.grad.device))
+
+
 def broadcast_parameters(tensors: Sequence[torch.Tensor], src: int = 0, group=None):
     """Rank-0 broadcast of parameters/buffers (reference DDP ctor)."""
     if not (dist.is_initialized() and dist.get_world_size(group) > 1):

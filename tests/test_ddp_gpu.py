@@ -1,10 +1,13 @@
-"""Native data-parallel step on the GPU with 2 ranks sharing one MI355X.
+"""Native data-parallel step on the GPU with 2 ranks sharing one MI355X, and the native
+communicator at world size 1.
 
-RCCL needs one GPU per rank, so on the single-GPU test box the collective
-backend is gloo (device tensors staged through the host); the code path under
-test — rank-0 broadcast, backward-completion bucketing, overlapped async
-all-reduce, 1/world folded into the fused Adam — is the one RCCL drives on a
-multi-GPU node (bench.py / train.py with backend nccl).
+RCCL refuses two ranks on one GPU, so the 2-rank tests run the default process group on gloo
+and the gradient buckets either through c10d (``PGDIST_COMM=c10d``: host-staged gloo
+collectives) or through the native communicator's P2P xGMI kernels between the two processes
+(``PGDIST_COMM=p2p``: IPC-mapped staging, collectives recorded into the replayed launch plan
+— the production data-parallel step minus RCCL).  RCCL itself is exercised at world size 1
+with the reducer forced on: every bucket is a recorded ncclAllReduce on the comm stream, and
+the weights after 6 replayed steps must be bitwise equal to the plain single-GPU step.
 """
 import os
 
@@ -17,8 +20,9 @@ from mp_util import free_port as _free_port, run_ranks as _run_ranks
 pytestmark = pytest.mark.gpu
 
 
-def _worker(rank, world, port, model_name, q):
+def _worker(rank, world, port, model_name, comm, q):
     os.environ["PGDIST_PLAN"] = "force"   # the replayed (launch-plan) step, as with RCCL
+    os.environ["PGDIST_COMM"] = comm
     import pgdist  # noqa: F401
     from pgdist.models import build_model
     from pgdist.engine.native_step import NativeTrainStep
@@ -42,23 +46,30 @@ def _worker(rank, world, port, model_name, q):
     dist.all_gather(allw, w)
     diff = max((a - w).abs().max().item() for a in allw)
     l, c, n = st.read_metrics()
-    q.put(("ok", rank, diff, n, len(st.reducer.buckets), bool(torch.isfinite(w).all())))
+    native = getattr(st.reducer, "native", False)
+    err = st.comm.error() if st.comm is not None else 0
+    q.put(("ok", rank, diff, n, len(st.reducer.buckets), bool(torch.isfinite(w).all()), native, err))
+    dist.barrier()
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("comm", ["c10d", "p2p"])
 @pytest.mark.parametrize("model_name", ["mobilenet_v2", "resnet50"])
-def test_native_ddp_two_ranks_one_gpu(model_name):
+def test_native_ddp_two_ranks_one_gpu(model_name, comm):
     """4 data-parallel steps, launch-plan replay forced (MobileNetV2): replicas stay identical."""
     world, port = 2, _free_port()
-    res = _run_ranks(_worker, world, (world, port, model_name), expect=world)
-    for _, rank, diff, n, nb, finite in res:
+    res = _run_ranks(_worker, world, (world, port, model_name, comm), expect=world)
+    for _, rank, diff, n, nb, finite, native, err in res:
+        assert native == (comm == "p2p")
+        assert err == 0
         assert finite
         assert diff == 0.0, f"replicas diverged on rank {rank}: {diff}"
         assert n == 32
         assert nb >= 3
 
 
-def _grad_worker(rank, world, port, q):
+def _grad_worker(rank, world, port, comm, q):
+    os.environ["PGDIST_COMM"] = comm
     import pgdist  # noqa: F401
     from pgdist.models import build_model
     from pgdist.engine.native_step import NativeTrainStep
@@ -106,24 +117,26 @@ def _grad_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_native_ddp_reduced_gradient_equals_sum_of_shards():
+@pytest.mark.parametrize("comm", ["c10d", "p2p"])
+def test_native_ddp_reduced_gradient_equals_sum_of_shards(comm):
     """After one data-parallel step the flat gradient buffer holds the SUM of the per-shard
     gradients (the 1/world is folded into Adam): checks the bucket launches are ordered after
     every producer of their gradients (main-stream dgrad-side BN grads and side-stream wgrads)."""
     world, port = 2, _free_port()
-    (_, per), = _run_ranks(_grad_worker, world, (world, port), expect=1)
+    (_, per), = _run_ranks(_grad_worker, world, (world, port, comm), expect=1)
     assert len(per) >= 3
     for bi, first, last, scale, err in per:
         assert scale > 0, f"bucket {bi} ({first} .. {last}) has an all-zero gradient"
         assert err < 1e-5, f"bucket {bi} ({first} .. {last}): rel err {err}"
 
 
-def _lazy_bn_grad_worker(rank, world, port, q):
+def _lazy_bn_grad_worker(rank, world, port, comm, q):
     """Lazy BN finalize (default mode) under data parallelism: the BN weight / bias gradients
     are written by the side-stream batched finalizes, and every gradient bucket holding them
     must be all-reduced only after those ran.  After one step each rank recomputes its LOCAL
     dgamma / dbeta from the backward accumulators (still intact until the next forward) and
     all-reduces them itself: the reducer's buckets must hold exactly that sum."""
+    os.environ["PGDIST_COMM"] = comm
     import pgdist  # noqa: F401
     from pgdist.models import build_model
     from pgdist.engine.native_step import NativeTrainStep
@@ -159,9 +172,52 @@ def _lazy_bn_grad_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_native_ddp_lazy_bn_gradients_reduced_after_side_finalize():
+@pytest.mark.parametrize("comm", ["c10d", "p2p"])
+def test_native_ddp_lazy_bn_gradients_reduced_after_side_finalize(comm):
     world, port = 2, _free_port()
-    res = _run_ranks(_lazy_bn_grad_worker, world, (world, port), expect=world)
+    res = _run_ranks(_lazy_bn_grad_worker, world, (world, port, comm), expect=world)
     for _, rank, err, scale in res:
         assert scale > 0
         assert err < 1e-6, f"rank {rank}: BN gradients in the buckets differ from the summed local ones ({err})"
+
+
+@pytest.mark.parametrize("comm,model_name", [("rccl", "mobilenet_v2"), ("p2p", "mobilenet_v2"), ("rccl", "resnet50")])
+def test_native_reducer_world1_bitwise_equals_plain_step(dev, comm, model_name):
+    """RCCL (or the P2P kernels) at world size 1 with the reducer forced on: buckets, comm
+    stream, event ordering and (MobileNetV2) the recorded launch plan replayed for steps 4-6.
+    In deterministic mode the weights, BN buffers and metrics after 6 steps are bitwise equal
+    to the plain single-GPU step's."""
+    from pgdist.models import build_model
+    from pgdist.engine.native_step import NativeTrainStep
+    from pgdist.ops import kernels as K
+    K.set_deterministic(True)
+    try:
+        g = torch.Generator(device=dev).manual_seed(7)
+        src = torch.randint(0, 256, (64, 32, 32, 3), dtype=torch.uint8, device=dev, generator=g)
+        labels = torch.randint(0, 10, (64,), device=dev, generator=g)
+
+        def run(force):
+            torch.manual_seed(100)
+            st = NativeTrainStep(build_model(model_name, num_classes=10), 8, dev, img_size=64, lr=1e-3,
+                                 force_ddp=force, comm=comm if force else None, bucket_mb=0.5,
+                                 first_bucket_mb=0.1, use_graph=False)
+            st.set_data(src, labels)
+            for i in range(6):
+                st.run(torch.arange(8, device=dev) + 8 * i)
+            torch.cuda.synchronize()
+            return st
+
+        plain, ddp = run(False), run(True)
+        assert plain.reducer is None
+        assert ddp.reducer is not None and ddp.reducer.native and len(ddp.reducer.buckets) >= 3
+        assert ddp.comm.error() == 0
+        if model_name == "mobilenet_v2":
+            assert ddp.use_plan and ddp.plan is not None and len(ddp.plan) > 0
+        assert torch.equal(plain.flat.master, ddp.flat.master)
+        bn = lambda st: [b for m in st.exe.model.modules() if isinstance(m, torch.nn.BatchNorm2d)   # noqa: E731
+                         for b in (m.running_mean, m.running_var)]
+        for a, b in zip(bn(plain), bn(ddp)):
+            assert torch.equal(a, b)
+        assert plain.read_metrics() == ddp.read_metrics()
+    finally:
+        K.set_deterministic(False)
