@@ -117,7 +117,7 @@ def main():
                        "per_gpu_batch": args.batch_size, "seq_len": None, "img_size": args.img_size,
                        "parallelism": f"dp{world}", "backend": meta.get("backend"),
                        "hip_graph": meta.get("graph"), "side_stream": meta.get("side_stream"),
-                       "fp8": bool(args.fp8)},
+                       "fp8": bool(args.fp8), "allreduce": meta.get("allreduce")},
         }
         print(json.dumps(out), flush=True)
     cleanup()

@@ -76,7 +76,10 @@ PRESETS = {
     "gpu128": dict(device="cuda", batch_size=128, save_path="best_mobilenetv2_cifar10_224.pth",
                    log_format="serial", seed=None),
     # cifar10_mpi_mobilenet_224.py
-    "mpi": dict(batch_size=128, save_path="best_mobilenetv2_cifar10_224_mpi.pth", log_format="ddp", seed=42),
+    # (bn_sync="broadcast": the reference DDP's broadcast_buffers=True, rank 0's BN running statistics
+    #  sent before every training forward; --bn-sync eval is the faster option: sync before eval/save)
+    "mpi": dict(batch_size=128, save_path="best_mobilenetv2_cifar10_224_mpi.pth", log_format="ddp", seed=42,
+                bn_sync="broadcast"),
     # BASELINE.json config 5: MobileNetV2 fp8 (e4m3 forward GEMMs), bs 512 per GPU, DDP
     "mpi_fp8": dict(batch_size=512, precision="fp8", backend="hip",
                     save_path="best_mobilenetv2_cifar10_224_mpi_fp8.pth", log_format="ddp", seed=42),

@@ -452,6 +452,7 @@ PYBIND11_MODULE(_pgdist_C, m) {
   m.def("comm_p2p_ready", &pgdist_rt::comm_p2p_ready);
   m.def("comm_stream", &pgdist_rt::comm_stream);
   m.def("comm_blocks", &pgdist_rt::comm_blocks);
+  m.def("comm_set_timeout", &pgdist_rt::comm_set_timeout);
   m.def("comm_region_bytes", &pgdist_rt::comm_region_bytes);
   m.def("comm_allreduce", &pgdist_rt::comm_allreduce, "in-place fp32 sum over ranks (recordable)");
   m.def("comm_broadcast", &pgdist_rt::comm_broadcast, "fp32 broadcast from root (recordable)");

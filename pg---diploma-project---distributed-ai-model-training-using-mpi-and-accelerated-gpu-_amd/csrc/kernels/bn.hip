@@ -256,6 +256,11 @@ const BnFin *take_bn_lz() {
   g_bn_lz = nullptr;
   return d;
 }
+// error recovery (plan.cpp): no descriptor stays armed for an unrelated later launch
+void bn_disarm() {
+  g_bn_fin = nullptr;
+  g_bn_lz = nullptr;
+}
 void launch_bn_finalize_batch(const void *tab, int n, int maxC, hipStream_t st) {
   if (n <= 0) return;
   hipLaunchKernelGGL(bn_finalize_batch_kernel, dim3((maxC + 127) / 128, n), dim3(128), 0, st,

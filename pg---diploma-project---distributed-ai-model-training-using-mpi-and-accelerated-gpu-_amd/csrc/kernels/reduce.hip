@@ -187,6 +187,11 @@ std::vector<PendingRed> g_red_pending;
 
 void wgrad_reduce_defer(bool on) { g_red_defer = on; }
 bool wgrad_reduce_deferring() { return g_red_defer; }
+// error recovery (plan.cpp): stop deferring and drop reductions recorded but not launched
+void wgrad_reduce_reset() {
+  g_red_defer = false;
+  g_red_pending.clear();
+}
 
 static void red_geom(int S, long long n, int target, int V, int &nb, int &rch, int &nch) {
   const long long nbl = (n + 16 * V - 1) / (16 * V);

@@ -271,6 +271,10 @@ void comm_p2p_open(int id, const std::vector<std::string> &handles) {
 bool comm_p2p_ready(int id) { return get(id).p2p; }
 uintptr_t comm_stream(int id) { return reinterpret_cast<uintptr_t>(get(id).stream); }
 int comm_blocks(int id) { return get(id).blocks; }
+void comm_set_timeout(int id, double seconds) {
+  if (!(seconds > 0)) throw std::invalid_argument("comm_set_timeout: seconds > 0");
+  get(id).timeout_ticks = (long long)(seconds * 1e8);
+}
 long long comm_region_bytes(int id) { return get(id).region; }
 
 void comm_allreduce(int id, const std::vector<uintptr_t> &bufs, long long n, int algo, bool bf16_wire,

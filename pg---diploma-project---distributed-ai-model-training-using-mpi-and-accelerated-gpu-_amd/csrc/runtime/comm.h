@@ -41,6 +41,7 @@ void comm_p2p_open(int id, const std::vector<std::string> &handles);  // every r
 bool comm_p2p_ready(int id);
 uintptr_t comm_stream(int id);
 int comm_blocks(int id);
+void comm_set_timeout(int id, double seconds);   // P2P barrier give-up for collectives issued afterwards
 long long comm_region_bytes(int id);
 
 // in-place sum over ranks of n fp32 elements at bufs[local rank]; the comm stream first waits

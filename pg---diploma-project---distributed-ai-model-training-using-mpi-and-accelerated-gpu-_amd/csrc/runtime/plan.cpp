@@ -9,11 +9,16 @@
 #include <string>
 #include <vector>
 
+int bn_rep();               // kernels/bn.hip: BN-statistics replica rows the producers use
+void bn_disarm();
+void wgrad_reduce_reset();  // kernels/reduce.hip
+
 namespace pgdist_rt {
 namespace {
 
 struct Plan {
   std::vector<PlanOp> ops;
+  int bn_rep = 0;   // the replica rows the recorded launches' BN accumulators were sized for
 };
 
 // heap-allocated and never destroyed: a plan may hold Python callbacks, which must not be
@@ -58,6 +63,7 @@ hipEvent_t ring_event() {
 void plan_record_begin() {
   if (g_rec) throw std::runtime_error("plan_record_begin: a recording is already open");
   g_rec = new Plan();
+  g_rec->bn_rep = bn_rep();
 }
 
 int plan_record_end() {
@@ -84,7 +90,23 @@ void plan_replay(int id) {
   auto it = plans().find(id);
   if (it == plans().end()) throw std::out_of_range("plan_replay: unknown plan " + std::to_string(id));
   if (g_rec) throw std::runtime_error("plan_replay: not allowed while recording");
-  for (auto &op : it->second.ops) op();
+  // the recorded producers read the host's replica-row count at launch: replaying after a BN
+  // mode switch would write rows past the accumulators sized at record time
+  if (it->second.bn_rep != bn_rep())
+    throw std::runtime_error("plan_replay: the BN statistics mode changed since this plan was recorded "
+                             "(set_deterministic before building the step); re-record it");
+  (void)hipGetLastError();
+  try {
+    for (auto &op : it->second.ops) op();
+  } catch (...) {
+    // a failed op (e.g. a Python callback raising) must not leave host launch state behind:
+    // deferred weight-gradient reductions or an armed BN descriptor would leak into later launches
+    wgrad_reduce_reset();
+    bn_disarm();
+    throw;
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("plan_replay: launch failed: ") + hipGetErrorString(e));
 }
 
 void plan_free(int id) { plans().erase(id); }

@@ -30,8 +30,20 @@ def build_bench_step(model_name: str, batch_size: int, device: torch.device, bac
                                              use_graph=int(use_graph) == 1, world_size=world_size, rank=rank,
                                              side_stream=side_stream, fp8=fp8, graph_forward=int(use_graph) == 2)
         graph = "forward" if step.graph_forward else step.graph_enabled
-        return step.bench_step, {"backend": "hip", "graph": graph, "side_stream": side_stream,
-                                 "fp8": fp8}
+        meta = {"backend": "hip", "graph": graph, "side_stream": side_stream, "fp8": fp8}
+        red = step.reducer
+        if red is not None:
+            meta["allreduce"] = {
+                "comm": "native" if getattr(red, "native", False) else "c10d",
+                "buckets_kib": [round((e - s) * 4 / 1024, 1) for s, e, _ in red.buckets],
+                "algos": list(getattr(red, "algos", ["c10d"] * len(red.buckets))),
+                "launch_plan": bool(step.use_plan),
+            }
+            tuning = getattr(step.comm, "tuning", None) if step.comm is not None else None
+            if tuning:
+                meta["allreduce"]["tuned_us"] = {str(k): {a: round(v, 1) for a, v in d.items()}
+                                                 for k, d in tuning.items()}
+        return step.bench_step, meta
     if fp8:
         raise NotImplementedError("fp8 runs on the native (hip) backend")
     return _torch_bench_step(model_name, batch_size, device, img_size, world_size, rank)

@@ -82,6 +82,8 @@ class Trainer:
 
         # ---- data (rank 0 first, then everyone: the reference's download barrier, :93-113)
         if self.rank == 0:
+            if self.ddp_log and cfg.data == "cifar10":
+                L.emit(L.download_line(), self.rank)
             self.train_data = load_dataset(cfg.data, cfg.data_root, True, cfg.synthetic_train_size)
         barrier(self.device if self.device.type == "cuda" else None)
         if self.rank != 0:

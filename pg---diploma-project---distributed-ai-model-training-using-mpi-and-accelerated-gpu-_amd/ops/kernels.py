@@ -25,8 +25,20 @@ def _s() -> int:
     return torch.cuda.current_stream().cuda_stream
 
 
+MAX_KERNEL_BYTES = 1 << 31
+
+
 def _p(t: Optional[torch.Tensor]) -> int:
-    return 0 if t is None else t.data_ptr()
+    """Device address of a kernel operand.  The kernels address operands through raw buffer
+    descriptors with 32-bit byte offsets and mask lanes with the offset 0x80000000
+    (common.h kOOB), so every operand must stay below 2 GiB: a larger one would let masked
+    lanes read / write real data."""
+    if t is None:
+        return 0
+    if t.numel() * t.element_size() >= MAX_KERNEL_BYTES:
+        raise ValueError(f"kernel operand of {t.numel() * t.element_size()} bytes: the HIP kernels take "
+                         "operands below 2 GiB (32-bit buffer offsets); reduce the batch size")
+    return t.data_ptr()
 
 
 def _chk(t: Optional[torch.Tensor], dtype, numel=None, name="tensor"):

@@ -73,12 +73,13 @@ class NativeComm:
     ``world`` ranks on one GPU (P2P only)."""
 
     def __init__(self, rank: int, world: int, device: torch.device, store=None, use_rccl: bool = True,
-                 p2p_bytes: int = 0, blocks: Optional[int] = None, timeout_s: float = 20.0,
+                 p2p_bytes: int = 0, blocks: Optional[int] = None, timeout_s: Optional[float] = None,
                  emulate: bool = False, tag: Optional[str] = None):
         self.rank, self.world, self.device = rank, world, device
         self.emulated = emulate
         self.nlocal = world if emulate else 1
         blocks = blocks or int(os.environ.get("PGDIST_P2P_BLOCKS", "32"))
+        timeout_s = timeout_s or float(os.environ.get("PGDIST_P2P_TIMEOUT", "60"))
         region = (int(p2p_bytes) + 255) // 256 * 256
         tag = tag or f"pgdist/comm/{next(_SEQ)}"
         uid = b""
@@ -98,17 +99,29 @@ class NativeComm:
                                     self.nlocal, float(timeout_s))
         self.region = region
         self.blocks = blocks
+        self.timeout_s = float(timeout_s)
         self.has_p2p = False
+        self.p2p_error = None
         if region > 0:
             if emulate or world == 1:
                 self.has_p2p = True
             else:
                 if store is None:
                     raise RuntimeError("NativeComm: a store is needed to exchange the P2P IPC handles")
-                store.set(f"{tag}/ipc/{rank}", lib().comm_p2p_handle(self.id))
+                try:
+                    h = lib().comm_p2p_handle(self.id)
+                except Exception as e:   # noqa: BLE001 - this rank publishes an empty handle
+                    h, self.p2p_error = b"", repr(e)
+                store.set(f"{tag}/ipc/{rank}", h)
                 handles = [store.get(f"{tag}/ipc/{r}") for r in range(world)]
-                lib().comm_p2p_open(self.id, handles)
-                self.has_p2p = True
+                if self.p2p_error is None and all(handles):
+                    try:
+                        lib().comm_p2p_open(self.id, handles)
+                        self.has_p2p = True
+                    except Exception as e:   # noqa: BLE001 - agreed on in validate_p2p
+                        self.p2p_error = repr(e)
+                elif self.p2p_error is None:
+                    self.p2p_error = "a peer could not export its staging buffer"
         self.stream = torch.cuda.ExternalStream(lib().comm_stream(self.id), device=device)
 
     # ------------------------------------------------------------------ factory
@@ -178,30 +191,52 @@ class NativeComm:
             out += ["oneshot", "twoshot"]
         return out
 
-    def validate_p2p(self) -> bool:
-        """Exact-integer P2P all-reduce check (every rank contributes rank+1+i%7): True on every
-        rank iff it succeeded on every rank (agreement through the default process group)."""
-        if not self.has_p2p or self.emulated:
+    def set_timeout(self, seconds: float):
+        """P2P barrier give-up (seconds) for collectives issued from now on."""
+        lib().comm_set_timeout(self.id, float(seconds))
+        self.timeout_s = float(seconds)
+
+    def _agree(self, ok: bool) -> bool:
+        if self.world == 1 or self.emulated:
+            return ok
+        return host_allreduce(torch.tensor([1.0 if ok else 0.0], dtype=torch.float64),
+                              dist.ReduceOp.MIN).item() > 0
+
+    def validate_p2p(self, timeout_s: float = 5.0) -> bool:
+        """Exact-integer P2P all-reduce check (every rank contributes rank+1+i%7, one-shot and
+        two-shot, fp32 and bf16 wire): True on every rank iff the staging was mapped and every
+        call succeeded on every rank.  Agreement (default process group) before the first
+        kernel and after each call, so a rank whose setup failed or a broken call costs at most
+        one barrier timeout (shortened to ``timeout_s`` meanwhile), never a hang or a mismatch."""
+        if self.emulated:
             return self.has_p2p
+        if not self._agree(self.has_p2p and self.p2p_error is None):
+            self.has_p2p = False
+            return False
         n = 1 << 16
-        ok = 1.0
+        keep = self.timeout_s
+        self.set_timeout(timeout_s)
         try:
             base = torch.arange(n, device=self.device, dtype=torch.float32).remainder_(7)
             expect = base * self.world + self.world * (self.world + 1) / 2
             for algo in ("oneshot", "twoshot"):
                 for bf in (False, True):
-                    t = base + (self.rank + 1)
-                    self.allreduce(t, algo, bf)
-                    self.join()
-                    torch.cuda.synchronize(self.device)
-                    if self.error() or not torch.equal(t, expect):
-                        ok = 0.0
-        except Exception:
-            ok = 0.0
-        if self.world > 1:
-            ok = host_allreduce(torch.tensor([ok], dtype=torch.float64), dist.ReduceOp.MIN).item()
-        self.has_p2p = ok > 0
-        return self.has_p2p
+                    ok = True
+                    try:
+                        t = base + (self.rank + 1)
+                        self.allreduce(t, algo, bf)
+                        self.join()
+                        torch.cuda.synchronize(self.device)
+                        ok = self.error() == 0 and torch.equal(t, expect)
+                    except Exception as e:   # noqa: BLE001 - reported, then P2P is off everywhere
+                        self.p2p_error = repr(e)
+                        ok = False
+                    if not self._agree(ok):
+                        self.has_p2p = False
+                        return False
+        finally:
+            self.set_timeout(keep)
+        return True
 
     def autotune(self, sizes: Sequence[int], candidates: Optional[Sequence[str]] = None, bf16_wire=False,
                  iters: int = 10) -> Dict[int, str]:

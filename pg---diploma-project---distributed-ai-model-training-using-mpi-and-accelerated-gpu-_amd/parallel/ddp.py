@@ -181,8 +181,9 @@ class NativeBucketReducer(BucketedGradReducer):
         self.buckets = b2
         sizes = [e - s for s, e, _ in self.buckets]
         if algo == "auto":
-            if comm.has_p2p and comm.world > 1 and not comm.validate_p2p():
-                print("[pgdist] P2P all-reduce failed validation: RCCL only", flush=True)
+            if comm.region > 0 and comm.world > 1 and not comm.validate_p2p():
+                print(f"[pgdist] P2P all-reduce unavailable or failed validation ({comm.p2p_error}): RCCL only",
+                      flush=True)
             choice = comm.autotune(sizes, bf16_wire=bf16_wire) if comm.world > 1 else {}
             self.algos = [choice.get(sz, "rccl" if comm.has_rccl else "oneshot") for sz in sizes]
         else:

@@ -17,6 +17,10 @@ def device_line(device) -> str:                                    # cifar10_ser
     return f"Device: {getattr(device, 'type', device)}"
 
 
+def download_line() -> str:                                        # cifar10_mpi_mobilenet_224.py:94
+    return "Downloading CIFAR-10 (if not present)..."
+
+
 def samples_lines(n_train: int, n_test: int):                      # :65-66
     return [f"Train samples: {n_train}", f"Test samples: {n_test}"]
 

@@ -245,3 +245,61 @@ def test_graph_modes_match_eager(dev, mode, deterministic):
             assert st.fwd_graph is not None
     assert torch.allclose(out["eager"][0], out[mode][0], rtol=0, atol=1e-6)
     assert abs(out["eager"][1][0] - out[mode][1][0]) < 1e-4 * max(1.0, abs(out["eager"][1][0]))
+
+
+def test_launch_plan_matches_eager_lazy_mode(dev, monkeypatch):
+    """Default mode (lazy BN finalize, atomic statistics, batched side-stream finalizes, deferred
+    multi-segment wgrad reductions): 6 steps replayed from the plan (recorded on the 3rd) vs 6
+    eager steps.  Float atomics make eager runs differ from each other by a noise floor; the
+    plan must stay within a small multiple of it (a wiring difference would be of the size of
+    the weight update itself)."""
+    from pgdist.engine.native_step import NativeTrainStep
+    src = torch.randint(0, 256, (16, 32, 32, 3), dtype=torch.uint8, device=dev,
+                        generator=torch.Generator(device=dev).manual_seed(3))
+    labels = torch.arange(16, device=dev) % 10
+    out = {}
+    for tag, plan in (("plan", "1"), ("eager", "0"), ("eager2", "0")):
+        monkeypatch.setenv("PGDIST_PLAN", plan)
+        torch.manual_seed(0)
+        st = NativeTrainStep(mobilenet_v2(10), 8, dev, img_size=64, lr=1e-3, use_graph=False)
+        assert st.exe.bn_mode == "lazy"
+        assert st.use_plan == (plan == "1")
+        w0 = st.flat.master.clone()
+        st.set_data(src, labels)
+        for i in range(6):
+            st.run((torch.arange(8, device=dev) + 3 * i) % 16)
+        torch.cuda.synchronize()
+        if plan == "1":
+            assert st.plan is not None and len(st.plan) > 200
+        out[tag] = (st.flat.master.clone(), st.read_metrics())
+    upd = (out["eager"][0] - w0).norm().item()
+    noise = (out["eager2"][0] - out["eager"][0]).norm().item()
+    diff = (out["plan"][0] - out["eager"][0]).norm().item()
+    assert upd > 0
+    assert diff <= 10 * noise + 1e-3 * upd, f"plan vs eager {diff:.3e}, eager noise {noise:.3e}, update {upd:.3e}"
+    lnoise = abs(out["eager2"][1][0] - out["eager"][1][0])
+    assert abs(out["plan"][1][0] - out["eager"][1][0]) <= 10 * lnoise + 1e-3 * abs(out["eager"][1][0])
+
+
+def test_bn_mode_switch_after_plan_recorded_rejected(dev, monkeypatch):
+    """A recorded plan's producers were sized for the BN replica rows at record time: replaying
+    it after set_deterministic() must fail loudly (it would overrun the accumulators)."""
+    from pgdist.ops import kernels as K
+    from pgdist.engine.native_step import NativeTrainStep
+    monkeypatch.setenv("PGDIST_PLAN", "1")
+    src = torch.randint(0, 256, (16, 32, 32, 3), dtype=torch.uint8, device=dev)
+    labels = torch.arange(16, device=dev) % 10
+    st = NativeTrainStep(mobilenet_v2(10), 8, dev, img_size=64, lr=1e-3, use_graph=False)
+    st.set_data(src, labels)
+    for i in range(3):
+        st.run(torch.arange(8, device=dev))
+    assert st.plan is not None
+    K.set_deterministic(True)
+    try:
+        with pytest.raises(RuntimeError, match="BN statistics mode changed"):
+            st.run(torch.arange(8, device=dev))
+    finally:
+        K.set_deterministic(False)
+    st.run(torch.arange(8, device=dev))   # the mode it was recorded in: replays again
+    torch.cuda.synchronize()
+    assert torch.isfinite(st.flat.master).all()

@@ -1,0 +1,98 @@
+"""NativeBucketReducer bookkeeping on the CPU (parallel/ddp.py): bucket alignment for the P2P
+kernels, the launch order / arguments handed to the communicator and the final join.  The
+communicator is a recorder (the real one is exercised on the GPU: tests/test_comm_gpu.py,
+tests/test_ddp_gpu.py)."""
+import torch
+
+import pgdist  # noqa: F401
+from pgdist.parallel.ddp import NativeBucketReducer
+
+
+class FakeComm:
+    def __init__(self, world=2, rccl=True, p2p=True):
+        self.world, self.has_rccl, self.has_p2p, self.region = world, rccl, p2p, 1 << 20
+        self.log = []
+        self.tuned = None
+        self.p2p_error = None
+
+    def validate_p2p(self):
+        self.log.append(("validate",))
+        return self.has_p2p
+
+    def autotune(self, sizes, bf16_wire=False):
+        self.tuned = list(sizes)
+        return {s: ("oneshot" if s * 4 <= 64 * 1024 else "rccl") for s in sizes}
+
+    def allreduce(self, t, algo, bf16, wait=()):
+        self.log.append(("ar", t.data_ptr(), t.numel(), algo, bf16))
+
+    def join(self, stream=None):
+        self.log.append(("join",))
+
+
+class _FakeStreamModule:
+    class S:
+        cuda_stream = 1
+
+    @staticmethod
+    def current_stream(dev=None):
+        return _FakeStreamModule.S()
+
+
+def _ranges():
+    out, o = [], 0
+    for i in range(30):
+        n = 100 * (1 + i % 5) + (i % 3)          # not multiples of 8
+        out.append((f"p{i}", o, o + n))
+        o = (o + n + 63) // 64 * 64              # FlatParams: 64-element aligned starts
+    return out, (o + 63) // 64 * 64
+
+
+def test_buckets_are_64_aligned_and_cover_the_buffer(monkeypatch):
+    monkeypatch.setattr(torch.cuda, "current_stream", _FakeStreamModule.current_stream)
+    ranges, n = _ranges()
+    comm = FakeComm()
+    red = NativeBucketReducer(comm, torch.zeros(n), ranges, bucket_cap_mb=0.01, first_bucket_mb=0.002)
+    assert ("validate",) in comm.log
+    assert len(red.buckets) > 3
+    prev = 0
+    for s, e, _ in red.buckets:
+        assert s == prev and s % 64 == 0 and (e % 64 == 0 or e == n) and (e - s) % 8 == 0
+        prev = e
+    assert prev == n
+    assert comm.tuned == [e - s for s, e, _ in red.buckets]
+    assert red.algos == ["oneshot" if (e - s) * 4 <= 64 * 1024 else "rccl" for s, e, _ in red.buckets]
+
+
+def test_launch_order_slices_and_join(monkeypatch):
+    monkeypatch.setattr(torch.cuda, "current_stream", _FakeStreamModule.current_stream)
+    ranges, n = _ranges()
+    comm = FakeComm()
+    g = torch.zeros(n)
+    red = NativeBucketReducer(comm, g, ranges, bucket_cap_mb=0.01, first_bucket_mb=0.002, algo="twoshot")
+    comm.log.clear()
+    red.begin()
+    for name, _, _ in reversed(ranges):   # backward completion order is the buffer order reversed here
+        red.mark_ready([name])
+    red.finish()
+    ars = [x for x in comm.log if x[0] == "ar"]
+    assert len(ars) == len(red.buckets)
+    for (tag, ptr, numel, algo, bf), (s, e, _) in zip(ars, red.buckets):
+        assert ptr == g[s:].data_ptr() and numel == e - s and algo == "twoshot" and not bf
+    assert comm.log[-1] == ("join",)
+
+
+def test_world1_reducer_only_runs_when_forced(monkeypatch):
+    monkeypatch.setattr(torch.cuda, "current_stream", _FakeStreamModule.current_stream)
+    ranges, n = _ranges()
+    comm = FakeComm(world=1, p2p=False)
+    red = NativeBucketReducer(comm, torch.zeros(n), ranges, algo="rccl")
+    assert not red.enabled
+    red.finish()
+    assert comm.log == []
+    red = NativeBucketReducer(comm, torch.zeros(n), ranges, algo="rccl", force=True)
+    assert red.enabled
+    red.begin()
+    red.mark_ready([r[0] for r in ranges])
+    red.finish()
+    assert [x[0] for x in comm.log] == ["ar"] * len(red.buckets) + ["join"]

@@ -26,6 +26,8 @@ def test_presets_match_reference_constants():
     assert (s.batch_size, s.device, s.epochs, s.lr) == (64, "cpu", 20, 1e-4)
     assert (g.batch_size, g.save_path) == (128, "best_mobilenetv2_cifar10_224.pth")
     assert (m.batch_size, m.seed, m.save_path) == (128, 42, "best_mobilenetv2_cifar10_224_mpi.pth")
+    # DDP default broadcast_buffers=True (cifar10_mpi_mobilenet_224.py:142-145): BN buffers every step
+    assert m.bn_sync == "broadcast"
     assert (s.step_size, s.gamma, s.img_size) == (10, 0.1, 224)
 
 
