@@ -5,7 +5,9 @@ A randomly initialised MobileNetV2 amplifies bf16 rounding through its 52
 BatchNorm layers (errors grow to O(10-30 %) at the last layers even for
 PyTorch's own bf16 autocast path), so the acceptance criterion is relative to
 that noise floor: per layer, and for logits and gradients, the native path must
-be at least as close to fp32 as torch-bf16 is (within a small margin)."""
+be at least as close to fp32 as torch-bf16 is (within a small margin).  The per-layer wiring
+check (every op recomputed from the executor's own inputs, rel <= 2e-2) is
+tests/test_executor_teacher_forced_gpu.py."""
 import copy
 
 import pytest

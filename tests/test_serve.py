@@ -71,7 +71,16 @@ def test_native_predictor_matches_torch(tmp_path, ckpt):
     img = str(_png(tmp_path, (90, 10, 240)))
     ref = Predictor(str(p), device="cpu").probs([img, img])
     nat = Predictor(str(p), device="cuda", backend="hip", max_batch=4).probs([img, img])
-    assert torch.allclose(nat, ref, atol=0.05)
+    # bf16 noise floor: the same fp32 module under torch bf16 autocast on the GPU
+    tp = Predictor(str(p), device="cuda")
+    from PIL import Image
+    x = eval_transform(np.asarray(Image.open(img).convert("RGB"))).cuda()
+    x = x if x.dim() == 4 else x.unsqueeze(0)
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        p16 = torch.softmax(tp.model(x).float(), 1).cpu()
+    floor = (p16[0] - ref[0]).abs().max().item()
+    err = (nat - ref).abs().max().item()
+    assert err <= 2 * floor + 5e-3, (err, floor)
     assert nat.argmax(1).tolist() == ref.argmax(1).tolist()
 
 
