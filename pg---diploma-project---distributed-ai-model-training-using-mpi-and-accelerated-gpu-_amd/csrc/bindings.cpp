@@ -21,6 +21,10 @@
 #include "runtime/plan.h"
 #include "runtime/runtime.h"
 
+namespace pgdist_rt {
+uintptr_t cu_masked_stream(int device, int num, int den);   // runtime/streams.cpp
+}
+
 namespace py = pybind11;
 typedef unsigned short bf16_t;
 typedef uintptr_t P;
@@ -84,7 +88,7 @@ void launch_head(const bf16_t *, const float *, const float *, const float *, co
                  int, float, float *, float *, float *, float *, float *, bf16_t *, float *, float *,
                  float *, hipStream_t);
 void launch_augment(const unsigned char *, const long long *, const long long *, int, int, int,
-                    int, int, const float *, unsigned long long, const float *, int, bf16_t *,
+                    int, int, const float *, unsigned long long, const float *, long long, bf16_t *,
                     long long *, float *, hipStream_t);
 void launch_step_begin(float *, hipStream_t);
 int colsum_rows(int);
@@ -318,7 +322,7 @@ PYBIND11_MODULE(_pgdist_C, m) {
   });
   // ---- data ----
   m.def("augment", [](P src, P idx, P labels_src, int nsrc, int B, int out_hw, int train,
-                      int double_resize, P params, unsigned long long seed, P hyper, int epoch_ctr,
+                      int double_resize, P params, unsigned long long seed, P hyper, long long epoch_ctr,
                       P out, P labels_out, P params_out, P s) {
     pgdist_rt::run_op([=] {
       launch_augment(ptr<unsigned char>(src), ptr<long long>(idx), ptr<long long>(labels_src), nsrc, B,
@@ -419,6 +423,9 @@ PYBIND11_MODULE(_pgdist_C, m) {
   m.def("plan_replay", &pgdist_rt::plan_replay, "re-issue a recorded step (GIL held: Python ops run inline)");
   m.def("plan_free", &pgdist_rt::plan_free);
   m.def("plan_size", &pgdist_rt::plan_size);
+  m.def("plan_recording_size", &pgdist_rt::plan_recording_size);
+  m.def("plan_time_ops", &pgdist_rt::plan_time_ops, py::call_guard<py::gil_scoped_release>(),
+        "isolated wall time (us) of each op range of a recorded plan (diagnostics; re-runs the ops)");
   m.def("plan_py", [](py::function fn) {
     fn();
     if (pgdist_rt::plan_recording()) {
@@ -461,6 +468,9 @@ PYBIND11_MODULE(_pgdist_C, m) {
   m.def("comm_time_allreduce", &pgdist_rt::comm_time_allreduce, py::call_guard<py::gil_scoped_release>());
   m.def("comm_error", &pgdist_rt::comm_error, py::call_guard<py::gil_scoped_release>());
   m.def("comm_destroy", &pgdist_rt::comm_destroy, py::call_guard<py::gil_scoped_release>());
+
+  m.def("cu_masked_stream", &pgdist_rt::cu_masked_stream,
+        "HIP stream whose kernels may use CU i iff i % den < num (returns the stream handle)");
 
   // ---- native runtime (host) ----
   m.def("read_cifar10_bin", &pgdist_rt::read_cifar10_bin, py::arg("paths"), py::arg("num_threads") = 4,

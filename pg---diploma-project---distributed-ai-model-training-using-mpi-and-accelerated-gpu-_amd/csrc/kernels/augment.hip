@@ -159,7 +159,7 @@ PG_DEVICE void jitter(float (&x)[3], const float *prm, float mean, bool stop_bef
 __global__ __launch_bounds__(256) void augment_params_kernel(
     const unsigned char *__restrict__ src, const long long *__restrict__ idx, int B, int S,
     int train, int dbl, const float *__restrict__ given, unsigned long long seed,
-    const float *__restrict__ hyper, int epoch_ctr, float *__restrict__ params) {
+    const float *__restrict__ hyper, long long epoch_ctr, float *__restrict__ params) {
   __shared__ float img[32 * 32 * 3];
   __shared__ float prm[kNP];
   __shared__ float red[4];
@@ -300,7 +300,7 @@ __global__ __launch_bounds__(256) void augment_render_kernel(
 
 void launch_augment(const unsigned char *src, const long long *idx, const long long *labels_src,
                     int nsrc, int B, int S, int train, int dbl, const float *given,
-                    unsigned long long seed, const float *hyper, int epoch_ctr, bf16_t *out,
+                    unsigned long long seed, const float *hyper, long long epoch_ctr, bf16_t *out,
                     long long *labels_out, float *params, hipStream_t st) {
   (void)nsrc;
   hipLaunchKernelGGL(augment_params_kernel, dim3(B, kMeanSplit), dim3(256), 0, st, src, idx, B, S, train, dbl,

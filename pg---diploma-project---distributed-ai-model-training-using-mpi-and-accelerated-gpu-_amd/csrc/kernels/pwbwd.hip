@@ -50,7 +50,11 @@ struct PwBwdArgs {
   const BnFin *fin;             // fused BN finalize in the tail (nullptr: none)
   const BnFin *lz;              // lazy finalize of ca / cb / cc (nullptr: materialised)
 };
-template <int KP, int BN, int BM>
+// RAWX (project convs with one wide N tile): xN holds the RAW producer activation Yt, the
+// ReLU6(BN) of the wgrad operand is applied after the transposed read and the epilogue takes
+// its mask operand from xN, so no register copy of the tile's Yt is kept (those registers
+// spilled at Ng = 144 / 192); the C tile then gets its own LDS region
+template <int KP, int BN, int BM, bool RAWX = false>
 struct BwdLds {
   static constexpr int LDA = KP + 8, LDX = BN + 8, LDC = BN + 8;
   static constexpr int WT = 0;                              // [BN][LDA] W^T tile (resident)
@@ -58,7 +62,7 @@ struct BwdLds {
   static constexpr int DYN = STG;                           //   dyN [BM][LDA]
   static constexpr int XN = DYN + BM * LDA * 2;             //   xN  [BM][LDX]
   static constexpr int STG_END = XN + BM * LDX * 2;
-  static constexpr int CS = STG;                            // C tile [BM][LDC] aliases the staging
+  static constexpr int CS = RAWX ? STG_END : STG;           // C tile [BM][LDC] (aliases the staging)
   static constexpr int RED = STG;                           // [BM/4][BN] floats at the very end
   static constexpr int CS_END = CS + BM * LDC * 2;
   static constexpr int RED_END = RED + (BM / 4) * BN * 4;
@@ -72,7 +76,8 @@ struct BwdLds {
 // 2 column halves; used when KP is large so the prefetched tile fits in registers)
 template <int EPI, int KP, int BN, int BM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void pw_bwd_fused_kernel(PwBwdArgs p) {
-  using L = BwdLds<KP, BN, BM>;
+  constexpr bool RAWX = EPI != EPI_BWD_LIN_ && BN >= 96;
+  using L = BwdLds<KP, BN, BM, RAWX>;
   constexpr int LDA = L::LDA, LDX = L::LDX, LDC = L::LDC;
   constexpr int CT = BN / 16;
   constexpr int RGS = BM / 16;                   // dgrad row groups of 16
@@ -206,15 +211,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
         }
       }
     }
-    uint4 ct[IX][4], cr[LIN ? IX : 1][4];   // this tile's epilogue operands (raw Yt, R)
+    uint4 ct[RAWX ? 1 : IX][4], cr[LIN ? IX : 1][4];   // this tile's epilogue operands (raw Yt, R)
 #pragma unroll
     for (int i = 0; i < IX; ++i) {
       const int it = tid + i * 256;
       const int c8 = (it % XC) * 8, m4 = it / XC;
       float v[4][8];
+      if constexpr (RAWX) {   // raw Yt row-major into xN (ReLU6(BN) applied at the wgrad read)
+        if (it < NX) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) *reinterpret_cast<uint4 *>(xN + (m4 * 4 + q) * LDX + c8) = tq[i][q];
+        }
+        continue;
+      }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        ct[i][q] = tq[i][q];
+        ct[RAWX ? 0 : i][q] = tq[i][q];
         if constexpr (LIN) {
           cr[i][q] = rq[i][q];
           unpack8(xq[i][q], v[q]);
@@ -273,7 +285,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
           const s16x4_t b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)pb);
           const s16x4_t b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)(pb + 4 * LDX));
           const s16x8_t af = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
-          const s16x8_t bf = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
+          s16x8_t bf = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
+          if constexpr (RAWX) {   // lane holds 8 rows of ONE column tj*16 + (lane & 15): x = relu6(Yt*s + t)
+            const int col = tj * 16 + (lane & 15);
+            const float s_ = Ps[3 * KP + col], t_ = Ps[3 * KP + BN + col];
+            float xv[8];
+            unpack8(__builtin_bit_cast(uint4, bf), xv);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) xv[j] = relu6f(fmaf(xv[j], s_, t_));
+            bf = __builtin_bit_cast(s16x8_t, pack8(xv));
+          }
           accW[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af),
                                                             __builtin_bit_cast(bf16x8_t, bf), accW[u], 0, 0, 0);
         }
@@ -307,7 +328,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
           if (row < p.M && n0 + c8 < p.Ng) {
             float v[8], yt[8];
             unpack8(*reinterpret_cast<const uint4 *>(Cs + (m4 * 4 + q) * LDC + c8), v);
-            unpack8(ct[i][q], yt);
+            if constexpr (RAWX) unpack8(*reinterpret_cast<const uint4 *>(xN + (m4 * 4 + q) * LDX + c8), yt);
+            else unpack8(ct[i][q], yt);
             if constexpr (!LIN) {
 #pragma unroll
               for (int j = 0; j < 8; ++j) v[j] *= relu6_mask(yt[j], es[j], et[j]);
@@ -385,6 +407,12 @@ BwdGeom bwd_geom(int M, int Kg, int Ng) {
   if (Ng <= 32) g.BN = 32;
   else if (Ng % 64 == 0 || Ng % 48 != 0 || g.KP >= 160) g.BN = 64;
   else g.BN = 48;
+  // project convs (small Kg, wide Ng = 96 / 144 / 192): ONE N tile spanning the whole row.
+  // With 48- / 64-column tiles each workgroup read and wrote 96- / 128-byte pieces of the
+  // 192..384-byte NHWC rows (partial 128-B lines, G and Y re-read per N tile): 1.6-2.0 TB/s
+  // (profiles/r3_roofline_base.txt); PGDIST_PWB_WIDE=0 restores the narrow tiles
+  static const bool wide = [] { const char *e = getenv("PGDIST_PWB_WIDE"); return !(e && atoi(e) == 0); }();
+  if (wide && g.KP <= 32 && (Ng == 96 || Ng == 144 || Ng == 192)) g.BN = Ng;
   // rows per tile: enough 4x8 staging items for all 256 threads, while the prefetched
   // (G, Y) tile stays within 2 waves/SIMD of registers
   const int chunks = (g.KP > g.BN ? g.KP : g.BN) / 8;
@@ -404,7 +432,7 @@ BwdGeom bwd_geom(int M, int Kg, int Ng) {
 template <int EPI, int KP, int BN, int BM>
 void launch_bwd_t(const PwBwdArgs &a, const BwdGeom &g, hipStream_t st) {
   hipLaunchKernelGGL((pw_bwd_fused_kernel<EPI, KP, BN, BM>), dim3(g.gx, g.nt), dim3(256),
-                     (BwdLds<KP, BN, BM>::BYTES), st, a);
+                     (BwdLds<KP, BN, BM, EPI != EPI_BWD_LIN_ && BN >= 96>::BYTES), st, a);
 }
 
 template <int EPI>
@@ -415,6 +443,9 @@ void launch_bwd_epi(const PwBwdArgs &a, const BwdGeom &g, hipStream_t st) {
   BWD_CASE(32, 48, 128) BWD_CASE(64, 48, 128) BWD_CASE(96, 48, 64) BWD_CASE(128, 48, 64)
   BWD_CASE(32, 64, 128) BWD_CASE(64, 64, 128) BWD_CASE(96, 64, 64) BWD_CASE(128, 64, 64)
   BWD_CASE(160, 32, 32) BWD_CASE(192, 32, 32) BWD_CASE(160, 64, 32) BWD_CASE(192, 64, 32)
+  if constexpr (EPI != EPI_BWD_LIN_) {   // wide project tiles (RAWX): the project convs only
+    BWD_CASE(32, 96, 64) BWD_CASE(32, 144, 64) BWD_CASE(32, 192, 64)
+  }
 #undef BWD_CASE
 }
 }  // namespace

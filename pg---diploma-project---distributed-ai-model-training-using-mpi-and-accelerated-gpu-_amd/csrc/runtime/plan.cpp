@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <chrono>
 #include <map>
 #include <memory>
 #include <stdexcept>
@@ -110,6 +111,28 @@ void plan_replay(int id) {
 }
 
 void plan_free(int id) { plans().erase(id); }
+
+std::size_t plan_recording_size() { return g_rec ? g_rec->ops.size() : 0; }
+
+std::vector<double> plan_time_ops(int id, const std::vector<std::pair<int, int>> &ranges, int iters) {
+  auto it = plans().find(id);
+  if (it == plans().end()) throw std::out_of_range("plan_time_ops: unknown plan " + std::to_string(id));
+  if (g_rec) throw std::runtime_error("plan_time_ops: not allowed while recording");
+  auto &ops = it->second.ops;
+  std::vector<double> out;
+  for (const auto &r : ranges) {
+    if (r.first < 0 || r.second > (int)ops.size() || r.first > r.second)
+      throw std::out_of_range("plan_time_ops: bad op range");
+    check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < iters; ++i)
+      for (int k = r.first; k < r.second; ++k) ops[k]();
+    check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    const auto t1 = std::chrono::steady_clock::now();
+    out.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count() / (iters > 0 ? iters : 1));
+  }
+  return out;
+}
 
 std::size_t plan_size(int id) {
   auto it = plans().find(id);

@@ -20,6 +20,7 @@
 #include <cstddef>
 #include <functional>
 #include <utility>
+#include <vector>
 
 namespace pgdist_rt {
 
@@ -33,6 +34,10 @@ void plan_append(PlanOp op);     // no-op unless recording
 void plan_replay(int id);
 void plan_free(int id);
 std::size_t plan_size(int id);
+std::size_t plan_recording_size();   // ops recorded so far in the open recording (0: none)
+// diagnostics: for each [first, last) op range, run it `iters` times in isolation (device
+// synchronised before and after) and return the mean wall time per repetition in us
+std::vector<double> plan_time_ops(int id, const std::vector<std::pair<int, int>> &ranges, int iters);
 
 // run now; also record when a plan is being recorded
 template <class F>

@@ -307,7 +307,7 @@ class MobileNetV2Executor:
         self.side_batch = max(1, int(os.environ.get("PGDIST_SIDE_BATCH", "3")))
         self.batch_reductions = os.environ.get("PGDIST_RED_BATCH", "1") == "1"
         if device.type == "cuda" and side_stream:
-            self.side = torch.cuda.Stream(device)
+            self.side = K.side_stream(device)
             K.register_side_stream(self.side)
         self.img = torch.zeros(B, img_size, img_size, 4, dtype=torch.bfloat16, device=device)
         self.labels = torch.zeros(B, dtype=torch.int64, device=device)

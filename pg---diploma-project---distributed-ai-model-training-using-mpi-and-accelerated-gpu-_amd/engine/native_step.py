@@ -60,6 +60,11 @@ def _dist_backend(group=None) -> str:
         return ""
 
 
+# augment(epoch_ctr=...) offset that makes the kernel's RNG key for step t that of step t + 1
+# (key = mix(step * 0x100000001B3 + epoch_ctr), csrc/kernels/augment.hip)
+AUG_NEXT_STEP = 0x100000001B3
+
+
 class NativeTrainStep:
     def __init__(self, model, batch: int, device: torch.device, img_size: int = 224, lr: float = 1e-4,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, world_size: int = 1,
@@ -144,6 +149,22 @@ class NativeTrainStep:
         self.use_plan = (not self.use_graph and not self.graph_forward and not gloo
                          and getattr(self.exe, "PLAN_SAFE", False) and plan_env in ("1", "force"))
         self.plan: Optional[K.LaunchPlan] = None
+        # augmentation prefetch (PGDIST_AUG_PREFETCH=0: off): when the caller passes the NEXT
+        # batch's indices, that batch is rendered on the weight-gradient side stream during this
+        # step's backward into the other half of a double buffer (images, labels, indices), so
+        # the GPU augmentation (~0.1 ms) leaves the critical path.  Its RNG stream is the one the
+        # main-stream augmentation of that step would use (step counter + 1), so a prefetched
+        # batch is bitwise the batch a non-prefetched step renders.  One launch plan per buffer
+        # parity; steps that neither have a prefetched batch nor prefetch one run eagerly.
+        self.prefetch = (self.use_plan and self.augment_enabled and self.train_augment and self.exe.side is not None
+                         and os.environ.get("PGDIST_AUG_PREFETCH", "1") == "1")
+        self._cur, self._have, self._next = 0, False, False
+        self._plans = {}
+        if self.prefetch:
+            self._imgs = [self.exe.img, torch.empty_like(self.exe.img)]
+            self._labs = [self.exe.labels, torch.empty_like(self.exe.labels)]
+            self._idxs = [self.idx, torch.empty_like(self.idx)]
+            self._prms = [self.aug_params, torch.empty_like(self.aug_params)]
 
     def _make_comm(self, mode: str, world_size: int) -> NativeComm:
         """Native communicator of this data-parallel step: RCCL (modes rccl / native) and the P2P
@@ -202,6 +223,7 @@ class NativeTrainStep:
         st.use_graph, st.graph, st._eager_runs = False, None, 0
         st.use_plan, st.plan = False, None
         st.graph_forward, st.fwd_graph = False, None
+        st.prefetch, st._have, st._next, st._plans = False, False, False, {}
         return st
 
     def set_data(self, src_u8: torch.Tensor, labels: torch.Tensor):
@@ -214,6 +236,9 @@ class NativeTrainStep:
         if getattr(self, "plan", None) is not None:   # the recorded augment launch reads the old pool
             self.plan.free()
             self.plan, self._eager_runs = None, 0
+        for p in getattr(self, "_plans", {}).values():
+            p.free()
+        self._plans, self._have = {}, False
 
     def sync_from_rank0(self):
         mods = [m for m in self.exe.model.modules() if isinstance(m, torch.nn.BatchNorm2d)]
@@ -237,7 +262,7 @@ class NativeTrainStep:
             K.image_prep(self.src, self.idx, self.src_labels, exe.img, exe.labels,
                          seed=self.seed + 17 * self.rank if self.train_augment else 0,
                          hyper=self.hyper if self.train_augment else None)
-        elif self.augment_enabled:
+        elif self.augment_enabled and not self._have:   # (a prefetched batch is already rendered)
             K.augment(self.src, self.idx, self.src_labels, exe.img, exe.labels, self.aug_params,
                       train=self.train_augment,
                       double_resize=self.double_resize, seed=self.seed + 17 * self.rank, hyper=self.hyper,
@@ -256,6 +281,16 @@ class NativeTrainStep:
     def _back(self):
         """Backward (+ bucketed all-reduce), Adam and metrics."""
         exe = self.exe
+        if self._next:
+            # render the next batch into the other buffer on the side stream: after this step's
+            # main-stream work so far (the previous step, which last read that buffer, is before it);
+            # the backward's final join orders it before the next step's forward
+            nb = 1 - self._cur
+            K.stream_wait(exe.side, torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(exe.side):
+                K.augment(self.src, self._idxs[nb], self.src_labels, self._imgs[nb], self._labs[nb], self._prms[nb],
+                          train=True, double_resize=self.double_resize, seed=self.seed + 17 * self.rank,
+                          hyper=self.hyper, epoch_ctr=AUG_NEXT_STEP, out_hw=self.S)
         native = getattr(self.reducer, "native", False)
         if native:   # host bookkeeping at record time only; the collectives are native plan ops
             self.reducer.side = exe.side
@@ -272,8 +307,14 @@ class NativeTrainStep:
                     1.0 / self.world)
         K.reduce_metrics(exe.loss, exe.correct, self.B, self.metrics)
 
-    def run(self, idx: torch.Tensor):
-        """One training step on the batch ``src[idx]`` (idx: int64 [B] on device)."""
+    def run(self, idx: torch.Tensor, next_idx: Optional[torch.Tensor] = None):
+        """One training step on the batch ``src[idx]`` (idx: int64 [B] on device).  With
+        ``next_idx`` (the next step's full batch) and prefetch enabled, that batch is augmented
+        during this step's backward on the side stream (the next ``run`` then ignores its idx
+        argument's contents only in the sense that the batch was already rendered from
+        ``next_idx``: callers pass the same indices again)."""
+        if self.prefetch and (next_idx is not None or self._have):
+            return self._run_prefetch(idx, next_idx)
         self.idx.copy_(idx, non_blocking=True)
         if self.graph_forward:
             if self.fwd_graph is None:
@@ -313,6 +354,30 @@ class NativeTrainStep:
                 self._body()
         self.graph.replay()
 
+    def _run_prefetch(self, idx, next_idx):
+        cur = self._cur
+        self.exe.img, self.exe.labels = self._imgs[cur], self._labs[cur]
+        self.idx, self.aug_params = self._idxs[cur], self._prms[cur]
+        if not self._have:
+            self.idx.copy_(idx, non_blocking=True)
+        self._next = next_idx is not None and next_idx.numel() == self.B
+        if self._next:
+            self._idxs[1 - cur].copy_(next_idx, non_blocking=True)
+        if self._have and self._next and self._eager_runs >= 2:
+            plan = self._plans.get(cur)
+            if plan is None:
+                plan = self._plans[cur] = K.LaunchPlan()
+                plan.record(self._body)   # runs this step eagerly while recording it
+            else:
+                plan.replay()
+            self.plan = plan
+        else:   # first / last step of a prefetch chain, and warm-up: eager
+            self._eager_runs += 1
+            self._body()
+        self._have = self._next
+        if self._next:
+            self._cur = 1 - cur
+
     @property
     def graph_enabled(self) -> bool:
         return self.use_graph
@@ -321,7 +386,9 @@ class NativeTrainStep:
         n = self._perm.numel()
         if self._pos + self.B > n:
             self._pos = 0
-        self.run(self._perm[self._pos:self._pos + self.B])
+        nxt = self._pos + self.B
+        nxt = nxt if nxt + self.B <= n else 0
+        self.run(self._perm[self._pos:self._pos + self.B], self._perm[nxt:nxt + self.B])
         self._pos += self.B
 
     # ------------------------------------------------------------------ metrics

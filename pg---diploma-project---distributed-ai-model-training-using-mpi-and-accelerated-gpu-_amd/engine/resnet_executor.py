@@ -189,7 +189,7 @@ class ResNet50Executor:
         self._side_pending = []
         self.side_batch = max(1, int(os.environ.get("PGDIST_SIDE_BATCH", "3")))
         if side_stream:
-            self.side = torch.cuda.Stream(device)
+            self.side = K.side_stream(device)
             K.register_side_stream(self.side)
         self.img = torch.zeros(B, img_size, img_size, 4, **bf16)
         self.labels = torch.zeros(B, dtype=torch.int64, device=device)

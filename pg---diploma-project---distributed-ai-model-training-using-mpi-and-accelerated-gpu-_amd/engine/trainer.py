@@ -198,13 +198,15 @@ class Trainer:
             with trace_range(f"train_epoch_{epoch}", prof):
                 for b in range(nb):
                     sl = didx[b * bs:(b + 1) * bs]
+                    # the next batch (augmented during this step's backward when it is full-size)
+                    nxt = didx[(b + 1) * bs:(b + 2) * bs] if b + 1 < nb else None
                     st = self.step if sl.numel() == bs else self._tail(sl.numel())
                     if self.timer is not None and sl.numel() == bs:
                         self.timer.start()
-                        st.run(sl)
+                        st.run(sl, nxt)
                         self.timer.stop()
                     else:
-                        st.run(sl)
+                        st.run(sl, nxt)
                     if self.watchdog is not None:
                         self.watchdog.kick(phase=f"train epoch {epoch} batch {b}")
                 return self.step.read_metrics()

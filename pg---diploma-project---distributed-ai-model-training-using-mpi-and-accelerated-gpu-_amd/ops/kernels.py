@@ -843,3 +843,72 @@ class LaunchPlan:
         if self.id is not None:
             lib().plan_free(self.id)
             self.id = None
+
+
+def side_stream(device):
+    """The weight-gradient side stream of an executor.  PGDIST_SIDE_CUS=num/den confines it to
+    that fraction of the CUs (runtime/streams.cpp, hipExtStreamCreateWithCUMask) so its wide
+    launches cannot take every CU slot from the critical-path stream; unset / 0: a plain
+    stream."""
+    spec = os.environ.get("PGDIST_SIDE_CUS", "0")
+    if spec and spec != "0":
+        num, den = (int(x) for x in spec.split("/"))
+        h = lib().cu_masked_stream(device.index or 0, num, den)
+        return torch.cuda.ExternalStream(h, device=device)
+    return torch.cuda.Stream(device)
+
+
+# --------------------------------------------------------------------------- launch log (diagnostics)
+# While a launch plan is recorded with the log on, every kernel wrapper call appends its op range
+# in the plan, its tensor operands' bytes and its integer shape arguments: scripts/roofline.py
+# then times each range in isolation (lib().plan_time_ops) for a per-op roofline table.
+_LOG = None
+_LOG_DEPTH = [0]
+# operands that are workspaces / whole pools / tiny side tables, not per-op traffic
+_LOG_SKIP = {"part", "wpart", "ws", "params_out", "given_params", "tab", "fin", "lz", "hyper", "src", "idx",
+             "labels_src", "labels_out", "labels", "W8", "wsc"}
+
+
+def launch_log_start():
+    global _LOG
+    _LOG = []
+
+
+def launch_log_stop():
+    global _LOG
+    out, _LOG = _LOG, None
+    return out
+
+
+def _logged(fn):
+    import functools
+    import inspect
+    sig = inspect.signature(fn)
+
+    @functools.wraps(fn)
+    def wrapper(*a, **kw):
+        if _LOG is None or _LOG_DEPTH[0] > 0:
+            return fn(*a, **kw)
+        before = lib().plan_recording_size()
+        _LOG_DEPTH[0] += 1
+        try:
+            r = fn(*a, **kw)
+        finally:
+            _LOG_DEPTH[0] -= 1
+        after = lib().plan_recording_size()
+        if after > before:
+            ba = sig.bind(*a, **kw).arguments
+            nb = sum(v.numel() * v.element_size() for k, v in ba.items()
+                     if torch.is_tensor(v) and k not in _LOG_SKIP)
+            ints = {k: v for k, v in ba.items() if isinstance(v, int) and not isinstance(v, bool)}
+            _LOG.append(dict(op=fn.__name__, first=before, last=after, bytes=nb, shape=ints, stream=_s()))
+        return r
+    return wrapper
+
+
+for _name in ("bn_fwd_finalize", "bn_bwd_finalize", "bn_apply", "bn_finalize_batch", "adam_flat", "f32_to_bf16",
+              "step_begin", "reduce_metrics", "dw_fwd", "dw_dgrad", "dw_wgrad", "pw_gemm", "pw_gemm_f8", "w8_quant",
+              "wt_transpose", "pw_bwd", "wgrad_reduce", "wgrad_reduce_flush", "pw_wgrad", "stem_fwd", "stem_wgrad",
+              "head", "augment", "conv_fwd", "conv_dgrad", "conv_wgrad", "bn_mat", "conv_wt", "res_out", "maxpool_fwd",
+              "maxpool_bwd", "avgpool", "head_bwd", "softmax_ce", "image_prep", "memset"):
+    globals()[_name] = _logged(globals()[_name])

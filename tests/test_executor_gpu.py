@@ -305,3 +305,29 @@ def test_bn_mode_switch_after_plan_recorded_rejected(dev, monkeypatch):
     st.run(torch.arange(8, device=dev))   # the mode it was recorded in: replays again
     torch.cuda.synchronize()
     assert torch.isfinite(st.flat.master).all()
+
+
+def test_augmentation_prefetch_matches_plain_steps(dev, deterministic, monkeypatch):
+    """Next-batch augmentation on the side stream (double-buffered, per-parity launch plans)
+    renders exactly the batch the main-stream augmentation would (same RNG stream), so 8 steps
+    with prefetch give bitwise the weights / metrics of 8 plain steps."""
+    from pgdist.engine.native_step import NativeTrainStep
+    src = torch.randint(0, 256, (64, 32, 32, 3), dtype=torch.uint8, device=dev,
+                        generator=torch.Generator(device=dev).manual_seed(5))
+    labels = torch.arange(64, device=dev) % 10
+    batches = [(torch.arange(8, device=dev) * 7 + 3 * i) % 64 for i in range(9)]
+    out = {}
+    for pf in ("1", "0"):
+        monkeypatch.setenv("PGDIST_AUG_PREFETCH", pf)
+        torch.manual_seed(0)
+        st = NativeTrainStep(mobilenet_v2(10), 8, dev, img_size=64, lr=1e-3, use_graph=False)
+        assert st.prefetch == (pf == "1")
+        st.set_data(src, labels)
+        for i in range(8):
+            st.run(batches[i], batches[i + 1] if i < 7 else None)
+        torch.cuda.synchronize()
+        if pf == "1":
+            assert len(st._plans) == 2          # one launch plan per buffer parity
+        out[pf] = (st.flat.master.clone(), st.read_metrics())
+    assert torch.equal(out["1"][0], out["0"][0])
+    assert out["1"][1] == out["0"][1]
