@@ -124,6 +124,10 @@ void launch_maxpool_bwd(const bf16_t *, const uint8_t *, const bf16_t *, const f
 void launch_avgpool(const bf16_t *, float *, int, int, int, hipStream_t);
 void launch_head_bwd(const float *, const bf16_t *, const bf16_t *, bf16_t *, float *, int, int, int, hipStream_t);
 void launch_softmax_ce(const float *, const long long *, int, int, float, float *, float *, float *, hipStream_t);
+long long fc_gemm_workspace_floats(int, int, int);
+void launch_fc_gemm(const float *, long long, long long, const float *, long long, long long, const float *, float *,
+                    int, int, int, float *, hipStream_t);
+void launch_col_sum(const float *, int, int, float *, hipStream_t);
 void launch_image_prep(const uint8_t *, const long long *, const long long *, int, int, int, unsigned long long,
                        const float *, bf16_t *, long long *, hipStream_t);
 
@@ -406,6 +410,17 @@ PYBIND11_MODULE(_pgdist_C, m) {
       launch_softmax_ce(ptr<float>(logits), ptr<long long>(labels), B, NC, scale, ptr<float>(loss),
                         ptr<float>(correct), ptr<float>(dlogits), S(s));
     });
+  });
+  m.def("fc_gemm_workspace_floats", &fc_gemm_workspace_floats);
+  m.def("fc_gemm", [](P A, long long sam, long long sak, P B, long long sbk, long long sbn, P bias, P C, int M, int N,
+                      int K, P ws, P s) {
+    pgdist_rt::run_op([=] {
+      launch_fc_gemm(ptr<float>(A), sam, sak, ptr<float>(B), sbk, sbn, ptr<float>(bias), ptr<float>(C), M, N, K,
+                     ptr<float>(ws), S(s));
+    });
+  });
+  m.def("col_sum", [](P X, int M, int N, P out, P s) {
+    pgdist_rt::run_op([=] { launch_col_sum(ptr<float>(X), M, N, ptr<float>(out), S(s)); });
   });
   m.def("image_prep", [](P src, P idx, P lab_src, int B, int H, int W, unsigned long long seed, P hyper, P out,
                          P lab_out, P s) {

@@ -313,7 +313,8 @@ class NativeTrainStep:
         during this step's backward on the side stream (the next ``run`` then ignores its idx
         argument's contents only in the sense that the batch was already rendered from
         ``next_idx``: callers pass the same indices again)."""
-        if self.prefetch and (next_idx is not None or self._have):
+        # (the 32x32 augmentation chain only: full-resolution sources take the short image_prep)
+        if self.prefetch and (next_idx is not None or self._have) and self.src.shape[1] == 32:
             return self._run_prefetch(idx, next_idx)
         self.idx.copy_(idx, non_blocking=True)
         if self.graph_forward:

@@ -13,7 +13,7 @@ forward, per bottleneck (x = block input, materialised)
   [projection]    yd = conv_s(x)                         + BNd partials -> finalize
   output          o = relu(BN3(y3) + (BNd(yd) | x))      (materialised, bf16)
 stem: 7x7 s2 conv on the 4-channel image, BN0, fused relu + 3x3 s2 max-pool (arg-max kept)
-head: average pool -> fc (hipBLASLt GEMM through torch.addmm, fp32) -> softmax CE kernel
+head: average pool -> fc (fp32 split-K GEMM kernels, csrc/kernels/fc.hip) -> softmax CE kernel
 
 backward walks the schedule in reverse.  Gz = dL/d(BN3(y3) + shortcut) is produced by
 the NEXT block's conv1 dgrad epilogue ((dx + shortcut grad) * 1[o > 0], with the BN3 and
@@ -85,6 +85,9 @@ class BlockPlan:
 
 
 class ResNet50Executor:
+    # a training step is native launches, stream joins and plan_py callbacks only (the fc head
+    # included: csrc/kernels/fc.hip), so NativeTrainStep replays it from a launch plan
+    PLAN_SAFE = True
     # on_params_ready issues only recordable native ops (NativeBucketReducer): called directly
     ready_native = False
 
@@ -180,6 +183,9 @@ class ResNet50Executor:
         self.fc_b = self.flat.w("fc.bias")
         self.fc_gw = self.flat.g("fc.weight").view(self.NC, self.C_last)
         self.fc_gb = self.flat.g("fc.bias")
+        C, NC = self.C_last, self.NC
+        self.ws_fc = torch.zeros(max(K.fc_gemm_workspace_floats(B, NC, C), K.fc_gemm_workspace_floats(NC, C, B),
+                                     K.fc_gemm_workspace_floats(B, C, NC), 1), **f32)
         # ---------------- workspaces (stream-ordered reuse)
         pf = max(K.bn_part_floats(P, C) for P, C in parts) + 1024
         self.ws_part = torch.zeros(pf, **f32)
@@ -224,17 +230,23 @@ class ResNet50Executor:
         return n <= 2 * cls.MAT_ELEMS if c.k == 3 else n <= cls.MAT_ELEMS // 2
 
     def _ready(self, names):
+        """Gradients of ``names`` are final once the work enqueued so far completes (same
+        contract as MobileNetV2Executor._ready): a call that launches a bucket first flushes the
+        deferred side-stream work; a native reducer's bucket launch is itself a recorded native
+        op, a host-side reducer runs as a launch-plan Python callback on the side stream."""
         if self.on_params_ready is None:
             return
-        if self.ready_native:   # native reducer: waits for the main and side streams itself
-            if self.ready_probe is None or self.ready_probe(names):
-                self._flush_side()
+        if self.side is not None and (self.ready_probe is None or self.ready_probe(names)):
+            self._flush_side()
+        if self.ready_native:
             self.on_params_ready(names)
             return
+        K.plan_py(lambda: self._ready_now(names))
+
+    def _ready_now(self, names):
         if self.side is None or (self.ready_probe is not None and not self.ready_probe(names)):
             self.on_params_ready(names)
             return
-        self._flush_side()   # the bucket's gradients: deferred weight-gradient work first
         self.side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.side):
             self.on_params_ready(names)
@@ -253,7 +265,7 @@ class ResNet50Executor:
     def _flush_side(self):
         if self.side is None or not self._side_pending:
             return
-        self.side.wait_stream(torch.cuda.current_stream(self.device))
+        K.stream_wait(self.side, torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.side):
             for fn in self._side_pending:
                 fn()
@@ -308,7 +320,9 @@ class ResNet50Executor:
         # head
         HW = self.Hf * self.Hf
         K.avgpool(self.blocks[-1].out, self.pooled, B, HW, self.C_last)
-        torch.addmm(self.fc_b, self.pooled, self.fc_w.t(), out=self.logits)
+        C, NC = self.C_last, self.NC
+        # logits[b][j] = fc_b[j] + sum_c pooled[b][c] * fc_w[j][c]
+        K.fc_gemm(self.pooled, C, 1, self.fc_w, 1, C, self.logits, B, NC, C, bias=self.fc_b, ws=self.ws_fc)
         K.softmax_ce(self.logits, self.labels, self.loss, self.correct, self.dlogits if train else None,
                      scale=1.0 / B)
 
@@ -317,9 +331,12 @@ class ResNet50Executor:
         f, B, ws, ws2, wg = self.flat, self.B, self.ws_part, self.ws_part2, self.ws_wgrad
         K.conv_wt(f.shadow, f.shadow_t, self.wt_tab, self.wt_tab.shape[0])
         # head: fc gradients (fp32 GEMMs) and the pooled gradient through the last ReLU
-        torch.mm(self.dlogits.t(), self.pooled, out=self.fc_gw)
-        torch.sum(self.dlogits, 0, out=self.fc_gb)
-        torch.mm(self.dlogits, self.fc_w, out=self.dpool)
+        C, NC = self.C_last, self.NC
+        # fc_gw[j][c] = sum_b dlogits[b][j] * pooled[b][c];  fc_gb[j] = sum_b dlogits[b][j]
+        # dpool[b][c] = sum_j dlogits[b][j] * fc_w[j][c]
+        K.fc_gemm(self.dlogits, 1, NC, self.pooled, C, 1, self.fc_gw, NC, C, B, ws=self.ws_fc)
+        K.col_sum(self.dlogits, B, NC, self.fc_gb)
+        K.fc_gemm(self.dlogits, NC, 1, self.fc_w, C, 1, self.dpool, B, C, NC, ws=self.ws_fc)
         self._ready(["fc.weight", "fc.bias"])
         last = self.blocks[-1]
         HW = self.Hf * self.Hf
@@ -393,7 +410,7 @@ class ResNet50Executor:
         self._ready([st.name] + bn0.param_names)
         self._flush_side()
         if self.side is not None:
-            torch.cuda.current_stream(self.device).wait_stream(self.side)
+            K.stream_wait(torch.cuda.current_stream(self.device), self.side)
 
     # ------------------------------------------------------------------ eval
     def all_bns(self):

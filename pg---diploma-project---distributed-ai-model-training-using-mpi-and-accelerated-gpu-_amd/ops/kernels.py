@@ -775,6 +775,41 @@ def softmax_ce(logits, labels, loss, correct, dlogits=None, scale=1.0):
     lib().softmax_ce(_p(logits), _p(labels), B, NC, float(scale), _p(loss), _p(correct), _p(dlogits), _s())
 
 
+def fc_gemm_workspace_floats(M, N, K):
+    return int(lib().fc_gemm_workspace_floats(M, N, K))
+
+
+def _strided_span(t, rows, cols, s_row, s_col, nm):
+    """the strided fp32 operand t(r, c) = t[r*s_row + c*s_col] must fit inside t"""
+    if t.dtype != F32 or not t.is_contiguous():
+        raise ValueError(f"fc_gemm: {nm} must be contiguous fp32")
+    need = (rows - 1) * s_row + (cols - 1) * s_col + 1
+    if s_row < 0 or s_col < 0 or t.numel() < need:
+        raise ValueError(f"fc_gemm: {nm} has {t.numel()} elements, the strides address {need}")
+
+
+def fc_gemm(A, sam, sak, B, sbk, sbn, C, M, N, K, bias=None, ws=None):
+    """fp32 C[m][n] = sum_k A[m*sam + k*sak] * B[k*sbk + n*sbn] (+ bias[n]); deterministic
+    (split-K partials in `ws`, fc_gemm_workspace_floats(M, N, K) floats, summed in a fixed order)."""
+    if min(M, N, K) < 1:
+        raise ValueError("fc_gemm: empty shape")
+    _strided_span(A, M, K, sam, sak, "A")
+    _strided_span(B, K, N, sbk, sbn, "B")
+    _chk(C, F32, M * N, "C")
+    _chk(bias, F32, N, "bias")
+    nws = fc_gemm_workspace_floats(M, N, K)
+    if nws:
+        _chk(ws, F32, nws, "ws")
+    lib().fc_gemm(_p(A), sam, sak, _p(B), sbk, sbn, _p(bias), _p(C), M, N, K, _p(ws) if nws else 0, _s())
+
+
+def col_sum(X, M, N, out):
+    """out[n] = sum over rows m of X[m][n] (fixed order)"""
+    _chk(X, F32, M * N, "X")
+    _chk(out, F32, N, "out")
+    lib().col_sum(_p(X), M, N, _p(out), _s())
+
+
 def image_prep(src, idx, labels_src, out, labels_out, seed=0, hyper=None):
     """uint8 [N,H,W,3] pool gathered by idx [B] -> random h-flip, ImageNet normalisation,
     NHWC bf16 [B,H,W,4] (4th channel 0)."""
@@ -910,5 +945,5 @@ for _name in ("bn_fwd_finalize", "bn_bwd_finalize", "bn_apply", "bn_finalize_bat
               "step_begin", "reduce_metrics", "dw_fwd", "dw_dgrad", "dw_wgrad", "pw_gemm", "pw_gemm_f8", "w8_quant",
               "wt_transpose", "pw_bwd", "wgrad_reduce", "wgrad_reduce_flush", "pw_wgrad", "stem_fwd", "stem_wgrad",
               "head", "augment", "conv_fwd", "conv_dgrad", "conv_wgrad", "bn_mat", "conv_wt", "res_out", "maxpool_fwd",
-              "maxpool_bwd", "avgpool", "head_bwd", "softmax_ce", "image_prep", "memset"):
+              "maxpool_bwd", "avgpool", "head_bwd", "softmax_ce", "fc_gemm", "col_sum", "image_prep", "memset"):
     globals()[_name] = _logged(globals()[_name])

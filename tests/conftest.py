@@ -36,3 +36,12 @@ def pytest_collection_modifyitems(config, items):
 def dev():
     import torch
     return torch.device("cuda", 0)
+
+
+@pytest.fixture
+def deterministic():
+    """fixed-order BN statistics (no float atomics) for bitwise comparisons"""
+    from pgdist.ops import kernels as K
+    K.set_deterministic(True)
+    yield
+    K.set_deterministic(False)

@@ -159,14 +159,6 @@ def test_native_train_step_fp8_loss_decreases(dev):
     assert losses[-1] < losses[0] * 0.5, losses
 
 
-@pytest.fixture
-def deterministic():
-    from pgdist.ops import kernels as K
-    K.set_deterministic(True)
-    yield
-    K.set_deterministic(False)
-
-
 def _one_step_grad(dev, B=8, S=64):
     from pgdist.engine.native_step import NativeTrainStep
     src = torch.randint(0, 256, (32, 32, 32, 3), dtype=torch.uint8, device=dev,

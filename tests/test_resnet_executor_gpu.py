@@ -94,6 +94,88 @@ def test_resnet_step_matches_autograd(dev, B, S, NC):
     assert _rel(exe.model.bn1.running_mean, ref.bn1.running_mean) < 0.02
 
 
+@pytest.mark.parametrize("M,N,K_,orient", [
+    (128, 1000, 2048, "fwd"), (128, 2048, 1000, "dpool"), (1000, 2048, 128, "dw"),
+    (5, 37, 100, "fwd"), (3, 70, 33, "dpool"), (37, 65, 7, "dw"), (64, 10, 2048, "fwd")])
+def test_fc_gemm_matches_fp32(dev, M, N, K_, orient):
+    """Native fp32 head GEMMs (csrc/kernels/fc.hip) vs torch fp32 matmul (TF32 off), in the three
+    operand orientations of the classifier forward / backward; split-K is deterministic."""
+    from pgdist.ops import kernels as K
+    torch.backends.cuda.matmul.allow_tf32 = False
+    g = torch.Generator(device=dev).manual_seed(M * 7 + N)
+    bias = None
+    if orient == "fwd":       # C = A[M,K] . W[N,K]^T + b
+        A = torch.randn(M, K_, device=dev, generator=g)
+        B = torch.randn(N, K_, device=dev, generator=g)
+        bias = torch.randn(N, device=dev, generator=g)
+        ref = A @ B.t() + bias
+        args = (A, K_, 1, B, 1, K_)
+    elif orient == "dpool":   # C = A[M,K] . B[K,N]
+        A = torch.randn(M, K_, device=dev, generator=g)
+        B = torch.randn(K_, N, device=dev, generator=g)
+        ref = A @ B
+        args = (A, K_, 1, B, N, 1)
+    else:                     # C = A[K,M]^T . B[K,N]
+        A = torch.randn(K_, M, device=dev, generator=g)
+        B = torch.randn(K_, N, device=dev, generator=g)
+        ref = A.t() @ B
+        args = (A, 1, M, B, N, 1)
+    ws = torch.empty(max(K.fc_gemm_workspace_floats(M, N, K_), 1), device=dev)
+    outs = []
+    for _ in range(2):
+        C = torch.full((M, N), float("nan"), device=dev)
+        K.fc_gemm(*args, C, M, N, K_, bias=bias, ws=ws)
+        outs.append(C)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    err = (outs[0] - ref).abs().max().item()
+    assert err <= 1e-5 * (K_ ** 0.5) * ref.abs().max().item() + 1e-5, err
+    X = torch.randn(M, N, device=dev, generator=g)
+    s = torch.empty(N, device=dev)
+    K.col_sum(X, M, N, s)
+    ref_s = X.double().sum(0).float()   # fp32 summation error ~ sqrt(M) ulp
+    assert (s - ref_s).abs().max().item() <= 2e-6 * M ** 0.5 * X.abs().max().item() * 4
+
+
+def test_fc_gemm_rejects_bad_operands(dev):
+    from pgdist.ops import kernels as K
+    A = torch.zeros(4, 8, device=dev)
+    B = torch.zeros(6, 8, device=dev)
+    C = torch.zeros(4, 6, device=dev)
+    with pytest.raises(ValueError, match="strides address"):
+        K.fc_gemm(A, 8, 1, B, 1, 8, C, 4, 6, 9)            # K beyond the operands
+    with pytest.raises(ValueError):
+        K.fc_gemm(A.double(), 8, 1, B, 1, 8, C, 4, 6, 8)
+    with pytest.raises(ValueError):
+        K.fc_gemm(A, 8, 1, B, 1, 8, C[:3], 4, 6, 8)
+
+
+def test_resnet_launch_plan_matches_eager(dev, deterministic, monkeypatch):
+    """The ResNet-50 step replayed from a native launch plan (recorded on the 3rd step; head
+    GEMMs native) gives bitwise the weights, Adam state and metrics of eager launching."""
+    from pgdist.engine.native_step import NativeTrainStep
+    src = torch.randint(0, 256, (16, 64, 64, 3), dtype=torch.uint8, device=dev,
+                        generator=torch.Generator(device=dev).manual_seed(3))
+    labels = torch.arange(16, device=dev) % 10
+    out = {}
+    for plan in ("1", "0"):
+        monkeypatch.setenv("PGDIST_PLAN", plan)
+        torch.manual_seed(0)
+        st = NativeTrainStep(build_model("resnet50", num_classes=10), 8, dev, img_size=64, lr=1e-3,
+                             use_graph=False)
+        assert st.use_plan == (plan == "1")
+        st.set_data(src, labels)
+        for i in range(5):
+            st.run((torch.arange(8, device=dev) + 3 * i) % 16)
+        torch.cuda.synchronize()
+        if plan == "1":
+            assert st.plan is not None and len(st.plan) > 300
+        out[plan] = (st.flat.master.clone(), st.flat.exp_avg.clone(), st.read_metrics())
+    assert torch.equal(out["1"][0], out["0"][0])
+    assert torch.equal(out["1"][1], out["0"][1])
+    assert out["1"][2] == out["0"][2]
+
+
 def test_resnet_native_step_loss_decreases(dev):
     from pgdist.engine.native_step import NativeTrainStep
     torch.manual_seed(0)
