@@ -904,6 +904,184 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs p) {
       }
 }
 
+// ===========================================================================
+// weight gradient on LDS-DMA operands (materialised dy, x without a prologue):
+//   part[z][n][k] = sum_{m in split z} dy[m][n] x[m][k]
+// Both operand tiles are streamed global -> LDS by buffer_load ... lds in their stored
+// (m-major) layout: a stage is 64 rows of dy [TN cols] and 64 gathered rows of x [TK cols of
+// one filter tap], 16-B chunks placed at chunk ^ 2*sw(row) (the swizzle is applied on the
+// source side: lane q of a row fetches chunk q ^ 2*sw(row)).  The MFMA operands are the
+// transposes (dy^T: n x m, x^T: k x m), read with the gfx950 transposing ds_read_b64_tr_b16:
+// a 16-lane group addresses 4 rows x 16 columns and every lane receives one column; rows
+// 8g .. 8g+3 of the two lane halves land in 8 distinct 32-B bank windows under the swizzle
+// (conflict-free).  No register staging, no ds_write: the former transposing stores of
+// conv_wgrad_kernel cost more LDS cycles than its MFMAs.  NBUF-deep stage ring as in
+// conv_glds_kernel; 1-D grid remapped so the workgroups of one m split share an XCD (its L2
+// holds the split's rows once for all (n, k) tiles).
+// ===========================================================================
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
+
+namespace {
+// pair-level swizzle of row r for rows of RB bytes (see above)
+template <int RB>
+PG_DEVICE int wg_sw(int r) {
+  if constexpr (RB == 256) return (r & 3) | (((r >> 3) & 1) << 2);
+  else return ((r >> 1) & 1) | (((r >> 3) & 1) << 1);
+}
+// q = n / d for 0 <= n < 2^24 (float reciprocal + one correction step each way)
+PG_DEVICE int fdiv(int n, int d, float inv) {
+  int q = (int)((float)n * inv);
+  if (q * d > n) --q;
+  else if ((q + 1) * d <= n) ++q;
+  return q;
+}
+}  // namespace
+
+template <int TN, int TK, int NBUF>
+__global__ __launch_bounds__(256) void conv_wgrad_dma_kernel(WgArgs p, int gx, int gy, int total) {
+  constexpr int MK = 64;
+  constexpr int RBN = TN * 2, RBK = TK * 2;              // staged row bytes
+  constexpr int CPN = RBN / 16, CPK = RBK / 16;          // 16-B chunks per row
+  constexpr int PN = MK * RBN / 1024, PK = MK * RBK / 1024;   // 1-KiB pieces per stage
+  constexpr int PNW = PN / 4, PKW = PK / 4, PW = PNW + PKW;   // per wave
+  constexpr int DBYTES = MK * RBN, SBYTES = MK * (RBN + RBK);
+  constexpr int QN = TN / 2, QK = TK / 2, RN = QN / 16, RK = QK / 16;
+  static_assert(PN % 4 == 0 && PK % 4 == 0, "whole pieces per wave");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave >> 1, wk = wave & 1;
+  // XCD-aware tile order: hardware ids go round-robin over the 8 XCDs; logical ids of one XCD
+  // are contiguous, and a split's (n, k) tiles are contiguous logical ids
+  int L = blockIdx.x;
+  if (total % 8 == 0) L = (L % 8) * (total / 8) + L / 8;
+  const int bx = L % gx, by = (L / gx) % gy, bz = L / (gx * gy);
+  const int n0 = bx * TN, k0 = by * TK;
+  const int mbeg = bz * p.rows_per_split;
+  const int mend = min(p.M, mbeg + p.rows_per_split);
+  const int nsteps = (mend - mbeg + MK - 1) / MK;
+  const int HWo = p.Ho * p.Wo;
+  const float inv_hw = 1.f / (float)HWo, inv_w = 1.f / (float)p.Wo;
+  // this k tile lies inside one filter tap (Ci % TK == 0)
+  const int tap = k0 / p.Ci, ci0 = k0 - tap * p.Ci;
+  const int tr = tap / p.S, ts = tap - tr * p.S;
+  const rsrc_t rg = make_rsrc(p.G, (uint32_t)((size_t)p.M * p.N * 2));
+  const rsrc_t rx = make_rsrc(p.X, (uint32_t)((size_t)(p.M / HWo) * p.Hi * p.Wi * p.Ci * 2));
+  // this lane's rows / source chunks in its pieces
+  const int drow0 = lane / CPN, dq = lane % CPN;
+  const int xrow0 = lane / CPK, xq = lane % CPK;
+
+  auto issue = [&](int step, int buf) {
+    const int m0 = mbeg + step * MK;
+    char *dbase = smem + buf * SBYTES;
+    char *xbase = dbase + DBYTES;
+#pragma unroll
+    for (int i = 0; i < PNW; ++i) {
+      const int piece = wave * PNW + i;
+      const int row = piece * (1024 / RBN) + drow0;
+      const int c = dq ^ (2 * wg_sw<RBN>(row));
+      const int m = m0 + row;
+      const uint32_t off = m < mend ? (uint32_t)(((size_t)m * p.N + n0 + c * 8) * 2) : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rg, (__attribute__((address_space(3))) void *)(dbase + piece * 1024), 16,
+                                               off, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < PKW; ++i) {
+      const int piece = wave * PKW + i;
+      const int row = piece * (1024 / RBK) + xrow0;
+      const int c = xq ^ (2 * wg_sw<RBK>(row));
+      const int m = m0 + row;
+      uint32_t off = kOOB;
+      if (m < mend) {
+        const int b = fdiv(m, HWo, inv_hw), rem = m - b * HWo;
+        const int oh = fdiv(rem, p.Wo, inv_w), ow = rem - oh * p.Wo;
+        const int ih = oh * p.stride - p.pad + tr, iw = ow * p.stride - p.pad + ts;
+        if (ih >= 0 && ih < p.Hi && iw >= 0 && iw < p.Wi)
+          off = (uint32_t)(((((size_t)b * p.Hi + ih) * p.Wi + iw) * p.Ci + ci0 + c * 8) * 2);
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) void *)(xbase + piece * 1024), 16,
+                                               off, 0, 0, 0);
+    }
+  };
+
+  f32x4_t acc[RN][RK];
+#pragma unroll
+  for (int a = 0; a < RN; ++a)
+#pragma unroll
+    for (int b = 0; b < RK; ++b) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  // transposed-read addressing: lane (i = lane & 15, g = lane >> 4) reads rows trow, trow + 4
+  // (+32 per sub-step), 8-B column piece tcol of a 16-column block; the swizzle term is the
+  // same for all of this lane's rows (sw ignores bit 2 and bits >= 4)
+  const int trow = 8 * (lane >> 4) + ((lane & 15) >> 2);
+  const int tc = lane & 3;                          // 8-B piece: chunk 2*blk + (tc >> 1), half tc & 1
+  const int swn = 2 * wg_sw<RBN>(trow), swk = 2 * wg_sw<RBK>(trow);
+  auto mma = [&](int buf) {
+    const char *Db = smem + buf * SBYTES;
+    const char *Xb = Db + DBYTES;
+#pragma unroll
+    for (int sub = 0; sub < MK / 32; ++sub) {
+      s16x8_t af[RN], bfr[RK];
+#pragma unroll
+      for (int a = 0; a < RN; ++a) {
+        const int blk = (wn * QN + a * 16) / 8;     // first chunk of the 16-column block
+        const char *pa = Db + (sub * 32 + trow) * RBN + (((blk + (tc >> 1)) ^ swn) * 16) + (tc & 1) * 8;
+        const s16x4_t a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)pa);
+        const s16x4_t a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)(pa + 4 * RBN));
+        af[a] = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int b = 0; b < RK; ++b) {
+        const int blk = (wk * QK + b * 16) / 8;
+        const char *pb = Xb + (sub * 32 + trow) * RBK + (((blk + (tc >> 1)) ^ swk) * 16) + (tc & 1) * 8;
+        const s16x4_t b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)pb);
+        const s16x4_t b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t *)(pb + 4 * RBK));
+        bfr[b] = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int a = 0; a < RN; ++a)
+#pragma unroll
+        for (int b = 0; b < RK; ++b) acc[a][b] = mfma16(af[a], bfr[b], acc[a][b]);
+    }
+  };
+
+  if constexpr (NBUF == 2) {
+    if (nsteps > 0) issue(0, 0);
+    for (int s = 0; s < nsteps; ++s) {
+      const int buf = s & 1;
+      if (s + 1 < nsteps) {
+        issue(s + 1, buf ^ 1);
+        glds_wait_barrier<PW>();
+      } else {
+        glds_wait_barrier<0>();
+      }
+      mma(buf);
+      glds_wait_barrier<PW>();
+    }
+  } else {
+    if (nsteps > 0) issue(0, 0);
+    if (nsteps > 1) issue(1, 1);
+    int buf = 0, nbuf = 2;
+    for (int s = 0; s < nsteps; ++s) {
+      if (s + 1 < nsteps) glds_wait_barrier<PW>();
+      else glds_wait_barrier<0>();
+      if (s + 2 < nsteps) issue(s + 2, nbuf);
+      mma(buf);
+      buf = buf == NBUF - 1 ? 0 : buf + 1;
+      nbuf = nbuf == NBUF - 1 ? 0 : nbuf + 1;
+    }
+  }
+  float *dst = p.out + (size_t)bz * p.N * p.Kw;
+#pragma unroll
+  for (int a = 0; a < RN; ++a)
+#pragma unroll
+    for (int b = 0; b < RK; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wn * QN + a * 16 + 4 * (lane >> 4) + j;
+        const int k = k0 + wk * QK + b * 16 + (lane & 15);
+        if (n < p.N) dst[(size_t)n * p.Kw + k] = acc[a][b][j];
+      }
+}
 
 // ===========================================================================
 // weight transposes for dgrad: dst[ci][t][co] = src[co][t][ci]  (bf16, batched by table)
@@ -1389,13 +1567,30 @@ namespace {
 struct WgGeom {
   int TN, TK, nsplit, rows;
 };
-WgGeom wg_geom(int N, int Kw, int M) {
+// LDS-DMA weight gradient (conv_wgrad_dma_kernel): materialised dy, x without a prologue,
+// Ci and N multiples of 64.  PGDIST_WG_DMA=0: off.
+bool wg_dma_ok(bool dm, int xpro, int Ci, int N) {
+  static const bool on = [] { const char *e = getenv("PGDIST_WG_DMA"); return !e || atoi(e) != 0; }();
+  return on && dm && xpro == CP_NONE && Ci % 64 == 0 && N % 64 == 0;
+}
+int wg_dma_nbuf() {
+  static const int v = [] { const char *e = getenv("PGDIST_WG_DMA_NBUF"); return e && atoi(e) == 3 ? 3 : 2; }();
+  return v;
+}
+
+WgGeom wg_geom(int N, int Kw, int M, bool dma = false, int Ci = 0) {
   WgGeom g{};
-  g.TN = N >= 128 ? 128 : 64;
-  g.TK = Kw >= 128 ? 128 : 64;
+  if (dma) {
+    g.TN = N % 128 == 0 ? 128 : 64;
+    g.TK = Ci % 128 == 0 ? 128 : 64;
+  } else {
+    g.TN = N >= 128 ? 128 : 64;
+    g.TK = Kw >= 128 ? 128 : 64;
+  }
   const long long tiles = (long long)((N + g.TN - 1) / g.TN) * ((Kw + g.TK - 1) / g.TK);
   static const int target = [] { const char *e = getenv("PGDIST_WG_TARGET"); return e ? atoi(e) : 1024; }();
-  long long ns = (target + tiles - 1) / tiles;
+  static const int target_dma = [] { const char *e = getenv("PGDIST_WGD_TARGET"); return e ? atoi(e) : 512; }();
+  long long ns = ((dma ? target_dma : target) + tiles - 1) / tiles;
   const long long max_ns = (M + 4 * kWgMK - 1) / (4 * kWgMK);   // >= 4 steps per split
   if (ns > max_ns) ns = max_ns;
   if (ns < 1) ns = 1;
@@ -1410,9 +1605,15 @@ void launch_wgrad_reduce(float *part, int S, long long n, float *grad, hipStream
 
 long long conv_wgrad_workspace_floats(int Nb, int H, int W, int Ci, int N, int R, int S, int st, int pad) {
   const int Ho = (H + 2 * pad - R) / st + 1, Wo = (W + 2 * pad - S) / st + 1;
-  const WgGeom g = wg_geom(N, R * S * Ci, Nb * Ho * Wo);
-  if (g.nsplit == 1) return 0;
-  return (long long)(g.nsplit + colsum_rows(g.nsplit)) * N * R * S * Ci;
+  long long need = 0;
+  for (int dma = 0; dma < 2; ++dma) {   // either kernel may run (dy materialised or not)
+    if (dma && !wg_dma_ok(true, CP_NONE, Ci, N)) continue;
+    const WgGeom g = wg_geom(N, R * S * Ci, Nb * Ho * Wo, dma != 0, Ci);
+    if (g.nsplit == 1) continue;
+    const long long n = (long long)(g.nsplit + colsum_rows(g.nsplit)) * N * R * S * Ci;
+    need = n > need ? n : need;
+  }
+  return need;
 }
 
 // dW [N][R][S][Ci] (fp32, overwritten) of y = conv(x);  G, Y [Nb][Ho][Wo][N];  x [Nb][H][W][Ci]
@@ -1428,11 +1629,34 @@ void launch_conv_wgrad(const bf16_t *G, const bf16_t *Y, const float *ga, const 
   a.R = R; a.S = S; a.stride = st; a.pad = pad;
   a.Kw = R * S * Ci;
   a.M = Nb * a.Ho * a.Wo;
+  const bool dm = Y == nullptr;   // G is the materialised dy (launch_bn_mat)
+  if (wg_dma_ok(dm, xpro, Ci, N)) {
+    const WgGeom g = wg_geom(N, a.Kw, a.M, true, Ci);
+    a.rows_per_split = g.rows;
+    a.out = g.nsplit == 1 ? grad : ws;
+    const int gx = N / g.TN, gy = a.Kw / g.TK, total = gx * gy * g.nsplit;
+    const size_t lds = (size_t)wg_dma_nbuf() * 64 * (g.TN + g.TK) * 2;
+#define WGD_L(TN_, TK_)                                                                                         \
+  do {                                                                                                         \
+    if (wg_dma_nbuf() == 3)                                                                                    \
+      hipLaunchKernelGGL((conv_wgrad_dma_kernel<TN_, TK_, 3>), dim3(total), dim3(256), lds, stream, a, gx, gy, \
+                         total);                                                                               \
+    else                                                                                                       \
+      hipLaunchKernelGGL((conv_wgrad_dma_kernel<TN_, TK_, 2>), dim3(total), dim3(256), lds, stream, a, gx, gy, \
+                         total);                                                                               \
+  } while (0)
+    if (g.TN == 128 && g.TK == 128) WGD_L(128, 128);
+    else if (g.TN == 128) WGD_L(128, 64);
+    else if (g.TK == 128) WGD_L(64, 128);
+    else WGD_L(64, 64);
+#undef WGD_L
+    if (g.nsplit > 1) launch_wgrad_reduce(ws, g.nsplit, (long long)N * a.Kw, grad, stream);
+    return;
+  }
   const WgGeom g = wg_geom(N, a.Kw, a.M);
   a.rows_per_split = g.rows;
   a.out = g.nsplit == 1 ? grad : ws;
   const dim3 grid((N + g.TN - 1) / g.TN, (a.Kw + g.TK - 1) / g.TK, g.nsplit);
-  const bool dm = Y == nullptr;   // G is the materialised dy (launch_bn_mat)
 #define WG_L(XP, TN_, TK_, CV_)                                                                                  \
   do {                                                                                                          \
     if (dm) hipLaunchKernelGGL((conv_wgrad_kernel<XP, TN_, TK_, CV_, true>), grid, dim3(256), 0, stream, a);     \

@@ -158,7 +158,10 @@ class ResNet50Executor:
         # ---------------- materialised operands of the LDS-DMA convs
         self.mat = K.conv_get_glds() != 0 and os.environ.get("PGDIST_RN_MAT", "1") != "0"
         act_mode = os.environ.get("PGDIST_RN_ACT", "auto")
-        dy_mode = os.environ.get("PGDIST_RN_DY", "auto")
+        # every dy materialised: the weight gradients then run on the LDS-DMA kernel
+        # (conv_wgrad_dma_kernel), which the extra bn_mat pass more than pays for
+        # (bench step 12.48 -> 12.28 ms on MI355X vs the per-layer "auto" policy)
+        dy_mode = os.environ.get("PGDIST_RN_DY", "all")
         if self.mat:
             for bp in self.blocks:
                 for c in (bp.c1, bp.c2, bp.c3) + ((bp.cd,) if bp.cd else ()):

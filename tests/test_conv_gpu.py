@@ -217,6 +217,9 @@ WGRAD_SHAPES = [
     (2, 8, 64, 256, 1, 2, 0),
     (8, 14, 128, 128, 3, 1, 1),
     (2, 7, 512, 2048, 1, 1, 0),
+    (16, 28, 128, 256, 3, 1, 1),    # many m splits (LDS-DMA wgrad with materialised dy)
+    (32, 14, 256, 64, 1, 1, 0),
+    (8, 28, 64, 128, 3, 2, 1),
 ]
 
 
