@@ -11,6 +11,7 @@ Here those are presets of one :class:`TrainConfig`.
 """
 import argparse
 import dataclasses
+import typing
 from dataclasses import dataclass, field
 from typing import Optional, Tuple
 
@@ -99,9 +100,14 @@ def add_cli_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
         elif f.name == "betas":
             p.add_argument(name, dest=f.name, type=float, nargs=2, default=None)
         else:
-            typ = {"int": int, "float": float}.get(str(f.type), None)
+            t = f.type
+            args = [a for a in typing.get_args(t) if a is not type(None)]   # Optional[X] -> X
+            if len(args) == 1:
+                t = args[0]
+            typ = {"int": int, "float": float, "Optional[int]": int,
+                   "Optional[float]": float}.get(str(t), None)
             if typ is None:
-                typ = int if f.type is int else float if f.type is float else str
+                typ = int if t is int else float if t is float else str
             p.add_argument(name, dest=f.name, type=typ, default=None)
     return p
 

@@ -327,6 +327,8 @@ class Trainer:
             if cfg.ckpt_dir and self.rank == 0:
                 self._save_full(epoch + 1, lr)
         total = time.time() - total
+        if self.world > 1:
+            self.replica_check()
         L.emit("", self.rank)
         L.emit(L.best_line(self.best_acc, self.ddp_log), self.rank)
         L.emit(L.total_time_line(total), self.rank)
@@ -339,6 +341,23 @@ class Trainer:
         if self.watchdog is not None:
             self.watchdog.stop()
         return history
+
+    def replica_check(self):
+        """Data-parallel consistency: parameters (and, with bn_sync eval/broadcast, the BN running
+        statistics that evaluation synchronises) must be bitwise identical on every rank."""
+        from ..parallel.ddp import replicas_identical
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        params = [self.step.flat.master] if self.backend == "hip" else \
+            [p for p in self.model.parameters()]
+        ok_p, dp = replicas_identical(params, self.device)
+        bufs = self._bn_buffers()
+        ok_b, db = replicas_identical(bufs, self.device)
+        self.replicas_ok = (ok_p, ok_b)
+        L.emit(f"[pgdist] replica check over {self.world} ranks: parameters "
+               f"{'identical' if ok_p else 'DIFFER'} (digest {int(dp[0]):x}), BN buffers "
+               f"{'identical' if ok_b else 'DIFFER'} (digest {int(db[0]):x}, bn_sync={self.cfg.bn_sync})",
+               self.rank)
 
     # ------------------------------------------------------------------ checkpoint/resume
     def _adam_step(self) -> int:

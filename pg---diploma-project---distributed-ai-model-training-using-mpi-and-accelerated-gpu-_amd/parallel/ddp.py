@@ -230,6 +230,32 @@ def verify_shapes(shapes: Sequence[Tuple[int, ...]], group=None):
             raise RuntimeError(f"parameter shapes differ between this rank and rank {r}")
 
 
+def replica_digest(tensors: Sequence[torch.Tensor]) -> List[float]:
+    """Bitwise digest of a list of tensors: per tensor a position-weighted sum of its raw 32-bit
+    words (int64 arithmetic, exact) folded into one number, plus the fp64 value sum.  Two
+    replicas with equal digests hold the same bits with overwhelming probability."""
+    h, s = 0, 0.0
+    for i, t in enumerate(tensors):
+        t = t.detach().contiguous()
+        raw = t.view(-1).view(torch.uint8)
+        pad = (-raw.numel()) % 4
+        if pad:
+            raw = torch.cat([raw, raw.new_zeros(pad)])
+        w = raw.view(torch.int32).to(torch.int64)
+        pos = torch.arange(w.numel(), device=w.device, dtype=torch.int64) % 65521 + 1
+        h = (h * 1000003 + int((w * pos).sum().item()) + i) % (1 << 52)
+        s += float(t.double().sum().item()) if t.is_floating_point() else float(t.sum().item())
+    return [float(h), s]
+
+
+def replicas_identical(tensors: Sequence[torch.Tensor], device, group=None):
+    """(identical, digest): the digests of every rank agree (MIN == MAX all-reduce)."""
+    d = replica_digest(tensors)
+    lo = all_reduce_scalars(d, device, op=dist.ReduceOp.MIN, group=group)
+    hi = all_reduce_scalars(d, device, op=dist.ReduceOp.MAX, group=group)
+    return lo == hi, d
+
+
 def all_reduce_scalars(values: Sequence[float], device, op=None, group=None) -> List[float]:
     """fp64 metric all-reduce (reference :187-196, :215-224)."""
     t = torch.tensor(list(values), dtype=torch.float64, device=device)

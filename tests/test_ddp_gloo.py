@@ -90,7 +90,7 @@ def _worker_trainer(rank, world, port, tmp, bn_sync, q):
     allrs = [torch.zeros_like(rs) for _ in range(world)]
     dist.all_gather(allrs, rs)
     q.put(("ok", rank, max((a - w).abs().max().item() for a in allw), tr.history[-1]["train_images"],
-           max((a - rs).abs().max().item() for a in allrs)))
+           max((a - rs).abs().max().item() for a in allrs), tr.replicas_ok))
     dist.destroy_process_group()
 
 
@@ -98,9 +98,10 @@ def _worker_trainer(rank, world, port, tmp, bn_sync, q):
 def test_trainer_two_ranks_keeps_replicas_in_sync(tmp_path, bn_sync):
     world, port = 2, _free_port()
     res = run_ranks(_worker_trainer, world, (world, port, str(tmp_path), bn_sync), expect=world, timeout=300)
-    for _, rank, diff, n, bn_diff in res:
+    for _, rank, diff, n, bn_diff, rep_ok in res:
         assert diff == 0.0
         assert n == 48
+        assert rep_ok == (True, bn_sync != "none")   # Trainer.replica_check agrees with the gather
         if bn_sync == "none":       # rank-local running statistics (different shards)
             assert bn_diff > 0.0
         else:                       # rank-0 statistics broadcast (reference DDP broadcast_buffers)
