@@ -471,14 +471,28 @@ PG_DEVICE void glds_wait_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
-template <int MODE, int EPI, int BM, int BN, int NBUF>
+// KS = 32 (64-B staged rows, 16 rows per piece): half the LDS per stage, so twice the
+// workgroups per CU at the same ring depth -- the 64-wide loop is latency-bound at two
+// workgroups per CU (PMC: 34 % of wave cycles parked at s_waitcnt / s_barrier).  Chunk kc of
+// row r sits at kc ^ f(r), f(r) = (4 - ((r >> 2) & 3)) & 3: the four rows of a 16-lane
+// ds_read_b128 group that share a bank window get distinct chunk slots.
+template <int KS>
+PG_DEVICE int glds_sw(int r) {
+  if constexpr (KS == 64) return r & 7;
+  else return (4 - ((r >> 2) & 3)) & 3;
+}
+
+template <int MODE, int EPI, int BM, int BN, int NBUF, int KS = 64>
 __global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs p) {
-  constexpr int KS = 64, ROWB = KS * 2;              // 128-B staged rows
-  constexpr int APW = BM / 32, BPW = BN / 32;         // 1-KiB pieces per wave per k-step
+  constexpr int ROWB = KS * 2;                        // staged row bytes
+  constexpr int RPP = 1024 / ROWB, CPR = ROWB / 16;   // rows per 1-KiB piece, 16-B chunks per row
+  constexpr int APW = BM / RPP / 4, BPW = BN / RPP / 4;   // pieces per wave per k-step
   constexpr int PW = APW + BPW;
   constexpr int RT = BM / 32, CTW = BN / 32;
   constexpr int ABYTES = BM * ROWB, BUFB = (BM + BN) * ROWB;
-  static_assert(NBUF == 2 || NBUF == 3, "2 or 3 LDS buffers");
+  static_assert(NBUF >= 2 && NBUF <= 4, "2 to 4 LDS buffers");
+  static_assert(KS == 32 || KS == 64, "k-step 32 or 64");
+  static_assert(APW >= 1 && BPW >= 1, "whole pieces per wave");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -502,8 +516,8 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs p) {
   const int Kc = MODE == CM_DGRAD ? p.ntap[cls] * p.Ci : p.K;
   const int nk = Kc / KS;
   const int HWc = p.Hc * p.Wc;
-  const int lrow = lane >> 3;                 // row of this lane inside a 1-KiB piece
-  const int lch = (lane & 7) ^ lrow;          // k-chunk this lane fetches (source swizzle)
+  const int lrow = lane / CPR;                          // row of this lane inside a 1-KiB piece
+  const int lch = (lane % CPR) ^ glds_sw<KS>(lrow);     // k-chunk this lane fetches (source swizzle)
   const rsrc_t ra = make_rsrc(p.A, (uint32_t)p.Nb * p.Hi * p.Wi * p.Ci * 2);
   const rsrc_t rw = make_rsrc(p.W, (uint32_t)p.N * p.Kw * 2);
 
@@ -511,7 +525,7 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs p) {
   int rb[APW], rh[APW], rwc[APW];
 #pragma unroll
   for (int i = 0; i < APW; ++i) {
-    const int m = m0 + (wave * APW + i) * 8 + lrow;
+    const int m = m0 + (wave * APW + i) * RPP + lrow;
     if (m < p.Mc) {
       const int b = m / HWc, rem = m % HWc, hh = rem / p.Wc, ww = rem % p.Wc;
       rb[i] = b;
@@ -524,7 +538,7 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs p) {
   uint32_t wrow[BPW];   // weight row byte offsets (kOOB past N)
 #pragma unroll
   for (int i = 0; i < BPW; ++i) {
-    const int n = n0 + (wave * BPW + i) * 8 + lrow;
+    const int n = n0 + (wave * BPW + i) * RPP + lrow;
     wrow[i] = n < p.N ? (uint32_t)n * p.Kw * 2 : kOOB;
   }
 
@@ -564,13 +578,14 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs p) {
 #pragma unroll
     for (int c = 0; c < CTW; ++c) acc[r][c] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   // fragment reads: row (lane & 15) of a 16-row block, k-chunk kc = 4*sub + (lane >> 4) stored at
-  // position kc ^ (row & 7) = kc ^ (lane & 7)
+  // position kc ^ glds_sw(row) (16-row blocks start at multiples of every swizzle period)
+  const int fsw = glds_sw<KS>(lane & 15);
   auto mma = [&](int buf) {
     const char *Ab = smem + buf * BUFB;
     const char *Bb = Ab + ABYTES;
 #pragma unroll
     for (int sub = 0; sub < KS / 32; ++sub) {
-      const int pos = ((4 * sub + (lane >> 4)) ^ (lane & 7)) * 16;
+      const int pos = ((4 * sub + (lane >> 4)) ^ fsw) * 16;
       s16x8_t af[RT];
 #pragma unroll
       for (int r = 0; r < RT; ++r)
@@ -599,16 +614,20 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs p) {
       glds_wait_barrier<PW>();          // every wave done reading buf before it is refilled
     }
   } else {
-    if (nk > 0) issue(0, 0);
-    if (nk > 1) issue(1, 1);
-    int buf = 0, nbuf = 2;
+    // ring: NBUF - 1 stages in flight; one barrier per k-step (stage ks landed everywhere AND
+    // every wave is done with stage ks - 1, whose buffer the next issue refills)
+#pragma unroll
+    for (int s = 0; s < NBUF - 1; ++s)
+      if (s < nk) issue(s, s);
+    int buf = 0, nbuf = NBUF - 1;
     for (int ks = 0; ks < nk; ++ks) {
-      if (ks + 1 < nk) glds_wait_barrier<PW>();
+      if (ks + NBUF - 2 < nk) glds_wait_barrier<(NBUF - 2) * PW>();
+      else if (NBUF == 4 && ks + 1 < nk) glds_wait_barrier<PW>();
       else glds_wait_barrier<0>();
-      if (ks + 2 < nk) issue(ks + 2, nbuf);
+      if (ks + NBUF - 1 < nk) issue(ks + NBUF - 1, nbuf);
       mma(buf);
-      buf = buf == 2 ? 0 : buf + 1;
-      nbuf = nbuf == 2 ? 0 : nbuf + 1;
+      buf = buf == NBUF - 1 ? 0 : buf + 1;
+      nbuf = nbuf == NBUF - 1 ? 0 : nbuf + 1;
     }
     glds_wait_barrier<0>();             // every wave done reading before the C tile reuses LDS
   }
@@ -1429,28 +1448,44 @@ void launch_geom(const ConvArgs &a, const Geom &g, hipStream_t st) {
 int conv_glds_default() {
   const char *e = getenv("PGDIST_CONV_GLDS");
   const int v = e ? atoi(e) : 2;
-  return v == 0 || v == 3 ? v : 2;
+  return v == 0 || v == 3 || v == 4 ? v : 2;
 }
 int g_conv_glds = conv_glds_default();
 bool glds_ok(int Ci) { return g_conv_glds != 0 && Ci % 64 == 0; }
 int glds_nbuf() { return g_conv_glds; }
 
-template <int MODE, int EPI, int BM, int BN, int NBUF>
+template <int MODE, int EPI, int BM, int BN, int NBUF, int KS>
 void launch_glds_t(const ConvArgs &a, const Geom &g, hipStream_t st) {
-  size_t lds = (size_t)NBUF * (BM + BN) * 128;
+  size_t lds = (size_t)NBUF * (BM + BN) * KS * 2;
   const size_t ctile = (size_t)BM * (BN + 8) * 2, red = (size_t)(256 / (BN / 8)) * BN * 4;
   if (ctile > lds) lds = ctile;
   if (red > lds) lds = red;
-  hipLaunchKernelGGL((conv_glds_kernel<MODE, EPI, BM, BN, NBUF>), dim3(g.nmt * g.nt, g.ncls), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((conv_glds_kernel<MODE, EPI, BM, BN, NBUF, KS>), dim3(g.nmt * g.nt, g.ncls), dim3(256), lds, st,
+                     a);
 }
 
+// LDS-DMA k-step: PGDIST_CONV_KS = 64 (default) | 32; ring depth PGDIST_CONV_GLDS (2..4)
+int glds_ks() {
+  static const int v = [] { const char *e = getenv("PGDIST_CONV_KS"); return e && atoi(e) == 32 ? 32 : 64; }();
+  return v;
+}
+
+// (256 x 128 tiles, one workgroup of 4 waves per CU at 2 or 3 LDS stages, measured slower on
+// every ResNet-50 layer: forward network total 2826 -> 3150 us, dgrad 3875 -> 4533 us; the
+// loop is latency-bound at one wave per SIMD, not operand-bandwidth-bound -- docs/PERF_NOTES.md)
 template <int MODE, int EPI>
 void launch_glds(const ConvArgs &a, const Geom &g, hipStream_t st) {
-  const bool three = glds_nbuf() == 3;
+  const int nb = glds_nbuf();
 #define LG_GLDS(BM_, BN_)                                                                               \
   if (g.BM == BM_ && g.BN == BN_) {                                                                     \
-    if (three) launch_glds_t<MODE, EPI, BM_, BN_, 3>(a, g, st);                                          \
-    else launch_glds_t<MODE, EPI, BM_, BN_, 2>(a, g, st);                                                \
+    if (glds_ks() == 32) {                                                                              \
+      if (nb == 4) launch_glds_t<MODE, EPI, BM_, BN_, 4, 32>(a, g, st);                                  \
+      else if (nb == 3) launch_glds_t<MODE, EPI, BM_, BN_, 3, 32>(a, g, st);                             \
+      else launch_glds_t<MODE, EPI, BM_, BN_, 2, 32>(a, g, st);                                          \
+    } else {                                                                                            \
+      if (nb == 3) launch_glds_t<MODE, EPI, BM_, BN_, 3, 64>(a, g, st);                                  \
+      else launch_glds_t<MODE, EPI, BM_, BN_, 2, 64>(a, g, st);                                          \
+    }                                                                                                   \
     return;                                                                                             \
   }
   LG_GLDS(128, 128)
