@@ -36,7 +36,8 @@ def _to_uint8_rgb(img) -> np.ndarray:
 
 def eval_transform(arr: np.ndarray, size: int = 224, mean=IMAGENET_MEAN, std=IMAGENET_STD) -> torch.Tensor:
     """uint8 HWC -> normalised float [1,3,size,size] (Resize((size,size)) + ToTensor + Normalize)."""
-    x = torch.from_numpy(arr).permute(2, 0, 1).float().div(255.0)[None]
+    x = torch.from_numpy(np.ascontiguousarray(arr) if arr.flags.writeable else arr.copy())
+    x = x.permute(2, 0, 1).float().div(255.0)[None]
     x = F.interpolate(x, size=(size, size), mode="bilinear", align_corners=False)
     m = torch.tensor(mean).view(1, 3, 1, 1)
     s = torch.tensor(std).view(1, 3, 1, 1)
