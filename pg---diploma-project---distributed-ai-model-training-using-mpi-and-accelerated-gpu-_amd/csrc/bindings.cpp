@@ -115,7 +115,7 @@ void launch_conv_wt(const bf16_t *, bf16_t *, const int *, int, hipStream_t);
 void launch_bn_mat(int, const bf16_t *, const bf16_t *, const float *, const float *, const float *, bf16_t *, int, int,
                    hipStream_t);
 void launch_res_out(const bf16_t *, const float *, const float *, const bf16_t *, const float *, const float *,
-                    bf16_t *, long long, int, hipStream_t);
+                    bf16_t *, long long, int, const void *, const void *, hipStream_t);
 void launch_maxpool_fwd(const bf16_t *, const float *, const float *, bf16_t *, uint8_t *, int, int, int, int,
                         hipStream_t);
 int maxpool_bwd_num_partials(int, int, int);
@@ -129,7 +129,13 @@ void launch_fc_gemm(const float *, long long, long long, const float *, long lon
                     int, int, int, float *, hipStream_t);
 void launch_col_sum(const float *, int, int, float *, hipStream_t);
 void launch_image_prep(const uint8_t *, const long long *, const long long *, int, int, int, unsigned long long,
-                       const float *, bf16_t *, long long *, hipStream_t);
+                       const float *, bf16_t *, long long *, int, hipStream_t);
+void launch_stem_w_s2d(const bf16_t *, bf16_t *, int, hipStream_t);
+void launch_s2d_image(const bf16_t *, bf16_t *, int, int, int, hipStream_t);
+void launch_conv_fwd_s2d(const bf16_t *, const bf16_t *, bf16_t *, float *, int, int, int, hipStream_t);
+long long conv_wgrad_s2d_workspace_floats(int, int, int);
+void launch_conv_wgrad_s2d(const bf16_t *, const bf16_t *, const float *, const float *, const float *,
+                           const bf16_t *, float *, float *, int, int, int, hipStream_t);
 
 template <typename T>
 static T *ptr(P p) { return reinterpret_cast<T *>(p); }
@@ -375,10 +381,10 @@ PYBIND11_MODULE(_pgdist_C, m) {
       launch_conv_wt(ptr<bf16_t>(src), ptr<bf16_t>(dst), ptr<int>(tab), n, S(s));
     });
   });
-  m.def("res_out", [](P y, P sc, P sh, P r, P rs, P rt, P out, long long M, int C, P s) {
+  m.def("res_out", [](P y, P sc, P sh, P r, P rs, P rt, P out, long long M, int C, P lz, P lz2, P s) {
     pgdist_rt::run_op([=] {
       launch_res_out(ptr<bf16_t>(y), ptr<float>(sc), ptr<float>(sh), ptr<bf16_t>(r), ptr<float>(rs),
-                     ptr<float>(rt), ptr<bf16_t>(out), M, C, S(s));
+                     ptr<float>(rt), ptr<bf16_t>(out), M, C, ptr<void>(lz), ptr<void>(lz2), S(s));
     });
   });
   m.def("maxpool_fwd", [](P y, P sc, P sh, P out, P idx, int Nb, int H, int W, int C, P s) {
@@ -423,10 +429,29 @@ PYBIND11_MODULE(_pgdist_C, m) {
     pgdist_rt::run_op([=] { launch_col_sum(ptr<float>(X), M, N, ptr<float>(out), S(s)); });
   });
   m.def("image_prep", [](P src, P idx, P lab_src, int B, int H, int W, unsigned long long seed, P hyper, P out,
-                         P lab_out, P s) {
+                         P lab_out, int s2d, P s) {
     pgdist_rt::run_op([=] {
       launch_image_prep(ptr<uint8_t>(src), ptr<long long>(idx), ptr<long long>(lab_src), B, H, W, seed,
-                        ptr<float>(hyper), ptr<bf16_t>(out), ptr<long long>(lab_out), S(s));
+                        ptr<float>(hyper), ptr<bf16_t>(out), ptr<long long>(lab_out), s2d, S(s));
+    });
+  });
+  // space-to-depth ResNet stem (kernels/conv.hip)
+  m.def("stem_w_s2d", [](P w, P w2, int N, P s) {
+    pgdist_rt::run_op([=] { launch_stem_w_s2d(ptr<bf16_t>(w), ptr<bf16_t>(w2), N, S(s)); });
+  });
+  m.def("s2d_image", [](P img, P x2, int B, int H, int W, P s) {
+    pgdist_rt::run_op([=] { launch_s2d_image(ptr<bf16_t>(img), ptr<bf16_t>(x2), B, H, W, S(s)); });
+  });
+  m.def("conv_fwd_s2d", [](P x2, P w2, P y, P part, int Nb, int H2, int N, P s) {
+    pgdist_rt::run_op([=] {
+      launch_conv_fwd_s2d(ptr<bf16_t>(x2), ptr<bf16_t>(w2), ptr<bf16_t>(y), ptr<float>(part), Nb, H2, N, S(s));
+    });
+  });
+  m.def("conv_wgrad_s2d_workspace_floats", &conv_wgrad_s2d_workspace_floats);
+  m.def("conv_wgrad_s2d", [](P G, P Y, P ga, P gb, P gc, P x2, P ws, P grad, int Nb, int H2, int N, P s) {
+    pgdist_rt::run_op([=] {
+      launch_conv_wgrad_s2d(ptr<bf16_t>(G), ptr<bf16_t>(Y), ptr<float>(ga), ptr<float>(gb), ptr<float>(gc),
+                            ptr<bf16_t>(x2), ptr<float>(ws), ptr<float>(grad), Nb, H2, N, S(s));
     });
   });
 

@@ -26,6 +26,7 @@
 // the current step's MFMAs.  When Ci % KSTEP == 0 a k-step lies inside one filter tap, so
 // the tap decomposition is one scalar division per step.  Workgroup ids put the N tiles
 // of one M tile 8 ids apart (same XCD L2; T1 of the CDNA guide).
+#include "../bnfin.h"
 #include "../common.h"
 
 #include <cstdlib>
@@ -59,6 +60,9 @@ struct ConvArgs {
   int Hc, Wc;           // dgrad: class image (Ho / st, Wo / st); fwd: Ho, Wo
   int nmt;              // M tiles per class
   int Nb;               // images (operand extents for the buffer descriptors)
+  int bn_rep;           // BN-statistics replica rows (g_bn_rep): P = ncls * nmt partial rows are
+                        // added atomically into min(P, bn_rep) rows of a zeroed accumulator;
+                        // bn_rep >= P (deterministic mode): one plainly stored row per tile
   int ntap[4];
   signed char tr[4][9], ts[4][9], tdh[4][9], tdw[4][9];
 };
@@ -76,6 +80,20 @@ PG_DEVICE void ld8f(const float *p, float (&v)[8]) {
   const float4 a = *reinterpret_cast<const float4 *>(p), b = *reinterpret_cast<const float4 *>(p + 4);
   v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
   v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+// Lazy BN finalize (bnfin.h bn_lazy) of channels [0, C) into LDS, sm[q*C + c] = parameter q
+// (forward: scale, shift; backward: a, b, c).  Every workgroup reduces the <= 8 replica rows
+// of the producer itself instead of waiting for a finalize launch between the two kernels;
+// the caller synchronises the workgroup before reading sm.
+PG_DEVICE void lz_stage(const BnFin *d, float *sm, int C, int npar) {
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float o0, o1, o2;
+    bn_lazy(d, c, o0, o1, o2);
+    sm[c] = o0;
+    sm[C + c] = o1;
+    if (npar == 3) sm[2 * C + c] = o2;
+  }
 }
 }  // namespace
 
@@ -203,9 +221,16 @@ PG_DEVICE void conv_epilogue(const ConvArgs &p, f32x4_t (&acc)[BM / 32][BN / 32]
   if constexpr (!STATS) return;
   const bool has_yt2 = E_YT2;
   __syncthreads();
-  // ---- BN partials of this tile's columns -> part[cls*nmt + mt][2][N] (and part2)
+  // ---- BN partials of this tile's columns -> row cls*nmt + mt of part[P][2][N] (and part2):
+  // stored, or added into replica row (cls*nmt + mt) % bn_rep (bn_part_add) when bn_rep < P
   const int prow = cls * nmt + mt;
+  const int P = (int)gridDim.y * nmt;
+  const bool rows_own = p.bn_rep >= P;
   const int nstat = has_yt2 ? 3 : 2;
+  auto put = [&](float *dst, int s, int col, float a) {
+    if (rows_own) dst[((size_t)prow * 2 + s) * p.N + col] = a;
+    else bn_part_add(dst, prow, P, p.bn_rep, p.N, s, col, a);
+  };
   for (int s = 0; s < nstat; ++s) {
     const int rgrp = tid / CH;
 #pragma unroll
@@ -215,9 +240,9 @@ PG_DEVICE void conv_epilogue(const ConvArgs &p, f32x4_t (&acc)[BM / 32][BN / 32]
       float a = 0.f;
       for (int g = 0; g < RSTEP; ++g) a += Red[g * BN + c];
       if (n0 + c < p.N) {
-        if (s < 2) p.part[((size_t)prow * 2 + s) * p.N + n0 + c] = a;
-        if (s == 0 && has_yt2) p.part2[((size_t)prow * 2) * p.N + n0 + c] = a;
-        if (s == 2) p.part2[((size_t)prow * 2 + 1) * p.N + n0 + c] = a;
+        if (s < 2) put(p.part, s, n0 + c, a);
+        if (s == 0 && has_yt2) put(p.part2, 0, n0 + c, a);
+        if (s == 2) put(p.part2, 1, n0 + c, a);
       }
     }
     __syncthreads();
@@ -482,7 +507,11 @@ PG_DEVICE int glds_sw(int r) {
   else return (4 - ((r >> 2) & 3)) & 3;
 }
 
-template <int MODE, int EPI, int BM, int BN, int NBUF, int KS = 64>
+// MT (multi-tap k-steps, Ci < KS, e.g. the space-to-depth stem with Ci = 16): the 8 chunks of a
+// staged 128-B row belong to different filter taps, so each lane decodes its own chunk's tap
+// (an integer division per k-step) and the bounds check is per chunk.  Without MT the tap is
+// uniform per k-step (Ci % KS == 0).
+template <int MODE, int EPI, int BM, int BN, int NBUF, int KS = 64, bool MT = false>
 __global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs p) {
   constexpr int ROWB = KS * 2;                        // staged row bytes
   constexpr int RPP = 1024 / ROWB, CPR = ROWB / 16;   // rows per 1-KiB piece, 16-B chunks per row
@@ -544,8 +573,15 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs p) {
 
   auto issue = [&](int ks, int buf) {
     const int k0 = ks * KS;
-    const int j = k0 / p.Ci;
-    const int ci = k0 - j * p.Ci + lch * 8;
+    int j, ci;
+    if constexpr (MT) {
+      const int kk = k0 + lch * 8;
+      j = kk / p.Ci;
+      ci = kk - j * p.Ci;
+    } else {
+      j = k0 / p.Ci;
+      ci = k0 - j * p.Ci + lch * 8;
+    }
     int dh, dw, wt;
     if constexpr (MODE == CM_FWD) {
       dh = j / p.S; dw = j - dh * p.S; wt = j;
@@ -641,15 +677,22 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs p) {
 // Thread t owns channel chunk t % C8 (coefficients in registers), rows t / C8 + i*(256/C8);
 // UR rows in flight per thread.  C8 = C/8 must divide 256 (checked by the launcher).
 // ===========================================================================
-template <int MODE>
+// LZ: the coefficients come from the producer's replica rows (lz, lz_stage), not from a, b, c
+template <int MODE, bool LZ>
 __global__ __launch_bounds__(256) void bn_mat_kernel(const bf16_t *__restrict__ G, const bf16_t *__restrict__ Y,
                                                     const float *__restrict__ a, const float *__restrict__ b,
                                                     const float *__restrict__ c, bf16_t *__restrict__ out, int M,
-                                                    int C) {
+                                                    int C, const BnFin *lz) {
+  extern __shared__ __attribute__((aligned(16))) float lzs[];
   constexpr int UR = 4;
   const int C8 = C >> 3, rpi = 256 / C8;
   const int cc = threadIdx.x % C8, r0 = threadIdx.x / C8;
   float a8[8], b8[8], c8[8];
+  if constexpr (LZ) {
+    lz_stage(lz, lzs, C, MODE == 1 ? 3 : 2);
+    __syncthreads();
+    a = lzs; b = lzs + C; c = lzs + 2 * C;
+  }
   ld8f(a + cc * 8, a8);
   ld8f(b + cc * 8, b8);
   if constexpr (MODE == 1) ld8f(c + cc * 8, c8);
@@ -1135,11 +1178,21 @@ __global__ __launch_bounds__(256) void conv_wt_kernel(const bf16_t *__restrict__
 // ===========================================================================
 // bottleneck output:  o = relu(y3*s3 + t3 + (yd*sd + td  |  x))       [M][C]
 // ===========================================================================
-template <bool PROJ>
+template <bool PROJ, bool LZ>
 __global__ __launch_bounds__(256) void res_out_kernel(const bf16_t *__restrict__ y, const float *__restrict__ s,
                                                       const float *__restrict__ t, const bf16_t *__restrict__ r,
                                                       const float *__restrict__ rs, const float *__restrict__ rt,
-                                                      bf16_t *__restrict__ out, long long n8, int C8) {
+                                                      bf16_t *__restrict__ out, long long n8, int C8,
+                                                      const BnFin *lz, const BnFin *lz2) {
+  extern __shared__ __attribute__((aligned(16))) float lzs[];
+  if constexpr (LZ) {   // BN3 (and the projection BN) finalized from the replica rows
+    const int C = C8 * 8;
+    lz_stage(lz, lzs, C, 2);
+    if constexpr (PROJ) lz_stage(lz2, lzs + 2 * C, C, 2);
+    __syncthreads();
+    s = lzs; t = lzs + C;
+    if constexpr (PROJ) { rs = lzs + 2 * C; rt = lzs + 3 * C; }
+  }
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
     const int c0 = (int)(i % C8) * 8;
     float v[8], rv[8], a[8], b[8];
@@ -1165,10 +1218,17 @@ __global__ __launch_bounds__(256) void res_out_kernel(const bf16_t *__restrict__
 // and backward (gather over the <= 4 windows that contain an input pixel) fused with the
 // stem BN's ReLU mask and its backward partial sums.  8 channels per thread.
 // ===========================================================================
+template <bool LZ>
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16_t *__restrict__ y, const float *__restrict__ s,
                                                           const float *__restrict__ t, bf16_t *__restrict__ out,
                                                           uint8_t *__restrict__ idx, int Nb, int H, int W, int C,
-                                                          int Ho, int Wo) {
+                                                          int Ho, int Wo, const BnFin *lz) {
+  extern __shared__ __attribute__((aligned(16))) float lzs[];
+  if constexpr (LZ) {
+    lz_stage(lz, lzs, C, 2);
+    __syncthreads();
+    s = lzs; t = lzs + C;
+  }
   const int C8 = C / 8;
   const long long total = (long long)Nb * Ho * Wo * C8;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
@@ -1209,7 +1269,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16_t *__restri
                                                           const bf16_t *__restrict__ y, const float *__restrict__ s,
                                                           const float *__restrict__ t, bf16_t *__restrict__ g,
                                                           float *__restrict__ part, int Nb, int H, int W, int C,
-                                                          int Ho, int Wo, int pix_per_wg) {
+                                                          int Ho, int Wo, int pix_per_wg, int rep) {
   __shared__ float red[2][32][64];
   const int C8 = C / 8;   // == 8
   const int cc = threadIdx.x % C8, pl = threadIdx.x / C8, PPI = 256 / C8;
@@ -1264,7 +1324,8 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16_t *__restri
     const int st = threadIdx.x / C, c = threadIdx.x % C;
     float v = 0.f;
     for (int q = 0; q < PPI; ++q) v += red[st][q][c];
-    part[((size_t)blockIdx.x * 2 + st) * C + c] = v;
+    if (rep >= (int)gridDim.x) part[((size_t)blockIdx.x * 2 + st) * C + c] = v;
+    else bn_part_add(part, blockIdx.x, gridDim.x, rep, C, st, c, v);
   }
 }
 
@@ -1294,8 +1355,9 @@ __global__ __launch_bounds__(256) void avgpool_kernel(const bf16_t *__restrict__
 // G[b][i][c] = dpool[b][c] / HW * (x > 0);  part[b][2][C] = (sum G, sum G*y) over the image
 __global__ __launch_bounds__(256) void head_bwd_kernel(const float *__restrict__ dpool, const bf16_t *__restrict__ x,
                                                        const bf16_t *__restrict__ y, bf16_t *__restrict__ G,
-                                                       float *__restrict__ part, int HW, int C) {
+                                                       float *__restrict__ part, int HW, int C, int rep) {
   const int b = blockIdx.x;
+  const bool own = rep >= (int)gridDim.x;
   for (int c8 = threadIdx.x; c8 < C / 8; c8 += blockDim.x) {
     float d[8], s0[8], s1[8];
     ld8f(dpool + (size_t)b * C + c8 * 8, d);
@@ -1314,9 +1376,17 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float *__restrict__
       }
       stg16(G + o, pack8(g));
     }
-    float *p0 = part + (size_t)b * 2 * C + c8 * 8;
+    if (own) {
+      float *p0 = part + (size_t)b * 2 * C + c8 * 8;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) { p0[k] = s0[k]; p0[C + k] = s1[k]; }
+      for (int k = 0; k < 8; ++k) { p0[k] = s0[k]; p0[C + k] = s1[k]; }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        bn_part_add(part, b, gridDim.x, rep, C, 0, c8 * 8 + k, s0[k]);
+        bn_part_add(part, b, gridDim.x, rep, C, 1, c8 * 8 + k, s1[k]);
+      }
+    }
   }
 }
 
@@ -1357,7 +1427,8 @@ __global__ __launch_bounds__(64) void softmax_ce_kernel(const float *__restrict_
 __global__ __launch_bounds__(256) void image_prep_kernel(const uint8_t *__restrict__ src, const long long *__restrict__ idx,
                                                          const long long *__restrict__ lab_src, int HW, int W,
                                                          unsigned long long seed, const float *__restrict__ hyper,
-                                                         bf16_t *__restrict__ out, long long *__restrict__ lab_out) {
+                                                         bf16_t *__restrict__ out, long long *__restrict__ lab_out,
+                                                         int s2d) {
   const int b = blockIdx.y;
   const long long si = idx[b];
   const uint64_t step = hyper ? (uint64_t)hyper[1] : 0;
@@ -1374,7 +1445,10 @@ __global__ __launch_bounds__(256) void image_prep_kernel(const uint8_t *__restri
     uint2 u;
     u.x = pack2(v[0], v[1]);
     u.y = pack2(v[2], v[3]);
-    *reinterpret_cast<uint2 *>(out + ((size_t)b * HW + p) * 4) = u;
+    // s2d: space-to-depth by 2, [B][H/2][W/2][16] with channel (dh*2 + dw)*4 + c (the ResNet stem)
+    const size_t o = s2d ? ((((size_t)b * (HW / W / 2) + (h >> 1)) * (W >> 1) + (w >> 1)) * 16 + ((h & 1) * 2 + (w & 1)) * 4)
+                         : ((size_t)b * HW + p) * 4;
+    *reinterpret_cast<uint2 *>(out + o) = u;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) lab_out[b] = lab_src[si];
 }
@@ -1454,14 +1528,14 @@ int g_conv_glds = conv_glds_default();
 bool glds_ok(int Ci) { return g_conv_glds != 0 && Ci % 64 == 0; }
 int glds_nbuf() { return g_conv_glds; }
 
-template <int MODE, int EPI, int BM, int BN, int NBUF, int KS>
+template <int MODE, int EPI, int BM, int BN, int NBUF, int KS, bool MT = false>
 void launch_glds_t(const ConvArgs &a, const Geom &g, hipStream_t st) {
   size_t lds = (size_t)NBUF * (BM + BN) * KS * 2;
   const size_t ctile = (size_t)BM * (BN + 8) * 2, red = (size_t)(256 / (BN / 8)) * BN * 4;
   if (ctile > lds) lds = ctile;
   if (red > lds) lds = red;
-  hipLaunchKernelGGL((conv_glds_kernel<MODE, EPI, BM, BN, NBUF, KS>), dim3(g.nmt * g.nt, g.ncls), dim3(256), lds, st,
-                     a);
+  hipLaunchKernelGGL((conv_glds_kernel<MODE, EPI, BM, BN, NBUF, KS, MT>), dim3(g.nmt * g.nt, g.ncls), dim3(256), lds,
+                     st, a);
 }
 
 // LDS-DMA k-step: PGDIST_CONV_KS = 64 (default) | 32; ring depth PGDIST_CONV_GLDS (2..4)
@@ -1548,6 +1622,7 @@ void launch_conv_fwd(int pro, const bf16_t *x, const float *pa, const float *pb,
   a.Nb = Nb;
   const Geom g = igemm_geom(a.Mc, N, a.Kw, Ci, 1);
   a.nmt = g.nmt;
+  a.bn_rep = g_bn_rep;
   if (Ci == 4) { launch_geom<CM_FWD, CP_NONE, CE_FWD, 4>(a, g, stream); return; }
   if (pro == CP_NONE && glds_ok(Ci)) { launch_glds<CM_FWD, CE_FWD>(a, g, stream); return; }
   if (pro == CP_BN_RELU) launch_geom<CM_FWD, CP_BN_RELU, CE_FWD, 8>(a, g, stream);
@@ -1581,6 +1656,7 @@ void launch_conv_dgrad(int epi, const bf16_t *G, const bf16_t *Y, const float *g
   const Geom g = igemm_geom(a.Mc, Cin, kmax, Cout, st * st);
   a.nmt = g.nmt;
   a.Nb = Nb;
+  a.bn_rep = g_bn_rep;
   if (Y == nullptr) {   // G is the materialised dy (launch_bn_mat): LDS-DMA kernel, no prologue
     if (epi == CE_BWD_RELU) { launch_glds<CM_DGRAD, CE_BWD_RELU>(a, g, stream); return; }
     if (!Rg && !X && !Yt && !Yt2) launch_glds<CM_DGRAD, CE_BWD_PLAIN>(a, g, stream);
@@ -1718,13 +1794,21 @@ void launch_conv_wt(const bf16_t *src, bf16_t *dst, const int *tab, int n, hipSt
   hipLaunchKernelGGL(conv_wt_kernel, dim3(256, n), dim3(256), 0, st, src, dst, tab);
 }
 
+// lz / lz2 (device BnFin descriptors, both or neither; lz2 only with the projection): lazy finalize
 void launch_res_out(const bf16_t *y, const float *s, const float *t, const bf16_t *r, const float *rs,
-                    const float *rt, bf16_t *out, long long M, int C, hipStream_t st) {
+                    const float *rt, bf16_t *out, long long M, int C, const void *lz, const void *lz2,
+                    hipStream_t st) {
   const long long n8 = M * (C / 8);
   int grid = (int)((n8 + 255) / 256);
-  if (grid > 16384) grid = 16384;
-  if (rs) hipLaunchKernelGGL((res_out_kernel<true>), dim3(grid), dim3(256), 0, st, y, s, t, r, rs, rt, out, n8, C / 8);
-  else hipLaunchKernelGGL((res_out_kernel<false>), dim3(grid), dim3(256), 0, st, y, s, t, r, rs, rt, out, n8, C / 8);
+  const int cap = lz ? (C > 256 ? 512 : 2048) : 16384;
+  if (grid > cap) grid = cap;
+  const BnFin *d = static_cast<const BnFin *>(lz), *d2 = static_cast<const BnFin *>(lz2);
+  const size_t lds = lz ? (size_t)(rs ? 4 : 2) * C * sizeof(float) : 0;
+#define RO(PJ, LZ_) \
+  hipLaunchKernelGGL((res_out_kernel<PJ, LZ_>), dim3(grid), dim3(256), lds, st, y, s, t, r, rs, rt, out, n8, C / 8, d, d2)
+  if (rs) { if (lz) RO(true, true); else RO(true, false); }
+  else { if (lz) RO(false, true); else RO(false, false); }
+#undef RO
 }
 
 void launch_maxpool_fwd(const bf16_t *y, const float *s, const float *t, bf16_t *out, uint8_t *idx, int Nb, int H,
@@ -1732,8 +1816,15 @@ void launch_maxpool_fwd(const bf16_t *y, const float *s, const float *t, bf16_t 
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
   const long long total = (long long)Nb * Ho * Wo * (C / 8);
   int grid = (int)((total + 255) / 256);
-  if (grid > 16384) grid = 16384;
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid), dim3(256), 0, st, y, s, t, out, idx, Nb, H, W, C, Ho, Wo);
+  const BnFin *lz = take_bn_lz();
+  const int cap = lz ? 2048 : 16384;
+  if (grid > cap) grid = cap;
+  if (lz)
+    hipLaunchKernelGGL((maxpool_fwd_kernel<true>), dim3(grid), dim3(256), (size_t)2 * C * sizeof(float), st, y, s, t,
+                       out, idx, Nb, H, W, C, Ho, Wo, lz);
+  else
+    hipLaunchKernelGGL((maxpool_fwd_kernel<false>), dim3(grid), dim3(256), 0, st, y, s, t, out, idx, Nb, H, W, C, Ho,
+                       Wo, lz);
 }
 
 constexpr int kMpPix = 512;   // input pixels per backward workgroup
@@ -1745,7 +1836,7 @@ void launch_maxpool_bwd(const bf16_t *gp, const uint8_t *idx, const bf16_t *y, c
                         bf16_t *g, float *part, int Nb, int H, int W, int C, hipStream_t st) {
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(maxpool_bwd_num_partials(Nb, H, W)), dim3(256), 0, st, gp, idx, y, s, t,
-                     g, part, Nb, H, W, C, Ho, Wo, kMpPix);
+                     g, part, Nb, H, W, C, Ho, Wo, kMpPix, g_bn_rep);
 }
 
 void launch_avgpool(const bf16_t *x, float *out, int Nb, int HW, int C, hipStream_t st) {
@@ -1754,7 +1845,7 @@ void launch_avgpool(const bf16_t *x, float *out, int Nb, int HW, int C, hipStrea
 
 void launch_head_bwd(const float *dpool, const bf16_t *x, const bf16_t *y, bf16_t *G, float *part, int Nb, int HW,
                      int C, hipStream_t st) {
-  hipLaunchKernelGGL(head_bwd_kernel, dim3(Nb), dim3(256), 0, st, dpool, x, y, G, part, HW, C);
+  hipLaunchKernelGGL(head_bwd_kernel, dim3(Nb), dim3(256), 0, st, dpool, x, y, G, part, HW, C, g_bn_rep);
 }
 
 void launch_softmax_ce(const float *logits, const long long *labels, int B, int NC, float scale, float *loss,
@@ -1763,20 +1854,146 @@ void launch_softmax_ce(const float *logits, const long long *labels, int B, int 
 }
 
 void launch_image_prep(const uint8_t *src, const long long *idx, const long long *lab_src, int B, int H, int W,
-                       unsigned long long seed, const float *hyper, bf16_t *out, long long *lab_out,
+                       unsigned long long seed, const float *hyper, bf16_t *out, long long *lab_out, int s2d,
                        hipStream_t st) {
   const int HW = H * W;
   hipLaunchKernelGGL(image_prep_kernel, dim3((HW + 255) / 256 < 64 ? (HW + 255) / 256 : 64, B), dim3(256), 0, st, src,
-                     idx, lab_src, HW, W, seed, hyper, out, lab_out);
+                     idx, lab_src, HW, W, seed, hyper, out, lab_out, s2d);
+}
+
+// ===========================================================================
+// Space-to-depth ResNet stem.  The 7x7 s2 p3 conv over the 4-channel image equals a 4x4 s1 conv
+// over its space-to-depth-by-2 image x2 [B][H/2][W/2][16] (channel (dh*2 + dw)*4 + c) with the
+// window rows oh-2 .. oh+1 (top / left padding 2, H/2 outputs):
+//   w2[n][r][s][(dh*2 + dw)*4 + c] = w[n][2r + dh - 1][2s + dw - 1][c]   (0 outside the 7x7)
+// so the GEMM K is 4*4*16 = 256 (four 64-wide k-steps of 4 taps x 16 channels, 128 contiguous
+// bytes of one x2 row per staged row) instead of 49 taps of 4 channels (8-B gathers).
+// ===========================================================================
+__global__ __launch_bounds__(256) void stem_w_s2d_kernel(const bf16_t *__restrict__ w, bf16_t *__restrict__ w2,
+                                                         int N) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;   // [N][4][4][16] element
+  if (i >= N * 256) return;
+  const int n = i >> 8, k = i & 255;
+  const int r = k >> 6, s = (k >> 4) & 3, q = k & 15, dh = q >> 3, dw = (q >> 2) & 1, c = q & 3;
+  const int kh = 2 * r + dh - 1, kw = 2 * s + dw - 1;
+  w2[i] = (kh >= 0 && kh < 7 && kw >= 0 && kw < 7) ? w[((n * 7 + kh) * 7 + kw) * 4 + c] : bf16_t(0);
+}
+
+// grad [N][7][7][4] of the 7x7 stem from the space-to-depth weight gradient g2 [N][4][4][16]
+__global__ __launch_bounds__(256) void stem_wgrad_s2d_kernel(const float *__restrict__ g2, float *__restrict__ grad,
+                                                             int N) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;   // [N][7][7][4] element
+  if (i >= N * 196) return;
+  const int n = i / 196, rem = i - n * 196, kh = rem / 28, kw = (rem / 4) % 7, c = rem & 3;
+  const int r = (kh + 1) >> 1, dh = (kh + 1) & 1, s = (kw + 1) >> 1, dw = (kw + 1) & 1;
+  grad[i] = g2[(size_t)n * 256 + ((r * 4 + s) * 16 + (dh * 2 + dw) * 4 + c)];
+}
+
+// NHWC 4-channel image [B][H][W][4] -> space-to-depth x2 [B][H/2][W/2][16] (one 8-B pixel per thread)
+__global__ __launch_bounds__(256) void s2d_image_kernel(const bf16_t *__restrict__ img, bf16_t *__restrict__ x2,
+                                                        long long npix, int H, int W) {
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i >= npix) return;
+  const int w = (int)(i % W), h = (int)((i / W) % H);
+  const long long b = i / ((long long)W * H);
+  const uint2 v = *reinterpret_cast<const uint2 *>(img + i * 4);
+  *reinterpret_cast<uint2 *>(x2 + (((b * (H / 2) + (h >> 1)) * (W / 2) + (w >> 1)) * 16 + ((h & 1) * 2 + (w & 1)) * 4)) = v;
+}
+
+void launch_s2d_image(const bf16_t *img, bf16_t *x2, int B, int H, int W, hipStream_t st) {
+  const long long n = (long long)B * H * W;
+  hipLaunchKernelGGL(s2d_image_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, img, x2, n, H, W);
+}
+
+void launch_stem_w_s2d(const bf16_t *w, bf16_t *w2, int N, hipStream_t st) {
+  hipLaunchKernelGGL(stem_w_s2d_kernel, dim3((N * 256 + 255) / 256), dim3(256), 0, st, w, w2, N);
+}
+
+namespace {
+ConvArgs stem_s2d_args(int Nb, int H2, int N) {
+  ConvArgs a{};
+  a.Hi = a.Wi = H2; a.Ci = 16;
+  a.Ho = a.Wo = H2;          // rows oh-2 .. oh+1: H2 outputs (not the H2 + 1 of a symmetric pad 2)
+  a.N = N; a.R = a.S = 4; a.stride = 1; a.pad = 2;
+  a.Kw = a.K = 256;
+  a.Mc = Nb * H2 * H2;
+  a.Hc = a.Wc = H2;
+  a.Nb = Nb;
+  a.bn_rep = g_bn_rep;
+  return a;
+}
+}  // namespace
+
+// y = stem(x2, w2) [Nb][H2][H2][N] + BN partials (P = conv_fwd_num_partials(Nb, H2, H2, N, 256, 16))
+void launch_conv_fwd_s2d(const bf16_t *x2, const bf16_t *w2, bf16_t *y, float *part, int Nb, int H2, int N,
+                         hipStream_t stream) {
+  ConvArgs a = stem_s2d_args(Nb, H2, N);
+  a.A = x2; a.W = w2; a.out = y; a.part = part;
+  const Geom g = igemm_geom(a.Mc, N, 256, 16, 1);
+  a.nmt = g.nmt;
+  if (g.BM == 128 && g.BN == 128) launch_glds_t<CM_FWD, CE_FWD, 128, 128, 2, 64, true>(a, g, stream);
+  else if (g.BM == 128 && g.BN == 64) launch_glds_t<CM_FWD, CE_FWD, 128, 64, 2, 64, true>(a, g, stream);
+  else if (g.BM == 64 && g.BN == 128) launch_glds_t<CM_FWD, CE_FWD, 64, 128, 2, 64, true>(a, g, stream);
+  else launch_glds_t<CM_FWD, CE_FWD, 64, 64, 2, 64, true>(a, g, stream);
+}
+
+long long conv_wgrad_s2d_workspace_floats(int Nb, int H2, int N) {
+  const WgGeom g = wg_geom(N, 256, Nb * H2 * H2);
+  return (long long)(g.nsplit + colsum_rows(g.nsplit)) * N * 256 + (long long)N * 256;
+}
+
+void wgrad_reduce_defer(bool on);
+bool wgrad_reduce_deferring();
+
+// stem weight gradient grad [N][7][7][4] (fp32, overwritten) from dy = ga*G + gb*Y + gc
+// ([Nb][H2][H2][N]) and the space-to-depth image x2 (register-staged split-M kernel, 16-B
+// gathers), reduced into a [N][256] scratch and permuted back to the 7x7 layout
+void launch_conv_wgrad_s2d(const bf16_t *G, const bf16_t *Y, const float *ga, const float *gb, const float *gc,
+                           const bf16_t *x2, float *ws, float *grad, int Nb, int H2, int N, hipStream_t stream) {
+  const ConvArgs c = stem_s2d_args(Nb, H2, N);
+  WgArgs a{};
+  a.G = G; a.Y = Y; a.ga = ga; a.gb = gb; a.gc = gc; a.X = x2;
+  a.N = N; a.Hi = c.Hi; a.Wi = c.Wi; a.Ci = c.Ci; a.Ho = c.Ho; a.Wo = c.Wo;
+  a.R = c.R; a.S = c.S; a.stride = 1; a.pad = c.pad; a.Kw = 256; a.M = c.Mc;
+  const WgGeom g = wg_geom(N, 256, a.M);
+  a.rows_per_split = g.rows;
+  float *g2 = ws + (size_t)(g.nsplit + colsum_rows(g.nsplit)) * N * 256;
+  a.out = g.nsplit == 1 ? g2 : ws;
+  const dim3 grid((N + g.TN - 1) / g.TN, (256 + g.TK - 1) / g.TK, g.nsplit);
+  const bool dm = Y == nullptr;
+#define WGS_L(TN_, TK_)                                                                                        \
+  do {                                                                                                        \
+    if (dm) hipLaunchKernelGGL((conv_wgrad_kernel<CP_NONE, TN_, TK_, 8, true>), grid, dim3(256), 0, stream, a);  \
+    else hipLaunchKernelGGL((conv_wgrad_kernel<CP_NONE, TN_, TK_, 8, false>), grid, dim3(256), 0, stream, a);    \
+  } while (0)
+  if (g.TN == 128) WGS_L(128, 128); else WGS_L(64, 128);
+#undef WGS_L
+  if (g.nsplit > 1) {
+    const bool deferring = wgrad_reduce_deferring();   // the permute below reads g2 right away
+    wgrad_reduce_defer(false);
+    launch_wgrad_reduce(ws, g.nsplit, (long long)N * 256, g2, stream);
+    wgrad_reduce_defer(deferring);
+  }
+  hipLaunchKernelGGL(stem_wgrad_s2d_kernel, dim3((N * 196 + 255) / 256), dim3(256), 0, stream, g2, grad, N);
 }
 
 // BN materialisation (bn_mat_kernel): mode 0 act = relu(Y*a + b); mode 1 dy = a*G + b*Y + c
 void launch_bn_mat(int mode, const bf16_t *G, const bf16_t *Y, const float *a, const float *b, const float *c,
                    bf16_t *out, int M, int C, hipStream_t stream) {
+  const BnFin *lz = take_bn_lz();
   const int C8 = C / 8, rpi = 256 / C8;
   long long blocks = ((long long)M + rpi * 4 - 1) / (rpi * 4);
-  if (blocks > 2048) blocks = 2048;
+  // lazy: every workgroup finalizes all C channels (16 replica-row loads each), so fewer
+  // (grid-stride) workgroups on the wide layers
+  const long long cap = lz && C > 256 ? 512 : 2048;
+  if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
-  if (mode == 1) hipLaunchKernelGGL(bn_mat_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, stream, G, Y, a, b, c, out, M, C);
-  else hipLaunchKernelGGL(bn_mat_kernel<0>, dim3((unsigned)blocks), dim3(256), 0, stream, G, Y, a, b, c, out, M, C);
+  const size_t lds = lz ? (size_t)(mode == 1 ? 3 : 2) * C * sizeof(float) : 0;
+#define BNM(MODE_)                                                                                             \
+  if (lz) hipLaunchKernelGGL((bn_mat_kernel<MODE_, true>), dim3((unsigned)blocks), dim3(256), lds, stream, G, Y, a, \
+                             b, c, out, M, C, lz);                                                             \
+  else hipLaunchKernelGGL((bn_mat_kernel<MODE_, false>), dim3((unsigned)blocks), dim3(256), 0, stream, G, Y, a, b, \
+                          c, out, M, C, lz);
+  if (mode == 1) { BNM(1) } else { BNM(0) }
+#undef BNM
 }

@@ -259,9 +259,12 @@ class NativeTrainStep:
         exe = self.exe
         K.step_begin(self.hyper)
         if self.augment_enabled and self.src.shape[1] != 32:
-            K.image_prep(self.src, self.idx, self.src_labels, exe.img, exe.labels,
+            s2d = getattr(exe, "stem_s2d", False)   # ResNet space-to-depth stem: render its input directly
+            if s2d:
+                exe.img_s2d_external = True
+            K.image_prep(self.src, self.idx, self.src_labels, exe.img2 if s2d else exe.img, exe.labels,
                          seed=self.seed + 17 * self.rank if self.train_augment else 0,
-                         hyper=self.hyper if self.train_augment else None)
+                         hyper=self.hyper if self.train_augment else None, s2d=s2d)
         elif self.augment_enabled and not self._have:   # (a prefetched batch is already rendered)
             K.augment(self.src, self.idx, self.src_labels, exe.img, exe.labels, self.aug_params,
                       train=self.train_augment,

@@ -41,7 +41,7 @@ import torch
 
 from ..models.resnet import ResNet, Bottleneck
 from ..ops import kernels as K
-from .executor import BNState
+from .executor import AtomicBNState, BNState
 from .flat import FlatParams
 
 
@@ -105,27 +105,22 @@ class ResNet50Executor:
         B = batch
         f32 = dict(dtype=torch.float32, device=device)
         bf16 = dict(dtype=torch.bfloat16, device=device)
-        parts, wgs = [], []
+        wgs = []
 
-        def fwd_parts(c: ConvSpec):
+        def wg_space(c: ConvSpec):
             ci = 4 if c.cin == 3 else c.cin
-            parts.append((K.conv_fwd_num_partials(B, c.Ho, c.Ho, c.cout, c.k * c.k * ci, ci), c.cout))
             wgs.append(K.conv_wgrad_workspace(B, c.H, c.H, ci, c.cout, c.k, c.k, c.stride, c.pad))
-
-        def dgrad_parts(c: ConvSpec):
-            parts.append((K.conv_dgrad_num_partials(B, c.H, c.H, c.cin, c.cout, c.k, c.k, c.stride), c.cin))
 
         # ---------------- stem + max-pool
         self.stem = ConvSpec("conv1.weight", 3, 64, 7, 2, 3, img_size)
         H0 = self.stem.Ho
         self.H0 = H0
-        self.bn0 = BNState(self.flat, model.bn1, "bn1", B * H0 * H0, 64, device)
-        fwd_parts(self.stem)
+        self.bn0 = AtomicBNState(self.flat, model.bn1, "bn1", B * H0 * H0, 64, device)
+        wg_space(self.stem)
         self.Hp = (H0 - 1) // 2 + 1
         self.pool = torch.empty(B * self.Hp * self.Hp, 64, **bf16)
         self.pool_idx = torch.empty(B * self.Hp * self.Hp, 64, dtype=torch.uint8, device=device)
         self.Gpool = torch.empty(B * self.Hp * self.Hp, 64, **bf16)
-        parts.append((K.maxpool_bwd_num_partials(B, H0, H0), 64))
         # ---------------- bottlenecks
         self.blocks: List[BlockPlan] = []
         H, x_in = self.Hp, self.pool
@@ -140,10 +135,11 @@ class ResNet50Executor:
                 c2 = ConvSpec(f"{pre}.conv2.weight", planes, planes, 3, s, 1, H)
                 c3 = ConvSpec(f"{pre}.conv3.weight", planes, cout, 1, 1, 0, Ho)
                 cd = ConvSpec(f"{pre}.downsample.0.weight", cin, cout, 1, s, 0, H) if blk.downsample is not None else None
-                bn1 = BNState(self.flat, blk.bn1, f"{pre}.bn1", Min, planes, device)
-                bn2 = BNState(self.flat, blk.bn2, f"{pre}.bn2", Mout, planes, device)
-                bn3 = BNState(self.flat, blk.bn3, f"{pre}.bn3", Mout, cout, device)
-                bnd = (BNState(self.flat, blk.downsample[1], f"{pre}.downsample.1", Mout, cout, device, need_g=False)
+                bn1 = AtomicBNState(self.flat, blk.bn1, f"{pre}.bn1", Min, planes, device)
+                bn2 = AtomicBNState(self.flat, blk.bn2, f"{pre}.bn2", Mout, planes, device)
+                bn3 = AtomicBNState(self.flat, blk.bn3, f"{pre}.bn3", Mout, cout, device)
+                bnd = (AtomicBNState(self.flat, blk.downsample[1], f"{pre}.downsample.1", Mout, cout, device,
+                                     need_g=False)
                        if cd is not None else None)
                 bp = BlockPlan(pre, cin, planes, cout, s, H, Ho, c1, c2, c3, cd, bn1, bn2, bn3, bnd)
                 bp.x_in = x_in
@@ -151,8 +147,7 @@ class ResNet50Executor:
                 if cd is not None:
                     bp.Rd = torch.empty(Min, cin, **bf16)
                 for c in (c1, c2, c3) + ((cd,) if cd else ()):
-                    fwd_parts(c)
-                    dgrad_parts(c)
+                    wg_space(c)
                 self.blocks.append(bp)
                 H, x_in = Ho, bp.out
         # ---------------- materialised operands of the LDS-DMA convs
@@ -175,7 +170,6 @@ class ResNet50Executor:
         self.Hf = H
         self.C_last = self.blocks[-1].cout
         self.NC = model.fc.out_features
-        parts.append((B, self.C_last))
         self.pooled = torch.zeros(B, self.C_last, **f32)
         self.logits = torch.zeros(B, self.NC, **f32)
         self.dlogits = torch.zeros(B, self.NC, **f32)
@@ -189,10 +183,22 @@ class ResNet50Executor:
         C, NC = self.C_last, self.NC
         self.ws_fc = torch.zeros(max(K.fc_gemm_workspace_floats(B, NC, C), K.fc_gemm_workspace_floats(NC, C, B),
                                      K.fc_gemm_workspace_floats(B, C, NC), 1), **f32)
-        # ---------------- workspaces (stream-ordered reuse)
-        pf = max(K.bn_part_floats(P, C) for P, C in parts) + 1024
-        self.ws_part = torch.zeros(pf, **f32)
-        self.ws_part2 = torch.zeros(pf, **f32)
+        # ---------------- BN statistics accumulators
+        # every producer (conv forward / dgrad epilogues, max-pool backward, head backward) adds
+        # its per-tile partial sums into min(P, bn_rep) replica rows of its BN's zeroed
+        # accumulator (common.h bn_part_add), so a finalize reduces <= 8 rows instead of one row
+        # per output tile (up to 3136 at 56x56: 5-37 us per finalize launch); one arena, one
+        # memset per step.  Deterministic mode: one plainly stored row per tile (bn_rep >= P).
+        o, spans = 0, []
+        for bn, (pf_, pb_) in self._bn_producer_rows().items():
+            bn.rows_f, bn.rows_b = K.bn_rows(pf_), K.bn_rows(pb_)
+            nf, nb = K.bn_part_floats(bn.rows_f, bn.C), K.bn_part_floats(bn.rows_b, bn.C)
+            spans.append((bn, o, nf, nb))
+            o += (nf + nb + 63) // 64 * 64
+        self.bn_arena = torch.zeros(o + 64, **f32)
+        for bn, o, nf, nb in spans:
+            bn.acc_f = self.bn_arena[o:o + nf]
+            bn.acc_b = self.bn_arena[o + nf:o + nf + nb]
         self.ws_wgrad = torch.zeros(max(wgs) + 1024, **f32)
         self.side = None
         self._side_pending = []
@@ -201,6 +207,18 @@ class ResNet50Executor:
             self.side = K.side_stream(device)
             K.register_side_stream(self.side)
         self.img = torch.zeros(B, img_size, img_size, 4, **bf16)
+        # space-to-depth stem (default; PGDIST_RN_STEM=direct: the 7x7 implicit GEMM over the
+        # 4-channel image): the 7x7 s2 conv runs as a 4x4 s1 conv over img2 [B,S/2,S/2,16]
+        # (K = 256 in four 64-wide LDS-DMA k-steps of 128 contiguous bytes per row instead of 49
+        # 8-byte tap gathers), its weight re-laid out each step (stem_w_s2d) and its gradient
+        # permuted back to the 7x7 layout.  img2 is written by image_prep(s2d=True) when the
+        # training step renders the batch (img_s2d_external), else converted from img.
+        self.stem_s2d = os.environ.get("PGDIST_RN_STEM", "s2d") == "s2d" and img_size % 2 == 0
+        self.img_s2d_external = False
+        if self.stem_s2d:
+            self.img2 = torch.zeros(B, img_size // 2, img_size // 2, 16, **bf16)
+            self.w2 = torch.zeros(64 * 256, **bf16)
+            self.ws_stem = torch.zeros(K.conv_wgrad_s2d_workspace(B, img_size // 2) + 1024, **f32)
         self.labels = torch.zeros(B, dtype=torch.int64, device=device)
         self.hyper = hyper if hyper is not None else torch.zeros(2, **f32)
         self.on_params_ready: Optional[Callable[[List[str]], None]] = None
@@ -216,6 +234,30 @@ class ResNet50Executor:
         self.wt_tab = torch.tensor(tab, dtype=torch.int32, device=device).contiguous()
 
     # ------------------------------------------------------------------ helpers
+    def _bn_producer_rows(self):
+        """{bn: (forward P, backward P)}: partial rows of the kernels producing each BN's
+        statistics (forward: its conv's epilogue; backward: the dgrad of the conv that consumes
+        it, the next block's conv1 dgrad for bn3 / bnd, head_bwd and maxpool_bwd)."""
+        B = self.B
+
+        def pf(c: ConvSpec):
+            ci = 4 if c.cin == 3 else c.cin
+            return K.conv_fwd_num_partials(B, c.Ho, c.Ho, c.cout, c.k * c.k * ci, ci)
+
+        def pd(c: ConvSpec):
+            return K.conv_dgrad_num_partials(B, c.H, c.H, c.cin, c.cout, c.k, c.k, c.stride)
+
+        rows = {self.bn0: (pf(self.stem), K.maxpool_bwd_num_partials(B, self.H0, self.H0))}
+        for i, bp in enumerate(self.blocks):
+            nxt = self.blocks[i + 1] if i + 1 < len(self.blocks) else None
+            rows[bp.bn1] = (pf(bp.c1), pd(bp.c2))
+            rows[bp.bn2] = (pf(bp.c2), pd(bp.c3))
+            rows[bp.bn3] = (pf(bp.c3), pd(nxt.c1) if nxt is not None else B)
+            if bp.bnd is not None:
+                assert nxt is not None, "a projection shortcut's BN gets its gradient from the next block"
+                rows[bp.bnd] = (pf(bp.cd), pd(nxt.c1))
+        return rows
+
     # Materialisation policy, from per-layer timings of every ResNet-50 conv on MI355X at bs 128
     # (scripts/conv_bench.py: dgrad vs bn_mat + dgrad on the materialised dy, fwdbn vs bn_mat +
     # fwd).  A 3x3 conv re-stages each operand element up to 9x per N tile, so its BN prologue is
@@ -274,9 +316,9 @@ class ResNet50Executor:
                 fn()
         self._side_pending.clear()
 
-    def _fin(self, bn: BNState, P: int, train: bool):
+    def _fin(self, bn: AtomicBNState, P: int, train: bool):
         if train:
-            bn.finalize_fwd(self.ws_part, P)
+            bn.finalize_fwd(bn.acc_f, P)
 
     def _conv(self, c: ConvSpec, pro, x, y, train, bn_out: BNState, bn_in: Optional[BNState] = None):
         B = self.B
@@ -284,7 +326,7 @@ class ResNet50Executor:
         if c.act and pro == K.CP_BN_RELU:   # relu(BN(x)) materialised once: plain LDS-DMA conv
             K.bn_mat(K.BN_MAT_ACT, x, bn_in.scale, bn_in.shift, bn_in.act)
             pro, x, bn_in = K.CP_NONE, bn_in.act, None
-        K.conv_fwd(pro, x, self.flat.b(c.name), y, self.ws_part, B, c.H, c.H, ci, c.cout, c.k, c.k, c.stride,
+        K.conv_fwd(pro, x, self.flat.b(c.name), y, bn_out.acc_f, B, c.H, c.H, ci, c.cout, c.k, c.k, c.stride,
                    c.pad, pa=bn_in.scale if bn_in is not None else None,
                    pb=bn_in.shift if bn_in is not None else None)
         self._fin(bn_out, K.conv_fwd_num_partials(B, c.Ho, c.Ho, c.cout, c.k * c.k * ci, ci), train)
@@ -309,7 +351,16 @@ class ResNet50Executor:
     # ------------------------------------------------------------------ forward
     def forward(self, train: bool = True):
         B = self.B
-        self._conv(self.stem, K.CP_NONE, self.img, self.bn0.y, train, self.bn0)
+        K.memset(self.bn_arena)   # every BN statistics accumulator of this step
+        if self.stem_s2d:
+            st, H2 = self.stem, self.S // 2
+            if not self.img_s2d_external:
+                K.s2d_image(self.img, self.img2, B, self.S, self.S)
+            K.stem_w_s2d(self.flat.b(st.name), self.w2)
+            K.conv_fwd_s2d(self.img2, self.w2, self.bn0.y, self.bn0.acc_f, B, H2)
+            self._fin(self.bn0, K.conv_fwd_num_partials(B, H2, H2, 64, 256, 16), train)
+        else:
+            self._conv(self.stem, K.CP_NONE, self.img, self.bn0.y, train, self.bn0)
         K.maxpool_fwd(self.bn0.y, self.bn0.scale, self.bn0.shift, self.pool, self.pool_idx, B, self.H0, self.H0, 64)
         for bp in self.blocks:
             self._conv(bp.c1, K.CP_NONE, bp.x_in, bp.bn1.y, train, bp.bn1)
@@ -331,7 +382,7 @@ class ResNet50Executor:
 
     # ------------------------------------------------------------------ backward
     def backward(self):
-        f, B, ws, ws2, wg = self.flat, self.B, self.ws_part, self.ws_part2, self.ws_wgrad
+        f, B, wg = self.flat, self.B, self.ws_wgrad
         K.conv_wt(f.shadow, f.shadow_t, self.wt_tab, self.wt_tab.shape[0])
         # head: fc gradients (fp32 GEMMs) and the pooled gradient through the last ReLU
         C, NC = self.C_last, self.NC
@@ -343,8 +394,8 @@ class ResNet50Executor:
         self._ready(["fc.weight", "fc.bias"])
         last = self.blocks[-1]
         HW = self.Hf * self.Hf
-        K.head_bwd(self.dpool, last.out, last.bn3.y, last.bn3.g, ws, B, HW, self.C_last)
-        last.bn3.finalize_bwd(ws, B)
+        K.head_bwd(self.dpool, last.out, last.bn3.y, last.bn3.g, last.bn3.acc_b, B, HW, self.C_last)
+        last.bn3.finalize_bwd(last.bn3.acc_b, B)
         self._ready(last.bn3.param_names)
         for i in range(len(self.blocks) - 1, -1, -1):
             bp = self.blocks[i]
@@ -354,9 +405,9 @@ class ResNet50Executor:
             c1, c2, c3, cd = bp.c1, bp.c2, bp.c3, bp.cd
             # conv3 dgrad -> G2 (ReLU mask of BN2) + BN2 partials
             g3, y3 = self._dy(c3, bn3.g, bn3)
-            K.conv_dgrad(K.CE_BWD_RELU, g3, y3, bn3.a, bn3.b, bn3.c, f.bt(c3.name), bn2.g, ws, B, Ho, Ho,
+            K.conv_dgrad(K.CE_BWD_RELU, g3, y3, bn3.a, bn3.b, bn3.c, f.bt(c3.name), bn2.g, bn2.acc_b, B, Ho, Ho,
                          c3.cin, c3.cout, 1, 1, 1, 0, Yt=bn2.y, es=bn2.scale, et=bn2.shift)
-            bn2.finalize_bwd(ws, K.conv_dgrad_num_partials(B, Ho, Ho, c3.cin, c3.cout, 1, 1, 1))
+            bn2.finalize_bwd(bn2.acc_b, K.conv_dgrad_num_partials(B, Ho, Ho, c3.cin, c3.cout, 1, 1, 1))
             self._wgrad(lambda bp=bp, g3=g3, y3=y3: K.conv_wgrad(
                 g3, y3, bp.bn3.a, bp.bn3.b, bp.bn3.c, ws=wg, grad=f.g(bp.c3.name), B=B, H=bp.Ho, W=bp.Ho,
                 Ci=bp.c3.cin, N=bp.c3.cout, R=1, S=1, stride=1, pad=0, **self._wx(bp.c3, bp.bn2.y, bp.bn2)))
@@ -372,9 +423,9 @@ class ResNet50Executor:
                 self._ready([cd.name])
             # conv2 dgrad -> G1 (ReLU mask of BN1) + BN1 partials
             g2, y2 = self._dy(c2, bn2.g, bn2)
-            K.conv_dgrad(K.CE_BWD_RELU, g2, y2, bn2.a, bn2.b, bn2.c, f.bt(c2.name), bn1.g, ws, B, H, H,
+            K.conv_dgrad(K.CE_BWD_RELU, g2, y2, bn2.a, bn2.b, bn2.c, f.bt(c2.name), bn1.g, bn1.acc_b, B, H, H,
                          c2.cin, c2.cout, 3, 3, c2.stride, 1, Yt=bn1.y, es=bn1.scale, et=bn1.shift)
-            bn1.finalize_bwd(ws, K.conv_dgrad_num_partials(B, H, H, c2.cin, c2.cout, 3, 3, c2.stride))
+            bn1.finalize_bwd(bn1.acc_b, K.conv_dgrad_num_partials(B, H, H, c2.cin, c2.cout, 3, 3, c2.stride))
             self._wgrad(lambda bp=bp, g2=g2, y2=y2: K.conv_wgrad(
                 g2, y2, bp.bn2.a, bp.bn2.b, bp.bn2.c, ws=wg, grad=f.g(bp.c2.name), B=B, H=bp.H, W=bp.H,
                 Ci=bp.c2.cin, N=bp.c2.cout, R=3, S=3, stride=bp.c2.stride, pad=1, **self._wx(bp.c2, bp.bn1.y, bp.bn1)))
@@ -387,12 +438,12 @@ class ResNet50Executor:
             g1, y1 = self._dy(c1, bn1.g, bn1)
             if prev is not None:
                 pds = prev.bnd is not None
-                K.conv_dgrad(K.CE_BWD_RES, g1, y1, bn1.a, bn1.b, bn1.c, f.bt(c1.name), prev.bn3.g, ws, B, H,
-                             H, c1.cin, c1.cout, 1, 1, 1, 0, Yt=prev.bn3.y, Rg=sc, X=prev.out,
-                             Yt2=prev.bnd.y if pds else None, part2=ws2 if pds else None)
-                prev.bn3.finalize_bwd(ws, P1)
+                K.conv_dgrad(K.CE_BWD_RES, g1, y1, bn1.a, bn1.b, bn1.c, f.bt(c1.name), prev.bn3.g, prev.bn3.acc_b, B,
+                             H, H, c1.cin, c1.cout, 1, 1, 1, 0, Yt=prev.bn3.y, Rg=sc, X=prev.out,
+                             Yt2=prev.bnd.y if pds else None, part2=prev.bnd.acc_b if pds else None)
+                prev.bn3.finalize_bwd(prev.bn3.acc_b, P1)
                 if pds:
-                    prev.bnd.finalize_bwd(ws2, P1)
+                    prev.bnd.finalize_bwd(prev.bnd.acc_b, P1)
             else:
                 K.conv_dgrad(K.CE_BWD_RES, g1, y1, bn1.a, bn1.b, bn1.c, f.bt(c1.name), self.Gpool, None, B,
                              H, H, c1.cin, c1.cout, 1, 1, 1, 0, Rg=sc)
@@ -405,11 +456,16 @@ class ResNet50Executor:
             self._ready(names)
         # max-pool + stem
         bn0 = self.bn0
-        K.maxpool_bwd(self.Gpool, self.pool_idx, bn0.y, bn0.scale, bn0.shift, bn0.g, ws, B, self.H0, self.H0, 64)
-        bn0.finalize_bwd(ws, K.maxpool_bwd_num_partials(B, self.H0, self.H0))
+        K.maxpool_bwd(self.Gpool, self.pool_idx, bn0.y, bn0.scale, bn0.shift, bn0.g, bn0.acc_b, B, self.H0, self.H0,
+                      64)
+        bn0.finalize_bwd(bn0.acc_b, K.maxpool_bwd_num_partials(B, self.H0, self.H0))
         st = self.stem
-        self._wgrad(lambda: K.conv_wgrad(bn0.g, bn0.y, bn0.a, bn0.b, bn0.c, self.img, wg, f.g(st.name), B, st.H,
-                                         st.H, 4, st.cout, 7, 7, 2, 3))
+        if self.stem_s2d:
+            self._wgrad(lambda: K.conv_wgrad_s2d(bn0.g, bn0.y, bn0.a, bn0.b, bn0.c, self.img2, self.ws_stem,
+                                                 f.g(st.name), B, self.S // 2))
+        else:
+            self._wgrad(lambda: K.conv_wgrad(bn0.g, bn0.y, bn0.a, bn0.b, bn0.c, self.img, wg, f.g(st.name), B,
+                                             st.H, st.H, 4, st.cout, 7, 7, 2, 3))
         self._ready([st.name] + bn0.param_names)
         self._flush_side()
         if self.side is not None:

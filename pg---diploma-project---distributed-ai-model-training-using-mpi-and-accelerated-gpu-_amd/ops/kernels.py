@@ -584,7 +584,9 @@ def conv_fwd(pro, x, w, y, part, B, H, W, Ci, N, R, S, stride, pad, pa=None, pb=
     _chk(x, BF16, B * H * W * Ci, "x")
     _chk(w, BF16, N * R * S * Ci, "w")
     _chk(y, BF16, B * Ho * Wo * N, "y")
-    _chk(part, F32, conv_fwd_num_partials(B, Ho, Wo, N, R * S * Ci, Ci) * 2 * N, "part")
+    # BN partial rows: min(P, bn_rep()) replica rows added atomically (zeroed accumulator), or
+    # one stored row per M tile in deterministic mode
+    _chk(part, F32, bn_rows(conv_fwd_num_partials(B, Ho, Wo, N, R * S * Ci, Ci)) * 2 * N, "part")
     if pro == CP_BN_RELU:
         _chk(pa, F32, Ci, "pa")
         _chk(pb, F32, Ci, "pb")
@@ -622,7 +624,7 @@ def conv_dgrad(epi, G, Y, ga, gb, gc, wt, dx, part, B, H, W, Cin, Cout, R, S, st
     _chk(wt, BF16, Cin * R * S * Cout, "wt")
     for t, nm in ((dx, "dx"), (Yt, "Yt"), (Rg, "Rg"), (X, "X"), (Yt2, "Yt2")):
         _chk(t, BF16, B * H * W * Cin, nm)
-    P = conv_dgrad_num_partials(B, H, W, Cin, Cout, R, S, stride)
+    P = bn_rows(conv_dgrad_num_partials(B, H, W, Cin, Cout, R, S, stride))   # rows written (see conv_fwd)
     if epi == CE_BWD_RELU:
         if Yt is None or es is None or et is None:
             raise ValueError("conv_dgrad(CE_BWD_RELU) needs Yt, es, et")
@@ -734,7 +736,8 @@ def maxpool_bwd_num_partials(B, H, W):
 
 def maxpool_bwd(gp, idx, y, s, t, g, part, B, H, W, C):
     """Max-pool backward fused with the stem BN's ReLU mask: g = route(gp) * 1[y*s+t > 0],
-    part <- (sum g, sum g*y) per workgroup (C == 64)."""
+    part <- (sum g, sum g*y) per workgroup (C == 64), atomically into bn_rows(P) replica rows of a
+    zeroed accumulator (deterministic mode: one stored row per workgroup)."""
     if C != 64:
         raise ValueError("maxpool_bwd: C must be 64")
     Ho, Wo = conv_out_hw(H, W, 3, 3, 2, 1)
@@ -742,7 +745,7 @@ def maxpool_bwd(gp, idx, y, s, t, g, part, B, H, W, C):
     _chk(idx, torch.uint8, B * Ho * Wo * C, "idx")
     _chk(y, BF16, B * H * W * C, "y")
     _chk(g, BF16, B * H * W * C, "g")
-    _chk(part, F32, maxpool_bwd_num_partials(B, H, W) * 2 * C, "part")
+    _chk(part, F32, bn_rows(maxpool_bwd_num_partials(B, H, W)) * 2 * C, "part")
     lib().maxpool_bwd(_p(gp), _p(idx), _p(y), _p(s), _p(t), _p(g), _p(part), B, H, W, C, _s())
 
 
@@ -755,13 +758,14 @@ def avgpool(x, out, B, HW, C):
 
 
 def head_bwd(dpool, x, y, G, part, B, HW, C):
-    """G = dpool/HW broadcast * 1[x > 0];  part[B][2][C] <- (sum G, sum G*y) per image."""
+    """G = dpool/HW broadcast * 1[x > 0];  part <- (sum G, sum G*y) per image, atomically into
+    bn_rows(B) replica rows of a zeroed accumulator (deterministic mode: row b = image b)."""
     if C % 8 or C // 8 > 256:
         raise ValueError("head_bwd: C % 8 and C <= 2048")
     _chk(dpool, F32, B * C, "dpool")
     for t, nm in ((x, "x"), (y, "y"), (G, "G")):
         _chk(t, BF16, B * HW * C, nm)
-    _chk(part, F32, B * 2 * C, "part")
+    _chk(part, F32, bn_rows(B) * 2 * C, "part")
     lib().head_bwd(_p(dpool), _p(x), _p(y), _p(G), _p(part), B, HW, C, _s())
 
 
@@ -810,9 +814,10 @@ def col_sum(X, M, N, out):
     lib().col_sum(_p(X), M, N, _p(out), _s())
 
 
-def image_prep(src, idx, labels_src, out, labels_out, seed=0, hyper=None):
+def image_prep(src, idx, labels_src, out, labels_out, seed=0, hyper=None, s2d=False):
     """uint8 [N,H,W,3] pool gathered by idx [B] -> random h-flip, ImageNet normalisation,
-    NHWC bf16 [B,H,W,4] (4th channel 0)."""
+    NHWC bf16 [B,H,W,4] (4th channel 0); ``s2d``: space-to-depth by 2 instead,
+    [B,H/2,W/2,16] with channel (dh*2 + dw)*4 + c (the input of :func:`conv_fwd_s2d`)."""
     B = idx.numel()
     if src.dtype != torch.uint8 or src.dim() != 4 or src.shape[3] != 3 or not src.is_contiguous():
         raise ValueError("image_prep: src must be contiguous uint8 [N,H,W,3]")
@@ -820,8 +825,57 @@ def image_prep(src, idx, labels_src, out, labels_out, seed=0, hyper=None):
     _chk(idx, torch.int64, B, "idx")
     _chk(out, BF16, B * H * W * 4, "out")
     _chk(labels_out, torch.int64, B, "labels_out")
+    if s2d and (H % 2 or W % 2):
+        raise ValueError("image_prep: space-to-depth needs even H and W")
     lib().image_prep(_p(src), _p(idx), _p(labels_src), B, H, W, int(seed) & ((1 << 64) - 1), _p(hyper), _p(out),
-                     _p(labels_out), _s())
+                     _p(labels_out), int(bool(s2d)), _s())
+
+
+# --------------------------------------------------------------------------- space-to-depth stem
+def s2d_image(img, x2, B, H, W):
+    """img [B,H,W,4] bf16 -> space-to-depth x2 [B,H/2,W/2,16] (layout of image_prep(s2d=True))."""
+    if H % 2 or W % 2:
+        raise ValueError("s2d_image: even H and W")
+    _chk(img, BF16, B * H * W * 4, "img")
+    _chk(x2, BF16, B * H * W * 4, "x2")
+    lib().s2d_image(_p(img), _p(x2), B, H, W, _s())
+
+
+def stem_w_s2d(w, w2, N=64):
+    """w [N,7,7,4] bf16 (the 7x7 stem weight, 4-channel storage) -> w2 [N,4,4,16] bf16 with
+    w2[n][r][s][(dh*2+dw)*4+c] = w[n][2r+dh-1][2s+dw-1][c] (zero outside the 7x7)."""
+    _chk(w, BF16, N * 196, "w")
+    _chk(w2, BF16, N * 256, "w2")
+    lib().stem_w_s2d(_p(w), _p(w2), N, _s())
+
+
+def conv_fwd_s2d(x2, w2, y, part, B, H2, N=64):
+    """The 7x7 s2 p3 stem as a 4x4 s1 conv over the space-to-depth image x2 [B,H2,H2,16]
+    (LDS-DMA kernel, multi-tap k-steps): y [B,H2,H2,N] bf16 + BN partial sums of y (rows as
+    :func:`conv_fwd`)."""
+    _chk(x2, BF16, B * H2 * H2 * 16, "x2")
+    _chk(w2, BF16, N * 256, "w2")
+    _chk(y, BF16, B * H2 * H2 * N, "y")
+    _chk(part, F32, bn_rows(conv_fwd_num_partials(B, H2, H2, N, 256, 16)) * 2 * N, "part")
+    lib().conv_fwd_s2d(_p(x2), _p(w2), _p(y), _p(part), B, H2, N, _s())
+
+
+def conv_wgrad_s2d_workspace(B, H2, N=64):
+    return lib().conv_wgrad_s2d_workspace_floats(B, H2, N)
+
+
+def conv_wgrad_s2d(G, Y, ga, gb, gc, x2, ws, grad, B, H2, N=64):
+    """Stem weight gradient grad [N,7,7,4] (fp32, overwritten) from dy = ga*G + gb*Y + gc
+    ([B,H2,H2,N]; or G itself with Y None) and the space-to-depth image x2."""
+    for t, nm in ((G, "G"), (Y, "Y")):
+        _chk(t, BF16, B * H2 * H2 * N, nm)
+    if Y is not None:
+        for t, nm in ((ga, "ga"), (gb, "gb"), (gc, "gc")):
+            _chk(t, F32, N, nm)
+    _chk(x2, BF16, B * H2 * H2 * 16, "x2")
+    _chk(ws, F32, conv_wgrad_s2d_workspace(B, H2, N), "ws")
+    _chk(grad, F32, N * 196, "grad")
+    lib().conv_wgrad_s2d(_p(G), _p(Y), _p(ga), _p(gb), _p(gc), _p(x2), _p(ws), _p(grad), B, H2, N, _s())
 
 
 # --------------------------------------------------------------------------- launch plans

@@ -85,7 +85,7 @@ def test_conv_fwd(dev, shape, pro, glds, glds_mode):
     Ho, Wo = K.conv_out_hw(H, H, R, R, st, pad)
     y = torch.empty(B, Ho, Wo, N, dtype=torch.bfloat16, device=dev)
     P = K.conv_fwd_num_partials(B, Ho, Wo, N, R * R * Ci, Ci)
-    part = torch.full((P, 2, N), float("nan"), device=dev)
+    part = torch.zeros(P, 2, N, device=dev)   # replica rows are added to atomically (bn_part_add)
     K.conv_fwd(pro, x.to(torch.bfloat16).contiguous(), w_store(w), y, part, B, H, H, Ci, N, R, R, st, pad,
                pa=s if pro else None, pb=t if pro else None)
     torch.cuda.synchronize()
@@ -274,6 +274,63 @@ def test_conv_wgrad_stem(dev):
     torch.cuda.synchronize()
     assert rel(grad[..., :3], ref) < 1e-2
     assert grad[..., 3].abs().max().item() == 0.0
+
+
+@pytest.mark.parametrize("B,H", [(2, 32), (3, 46), (2, 224)])
+def test_stem_s2d_fwd_wgrad(dev, B, H):
+    """Space-to-depth stem: the 7x7 s2 p3 conv as a 4x4 s1 conv over the s2d image (LDS-DMA
+    kernel with multi-tap k-steps) and its weight gradient (permuted back to [N][7][7][4]) vs
+    the fp32 PyTorch conv / autograd on the same bf16 values; image_prep(s2d=True) and
+    s2d_image give the same layout."""
+    N, H2 = 64, H // 2
+    x3 = bfr(rnd(B, H, H, 3, dev=dev, seed=71))
+    x4 = torch.cat([x3, torch.zeros(B, H, H, 1, device=dev)], 3).to(torch.bfloat16).contiguous()
+    w = bfr(rnd(N, 3, 7, 7, dev=dev, scale=0.1, seed=72))
+    w4 = torch.cat([w, torch.zeros(N, 1, 7, 7, device=dev)], 1)
+    x2 = torch.empty(B, H2, H2, 16, dtype=torch.bfloat16, device=dev)
+    K.s2d_image(x4, x2, B, H, H)
+    ref_x2 = x4.view(B, H2, 2, H2, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(B, H2, H2, 16)
+    assert torch.equal(x2, ref_x2)
+    w2 = torch.empty(N * 256, dtype=torch.bfloat16, device=dev)
+    K.stem_w_s2d(w_store(w4), w2)
+    y = torch.empty(B, H2, H2, N, dtype=torch.bfloat16, device=dev)
+    P = K.conv_fwd_num_partials(B, H2, H2, N, 256, 16)
+    part = torch.zeros(P, 2, N, device=dev)
+    K.conv_fwd_s2d(x2, w2, y, part, B, H2)
+    torch.cuda.synchronize()
+    ref = nhwc(F.conv2d(nchw(x3), w, stride=2, padding=3))
+    assert rel(y, ref) < 1e-2, rel(y, ref)
+    assert torch.allclose(part.sum(0)[0], y.float().reshape(-1, N).sum(0), rtol=1e-3, atol=1e-2)
+    # weight gradient
+    G = bfr(rnd(B, H2, H2, N, dev=dev, seed=73))
+    Y = bfr(rnd(B, H2, H2, N, dev=dev, seed=74))
+    ga, gb = bn_params(N, dev, 75)
+    gc = torch.randn(N, device=dev) * 0.1
+    dy = bfr(ga * G + gb * Y + gc)
+    wref = _wgrad_ref(x3, dy, (N, 3, 7, 7), 2, 3).permute(0, 2, 3, 1)
+    ws = torch.zeros(K.conv_wgrad_s2d_workspace(B, H2), device=dev)
+    grad = torch.full((N, 7, 7, 4), float("nan"), device=dev)
+    bf = lambda t: t.to(torch.bfloat16).contiguous()  # noqa: E731
+    K.conv_wgrad_s2d(bf(G), bf(Y), ga, gb, gc, x2, ws, grad, B, H2)
+    torch.cuda.synchronize()
+    assert rel(grad[..., :3], wref) < 1e-2, rel(grad[..., :3], wref)
+    assert grad[..., 3].abs().max().item() == 0.0
+
+
+def test_image_prep_s2d(dev):
+    src = torch.randint(0, 256, (4, 24, 24, 3), dtype=torch.uint8, device=dev)
+    labels = torch.arange(4, device=dev)
+    idx = torch.tensor([3, 1], device=dev)
+    hyper = torch.tensor([0.0, 5.0], device=dev)
+    out = torch.empty(2, 24, 24, 4, dtype=torch.bfloat16, device=dev)
+    out2 = torch.empty(2, 12, 12, 16, dtype=torch.bfloat16, device=dev)
+    lab = torch.empty(2, dtype=torch.int64, device=dev)
+    K.image_prep(src, idx, labels, out, lab, seed=9, hyper=hyper)
+    K.image_prep(src, idx, labels, out2, lab, seed=9, hyper=hyper, s2d=True)
+    conv = torch.empty_like(out2)
+    K.s2d_image(out, conv, 2, 24, 24)
+    torch.cuda.synchronize()
+    assert torch.equal(out2, conv)
 
 
 def test_res_out(dev):
