@@ -106,7 +106,7 @@ void launch_conv_fwd(int, const bf16_t *, const float *, const float *, const bf
 void launch_conv_dgrad(int, const bf16_t *, const bf16_t *, const float *, const float *, const float *,
                        const bf16_t *, bf16_t *, const bf16_t *, const float *, const float *, const bf16_t *,
                        const bf16_t *, const bf16_t *, float *, float *, int, int, int, int, int, int, int, int,
-                       int, hipStream_t);
+                       int, const uint8_t *, hipStream_t);
 long long conv_wgrad_workspace_floats(int, int, int, int, int, int, int, int, int);
 void launch_conv_wgrad(const bf16_t *, const bf16_t *, const float *, const float *, const float *,
                        const bf16_t *, const float *, const float *, int, float *, float *, int, int, int, int,
@@ -115,7 +115,7 @@ void launch_conv_wt(const bf16_t *, bf16_t *, const int *, int, hipStream_t);
 void launch_bn_mat(int, const bf16_t *, const bf16_t *, const float *, const float *, const float *, bf16_t *, int, int,
                    hipStream_t);
 void launch_res_out(const bf16_t *, const float *, const float *, const bf16_t *, const float *, const float *,
-                    bf16_t *, long long, int, const void *, const void *, hipStream_t);
+                    bf16_t *, long long, int, const void *, const void *, uint8_t *, hipStream_t);
 void launch_maxpool_fwd(const bf16_t *, const float *, const float *, bf16_t *, uint8_t *, int, int, int, int,
                         hipStream_t);
 int maxpool_bwd_num_partials(int, int, int);
@@ -353,12 +353,12 @@ PYBIND11_MODULE(_pgdist_C, m) {
   });
   m.def("conv_dgrad", [](int epi, P G, P Y, P ga, P gb, P gc, P wt, P dx, P Yt, P es, P et, P Rg, P X, P Yt2,
                          P part, P part2, int Nb, int H, int W, int Cin, int Cout, int R, int Sk, int st, int pad,
-                         P s) {
+                         P Xm, P s) {
     pgdist_rt::run_op([=] {
       launch_conv_dgrad(epi, ptr<bf16_t>(G), ptr<bf16_t>(Y), ptr<float>(ga), ptr<float>(gb), ptr<float>(gc),
                         ptr<bf16_t>(wt), ptr<bf16_t>(dx), ptr<bf16_t>(Yt), ptr<float>(es), ptr<float>(et),
                         ptr<bf16_t>(Rg), ptr<bf16_t>(X), ptr<bf16_t>(Yt2), ptr<float>(part), ptr<float>(part2), Nb,
-                        H, W, Cin, Cout, R, Sk, st, pad, S(s));
+                        H, W, Cin, Cout, R, Sk, st, pad, ptr<uint8_t>(Xm), S(s));
     });
   });
   m.def("conv_wgrad_workspace_floats", &conv_wgrad_workspace_floats);
@@ -381,10 +381,10 @@ PYBIND11_MODULE(_pgdist_C, m) {
       launch_conv_wt(ptr<bf16_t>(src), ptr<bf16_t>(dst), ptr<int>(tab), n, S(s));
     });
   });
-  m.def("res_out", [](P y, P sc, P sh, P r, P rs, P rt, P out, long long M, int C, P lz, P lz2, P s) {
+  m.def("res_out", [](P y, P sc, P sh, P r, P rs, P rt, P out, long long M, int C, P lz, P lz2, P mask, P s) {
     pgdist_rt::run_op([=] {
       launch_res_out(ptr<bf16_t>(y), ptr<float>(sc), ptr<float>(sh), ptr<bf16_t>(r), ptr<float>(rs),
-                     ptr<float>(rt), ptr<bf16_t>(out), M, C, ptr<void>(lz), ptr<void>(lz2), S(s));
+                     ptr<float>(rt), ptr<bf16_t>(out), M, C, ptr<void>(lz), ptr<void>(lz2), ptr<uint8_t>(mask), S(s));
     });
   });
   m.def("maxpool_fwd", [](P y, P sc, P sh, P out, P idx, int Nb, int H, int W, int C, P s) {

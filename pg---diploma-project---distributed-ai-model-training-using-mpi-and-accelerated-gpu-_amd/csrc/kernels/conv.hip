@@ -37,7 +37,10 @@ enum { CM_FWD = 0, CM_DGRAD = 1 };
 enum { CP_NONE = 0, CP_BN_RELU = 1, CP_BNBWD = 3 };
 // backward epilogues: ReLU mask of the producer BN, or (+R) (*1[X>0]) with statistics against
 // Yt (and Yt2); the operand set is a template choice so every epilogue load is unconditional
-enum { CE_FWD = 0, CE_BWD_RELU = 1, CE_BWD_PLAIN = 2, CE_BWD_R = 3, CE_BWD_RXY = 4, CE_BWD_RXYY = 5 };
+// CE_BWD_RXYM / CE_BWD_RXYYM: the ReLU mask 1[X > 0] comes from a bit mask Xm [M][N/8] (bit j of
+// byte (m*N + n)/8 = channel n % 8 ... of pixel m) written by res_out instead of the bf16 X itself
+enum { CE_FWD = 0, CE_BWD_RELU = 1, CE_BWD_PLAIN = 2, CE_BWD_R = 3, CE_BWD_RXY = 4, CE_BWD_RXYY = 5,
+       CE_BWD_RXYM = 6, CE_BWD_RXYYM = 7 };
 
 struct ConvArgs {
   const bf16_t *A;      // gathered image [Nb][Hi][Wi][Ci]  (fwd: x, dgrad: G of this layer's BN)
@@ -48,6 +51,7 @@ struct ConvArgs {
   const bf16_t *Yt;     // epilogue statistics partner [Nb][Ho][Wo][N]
   const bf16_t *Yt2;    // second partner (CE_BWD_RES)
   const bf16_t *X;      // CE_BWD_RES: mask tensor (x > 0), may be null
+  const uint8_t *Xm;    // CE_BWD_RXYM / RXYYM: the same mask as bits (res_out mask output)
   const bf16_t *Rg;     // CE_BWD_RES: added gradient, may be null
   const float *es, *et; // CE_BWD_RELU: producer BN scale / shift (mask y*s+t > 0)
   float *part, *part2;  // [P][2][N]
@@ -118,10 +122,11 @@ PG_DEVICE void conv_epilogue(const ConvArgs &p, f32x4_t (&acc)[BM / 32][BN / 32]
   // bf16 C tile in LDS, then 16-B row chunks.  The epilogue operands of the
   // first EB rows are loaded before the C tile is staged; rows past the end are clamped to
   // a valid row (loads are unconditional, results discarded) so hipcc keeps them in flight.
-  constexpr bool E_R = EPI == CE_BWD_R || EPI == CE_BWD_RXY || EPI == CE_BWD_RXYY;
+  constexpr bool E_XM = EPI == CE_BWD_RXYM || EPI == CE_BWD_RXYYM;
+  constexpr bool E_R = EPI == CE_BWD_R || EPI == CE_BWD_RXY || EPI == CE_BWD_RXYY || E_XM;
   constexpr bool E_X = EPI == CE_BWD_RXY || EPI == CE_BWD_RXYY;
-  constexpr bool E_YT = EPI == CE_BWD_RELU || EPI == CE_BWD_RXY || EPI == CE_BWD_RXYY;
-  constexpr bool E_YT2 = EPI == CE_BWD_RXYY;
+  constexpr bool E_YT = EPI == CE_BWD_RELU || EPI == CE_BWD_RXY || EPI == CE_BWD_RXYY || E_XM;
+  constexpr bool E_YT2 = EPI == CE_BWD_RXYY || EPI == CE_BWD_RXYYM;
   constexpr bool STATS = EPI == CE_FWD || E_YT;
   constexpr int EB = NP < 4 ? NP : 4;
   const int my_chunk = tid % CH;
@@ -135,6 +140,7 @@ PG_DEVICE void conv_epilogue(const ConvArgs &p, f32x4_t (&acc)[BM / 32][BN / 32]
     ld8f(p.et + ncol0, et);
   }
   uint4 oy[EB], orr[EB], ox[EB], oy2[EB];
+  uint32_t oxm[EB];
   size_t offs[EB];
   bool okr[EB];
   auto issue = [&](int i0) {
@@ -155,6 +161,7 @@ PG_DEVICE void conv_epilogue(const ConvArgs &p, f32x4_t (&acc)[BM / 32][BN / 32]
       if constexpr (E_YT) oy[e] = ldg16(p.Yt + offs[e]);
       if constexpr (E_R) orr[e] = ldg16(p.Rg + offs[e]);
       if constexpr (E_X) ox[e] = ldg16(p.X + offs[e]);
+      if constexpr (E_XM) oxm[e] = p.Xm[offs[e] >> 3];   // ncol0 % 8 == 0: one byte per 8 channels
       if constexpr (E_YT2) oy2[e] = ldg16(p.Yt2 + offs[e]);
     }
   };
@@ -199,6 +206,10 @@ PG_DEVICE void conv_epilogue(const ConvArgs &p, f32x4_t (&acc)[BM / 32][BN / 32]
           unpack8(ox[e], xv);
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] = xv[j] > 0.f ? v[j] : 0.f;
+        }
+        if constexpr (E_XM) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = (oxm[e] >> j) & 1u ? v[j] : 0.f;
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = bf2f(f2bf(v[j]));
@@ -1178,12 +1189,14 @@ __global__ __launch_bounds__(256) void conv_wt_kernel(const bf16_t *__restrict__
 // ===========================================================================
 // bottleneck output:  o = relu(y3*s3 + t3 + (yd*sd + td  |  x))       [M][C]
 // ===========================================================================
+// mask (optional, [M][C/8] bytes): bit j of byte i = out element 8i + j > 0 (the ReLU mask the
+// next block's conv1 dgrad applies, CE_BWD_RXYM: 1/16 of the bytes of re-reading out)
 template <bool PROJ, bool LZ>
 __global__ __launch_bounds__(256) void res_out_kernel(const bf16_t *__restrict__ y, const float *__restrict__ s,
                                                       const float *__restrict__ t, const bf16_t *__restrict__ r,
                                                       const float *__restrict__ rs, const float *__restrict__ rt,
                                                       bf16_t *__restrict__ out, long long n8, int C8,
-                                                      const BnFin *lz, const BnFin *lz2) {
+                                                      const BnFin *lz, const BnFin *lz2, uint8_t *__restrict__ mask) {
   extern __shared__ __attribute__((aligned(16))) float lzs[];
   if constexpr (LZ) {   // BN3 (and the projection BN) finalized from the replica rows
     const int C = C8 * 8;
@@ -1209,7 +1222,15 @@ __global__ __launch_bounds__(256) void res_out_kernel(const bf16_t *__restrict__
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = reluf(fmaf(v[k], a[k], b[k]) + rv[k]);
-    stg16(out + i * 8, pack8(v));
+    const uint4 o = pack8(v);
+    stg16(out + i * 8, o);
+    if (mask) {   // from the stored bf16 values (relu >= 0: nonzero bits <=> > 0)
+      const uint32_t w[4] = {o.x, o.y, o.z, o.w};
+      uint32_t m = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) m |= ((w[k] & 0xffffu) ? 1u : 0u) << (2 * k) | ((w[k] >> 16) ? 1u : 0u) << (2 * k + 1);
+      mask[i] = (uint8_t)m;
+    }
   }
 }
 
@@ -1637,10 +1658,11 @@ void launch_conv_fwd(int pro, const bf16_t *x, const float *pa, const float *pb,
 void launch_conv_dgrad(int epi, const bf16_t *G, const bf16_t *Y, const float *ga, const float *gb, const float *gc,
                        const bf16_t *wt, bf16_t *dx, const bf16_t *Yt, const float *es, const float *et,
                        const bf16_t *Rg, const bf16_t *X, const bf16_t *Yt2, float *part, float *part2, int Nb, int H,
-                       int W, int Cin, int Cout, int R, int S, int st, int pad, hipStream_t stream) {
+                       int W, int Cin, int Cout, int R, int S, int st, int pad, const uint8_t *Xm,
+                       hipStream_t stream) {
   ConvArgs a{};
   a.A = G; a.A2 = Y; a.pa = ga; a.pb = gb; a.pc = gc; a.W = wt; a.out = dx;
-  a.Yt = Yt; a.Yt2 = Yt2; a.X = X; a.Rg = Rg; a.es = es; a.et = et; a.part = part; a.part2 = part2;
+  a.Yt = Yt; a.Yt2 = Yt2; a.X = X; a.Xm = Xm; a.Rg = Rg; a.es = es; a.et = et; a.part = part; a.part2 = part2;
   a.Hi = (H + 2 * pad - R) / st + 1;
   a.Wi = (W + 2 * pad - S) / st + 1;
   a.Ci = Cout;
@@ -1659,16 +1681,20 @@ void launch_conv_dgrad(int epi, const bf16_t *G, const bf16_t *Y, const float *g
   a.bn_rep = g_bn_rep;
   if (Y == nullptr) {   // G is the materialised dy (launch_bn_mat): LDS-DMA kernel, no prologue
     if (epi == CE_BWD_RELU) { launch_glds<CM_DGRAD, CE_BWD_RELU>(a, g, stream); return; }
-    if (!Rg && !X && !Yt && !Yt2) launch_glds<CM_DGRAD, CE_BWD_PLAIN>(a, g, stream);
-    else if (Rg && !X && !Yt && !Yt2) launch_glds<CM_DGRAD, CE_BWD_R>(a, g, stream);
+    if (!Rg && !X && !Xm && !Yt && !Yt2) launch_glds<CM_DGRAD, CE_BWD_PLAIN>(a, g, stream);
+    else if (Rg && !X && !Xm && !Yt && !Yt2) launch_glds<CM_DGRAD, CE_BWD_R>(a, g, stream);
+    else if (Rg && Xm && Yt && !Yt2) launch_glds<CM_DGRAD, CE_BWD_RXYM>(a, g, stream);
+    else if (Rg && Xm && Yt && Yt2) launch_glds<CM_DGRAD, CE_BWD_RXYYM>(a, g, stream);
     else if (Rg && X && Yt && !Yt2) launch_glds<CM_DGRAD, CE_BWD_RXY>(a, g, stream);
     else if (Rg && X && Yt && Yt2) launch_glds<CM_DGRAD, CE_BWD_RXYY>(a, g, stream);
     return;
   }
   if (epi == CE_BWD_RELU) { launch_geom<CM_DGRAD, CP_BNBWD, CE_BWD_RELU, 8>(a, g, stream); return; }
   // (dx + Rg) * 1[X > 0] with statistics against Yt (, Yt2): supported operand sets
-  if (!Rg && !X && !Yt && !Yt2) launch_geom<CM_DGRAD, CP_BNBWD, CE_BWD_PLAIN, 8>(a, g, stream);
-  else if (Rg && !X && !Yt && !Yt2) launch_geom<CM_DGRAD, CP_BNBWD, CE_BWD_R, 8>(a, g, stream);
+  if (!Rg && !X && !Xm && !Yt && !Yt2) launch_geom<CM_DGRAD, CP_BNBWD, CE_BWD_PLAIN, 8>(a, g, stream);
+  else if (Rg && !X && !Xm && !Yt && !Yt2) launch_geom<CM_DGRAD, CP_BNBWD, CE_BWD_R, 8>(a, g, stream);
+  else if (Rg && Xm && Yt && !Yt2) launch_geom<CM_DGRAD, CP_BNBWD, CE_BWD_RXYM, 8>(a, g, stream);
+  else if (Rg && Xm && Yt && Yt2) launch_geom<CM_DGRAD, CP_BNBWD, CE_BWD_RXYYM, 8>(a, g, stream);
   else if (Rg && X && Yt && !Yt2) launch_geom<CM_DGRAD, CP_BNBWD, CE_BWD_RXY, 8>(a, g, stream);
   else if (Rg && X && Yt && Yt2) launch_geom<CM_DGRAD, CP_BNBWD, CE_BWD_RXYY, 8>(a, g, stream);
 }
@@ -1797,7 +1823,7 @@ void launch_conv_wt(const bf16_t *src, bf16_t *dst, const int *tab, int n, hipSt
 // lz / lz2 (device BnFin descriptors, both or neither; lz2 only with the projection): lazy finalize
 void launch_res_out(const bf16_t *y, const float *s, const float *t, const bf16_t *r, const float *rs,
                     const float *rt, bf16_t *out, long long M, int C, const void *lz, const void *lz2,
-                    hipStream_t st) {
+                    uint8_t *mask, hipStream_t st) {
   const long long n8 = M * (C / 8);
   int grid = (int)((n8 + 255) / 256);
   const int cap = lz ? (C > 256 ? 512 : 2048) : 16384;
@@ -1805,7 +1831,8 @@ void launch_res_out(const bf16_t *y, const float *s, const float *t, const bf16_
   const BnFin *d = static_cast<const BnFin *>(lz), *d2 = static_cast<const BnFin *>(lz2);
   const size_t lds = lz ? (size_t)(rs ? 4 : 2) * C * sizeof(float) : 0;
 #define RO(PJ, LZ_) \
-  hipLaunchKernelGGL((res_out_kernel<PJ, LZ_>), dim3(grid), dim3(256), lds, st, y, s, t, r, rs, rt, out, n8, C / 8, d, d2)
+  hipLaunchKernelGGL((res_out_kernel<PJ, LZ_>), dim3(grid), dim3(256), lds, st, y, s, t, r, rs, rt, out, n8, C / 8, d, d2, \
+                     mask)
   if (rs) { if (lz) RO(true, true); else RO(true, false); }
   else { if (lz) RO(false, true); else RO(false, false); }
 #undef RO

@@ -81,6 +81,7 @@ class BlockPlan:
     bnd: Optional[BNState]
     x_in: torch.Tensor = None     # block input (previous output or max-pool output)
     out: torch.Tensor = None      # block output o (materialised)
+    out_mask: torch.Tensor = None  # 1[o > 0] as bits, uint8 [M, C/8] (the next block's conv1 dgrad)
     Rd: torch.Tensor = None       # projection-shortcut data gradient (dgrad of cd)
 
 
@@ -150,6 +151,11 @@ class ResNet50Executor:
                     wg_space(c)
                 self.blocks.append(bp)
                 H, x_in = Ho, bp.out
+        # ReLU mask of every block output but the last as bits (res_out writes it, the next block's
+        # conv1 dgrad epilogue reads 1/16 of the bytes of re-reading o; PGDIST_RN_XMASK=0: off)
+        if os.environ.get("PGDIST_RN_XMASK", "1") == "1":
+            for bp in self.blocks[:-1]:
+                bp.out_mask = torch.empty(bp.out.shape[0], bp.cout // 8, dtype=torch.uint8, device=device)
         # ---------------- materialised operands of the LDS-DMA convs
         self.mat = K.conv_get_glds() != 0 and os.environ.get("PGDIST_RN_MAT", "1") != "0"
         act_mode = os.environ.get("PGDIST_RN_ACT", "auto")
@@ -199,7 +205,51 @@ class ResNet50Executor:
         for bn, o, nf, nb in spans:
             bn.acc_f = self.bn_arena[o:o + nf]
             bn.acc_b = self.bn_arena[o + nf:o + nf + nb]
+        # lazy BN finalize (default outside deterministic mode; PGDIST_BN_LAZY=0: a finalize launch
+        # after every producer): the consumers that support it -- max-pool, the bn_mat passes
+        # (relu(BN(y)) forward, dy = a*G + b*Y + c backward) and the block output res_out --
+        # compute the BN parameters they need from the replica rows in their prologue, so no
+        # finalize launch sits between producer and consumer on the main stream.  The side
+        # outputs (mean / rstd / scale / shift / running statistics) come from one batched
+        # finalize at the end of the forward; the backward ones (coef, dgamma / dbeta) from
+        # batched finalizes on the weight-gradient side stream ahead of the gradient buckets.
+        # A BN whose consumer needs materialised parameters (a conv with the BN+ReLU prologue, a
+        # dgrad / wgrad with the BN-backward prologue) keeps its finalize launch.
+        # opt-in (PGDIST_BN_LAZY=1): measured on MI355X at bs128, 11.98 ms/step lazy vs 11.83 with
+        # the finalize launches (the bn_mat passes are 50 of the lazy consumers, and each of their
+        # workgroups re-reducing all C channels costs more than the ~3 us launch it replaces)
+        self.lazy_bn = not K.deterministic() and os.environ.get("PGDIST_BN_LAZY", "0") == "1"
+        bns = self.all_bns()
+        self.bn_ctr = torch.zeros(8 * len(bns) + 16, dtype=torch.int32, device=device)
+        self._fin_tabs = {}
+        self.fwd_lazy: List[AtomicBNState] = []
+        if self.lazy_bn:
+            self.refresh_bn_fin()
+            # forward: consumers bn0 -> max-pool, bn1 -> conv2 input, bn2 -> conv3 input, bn3 / bnd
+            # -> res_out; backward: each BN's coefficients -> bn_mat of its conv's dy (the stem's
+            # on the side stream, after its side finalize)
+            self.bn0.lz_f, self.bn0.lz_b = self.bn0.desc_f, self.bn0.desc_b
+            for bp in self.blocks:
+                for bn, c_in, c_dy in ((bp.bn1, bp.c2, bp.c1), (bp.bn2, bp.c3, bp.c2), (bp.bn3, None, bp.c3),
+                                       (bp.bnd, None, bp.cd)):
+                    if bn is None:
+                        continue
+                    if c_in is None or c_in.act:
+                        bn.lz_f = bn.desc_f
+                    if c_dy.dy is not None:
+                        bn.lz_b = bn.desc_b
+            self.fwd_lazy = [bn for bn in bns if bn.lz_f is not None]
+            self.fwd_fin_tab = K.bn_desc_table([bn.desc_f for bn in self.fwd_lazy])
+            self.fwd_fin_maxc = max(bn.C for bn in self.fwd_lazy)
         self.ws_wgrad = torch.zeros(max(wgs) + 1024, **f32)
+        # one split-partial workspace per weight gradient of a flushed side-stream group: the
+        # group's split-M reductions then run as one multi-segment launch after its wgrads
+        # (PGDIST_RED_BATCH=0: a reduction launch per wgrad)
+        # opt-in (PGDIST_RED_BATCH=1): measured 11.80 ms/step with a reduction per wgrad vs 11.89-11.93
+        # batched (same reduction time; the batch delays the next group's start on the side stream)
+        self.batch_reductions = os.environ.get("PGDIST_RED_BATCH", "0") == "1"
+        nws = max(1, int(os.environ.get("PGDIST_SIDE_BATCH", "3"))) if self.batch_reductions else 1
+        self.ws_wgrad_pool = [self.ws_wgrad] + [torch.zeros_like(self.ws_wgrad) for _ in range(nws - 1)]
         self.side = None
         self._side_pending = []
         self.side_batch = max(1, int(os.environ.get("PGDIST_SIDE_BATCH", "3")))
@@ -234,6 +284,15 @@ class ResNet50Executor:
         self.wt_tab = torch.tensor(tab, dtype=torch.int32, device=device).contiguous()
 
     # ------------------------------------------------------------------ helpers
+    def refresh_bn_fin(self):
+        """(Re)build the lazy-finalize descriptors in place (after the BN running buffers were
+        re-homed, e.g. coalesced for the per-step buffer broadcast), so recorded plans and the
+        batched-finalize tables keep valid pointers."""
+        if not self.lazy_bn:
+            return
+        for i, bn in enumerate(self.all_bns()):
+            bn.build_desc(self.bn_ctr[8 * i:8 * i + 1], self.bn_ctr[8 * i + 4:8 * i + 5])
+
     def _bn_producer_rows(self):
         """{bn: (forward P, backward P)}: partial rows of the kernels producing each BN's
         statistics (forward: its conv's epilogue; backward: the dgrad of the conv that consumes
@@ -296,15 +355,17 @@ class ResNet50Executor:
         with torch.cuda.stream(self.side):
             self.on_params_ready(names)
 
-    def _wgrad(self, fn):
+    def _wgrad(self, fn, fins=()):
         """Weight-gradient work on the side stream, deferred in groups of ``side_batch`` (one
         side-stream join per group: each join's event record idles the main stream ~5 us;
-        see MobileNetV2Executor._wgrad)."""
+        see MobileNetV2Executor._wgrad).  ``fins``: (bn, P) backward finalizes of lazy BNs whose
+        statistics are complete by now, run (batched) ahead of the group's weight gradients."""
         if self.side is None:
-            fn()
+            self._side_fins(list(fins))
+            fn(self.ws_wgrad)
             return
-        self._side_pending.append(fn)
-        if len(self._side_pending) >= self.side_batch:
+        self._side_pending.append((fins, fn))
+        if len(self._side_pending) >= min(self.side_batch, len(self.ws_wgrad_pool)):
             self._flush_side()
 
     def _flush_side(self):
@@ -312,9 +373,31 @@ class ResNet50Executor:
             return
         K.stream_wait(self.side, torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.side):
-            for fn in self._side_pending:
-                fn()
+            self._side_fins([f for fins, _ in self._side_pending for f in fins])
+            K.wgrad_reduce_defer(self.batch_reductions)
+            try:
+                for j, (_, fn) in enumerate(self._side_pending):
+                    fn(self.ws_wgrad_pool[j])
+            finally:
+                K.wgrad_reduce_defer(False)
+            if self.batch_reductions:
+                K.wgrad_reduce_flush()
         self._side_pending.clear()
+
+    def _side_fins(self, fins):
+        """Backward finalizes (coef, dgamma / dbeta) of lazy BNs as one batched launch."""
+        fins = [(bn, P) for bn, P in fins if bn.lz_b is not None]
+        if not fins:
+            return
+        if len(fins) == 1:
+            bn, P = fins[0]
+            bn.finalize_bwd(bn.acc_b, P, force=True)
+            return
+        key = tuple(id(bn) for bn, _ in fins)
+        tab = self._fin_tabs.get(key)
+        if tab is None:
+            tab = self._fin_tabs[key] = K.bn_desc_table([bn.desc_b for bn, _ in fins])
+        K.bn_finalize_batch(tab, len(fins), max(bn.C for bn, _ in fins))
 
     def _fin(self, bn: AtomicBNState, P: int, train: bool):
         if train:
@@ -324,7 +407,7 @@ class ResNet50Executor:
         B = self.B
         ci = 4 if c.cin == 3 else c.cin
         if c.act and pro == K.CP_BN_RELU:   # relu(BN(x)) materialised once: plain LDS-DMA conv
-            K.bn_mat(K.BN_MAT_ACT, x, bn_in.scale, bn_in.shift, bn_in.act)
+            K.bn_mat(K.BN_MAT_ACT, x, bn_in.scale, bn_in.shift, bn_in.act, lz=bn_in.lz_f if train else None)
             pro, x, bn_in = K.CP_NONE, bn_in.act, None
         K.conv_fwd(pro, x, self.flat.b(c.name), y, bn_out.acc_f, B, c.H, c.H, ci, c.cout, c.k, c.k, c.stride,
                    c.pad, pa=bn_in.scale if bn_in is not None else None,
@@ -336,7 +419,7 @@ class ResNet50Executor:
         into c.dy (LDS-DMA kernels, Y = None), or the pair for the fused BN-backward prologue."""
         if c.dy is None:
             return G, bn.y
-        K.bn_mat(K.BN_MAT_BWD, bn.y, bn.a, bn.b, c.dy, G=G, c=bn.c)
+        K.bn_mat(K.BN_MAT_BWD, bn.y, bn.a, bn.b, c.dy, G=G, c=bn.c, lz=bn.lz_b)
         return c.dy, None
 
     @staticmethod
@@ -361,16 +444,23 @@ class ResNet50Executor:
             self._fin(self.bn0, K.conv_fwd_num_partials(B, H2, H2, 64, 256, 16), train)
         else:
             self._conv(self.stem, K.CP_NONE, self.img, self.bn0.y, train, self.bn0)
-        K.maxpool_fwd(self.bn0.y, self.bn0.scale, self.bn0.shift, self.pool, self.pool_idx, B, self.H0, self.H0, 64)
+        L = (lambda bn: bn.lz_f) if train else (lambda bn: None)   # lazy consumers (training only)  # noqa: E731
+        K.maxpool_fwd(self.bn0.y, self.bn0.scale, self.bn0.shift, self.pool, self.pool_idx, B, self.H0, self.H0, 64,
+                      lz=L(self.bn0))
         for bp in self.blocks:
             self._conv(bp.c1, K.CP_NONE, bp.x_in, bp.bn1.y, train, bp.bn1)
             self._conv(bp.c2, K.CP_BN_RELU, bp.bn1.y, bp.bn2.y, train, bp.bn2, bp.bn1)
             self._conv(bp.c3, K.CP_BN_RELU, bp.bn2.y, bp.bn3.y, train, bp.bn3, bp.bn2)
             if bp.cd is not None:
                 self._conv(bp.cd, K.CP_NONE, bp.x_in, bp.bnd.y, train, bp.bnd)
-                K.res_out(bp.bn3.y, bp.bn3.scale, bp.bn3.shift, bp.bnd.y, bp.out, rs=bp.bnd.scale, rt=bp.bnd.shift)
+                lz = (L(bp.bn3), L(bp.bnd)) if L(bp.bn3) is not None and L(bp.bnd) is not None else (None, None)
+                K.res_out(bp.bn3.y, bp.bn3.scale, bp.bn3.shift, bp.bnd.y, bp.out, rs=bp.bnd.scale, rt=bp.bnd.shift,
+                          lz=lz[0], lz2=lz[1], mask=bp.out_mask if train else None)
             else:
-                K.res_out(bp.bn3.y, bp.bn3.scale, bp.bn3.shift, bp.x_in, bp.out)
+                K.res_out(bp.bn3.y, bp.bn3.scale, bp.bn3.shift, bp.x_in, bp.out, lz=L(bp.bn3),
+                          mask=bp.out_mask if train else None)
+        if train and self.fwd_lazy:   # side outputs of the lazily consumed BNs, one launch
+            K.bn_finalize_batch(self.fwd_fin_tab, len(self.fwd_lazy), self.fwd_fin_maxc)
         # head
         HW = self.Hf * self.Hf
         K.avgpool(self.blocks[-1].out, self.pooled, B, HW, self.C_last)
@@ -382,7 +472,7 @@ class ResNet50Executor:
 
     # ------------------------------------------------------------------ backward
     def backward(self):
-        f, B, wg = self.flat, self.B, self.ws_wgrad
+        f, B = self.flat, self.B
         K.conv_wt(f.shadow, f.shadow_t, self.wt_tab, self.wt_tab.shape[0])
         # head: fc gradients (fp32 GEMMs) and the pooled gradient through the last ReLU
         C, NC = self.C_last, self.NC
@@ -396,7 +486,9 @@ class ResNet50Executor:
         HW = self.Hf * self.Hf
         K.head_bwd(self.dpool, last.out, last.bn3.y, last.bn3.g, last.bn3.acc_b, B, HW, self.C_last)
         last.bn3.finalize_bwd(last.bn3.acc_b, B)
-        self._ready(last.bn3.param_names)
+        pend_fins = [(last.bn3, B)]   # lazy: finalized on the side stream with the next wgrad group
+        if last.bn3.lz_b is None:
+            self._ready(last.bn3.param_names)
         for i in range(len(self.blocks) - 1, -1, -1):
             bp = self.blocks[i]
             prev = self.blocks[i - 1] if i > 0 else None
@@ -407,28 +499,34 @@ class ResNet50Executor:
             g3, y3 = self._dy(c3, bn3.g, bn3)
             K.conv_dgrad(K.CE_BWD_RELU, g3, y3, bn3.a, bn3.b, bn3.c, f.bt(c3.name), bn2.g, bn2.acc_b, B, Ho, Ho,
                          c3.cin, c3.cout, 1, 1, 1, 0, Yt=bn2.y, es=bn2.scale, et=bn2.shift)
-            bn2.finalize_bwd(bn2.acc_b, K.conv_dgrad_num_partials(B, Ho, Ho, c3.cin, c3.cout, 1, 1, 1))
-            self._wgrad(lambda bp=bp, g3=g3, y3=y3: K.conv_wgrad(
-                g3, y3, bp.bn3.a, bp.bn3.b, bp.bn3.c, ws=wg, grad=f.g(bp.c3.name), B=B, H=bp.Ho, W=bp.Ho,
-                Ci=bp.c3.cin, N=bp.c3.cout, R=1, S=1, stride=1, pad=0, **self._wx(bp.c3, bp.bn2.y, bp.bn2)))
-            self._ready([c3.name] + bn2.param_names)
+            P2 = K.conv_dgrad_num_partials(B, Ho, Ho, c3.cin, c3.cout, 1, 1, 1)
+            bn2.finalize_bwd(bn2.acc_b, P2)
+            self._wgrad(lambda ws, bp=bp, g3=g3, y3=y3: K.conv_wgrad(
+                g3, y3, bp.bn3.a, bp.bn3.b, bp.bn3.c, ws=ws, grad=f.g(bp.c3.name), B=B, H=bp.Ho, W=bp.Ho,
+                Ci=bp.c3.cin, N=bp.c3.cout, R=1, S=1, stride=1, pad=0, **self._wx(bp.c3, bp.bn2.y, bp.bn2)),
+                fins=pend_fins + [(bn2, P2)])
+            self._ready([c3.name] + bn2.param_names + [n for bn_, _ in pend_fins for n in bn_.param_names
+                                                       if bn_.lz_b is not None])
+            pend_fins = []
             # projection shortcut: data gradient (summed in conv1's dgrad epilogue) + weight gradient
             if cd is not None:
                 gd, yd = self._dy(cd, bn3.g, bnd)
                 K.conv_dgrad(K.CE_BWD_RES, gd, yd, bnd.a, bnd.b, bnd.c, f.bt(cd.name), bp.Rd, None, B, H, H,
                              cd.cin, cd.cout, 1, 1, cd.stride, 0)
-                self._wgrad(lambda bp=bp, gd=gd, yd=yd: K.conv_wgrad(
-                    gd, yd, bp.bnd.a, bp.bnd.b, bp.bnd.c, ws=wg, grad=f.g(bp.cd.name), B=B, H=bp.H, W=bp.H,
+                self._wgrad(lambda ws, bp=bp, gd=gd, yd=yd: K.conv_wgrad(
+                    gd, yd, bp.bnd.a, bp.bnd.b, bp.bnd.c, ws=ws, grad=f.g(bp.cd.name), B=B, H=bp.H, W=bp.H,
                     Ci=bp.cd.cin, N=bp.cd.cout, R=1, S=1, stride=bp.cd.stride, pad=0, **self._wx(bp.cd, bp.x_in, None)))
                 self._ready([cd.name])
             # conv2 dgrad -> G1 (ReLU mask of BN1) + BN1 partials
             g2, y2 = self._dy(c2, bn2.g, bn2)
             K.conv_dgrad(K.CE_BWD_RELU, g2, y2, bn2.a, bn2.b, bn2.c, f.bt(c2.name), bn1.g, bn1.acc_b, B, H, H,
                          c2.cin, c2.cout, 3, 3, c2.stride, 1, Yt=bn1.y, es=bn1.scale, et=bn1.shift)
-            bn1.finalize_bwd(bn1.acc_b, K.conv_dgrad_num_partials(B, H, H, c2.cin, c2.cout, 3, 3, c2.stride))
-            self._wgrad(lambda bp=bp, g2=g2, y2=y2: K.conv_wgrad(
-                g2, y2, bp.bn2.a, bp.bn2.b, bp.bn2.c, ws=wg, grad=f.g(bp.c2.name), B=B, H=bp.H, W=bp.H,
-                Ci=bp.c2.cin, N=bp.c2.cout, R=3, S=3, stride=bp.c2.stride, pad=1, **self._wx(bp.c2, bp.bn1.y, bp.bn1)))
+            P1b = K.conv_dgrad_num_partials(B, H, H, c2.cin, c2.cout, 3, 3, c2.stride)
+            bn1.finalize_bwd(bn1.acc_b, P1b)
+            self._wgrad(lambda ws, bp=bp, g2=g2, y2=y2: K.conv_wgrad(
+                g2, y2, bp.bn2.a, bp.bn2.b, bp.bn2.c, ws=ws, grad=f.g(bp.c2.name), B=B, H=bp.H, W=bp.H,
+                Ci=bp.c2.cin, N=bp.c2.cout, R=3, S=3, stride=bp.c2.stride, pad=1, **self._wx(bp.c2, bp.bn1.y, bp.bn1)),
+                fins=[(bn1, P1b)])
             self._ready([c2.name] + bn1.param_names)
             # conv1 dgrad + shortcut gradient -> gradient of the block input:
             #   previous block: Gz_prev = (dx + sc) * 1[o_prev > 0], BN3 (+BNd) partials of that block
@@ -439,7 +537,8 @@ class ResNet50Executor:
             if prev is not None:
                 pds = prev.bnd is not None
                 K.conv_dgrad(K.CE_BWD_RES, g1, y1, bn1.a, bn1.b, bn1.c, f.bt(c1.name), prev.bn3.g, prev.bn3.acc_b, B,
-                             H, H, c1.cin, c1.cout, 1, 1, 1, 0, Yt=prev.bn3.y, Rg=sc, X=prev.out,
+                             H, H, c1.cin, c1.cout, 1, 1, 1, 0, Yt=prev.bn3.y, Rg=sc,
+                             X=prev.out if prev.out_mask is None else None, Xm=prev.out_mask,
                              Yt2=prev.bnd.y if pds else None, part2=prev.bnd.acc_b if pds else None)
                 prev.bn3.finalize_bwd(prev.bn3.acc_b, P1)
                 if pds:
@@ -447,9 +546,11 @@ class ResNet50Executor:
             else:
                 K.conv_dgrad(K.CE_BWD_RES, g1, y1, bn1.a, bn1.b, bn1.c, f.bt(c1.name), self.Gpool, None, B,
                              H, H, c1.cin, c1.cout, 1, 1, 1, 0, Rg=sc)
-            self._wgrad(lambda bp=bp, g1=g1, y1=y1: K.conv_wgrad(
-                g1, y1, bp.bn1.a, bp.bn1.b, bp.bn1.c, ws=wg, grad=f.g(bp.c1.name), B=B, H=bp.H, W=bp.H,
-                Ci=bp.c1.cin, N=bp.c1.cout, R=1, S=1, stride=1, pad=0, **self._wx(bp.c1, bp.x_in, None)))
+            fins1 = [] if prev is None else [(prev.bn3, P1)] + ([(prev.bnd, P1)] if prev.bnd is not None else [])
+            self._wgrad(lambda ws, bp=bp, g1=g1, y1=y1: K.conv_wgrad(
+                g1, y1, bp.bn1.a, bp.bn1.b, bp.bn1.c, ws=ws, grad=f.g(bp.c1.name), B=B, H=bp.H, W=bp.H,
+                Ci=bp.c1.cin, N=bp.c1.cout, R=1, S=1, stride=1, pad=0, **self._wx(bp.c1, bp.x_in, None)),
+                fins=fins1)
             names = [c1.name]
             if prev is not None:
                 names += prev.bn3.param_names + (prev.bnd.param_names if prev.bnd is not None else [])
@@ -458,14 +559,25 @@ class ResNet50Executor:
         bn0 = self.bn0
         K.maxpool_bwd(self.Gpool, self.pool_idx, bn0.y, bn0.scale, bn0.shift, bn0.g, bn0.acc_b, B, self.H0, self.H0,
                       64)
-        bn0.finalize_bwd(bn0.acc_b, K.maxpool_bwd_num_partials(B, self.H0, self.H0))
+        P0 = K.maxpool_bwd_num_partials(B, self.H0, self.H0)
+        bn0.finalize_bwd(bn0.acc_b, P0)
         st = self.stem
+        # the stem weight gradient reads bn0's materialised coefficients (lazy: its side finalize
+        # runs first in the same group).  In the s2d form it runs on the MAIN stream (own
+        # split-M workspace), concurrently with the side stream's remaining layer-1 weight
+        # gradients: the main stream is otherwise idle from here to the optimizer, which waits
+        # for the side stream (~0.5 ms measured)
         if self.stem_s2d:
-            self._wgrad(lambda: K.conv_wgrad_s2d(bn0.g, bn0.y, bn0.a, bn0.b, bn0.c, self.img2, self.ws_stem,
-                                                 f.g(st.name), B, self.S // 2))
+            stem_wg = lambda ws=None: K.conv_wgrad_s2d(bn0.g, bn0.y, bn0.a, bn0.b, bn0.c, self.img2,  # noqa: E731
+                                                       self.ws_stem, f.g(st.name), B, self.S // 2)
+            if bn0.lz_b is None and os.environ.get("PGDIST_RN_STEM_MAIN", "1") == "1":
+                self._flush_side()
+                stem_wg()
+            else:
+                self._wgrad(stem_wg, fins=[(bn0, P0)])
         else:
-            self._wgrad(lambda: K.conv_wgrad(bn0.g, bn0.y, bn0.a, bn0.b, bn0.c, self.img, wg, f.g(st.name), B,
-                                             st.H, st.H, 4, st.cout, 7, 7, 2, 3))
+            self._wgrad(lambda ws: K.conv_wgrad(bn0.g, bn0.y, bn0.a, bn0.b, bn0.c, self.img, ws, f.g(st.name), B,
+                                                st.H, st.H, 4, st.cout, 7, 7, 2, 3), fins=[(bn0, P0)])
         self._ready([st.name] + bn0.param_names)
         self._flush_side()
         if self.side is not None:

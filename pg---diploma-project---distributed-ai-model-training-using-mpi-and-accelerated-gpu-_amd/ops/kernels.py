@@ -595,14 +595,15 @@ def conv_fwd(pro, x, w, y, part, B, H, W, Ci, N, R, S, stride, pad, pa=None, pb=
 
 
 def conv_dgrad(epi, G, Y, ga, gb, gc, wt, dx, part, B, H, W, Cin, Cout, R, S, stride, pad, Yt=None, es=None,
-               et=None, Rg=None, X=None, Yt2=None, part2=None):
+               et=None, Rg=None, X=None, Yt2=None, part2=None, Xm=None):
     """Data gradient of y = conv(x, w) with this layer's BN backward fused on the way in:
     dy = ga*G + gb*Y + gc  ([B,Ho,Wo,Cout]),  dx = conv^T(dy, wt)  ([B,H,W,Cin]), or with
     Y = None: G is dy itself, materialised by :func:`bn_mat` (LDS-DMA kernel, no prologue), where
     wt = w transposed to [Cin,R,S,Cout] (:func:`conv_wt`).  Epilogues:
       CE_BWD_RELU  dx *= 1[Yt*es + et > 0];  part <- (sum dx, sum dx*Yt)
       CE_BWD_RES   dx = (dx + Rg) * 1[X > 0]  (null operands skipped);
-                   part <- (sum dx, sum dx*Yt), part2 <- (sum dx, sum dx*Yt2) when given."""
+                   part <- (sum dx, sum dx*Yt), part2 <- (sum dx, sum dx*Yt2) when given.
+    ``Xm`` instead of X: the ReLU mask as bits, uint8 [B*H*W, Cin/8] (res_out's ``mask``)."""
     _conv_check(Cout, Cin, "conv_dgrad")
     if Y is None and (Cout % 64 or conv_get_glds() == 0):
         raise ValueError("conv_dgrad: a materialised dy (Y=None) needs Cout % 64 == 0 and the LDS-DMA kernel "
@@ -629,8 +630,14 @@ def conv_dgrad(epi, G, Y, ga, gb, gc, wt, dx, part, B, H, W, Cin, Cout, R, S, st
         if Yt is None or es is None or et is None:
             raise ValueError("conv_dgrad(CE_BWD_RELU) needs Yt, es, et")
         _chk(part, F32, P * 2 * Cin, "part")
+    if Xm is not None:
+        if X is not None:
+            raise ValueError("conv_dgrad: X or Xm, not both")
+        _chk(Xm, torch.uint8, B * H * W * Cin // 8, "Xm")
+    if epi == CE_BWD_RELU:
+        pass
     elif epi == CE_BWD_RES:
-        ops = (Rg is not None, X is not None, Yt is not None, Yt2 is not None)
+        ops = (Rg is not None, X is not None or Xm is not None, Yt is not None, Yt2 is not None)
         if ops not in ((False, False, False, False), (True, False, False, False), (True, True, True, False),
                        (True, True, True, True)):
             raise ValueError("conv_dgrad(CE_BWD_RES): operand sets {} | {Rg} | {Rg,X,Yt} | {Rg,X,Yt,Yt2}")
@@ -643,7 +650,8 @@ def conv_dgrad(epi, G, Y, ga, gb, gc, wt, dx, part, B, H, W, Cin, Cout, R, S, st
     else:
         raise ValueError(f"conv_dgrad: bad epilogue {epi}")
     lib().conv_dgrad(int(epi), _p(G), _p(Y), _p(ga), _p(gb), _p(gc), _p(wt), _p(dx), _p(Yt), _p(es), _p(et),
-                     _p(Rg), _p(X), _p(Yt2), _p(part), _p(part2), B, H, W, Cin, Cout, R, S, stride, pad, _s())
+                     _p(Rg), _p(X), _p(Yt2), _p(part), _p(part2), B, H, W, Cin, Cout, R, S, stride, pad, _p(Xm),
+                     _s())
 
 
 def conv_wgrad_workspace(B, H, W, Ci, N, R, S, stride, pad):
@@ -678,11 +686,13 @@ def conv_wgrad(G, Y, ga, gb, gc, x, ws, grad, B, H, W, Ci, N, R, S, stride, pad,
 BN_MAT_ACT, BN_MAT_BWD = 0, 1
 
 
-def bn_mat(mode, Y, a, b, out, G=None, c=None):
+def bn_mat(mode, Y, a, b, out, G=None, c=None, lz=None):
     """Materialise a BN-transformed [M, C] bf16 operand for the LDS-DMA convs:
     BN_MAT_ACT  out = relu(Y*a + b)        (producer BN + ReLU: the next conv's input)
     BN_MAT_BWD  out = a*G + b*Y + c        (this layer's BN backward: dgrad / wgrad dy)
-    C/8 must divide 256 (C in 8, 16, ..., 2048 powers of two)."""
+    C/8 must divide 256 (C in 8, 16, ..., 2048 powers of two).  ``lz``: lazy finalize
+    descriptor (bn_fin_desc of this BN, forward for ACT / backward for BWD): the kernel computes
+    a, b (, c) from the producer's replica rows itself; a, b, c are then not read."""
     M, C = Y.shape
     if C % 8 or 256 % (C // 8):
         raise ValueError(f"bn_mat: C={C} (C/8 must divide 256)")
@@ -697,6 +707,7 @@ def bn_mat(mode, Y, a, b, out, G=None, c=None):
         _chk(c, F32, C, "c")
     elif mode != BN_MAT_ACT:
         raise ValueError(f"bn_mat: bad mode {mode}")
+    _arm_lz(lz)
     lib().bn_mat(int(mode), _p(G), _p(Y), _p(a), _p(b), _p(c), _p(out), M, C, _s())
 
 
@@ -709,24 +720,36 @@ def conv_wt(src, dst, tab, n):
     lib().conv_wt(_p(src), _p(dst), _p(tab), int(n), _s())
 
 
-def res_out(y, s, t, r, out, rs=None, rt=None):
-    """Bottleneck output out = relu(y*s + t + r'), r' = r*rs + rt (projection shortcut BN) or r."""
+def res_out(y, s, t, r, out, rs=None, rt=None, lz=None, lz2=None, mask=None):
+    """Bottleneck output out = relu(y*s + t + r'), r' = r*rs + rt (projection shortcut BN) or r.
+    ``lz`` (, ``lz2`` with the projection): lazy finalize descriptors of the two BNs (s, t / rs,
+    rt computed from the producers' replica rows in the kernel).  ``mask``: uint8 [M, C/8]
+    also written, bit j of byte i = (out element 8i+j > 0) (conv_dgrad's ``Xm``)."""
     M, C = y.shape
     if C % 8:
         raise ValueError("res_out: C % 8")
     for x_, nm in ((y, "y"), (r, "r"), (out, "out")):
         _chk(x_, BF16, M * C, nm)
-    lib().res_out(_p(y), _p(s), _p(t), _p(r), _p(rs), _p(rt), _p(out), M, C, _s())
+    ok = (lz is None and lz2 is None) or (lz is not None and (rs is None) == (lz2 is None))
+    if not ok:
+        raise ValueError("res_out: lz (and lz2 with the projection BN) both or neither")
+    for d in (lz, lz2):
+        if d is not None and not (d.is_cuda and d.dtype == torch.uint8):
+            raise TypeError("res_out: lz descriptors from bn_fin_desc")
+    _chk(mask, torch.uint8, M * C // 8, "mask")
+    lib().res_out(_p(y), _p(s), _p(t), _p(r), _p(rs), _p(rt), _p(out), M, C, _p(lz), _p(lz2), _p(mask), _s())
 
 
-def maxpool_fwd(y, s, t, out, idx, B, H, W, C):
-    """3x3 s2 p1 max-pool of relu(y*s+t) -> out [B,Ho,Wo,C] bf16 + arg-max tap (uint8)."""
+def maxpool_fwd(y, s, t, out, idx, B, H, W, C, lz=None):
+    """3x3 s2 p1 max-pool of relu(y*s+t) -> out [B,Ho,Wo,C] bf16 + arg-max tap (uint8);
+    ``lz``: s, t from the producer's replica rows (lazy finalize descriptor)."""
     Ho, Wo = conv_out_hw(H, W, 3, 3, 2, 1)
     if C % 8:
         raise ValueError("maxpool: C % 8")
     _chk(y, BF16, B * H * W * C, "y")
     _chk(out, BF16, B * Ho * Wo * C, "out")
     _chk(idx, torch.uint8, B * Ho * Wo * C, "idx")
+    _arm_lz(lz)
     lib().maxpool_fwd(_p(y), _p(s), _p(t), _p(out), _p(idx), B, H, W, C, _s())
 
 

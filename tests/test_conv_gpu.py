@@ -333,6 +333,48 @@ def test_image_prep_s2d(dev):
     assert torch.equal(out2, conv)
 
 
+@pytest.mark.parametrize("mat", [False, True])
+def test_conv_dgrad_bitmask(dev, mat):
+    """res_out's ReLU bit mask (uint8 [M, C/8]) as the dgrad's Xm gives bitwise the dx and BN
+    partials of the bf16 X operand (CE_BWD_RXYM / RXYYM vs RXY / RXYY)."""
+    B, H, Cin, Cout = 4, 14, 256, 64
+    g = torch.Generator(device=dev).manual_seed(81)
+    y = torch.randn(B * H * H, Cin, device=dev, generator=g).to(torch.bfloat16)
+    r = torch.randn(B * H * H, Cin, device=dev, generator=g).to(torch.bfloat16)
+    s3 = torch.rand(Cin, device=dev, generator=g) + 0.5
+    t3 = torch.randn(Cin, device=dev, generator=g) * 0.3
+    X = torch.empty_like(y)
+    mask = torch.empty(B * H * H, Cin // 8, dtype=torch.uint8, device=dev)
+    K.res_out(y, s3, t3, r, X, mask=mask)
+    bits = torch.stack([(mask >> j) & 1 for j in range(8)], 2).reshape(-1, Cin).bool()
+    assert torch.equal(bits, X.float() > 0)
+    G = torch.randn(B * H * H, Cout, device=dev, generator=g).to(torch.bfloat16)
+    Yv = torch.randn(B * H * H, Cout, device=dev, generator=g).to(torch.bfloat16)
+    ga, gb = (torch.randn(Cout, device=dev, generator=g) * 0.1 for _ in range(2))
+    gc = torch.randn(Cout, device=dev, generator=g) * 0.01
+    wt = (torch.randn(Cin * Cout, device=dev, generator=g) * 0.05).to(torch.bfloat16)
+    Rg = torch.randn(B * H * H, Cin, device=dev, generator=g).to(torch.bfloat16)
+    Yt = torch.randn(B * H * H, Cin, device=dev, generator=g).to(torch.bfloat16)
+    Yt2 = torch.randn(B * H * H, Cin, device=dev, generator=g).to(torch.bfloat16)
+    if mat:
+        Gk, Yk = _mat_dy(G.float().view(B, H, H, Cout), Yv.float().view(B, H, H, Cout), ga, gb, gc), None
+    else:
+        Gk, Yk = G, Yv
+    P = K.conv_dgrad_num_partials(B, H, H, Cin, Cout, 1, 1, 1)
+    res = []
+    for use_mask in (False, True):
+        dx = torch.empty(B * H * H, Cin, dtype=torch.bfloat16, device=dev)
+        part = torch.zeros(P, 2, Cin, device=dev)
+        part2 = torch.zeros(P, 2, Cin, device=dev)
+        K.conv_dgrad(K.CE_BWD_RES, Gk, Yk, ga, gb, gc, wt, dx, part, B, H, H, Cin, Cout, 1, 1, 1, 0, Yt=Yt, Rg=Rg,
+                     X=None if use_mask else X, Xm=mask if use_mask else None, Yt2=Yt2, part2=part2)
+        torch.cuda.synchronize()
+        res.append((dx, part.sum(0), part2.sum(0)))
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.allclose(res[0][1], res[1][1], rtol=1e-5, atol=1e-4)
+    assert torch.allclose(res[0][2], res[1][2], rtol=1e-5, atol=1e-4)
+
+
 def test_res_out(dev):
     M, C = 1000, 256
     y, r = bfr(rnd(M, C, dev=dev, seed=41)), bfr(rnd(M, C, dev=dev, seed=42))

@@ -193,3 +193,44 @@ def test_resnet_native_step_loss_decreases(dev):
             losses.append(l / n)
     assert losses[-1] < losses[0] * 0.5, losses
     assert torch.isfinite(st.flat.master).all()
+
+
+@pytest.mark.parametrize("stem", ["s2d", "direct"])
+def test_resnet_lazy_bn_matches_launch(dev, monkeypatch, stem):
+    """Lazy BN finalize (consumers compute the parameters from the replica rows; side outputs
+    batched at the end of the forward / on the side stream) vs a finalize launch after every
+    producer: after 4 replayed training steps the weights, Adam moments, BN running statistics
+    and metrics agree within the float-atomic noise floor of the replica rows (both modes add the
+    statistics atomically; estimated by running the launch mode twice)."""
+    from pgdist.engine.native_step import NativeTrainStep
+    monkeypatch.setenv("PGDIST_RN_STEM", stem)
+    src = torch.randint(0, 256, (16, 64, 64, 3), dtype=torch.uint8, device=dev,
+                        generator=torch.Generator(device=dev).manual_seed(5))
+    labels = torch.arange(16, device=dev) % 10
+    out = []
+    for lazy in ("0", "0", "1"):
+        monkeypatch.setenv("PGDIST_BN_LAZY", lazy)
+        torch.manual_seed(0)
+        st = NativeTrainStep(build_model("resnet50", num_classes=10), 8, dev, img_size=64, lr=1e-3,
+                             use_graph=False)
+        assert st.exe.lazy_bn == (lazy == "1")
+        st.set_data(src, labels)
+        losses = []
+        for i in range(4):
+            st.run((torch.arange(8, device=dev) + 3 * i) % 16)
+            lsum, _, n = st.read_metrics()
+            losses.append(lsum / n)
+        torch.cuda.synchronize()
+        rs = torch.cat([m.running_var.flatten() for m in st.exe.model.modules()
+                        if isinstance(m, torch.nn.BatchNorm2d)])
+        nbt = [int(m.num_batches_tracked) for m in st.exe.model.modules() if isinstance(m, torch.nn.BatchNorm2d)]
+        out.append((st.flat.master.clone(), st.flat.exp_avg.clone(), rs, nbt, losses))
+    (w0, m0, r0, n0, k0), (w1, m1, r1, _, k1), (w2, m2, r2, n2, k2) = out
+    assert n2 == n0 and set(n2) == {4}
+    # the first step's forward sees identical weights: its loss agrees to the atomic noise
+    # (a consumer reading stale BN parameters would be off by far more)
+    assert abs(k2[0] - k0[0]) <= 1e-3 * abs(k0[0]) + 10 * abs(k1[0] - k0[0]), (k0, k1, k2)
+    noise = max(_rel(w1, w0), 1e-6)
+    assert _rel(w2, w0) < max(20 * noise, 1e-4), (_rel(w2, w0), noise)
+    assert _rel(m2, m0) < max(20 * max(_rel(m1, m0), 1e-6), 1e-3)
+    assert _rel(r2, r0) < max(20 * max(_rel(r1, r0), 1e-6), 1e-4)
