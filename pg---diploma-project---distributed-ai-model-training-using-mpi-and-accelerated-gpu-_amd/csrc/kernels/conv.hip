@@ -71,6 +71,11 @@ struct ConvArgs {
   signed char tr[4][9], ts[4][9], tdh[4][9], tdw[4][9];
 };
 
+int env_int(const char *name, int dflt) {
+  const char *e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
 // 16x16x32 bf16 MFMA on raw 8 x bf16 fragments
 PG_DEVICE f32x4_t mfma16(const s16x8_t &a, const s16x8_t &b, const f32x4_t &c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
@@ -166,13 +171,27 @@ PG_DEVICE void conv_epilogue(const ConvArgs &p, f32x4_t (&acc)[BM / 32][BN / 32]
     }
   };
   issue(0);
+  // C tile to LDS as 4-byte column pairs: lane l holds rows 4q..4q+3 of column l & 15; the
+  // neighbour column's values come from lane l ^ 1 (DPP quad_perm [1,0,3,2]), so an even lane
+  // writes rows 4q, 4q+1 and an odd lane rows 4q+2, 4q+3 of the column pair (2 ds_write_b32
+  // instead of 4 ds_write_b16 per 16x16 fragment)
+  const bool odd = lane & 1;
 #pragma unroll
   for (int c = 0; c < CTW; ++c) {
-    const int col = wn * (BN / 2) + c * 16 + (lane & 15);
+    const int col = wn * (BN / 2) + c * 16 + (lane & 14);
 #pragma unroll
-    for (int r = 0; r < RT; ++r)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) Cs[(wm * (BM / 2) + r * 16 + 4 * (lane >> 4) + j) * LDC + col] = f2bf(acc[r][c][j]);
+    for (int r = 0; r < RT; ++r) {
+      const uint32_t lo = pack2(acc[r][c][0], acc[r][c][1]), hi = pack2(acc[r][c][2], acc[r][c][3]);
+      const uint32_t send = odd ? lo : hi;
+      const uint32_t recv = (uint32_t)__builtin_amdgcn_mov_dpp((int)send, 0xB1, 0xF, 0xF, false);
+      const uint32_t mine = odd ? hi : lo;
+      // even: rows 4q (mine.lo, recv.lo), 4q+1 (mine.hi, recv.hi); odd: rows 4q+2 (recv.lo, mine.lo), 4q+3 (recv.hi, mine.hi)
+      const uint32_t a0 = odd ? ((recv & 0xffffu) | (mine << 16)) : ((mine & 0xffffu) | (recv << 16));
+      const uint32_t a1 = odd ? ((recv >> 16) | (mine & 0xffff0000u)) : ((mine >> 16) | (recv & 0xffff0000u));
+      const int row = wm * (BM / 2) + r * 16 + 4 * (lane >> 4) + (odd ? 2 : 0);
+      *reinterpret_cast<uint32_t *>(Cs + row * LDC + col) = a0;
+      *reinterpret_cast<uint32_t *>(Cs + (row + 1) * LDC + col) = a1;
+    }
   }
   __syncthreads();
 #pragma unroll
@@ -1011,9 +1030,13 @@ PG_DEVICE int fdiv(int n, int d, float inv) {
 }
 }  // namespace
 
-template <int TN, int TK, int NBUF>
+// MK: m rows per stage (64, or 32 for a deeper ring in the same LDS: with 4 stages of 32 rows
+// three stages are in flight instead of one, for the latency-bound splits with few MFMAs per
+// stage); NBUF: ring depth (2..4, one barrier per stage from 3 on)
+template <int TN, int TK, int NBUF, int MK = 64>
 __global__ __launch_bounds__(256) void conv_wgrad_dma_kernel(WgArgs p, int gx, int gy, int total) {
-  constexpr int MK = 64;
+  static_assert(MK == 32 || MK == 64, "32- or 64-row stages");
+  static_assert(NBUF >= 2 && NBUF <= 4, "2 to 4 stages");
   constexpr int RBN = TN * 2, RBK = TK * 2;              // staged row bytes
   constexpr int CPN = RBN / 16, CPK = RBK / 16;          // 16-B chunks per row
   constexpr int PN = MK * RBN / 1024, PK = MK * RBK / 1024;   // 1-KiB pieces per stage
@@ -1131,13 +1154,17 @@ __global__ __launch_bounds__(256) void conv_wgrad_dma_kernel(WgArgs p, int gx, i
       glds_wait_barrier<PW>();
     }
   } else {
-    if (nsteps > 0) issue(0, 0);
-    if (nsteps > 1) issue(1, 1);
-    int buf = 0, nbuf = 2;
+    // ring: NBUF - 1 stages in flight, one barrier per stage (stage s landed everywhere AND every
+    // wave is done with stage s - 1, whose buffer the next issue refills)
+#pragma unroll
+    for (int q = 0; q < NBUF - 1; ++q)
+      if (q < nsteps) issue(q, q);
+    int buf = 0, nbuf = NBUF - 1;
     for (int s = 0; s < nsteps; ++s) {
-      if (s + 1 < nsteps) glds_wait_barrier<PW>();
+      if (s + NBUF - 2 < nsteps) glds_wait_barrier<(NBUF - 2) * PW>();
+      else if (NBUF == 4 && s + 1 < nsteps) glds_wait_barrier<PW>();
       else glds_wait_barrier<0>();
-      if (s + 2 < nsteps) issue(s + 2, nbuf);
+      if (s + NBUF - 1 < nsteps) issue(s + NBUF - 1, nbuf);
       mma(buf);
       buf = buf == NBUF - 1 ? 0 : buf + 1;
       nbuf = nbuf == NBUF - 1 ? 0 : nbuf + 1;
@@ -1551,7 +1578,15 @@ int glds_nbuf() { return g_conv_glds; }
 
 template <int MODE, int EPI, int BM, int BN, int NBUF, int KS, bool MT = false>
 void launch_glds_t(const ConvArgs &a, const Geom &g, hipStream_t st) {
-  size_t lds = (size_t)NBUF * (BM + BN) * KS * 2;
+  // one k-step (K <= KS: the 1x1 convs on 64 channels, memory-bound): the kernel only ever fills
+  // buffer 0, so one stage of LDS (the C tile sets the size) lets twice the workgroups per CU
+  // share the memory latency
+  int kmax = a.K;
+  if (MODE == CM_DGRAD)
+    for (int c = 0; c < g.ncls; ++c) kmax = a.ntap[c] * a.Ci > kmax ? a.ntap[c] * a.Ci : kmax;
+  static const bool one_stage = env_int("PGDIST_CONV_1STAGE", 1) != 0;
+  const int stages = (one_stage && kmax <= KS) ? 1 : NBUF;
+  size_t lds = (size_t)stages * (BM + BN) * KS * 2;
   const size_t ctile = (size_t)BM * (BN + 8) * 2, red = (size_t)(256 / (BN / 8)) * BN * 4;
   if (ctile > lds) lds = ctile;
   if (red > lds) lds = red;
@@ -1710,9 +1745,30 @@ bool wg_dma_ok(bool dm, int xpro, int Ci, int N) {
   static const bool on = [] { const char *e = getenv("PGDIST_WG_DMA"); return !e || atoi(e) != 0; }();
   return on && dm && xpro == CP_NONE && Ci % 64 == 0 && N % 64 == 0;
 }
-int wg_dma_nbuf() {
-  static const int v = [] { const char *e = getenv("PGDIST_WG_DMA_NBUF"); return e && atoi(e) == 3 ? 3 : 2; }();
-  return v;
+// Per-shape configuration of the LDS-DMA weight gradient: split-M grid-size target, m rows per
+// stage and ring depth.  Measured per ResNet-50 layer at bs128 on MI355X (scripts/conv_bench.py
+// wgradma, profiles/r3b_wgrad_dma_cfg.txt): the 3x3 layers are latency-bound (few MFMAs per
+// stage): the 64x64-tile ones (32 KB of LDS per workgroup, up to 5 per CU) and the 14x14 maps
+// want a 1024-workgroup grid (l1.c2 150 -> 98 us, l3.c2 84 -> 76), the 7x7 maps (3-4 splits) a
+// 3-deep ring of 32-row stages (l4.c2 103 -> 82); the 1x1 layers and the 28x28 3x3 ones keep
+// 512 workgroups and 2 x 64-row stages (network total 4024 -> ~3750 us).
+// PGDIST_WGD_TARGET / PGDIST_WG_DMA_MK / PGDIST_WG_DMA_NBUF override every shape.
+struct WgDmaCfg {
+  int target, mk, nbuf;
+};
+WgDmaCfg wg_dma_cfg(int N, int Ci, int M, int taps) {
+  static const int e_t = env_int("PGDIST_WGD_TARGET", 0), e_mk = env_int("PGDIST_WG_DMA_MK", 0),
+                   e_nb = env_int("PGDIST_WG_DMA_NBUF", 0);
+  const int TN = N % 128 == 0 ? 128 : 64, TK = Ci % 128 == 0 ? 128 : 64;
+  WgDmaCfg c{512, 64, 2};
+  if (taps > 1) {
+    if (M <= 8192) { c.mk = 32; c.nbuf = 3; }
+    else if (M <= 32768 || (TN == 64 && TK == 64)) c.target = 1024;
+  }
+  if (e_t > 0) c.target = e_t;
+  if (e_mk == 32 || e_mk == 64) c.mk = e_mk;
+  if (e_nb >= 2 && e_nb <= 4) c.nbuf = e_nb;
+  return c;
 }
 
 WgGeom wg_geom(int N, int Kw, int M, bool dma = false, int Ci = 0) {
@@ -1725,9 +1781,8 @@ WgGeom wg_geom(int N, int Kw, int M, bool dma = false, int Ci = 0) {
     g.TK = Kw >= 128 ? 128 : 64;
   }
   const long long tiles = (long long)((N + g.TN - 1) / g.TN) * ((Kw + g.TK - 1) / g.TK);
-  static const int target = [] { const char *e = getenv("PGDIST_WG_TARGET"); return e ? atoi(e) : 1024; }();
-  static const int target_dma = [] { const char *e = getenv("PGDIST_WGD_TARGET"); return e ? atoi(e) : 512; }();
-  long long ns = ((dma ? target_dma : target) + tiles - 1) / tiles;
+  static const int target = env_int("PGDIST_WG_TARGET", 1024);
+  long long ns = ((dma ? wg_dma_cfg(N, Ci, M, Kw / Ci).target : target) + tiles - 1) / tiles;
   const long long max_ns = (M + 4 * kWgMK - 1) / (4 * kWgMK);   // >= 4 steps per split
   if (ns > max_ns) ns = max_ns;
   if (ns < 1) ns = 1;
@@ -1772,21 +1827,25 @@ void launch_conv_wgrad(const bf16_t *G, const bf16_t *Y, const float *ga, const 
     a.rows_per_split = g.rows;
     a.out = g.nsplit == 1 ? grad : ws;
     const int gx = N / g.TN, gy = a.Kw / g.TK, total = gx * gy * g.nsplit;
-    const size_t lds = (size_t)wg_dma_nbuf() * 64 * (g.TN + g.TK) * 2;
+    const WgDmaCfg cfg = wg_dma_cfg(N, Ci, a.M, R * S);
+    const int nb = cfg.nbuf, mk = cfg.mk;
+    const size_t lds = (size_t)nb * mk * (g.TN + g.TK) * 2;
+#define WGD_K(TN_, TK_, NB_, MK_) \
+  hipLaunchKernelGGL((conv_wgrad_dma_kernel<TN_, TK_, NB_, MK_>), dim3(total), dim3(256), lds, stream, a, gx, gy, total)
 #define WGD_L(TN_, TK_)                                                                                         \
   do {                                                                                                         \
-    if (wg_dma_nbuf() == 3)                                                                                    \
-      hipLaunchKernelGGL((conv_wgrad_dma_kernel<TN_, TK_, 3>), dim3(total), dim3(256), lds, stream, a, gx, gy, \
-                         total);                                                                               \
-    else                                                                                                       \
-      hipLaunchKernelGGL((conv_wgrad_dma_kernel<TN_, TK_, 2>), dim3(total), dim3(256), lds, stream, a, gx, gy, \
-                         total);                                                                               \
+    if (mk == 32) {                                                                                            \
+      if (nb == 4) WGD_K(TN_, TK_, 4, 32); else if (nb == 3) WGD_K(TN_, TK_, 3, 32); else WGD_K(TN_, TK_, 2, 32); \
+    } else {                                                                                                   \
+      if (nb == 4) WGD_K(TN_, TK_, 4, 64); else if (nb == 3) WGD_K(TN_, TK_, 3, 64); else WGD_K(TN_, TK_, 2, 64); \
+    }                                                                                                          \
   } while (0)
     if (g.TN == 128 && g.TK == 128) WGD_L(128, 128);
     else if (g.TN == 128) WGD_L(128, 64);
     else if (g.TK == 128) WGD_L(64, 128);
     else WGD_L(64, 64);
 #undef WGD_L
+#undef WGD_K
     if (g.nsplit > 1) launch_wgrad_reduce(ws, g.nsplit, (long long)N * a.Kw, grad, stream);
     return;
   }
