@@ -171,28 +171,13 @@ PG_DEVICE void conv_epilogue(const ConvArgs &p, f32x4_t (&acc)[BM / 32][BN / 32]
     }
   };
   issue(0);
-  // C tile to LDS as 4-byte column pairs: lane l holds rows 4q..4q+3 of column l & 15; the
-  // neighbour column's values come from lane l ^ 1 (DPP quad_perm [1,0,3,2]), so an even lane
-  // writes rows 4q, 4q+1 and an odd lane rows 4q+2, 4q+3 of the column pair (2 ds_write_b32
-  // instead of 4 ds_write_b16 per 16x16 fragment)
-  const bool odd = lane & 1;
+  // C tile to LDS as 4-byte column pairs (common.h frag_store_bf16)
 #pragma unroll
-  for (int c = 0; c < CTW; ++c) {
-    const int col = wn * (BN / 2) + c * 16 + (lane & 14);
+  for (int c = 0; c < CTW; ++c)
 #pragma unroll
-    for (int r = 0; r < RT; ++r) {
-      const uint32_t lo = pack2(acc[r][c][0], acc[r][c][1]), hi = pack2(acc[r][c][2], acc[r][c][3]);
-      const uint32_t send = odd ? lo : hi;
-      const uint32_t recv = (uint32_t)__builtin_amdgcn_mov_dpp((int)send, 0xB1, 0xF, 0xF, false);
-      const uint32_t mine = odd ? hi : lo;
-      // even: rows 4q (mine.lo, recv.lo), 4q+1 (mine.hi, recv.hi); odd: rows 4q+2 (recv.lo, mine.lo), 4q+3 (recv.hi, mine.hi)
-      const uint32_t a0 = odd ? ((recv & 0xffffu) | (mine << 16)) : ((mine & 0xffffu) | (recv << 16));
-      const uint32_t a1 = odd ? ((recv >> 16) | (mine & 0xffff0000u)) : ((mine >> 16) | (recv & 0xffff0000u));
-      const int row = wm * (BM / 2) + r * 16 + 4 * (lane >> 4) + (odd ? 2 : 0);
-      *reinterpret_cast<uint32_t *>(Cs + row * LDC + col) = a0;
-      *reinterpret_cast<uint32_t *>(Cs + (row + 1) * LDC + col) = a1;
-    }
-  }
+    for (int r = 0; r < RT; ++r)
+      frag_store_bf16(Cs, LDC, wm * (BM / 2) + r * 16, wn * (BN / 2) + c * 16, acc[r][c][0], acc[r][c][1],
+                      acc[r][c][2], acc[r][c][3]);
   __syncthreads();
 #pragma unroll
   for (int i0 = 0; i0 < NP; i0 += EB) {

@@ -133,6 +133,9 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
   constexpr int BM = 32 * RG;               // rows per M tile
   constexpr int CH = BN / 8;                // 16-B chunks per C row
   constexpr int RSTEP = 256 / CH;           // rows covered per epilogue pass
+  // BN = 96 / 144 (one N tile over the whole expand width): 256 % CH != 0, the last
+  // 256 - RSTEP * CH threads sit out the epilogue passes and the partial-sum reduction
+  constexpr bool EP_ALL = RSTEP * CH == 256;
   constexpr int NP = (BM + RSTEP - 1) / RSTEP;
   constexpr int NPAR = PRO == ACT_NONE ? 0 : (PRO == PRO_BNBWD ? 3 : 2);
   constexpr bool HAS_A2 = PRO == PRO_BNBWD || PRO == PRO_BNRES;
@@ -200,6 +203,7 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
 
   const int my_chunk = tid % CH;            // fixed epilogue column chunk
   const int ncol0 = n0 + my_chunk * 8;
+  const bool ep_on = EP_ALL || tid < RSTEP * CH;
   float st0[8], st1[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) st0[j] = st1[j] = 0.f;
@@ -314,13 +318,17 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
 #pragma unroll
     for (int f = 0; f < 2; ++f)
 #pragma unroll
-      for (int c = 0; c < CT; ++c)
+      for (int c = 0; c < CT; ++c) {
+        if constexpr (KS == 1) {   // bf16 column pairs (common.h frag_store_bf16)
+          const float sc = F8 ? csc[c] : 1.f;
+          frag_store_bf16(Cs, LDC, rg * 32 + f * 16, c * 16, acc[f][c][0] * sc, acc[f][c][1] * sc,
+                          acc[f][c][2] * sc, acc[f][c][3] * sc);
+        } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int r = rg * 32 + f * 16 + 4 * (lane >> 4) + j, col = c * 16 + (lane & 15);
-          if constexpr (KS == 1) Cs[r * LDC + col] = f2bf(F8 ? acc[f][c][j] * csc[c] : acc[f][c][j]);
-          else Cf[(kp * BM + r) * LDF + col] = acc[f][c][j];
+          for (int j = 0; j < 4; ++j)
+            Cf[(kp * BM + rg * 32 + f * 16 + 4 * (lane >> 4) + j) * LDF + c * 16 + (lane & 15)] = acc[f][c][j];
         }
+      }
     __syncthreads();
 #pragma unroll
     for (int i0 = 0; i0 < NP; i0 += EB) {
@@ -340,7 +348,7 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
       for (int e = 0; e < EB; ++e) {
       const int i = i0 + e;
       const int rr = tid / CH + i * RSTEP, row = m0 + rr;
-      if (i < NP && rr < BM && row < p.M && ncol0 < p.N) {
+      if (ep_on && i < NP && rr < BM && row < p.M && ncol0 < p.N) {
         float v[8];
         if constexpr (KS == 1) {
           unpack8(*reinterpret_cast<const uint4 *>(Cs + rr * LDC + my_chunk * 8), v);
@@ -391,8 +399,10 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
   // ---- per-workgroup BN partials: reduce the RSTEP threads sharing a column chunk
   for (int s = 0; s < 2; ++s) {
     const int rgrp = tid / CH;
+    if (ep_on) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) Red[rgrp * BN + my_chunk * 8 + j] = s == 0 ? st0[j] : st1[j];
+      for (int j = 0; j < 8; ++j) Red[rgrp * BN + my_chunk * 8 + j] = s == 0 ? st0[j] : st1[j];
+    }
     __syncthreads();
     for (int c = tid; c < BN; c += 256) {
       float a = 0.f;
@@ -651,15 +661,23 @@ struct PwGeom {
   int BN, KS, bdirect, nt, nmt, gx;
   size_t lds;
 };
-static PwGeom pw_geom(int M, int N, int K, int pro) {
+// allow_wide: BN = N for N = 96 / 144 (bf16 forward only; the fp8 launcher passes false).  The
+// partial-row count P = gx of a wide launch is >= that of the narrow one, so sizing the BN
+// accumulators with pw_gemm_num_partials (which assumes wide) covers every launch.
+static PwGeom pw_geom(int M, int N, int K, int pro, bool allow_wide = true) {
   PwGeom g;
   const int Kp64 = (K + 63) / 64 * 64;
   g.bdirect = (Kp64 > 192) || (M < 65536);
   const int kstep = g.bdirect ? 32 : 64;
   const int Kp = (K + kstep - 1) / kstep * kstep;
   const int nsteps = Kp / kstep;
+  static const int wide = [] { const char *e = getenv("PGDIST_PW_WIDE_FWD"); return e ? atoi(e) : 1; }();
   if (!g.bdirect) {
     g.BN = N <= 32 ? 32 : 64;     // BN = 128 costs occupancy (1-2 waves/SIMD) for no bandwidth gain
+    // N = 96 / 144 (the expand convs at 112x112 / 56x56): one N tile over the whole row (full
+    // 192 / 288-B output rows instead of 64 + 32 or 64 + 64 + 16 column slices, no MFMA / LDS
+    // work on padding columns, A read once)
+    if (wide && allow_wide && pro != PRO_BNBWD && (N == 96 || N == 144)) g.BN = N;
     g.KS = 1;
   } else {
     g.BN = (N % 64 == 0) ? 64 : 32;
@@ -704,6 +722,10 @@ static void launch_pw_t(const PwArgs &a, const PwGeom &g, hipStream_t st) {
 template <int PRO, int EPI>
 static void launch_pw_geom(const PwArgs &a, const PwGeom &g, hipStream_t st) {
   if (!g.bdirect) {
+    if constexpr (EPI == EPI_FWD) {
+      if (g.BN == 96) { launch_pw_t<PRO, EPI, 96, 1, false>(a, g, st); return; }
+      if (g.BN == 144) { launch_pw_t<PRO, EPI, 144, 1, false>(a, g, st); return; }
+    }
     if (g.BN == 32) launch_pw_t<PRO, EPI, 32, 1, false>(a, g, st);
     else launch_pw_t<PRO, EPI, 64, 1, false>(a, g, st);
     return;
@@ -745,7 +767,7 @@ void launch_pw_tile_f8(int pro, const bf16_t *A, const float *pa, const float *p
 void launch_pw_gemm_f8(int pro, const bf16_t *A, const float *pa, const float *pb, const uint8_t *W8, int ldw8,
                        const float *wsc, float asc, bf16_t *out, float *part, int M, int N, int K,
                        hipStream_t st) {
-  PwGeom g = pw_geom(M, N, K, pro);
+  PwGeom g = pw_geom(M, N, K, pro, false);
   if (g.bdirect) {
     launch_pw_tile_f8(pro, A, pa, pb, W8, ldw8, wsc, asc, out, part, M, N, K, st);
     return;

@@ -261,9 +261,8 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
     const float csc = (F8 && n0 + col < p.N) ? p.wsc[n0 + col] / p.asc : 1.f;
 #pragma unroll
     for (int r = 0; r < RT; ++r)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        Cs[(wm * (BM / 2) + r * 16 + 4 * (lane >> 4) + j) * LDC + col] = f2bf(F8 ? acc[r][c][j] * csc : acc[r][c][j]);
+      frag_store_bf16(Cs, LDC, wm * (BM / 2) + r * 16, wn * (BN / 2) + c * 16, acc[r][c][0] * csc,
+                      acc[r][c][1] * csc, acc[r][c][2] * csc, acc[r][c][3] * csc);
   }
   __syncthreads();
   const int my_chunk = tid % CH, ncol0 = n0 + my_chunk * 8;
