@@ -677,7 +677,8 @@ static PwGeom pw_geom(int M, int N, int K, int pro, bool allow_wide = true) {
     // N = 96 / 144 (the expand convs at 112x112 / 56x56): one N tile over the whole row (full
     // 192 / 288-B output rows instead of 64 + 32 or 64 + 64 + 16 column slices, no MFMA / LDS
     // work on padding columns, A read once)
-    if (wide && allow_wide && pro != PRO_BNBWD && (N == 96 || N == 144)) g.BN = N;
+    // PGDIST_PW_WIDE_FWD=2 also N = 192 (the 28x28 expand convs, three exact 64-wide tiles otherwise)
+    if (wide && allow_wide && pro != PRO_BNBWD && (N == 96 || N == 144 || (wide >= 2 && N == 192))) g.BN = N;
     g.KS = 1;
   } else {
     g.BN = (N % 64 == 0) ? 64 : 32;
@@ -725,6 +726,7 @@ static void launch_pw_geom(const PwArgs &a, const PwGeom &g, hipStream_t st) {
     if constexpr (EPI == EPI_FWD) {
       if (g.BN == 96) { launch_pw_t<PRO, EPI, 96, 1, false>(a, g, st); return; }
       if (g.BN == 144) { launch_pw_t<PRO, EPI, 144, 1, false>(a, g, st); return; }
+      if (g.BN == 192) { launch_pw_t<PRO, EPI, 192, 1, false>(a, g, st); return; }
     }
     if (g.BN == 32) launch_pw_t<PRO, EPI, 32, 1, false>(a, g, st);
     else launch_pw_t<PRO, EPI, 64, 1, false>(a, g, st);
