@@ -837,6 +837,10 @@ bool wgrad_reduce_deferring();
 // split-M geometry: tiles of TN x TK outputs, S splits of >= kMinRowsPerSplit rows each
 static constexpr int kMinRowsPerSplit = 512;
 static void wgrad_geom(int M, int N, int K, int &TN, int &TK, int &S, int &rps) {
+  static const int min_rows = [] {   // PGDIST_PWWG_MINROWS: rows per split floor (tuning experiments)
+    const char *e = getenv("PGDIST_PWWG_MINROWS");
+    return e && atoi(e) >= kWMK ? atoi(e) / kWMK * kWMK : kMinRowsPerSplit;
+  }();
   TN = N <= 32 ? 32 : (N <= 64 ? 64 : 128);
   TK = K <= 32 ? 32 : (K <= 64 ? 64 : 128);
   const int tiles = ((N + TN - 1) / TN) * ((K + TK - 1) / TK);
@@ -845,7 +849,7 @@ static void wgrad_geom(int M, int N, int K, int &TN, int &TK, int &S, int &rps) 
     return e && atoi(e) > 0 ? atoi(e) : 1024;
   }();
   S = (target + tiles - 1) / tiles;
-  const int max_s = (M + kMinRowsPerSplit - 1) / kMinRowsPerSplit;
+  const int max_s = (M + min_rows - 1) / min_rows;
   if (S > max_s) S = max_s;
   if (S < 1) S = 1;
   rps = ((M + S - 1) / S + kWMK - 1) / kWMK * kWMK;
