@@ -75,7 +75,10 @@ struct BwdLds {
 // BM = 64 rows per tile (4 waves x 16 rows for the dgrad MFMA) or 32 (2 row groups x
 // 2 column halves; used when KP is large so the prefetched tile fits in registers)
 template <int EPI, int KP, int BN, int BM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void pw_bwd_fused_kernel(PwBwdArgs p) {
+#ifndef PGDIST_PWB_WPE
+#define PGDIST_PWB_WPE 2   // minimum waves per SIMD for the register allocation (A/B build define)
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PGDIST_PWB_WPE))) void pw_bwd_fused_kernel(PwBwdArgs p) {
   constexpr bool RAWX = EPI != EPI_BWD_LIN_ && BN >= 96;
   using L = BwdLds<KP, BN, BM, RAWX>;
   constexpr int LDA = L::LDA, LDX = L::LDX, LDC = L::LDC;

@@ -834,13 +834,23 @@ void launch_wgrad_reduce(float *part, int S, long long n, float *grad, hipStream
 void wgrad_reduce_defer(bool on);
 bool wgrad_reduce_deferring();
 
-// split-M geometry: tiles of TN x TK outputs, S splits of >= kMinRowsPerSplit rows each
-static constexpr int kMinRowsPerSplit = 512;
+// split-M geometry: tiles of TN x TK outputs, S splits of >= min_rows rows each.  The floor is
+// 512 rows for large weights and 256 when N*K <= 200k: the 14x14 / 7x7 MobileNetV2 weight
+// gradients (M = 25088 / 6272) then run 2x the splits (e.g. 147 -> 294 workgroups for
+// 64x384), 718 -> 604 us over the 22 pw_wgrad launches; the 1280x320 / 320x960 weights got
+// slower at 256 (twice the fp32 partials to write and reduce): profiles/r3b_pwwg_sweep.txt.
+static constexpr int kMinRowsPerSplit = 512, kMinRowsSmallW = 256;
+static constexpr long long kSmallW = 200000;
 static void wgrad_geom(int M, int N, int K, int &TN, int &TK, int &S, int &rps) {
-  static const int min_rows = [] {   // PGDIST_PWWG_MINROWS: rows per split floor (tuning experiments)
+  static const int env_rows = [] {   // PGDIST_PWWG_MINROWS: rows per split floor, all shapes (tuning)
     const char *e = getenv("PGDIST_PWWG_MINROWS");
-    return e && atoi(e) >= kWMK ? atoi(e) / kWMK * kWMK : kMinRowsPerSplit;
+    return e && atoi(e) >= kWMK ? atoi(e) / kWMK * kWMK : 0;
   }();
+  static const int env_small = [] {   // PGDIST_PWWG_MINROWS_SMALL: the floor for N*K <= 200k (tuning)
+    const char *e = getenv("PGDIST_PWWG_MINROWS_SMALL");
+    return e && atoi(e) >= kWMK ? atoi(e) / kWMK * kWMK : kMinRowsSmallW;
+  }();
+  const int min_rows = env_rows ? env_rows : ((long long)N * K <= kSmallW ? env_small : kMinRowsPerSplit);
   TN = N <= 32 ? 32 : (N <= 64 ? 64 : 128);
   TK = K <= 32 ? 32 : (K <= 64 ? 64 : 128);
   const int tiles = ((N + TN - 1) / TN) * ((K + TK - 1) / TK);
