@@ -41,6 +41,8 @@ void launch_adam_flat(float *, const float *, float *, float *, bf16_t *, long l
                       float, float, float, float, float, hipStream_t);
 void launch_f32_to_bf16(const float *, bf16_t *, long long, hipStream_t);
 int dw_fwd_num_partials(int, int, int, int, int);
+void dw_set_geom_mode(int);
+int dw_geom_mode();
 int bn_rep();
 void bn_fin_arm(const void *desc);
 void bn_lz_arm(const void *desc);
@@ -201,6 +203,8 @@ PYBIND11_MODULE(_pgdist_C, m) {
   });
   // ---- depthwise ----
   m.def("dw_fwd_num_partials", &dw_fwd_num_partials);
+  m.def("dw_set_geom_mode", &dw_set_geom_mode);
+  m.def("dw_geom_mode", &dw_geom_mode);
   m.def("bn_rep", &bn_rep, "replica rows of the atomic BN-statistics accumulators");
   m.def("bn_fin_arm", [](P d) { pgdist_rt::run_op([=] { bn_fin_arm(reinterpret_cast<const void *>(d)); }); },
         "arm a device BnFin descriptor for the next BN-statistics producer launch (finalize fused in its tail)");

@@ -34,6 +34,9 @@ constexpr int CPT = 4;        // channels per thread
 // 40 and 14 slower), the side-stream weight gradients keep 28
 constexpr int kRows = 56;
 constexpr int kWRows = 28;
+#ifndef PGDIST_DW_GEOM_DEFAULT
+#define PGDIST_DW_GEOM_DEFAULT 2   // occupancy-aware geometry kinds (see dw_geom); env PGDIST_DW_GEOM
+#endif
 
 struct DwGeom {
   int B, H, W, C, Ho, Wo;
@@ -351,8 +354,18 @@ __global__ __launch_bounds__(256) void dw_fwd_lds_kernel(
 // rows (g, y of this layer's BN backward, halo columns) of dy row r0-1+k and yprev (the
 // producer's pre-BN activation, own columns: ReLU6 mask + fused weight gradient) of input row
 // r0+k-2; step k >= 2 emits input row r0+k-2.  Per step: 3 DMA + 1 store.
+// PGDIST_DW_DGRAD_WPE (build define, A/B only): minimum waves per SIMD for the register
+// allocation.  The fused weight-gradient variant needs 175 VGPRs unconstrained (2 waves per
+// SIMD); waves_per_eu 3 forces <= 168 with 36 B of scratch in the row loop and measured 30-80 %
+// slower (56x56x144: 209.6 -> 277.4 us, 112x112x32: 152.9 -> 271.1 us; waves_per_eu 1 equals
+// the unconstrained build): profiles/r3b_pwwg_sweep.txt.  Unset: no attribute.
+#ifdef PGDIST_DW_DGRAD_WPE
+#define PGDIST_DW_DGRAD_ATTR __attribute__((amdgpu_waves_per_eu(PGDIST_DW_DGRAD_WPE)))
+#else
+#define PGDIST_DW_DGRAD_ATTR
+#endif
 template <bool WG, int D = kDepth>
-__global__ __launch_bounds__(256) void dw_dgrad_s1_lds_kernel(
+__global__ __launch_bounds__(256) PGDIST_DW_DGRAD_ATTR void dw_dgrad_s1_lds_kernel(
     const bf16_t *__restrict__ gin, const bf16_t *__restrict__ yself, const float *__restrict__ coef,
     const bf16_t *__restrict__ w, const bf16_t *__restrict__ yprev, const float *__restrict__ ps,
     const float *__restrict__ pt, bf16_t *__restrict__ gout, float *__restrict__ part, DwGeom g,
@@ -506,7 +519,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_s1_lds_kernel(
 // 2(o-1)+1 (own columns); step k >= 1 emits those two input rows (tap dh = 1 with dy row o-1;
 // dh = 2 with row o-1 and dh = 0 with row o).  Per step: 4 DMA + 2 stores.
 template <bool WG, int D = kDepth>
-__global__ __launch_bounds__(256) void dw_dgrad_s2_lds_kernel(
+__global__ __launch_bounds__(256) PGDIST_DW_DGRAD_ATTR void dw_dgrad_s2_lds_kernel(
     const bf16_t *__restrict__ gin, const bf16_t *__restrict__ yself, const float *__restrict__ coef,
     const bf16_t *__restrict__ w, const bf16_t *__restrict__ yprev, const float *__restrict__ ps,
     const float *__restrict__ pt, bf16_t *__restrict__ gout, float *__restrict__ part, DwGeom g,
@@ -862,6 +875,42 @@ static int dw_cc_narrow(int C, int gw, int kind, int stride, int cc0) {
   return best;
 }
 
+// Occupancy-aware geometry (bit per kind in g_dw_geom_mask: 1 fwd, 2 dgrad, 4 wgrad).  A
+// workgroup walks its R-row strip step by step (one DMA-ring row per step), so a launch lasts
+// about ceil(workgroups / resident slots) rounds x (steps per strip + ring fill); the default
+// geometry (CC <= 64, R = 56) can land just past a round: 56x56x144 dgrad = 1152 workgroups
+// on 512 slots (the fused-wgrad dgrad holds 175 VGPRs: 2 per CU) = 3 rounds, where 72-channel
+// slabs of 14 columns (56 = 4 x 14) make 1024 = 2 rounds.  The model picks (CC, R) over the
+// multiples of 8 dividing C (<= 128) and 1..8 strips per map, and replaces the default only
+// when it predicts >= 10 % fewer step-rounds.  Slots = 256 CUs x resident workgroups per CU of
+// each kernel family at its default ring depth (VGPR / LDS bound, from the gfx950 ISA):
+// forward 4, weight gradient 3, dgrad stride 2: 3, stride 1: 2 on the >= 56-row maps (the
+// executor fuses the weight gradient there; the partial count must not depend on whether a
+// launch fuses it) and 3 below.
+// Measured (profiles/r3c_dw_geom_ab.txt): 56x56x144 dgrad 209 -> 157 us, but the model's
+// picks for the forward (+14 us over 17 layers), the stride-2 dgrad (56x56x144: 89 -> 117 us)
+// and the 28x28 dgrad (38 -> 45 us) were slower -- rounds are not the whole cost where the
+// kernel is bandwidth-bound or the strip gets short.  So by default (mask 2) it applies only to
+// the stride-1 dgrad on >= 56-row maps; bit 8 lifts that restriction (experiments).
+int g_dw_geom_mask = [] {
+  const char *e = getenv("PGDIST_DW_GEOM");
+  return e ? atoi(e) : PGDIST_DW_GEOM_DEFAULT;
+}();
+static int dw_occ(int kind, int stride, int gh) {
+  return kind == 0 ? 4 : kind == 2 ? 3 : (stride == 1 && gh >= 56 ? 2 : 3);
+}
+static int dw_fix_rows(int kind, int stride, int R, int gh) {
+  if (kind == 1 && stride == 2 && (R & 1)) ++R;  // dgrad s2 tiles start on even input rows
+  if (R > gh) R = (kind == 1 && stride == 2) ? ((gh + 1) & ~1) : gh;
+  return R;
+}
+static long long dw_cost(int kind, int stride, int B, int gh, int gw, int C, int cc, int twc, int R) {
+  const long long nwg = (long long)B * ((gh + R - 1) / R) * ((gw + twc - 1) / twc) * (C / cc);
+  const long long slots = 256LL * dw_occ(kind, stride, gh);
+  const int steps = (kind == 1 && stride == 2) ? R / 2 : R;
+  return ((nwg + slots - 1) / slots) * (steps + 4);
+}
+
 // kind 0 = fwd (tiles over the output grid), 1 = dgrad (input grid), 2 = wgrad (output grid)
 DwGeom dw_geom(int kind, int B, int H, int W, int C, int stride) {
   DwGeom g;
@@ -890,8 +939,25 @@ DwGeom dw_geom(int kind, int B, int H, int W, int C, int stride) {
   int R = env_rows > 0 ? env_rows : kRows;
   if (kind == 2) R = env_wrows > 0 ? env_wrows : kWRows;
   // (PGDIST_DW_ROWS / PGDIST_DW_WROWS override the strip length for tuning experiments)
-  if (kind == 1 && stride == 2 && (R & 1)) ++R;  // dgrad s2 tiles start on even input rows
-  if (R > gh) R = (kind == 1 && stride == 2) ? ((gh + 1) & ~1) : gh;
+  R = dw_fix_rows(kind, stride, R, gh);
+  if ((g_dw_geom_mask & (1 << kind)) && ((g_dw_geom_mask & 8) || (kind == 1 && stride == 1 && gh >= 56))) {
+    const long long cur = dw_cost(kind, stride, B, gh, gw, C, g.CC, g.TWc, R);
+    long long best = cur;
+    int bcc = g.CC, btw = g.TWc, bR = R;
+    for (int ns = 1; ns <= 8; ++ns) {
+      const int r = dw_fix_rows(kind, stride, (gh + ns - 1) / ns, gh);
+      if (ns > 1 && r < 7) break;
+      for (int cc = 8; cc <= 128; cc += 8) {
+        if (C % cc) continue;
+        int t = dw_twc_max(cc, kind, stride);
+        if (t < 1) continue;
+        if (t > gw) t = gw;
+        const long long c = dw_cost(kind, stride, B, gh, gw, C, cc, t, r);
+        if (c < best) best = c, bcc = cc, btw = t, bR = r;
+      }
+    }
+    if (best * 10 <= cur * 9) g.CC = bcc, g.TWc = btw, R = bR;
+  }
   g.R = R;
   g.tiles_w = (gw + g.TWc - 1) / g.TWc;
   g.tiles_h = (gh + g.R - 1) / g.R;
@@ -900,6 +966,11 @@ DwGeom dw_geom(int kind, int B, int H, int W, int C, int stride) {
 
 int dw_grid_x(const DwGeom &g) { return g.B * g.tiles_h * g.tiles_w; }
 }  // namespace
+
+// geometry mode (tests / tuning): must not change while workspaces sized by the *_num_partials /
+// *_workspace_floats of another mode are in use
+void dw_set_geom_mode(int mask) { g_dw_geom_mask = mask; }
+int dw_geom_mode() { return g_dw_geom_mask; }
 
 int dw_fwd_num_partials(int B, int H, int W, int C, int stride) { return dw_grid_x(dw_geom(0, B, H, W, C, stride)); }
 int dw_dgrad_num_partials(int B, int H, int W, int C, int stride) { return dw_grid_x(dw_geom(1, B, H, W, C, stride)); }

@@ -219,6 +219,17 @@ def dw_num_partials(kind, B, H, W, C, stride):
     return f(B, H, W, C, stride)
 
 
+def dw_set_geom_mode(mask):
+    """Occupancy-aware depthwise tile geometry per kernel kind (bit 1 fwd, 2 dgrad, 4 wgrad;
+    default from PGDIST_DW_GEOM).  Partial counts and workspaces depend on it: switch only
+    before sizing them (tests / tuning)."""
+    lib().dw_set_geom_mode(int(mask))
+
+
+def dw_geom_mode():
+    return lib().dw_geom_mode()
+
+
 def _dw_check(B, H, W, C, stride):
     if C % 8 or C // 8 > 256:
         raise ValueError(f"depthwise: C={C} must be a multiple of 8 and <= 2048")

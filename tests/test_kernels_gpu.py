@@ -201,6 +201,57 @@ def test_dw_dgrad_wgrad(dev, B, H, W, C, stride):
     assert rel(grad2.view(9, C).t().reshape(C, 1, 3, 3), wref) < 1e-3
 
 
+def _dw_all(B, H, C, stride, dev):
+    """fwd y, BN sums, fused dgrad gout, its BN sums and weight gradient, separate weight gradient"""
+    x = bf(rnd(B, H, H, C, dev=dev, seed=21))
+    s, t = bn_params(C, dev, 2)
+    w = tapmajor(bf(rnd(C, 1, 3, 3, dev=dev, seed=3) * 0.3))
+    Ho, _ = K.dw_out_hw(H, H, stride)
+    y = torch.empty(B, Ho, Ho, C, dtype=torch.bfloat16, device=dev)
+    Pf = K.dw_num_partials("fwd", B, H, H, C, stride)
+    pf = torch.zeros(K.bn_rows(Pf) * 2 * C, device=dev)
+    K.dw_fwd(x, s, t, K.ACT_BN_RELU6, w, y, pf, B, H, H, C, stride)
+    g = bf(rnd(B, Ho, Ho, C, dev=dev, seed=12))
+    gen = torch.Generator(device="cpu").manual_seed(7)
+    coef = (torch.rand(3, C, generator=gen) + torch.tensor([[0.5], [-0.5], [-0.5]])).to(dev).contiguous()
+    gout = torch.empty(B, H, H, C, dtype=torch.bfloat16, device=dev)
+    Pd = K.dw_num_partials("dgrad", B, H, H, C, stride)
+    pd = torch.zeros(K.bn_rows(Pd) * 2 * C, device=dev)
+    wp = torch.zeros(K.dw_dgrad_wgrad_workspace(B, H, H, C, stride), device=dev)
+    K.dw_dgrad(g, y, coef, w, x, s, t, gout, pd, B, H, H, C, stride, wpart=wp)
+    gw1 = torch.empty(C * 9, device=dev)
+    K.wgrad_reduce(wp, Pd, 9 * C, gw1)
+    ws = torch.zeros(K.dw_wgrad_workspace(B, H, H, C, stride), device=dev)
+    gw2 = torch.empty(C * 9, device=dev)
+    K.dw_wgrad(g, y, coef, x, s, t, ws, gw2, B, H, H, C, stride)
+    torch.cuda.synchronize()
+    return (y, sum_parts(pf, K.bn_rows(Pf), C), gout, sum_parts(pd, K.bn_rows(Pd), C), gw1, gw2,
+            (Pf, Pd, K.dw_num_partials("wgrad", B, H, H, C, stride)))
+
+
+@pytest.mark.parametrize("H,C,stride", [(56, 144, 1), (56, 144, 2), (28, 192, 2), (112, 32, 1)])
+def test_dw_occupancy_geometry(dev, H, C, stride):
+    """The occupancy-aware tile geometry (dw_set_geom_mode 15: every kind, unrestricted; channel
+    slab / strip length chosen per launch from the resident-workgroup count) computes the same convolution as the default
+    geometry at the MobileNetV2 bs128 shapes: identical activations and dgrad, BN sums and
+    weight gradients equal up to float summation order."""
+    B = 128
+    old = K.dw_geom_mode()
+    try:
+        K.dw_set_geom_mode(0)
+        ref = _dw_all(B, H, C, stride, dev)
+        K.dw_set_geom_mode(15)
+        out = _dw_all(B, H, C, stride, dev)
+    finally:
+        K.dw_set_geom_mode(old)
+    assert torch.equal(out[0], ref[0]) and torch.equal(out[2], ref[2])
+    for a, b in zip(out[1:6], ref[1:6]):
+        if a.dtype != torch.bfloat16:
+            assert rel(a, b) < 1e-4
+    if (H, C) == (56, 144):
+        assert out[6] != ref[6]   # the model re-tiles these layers
+
+
 # ----------------------------------------------------------------------------- pointwise
 # small M -> L2-direct weights with the K split over waves (KS 1/2/4); M >= 65536 -> LDS-resident weights
 PW_CASES = [(1000, 16, 96), (4096, 24, 144), (777, 96, 24), (3000, 320, 1280), (2048, 160, 960),
