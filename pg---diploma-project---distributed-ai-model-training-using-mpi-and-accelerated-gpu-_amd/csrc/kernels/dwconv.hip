@@ -35,7 +35,7 @@ constexpr int CPT = 4;        // channels per thread
 constexpr int kRows = 56;
 constexpr int kWRows = 28;
 #ifndef PGDIST_DW_GEOM_DEFAULT
-#define PGDIST_DW_GEOM_DEFAULT 2   // occupancy-aware geometry kinds (see dw_geom); env PGDIST_DW_GEOM
+#define PGDIST_DW_GEOM_DEFAULT 3   // occupancy-aware geometry kinds (see dw_geom); env PGDIST_DW_GEOM
 #endif
 
 struct DwGeom {
@@ -887,11 +887,12 @@ static int dw_cc_narrow(int C, int gw, int kind, int stride, int cc0) {
 // forward 4, weight gradient 3, dgrad stride 2: 3, stride 1: 2 on the >= 56-row maps (the
 // executor fuses the weight gradient there; the partial count must not depend on whether a
 // launch fuses it) and 3 below.
-// Measured (profiles/r3c_dw_geom_ab.txt): 56x56x144 dgrad 209 -> 157 us, but the model's
-// picks for the forward (+14 us over 17 layers), the stride-2 dgrad (56x56x144: 89 -> 117 us)
-// and the 28x28 dgrad (38 -> 45 us) were slower -- rounds are not the whole cost where the
-// kernel is bandwidth-bound or the strip gets short.  So by default (mask 2) it applies only to
-// the stride-1 dgrad on >= 56-row maps; bit 8 lifts that restriction (experiments).
+// Measured (profiles/r3c_dw_geom_ab.txt): 56x56x144 dgrad 209 -> 157 us and forward 57 -> 48 us
+// (both 72-channel slabs of 14 columns), but the model's stride-2 picks (forward 112x112x96:
+// 91 -> 116 us, dgrad 56x56x144: 89 -> 117 us) and the 28x28 dgrad (38 -> 45 us) were slower --
+// rounds are not the whole cost where the kernel is bandwidth-bound or the strip gets short.
+// So by default (mask 3) it applies to the stride-1 forward / dgrad on >= 56-row maps only;
+// bit 8 lifts that restriction (experiments).
 int g_dw_geom_mask = [] {
   const char *e = getenv("PGDIST_DW_GEOM");
   return e ? atoi(e) : PGDIST_DW_GEOM_DEFAULT;
@@ -940,7 +941,7 @@ DwGeom dw_geom(int kind, int B, int H, int W, int C, int stride) {
   if (kind == 2) R = env_wrows > 0 ? env_wrows : kWRows;
   // (PGDIST_DW_ROWS / PGDIST_DW_WROWS override the strip length for tuning experiments)
   R = dw_fix_rows(kind, stride, R, gh);
-  if ((g_dw_geom_mask & (1 << kind)) && ((g_dw_geom_mask & 8) || (kind == 1 && stride == 1 && gh >= 56))) {
+  if ((g_dw_geom_mask & (1 << kind)) && ((g_dw_geom_mask & 8) || (kind <= 1 && stride == 1 && gh >= 56))) {
     const long long cur = dw_cost(kind, stride, B, gh, gw, C, g.CC, g.TWc, R);
     long long best = cur;
     int bcc = g.CC, btw = g.TWc, bR = R;
@@ -1014,10 +1015,16 @@ void launch_dw_dgrad(const bf16_t *gin, const bf16_t *yself, const float *coef, 
   const dim3 grid(dw_grid_x(g) * (C / g.CC)), block(256);
   // ring depth (rows in flight): 3 by default -- 39 KB of LDS per workgroup, 4 workgroups per CU
   // instead of 3 at depth 4 (MobileNetV2 bs128: 5.02 -> 4.94 ms/step); PGDIST_DW_DDEPTH=2|3|4
+  // PGDIST_DW_DDEPTH_WG: ring depth of the fused dgrad + wgrad variants (their VGPRs, not LDS,
+  // bound the resident workgroups: 175 -> 2 per CU at stride 1, 139 -> 3 at stride 2)
   static const int env_d = [] { const char *e = getenv("PGDIST_DW_DDEPTH"); return e ? atoi(e) : 3; }();
+  static const int env_dwg = [] { const char *e = getenv("PGDIST_DW_DDEPTH_WG"); return e ? atoi(e) : 3; }();
+  static const int env_ds1 = [] { const char *e = getenv("PGDIST_DW_DDEPTH_S1"); return e ? atoi(e) : 0; }();
+  const int D = wpart ? env_dwg : (stride == 1 && env_ds1 ? env_ds1 : env_d);
 #define DWD(KER, WGF)                                                                                     \
-  if (env_d == 2) hipLaunchKernelGGL((KER<WGF, 2>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g, wpart); \
-  else if (env_d == 4) hipLaunchKernelGGL((KER<WGF, 4>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g, wpart); \
+  if (D == 2) hipLaunchKernelGGL((KER<WGF, 2>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g, wpart); \
+  else if (D == 4) hipLaunchKernelGGL((KER<WGF, 4>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g, wpart); \
+  else if (D == 5) hipLaunchKernelGGL((KER<WGF, 5>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g, wpart); \
   else hipLaunchKernelGGL((KER<WGF, 3>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g, wpart);
   if (wpart) {
     if (stride == 1) { DWD(dw_dgrad_s1_lds_kernel, true) }
