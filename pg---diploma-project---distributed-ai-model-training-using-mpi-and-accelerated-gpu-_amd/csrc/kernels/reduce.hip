@@ -44,6 +44,9 @@ int *reduce_counters(int n, hipStream_t st) {
 // read as 16 x 16-B pieces = 256 contiguous bytes); the rows are split into nch chunks so
 // the grid has ~2k workgroups, and the last-arriving workgroup of a column block sums the
 // nch level-1 rows (<= kWredMaxChunks) the same way.
+#ifndef PGDIST_RED_ROWS4
+#define PGDIST_RED_ROWS4 0
+#endif
 constexpr int kWredMaxChunks = 128;
 constexpr int kWredTargetWgs = 2048;
 constexpr int kWredSideWgs = 384;
@@ -72,9 +75,9 @@ PG_DEVICE void col_reduce_body(const float *__restrict__ part, int R, long long 
   const int cg = threadIdx.x & 15, stripe = threadIdx.x >> 4;
   const long long c0 = ((long long)bx * 16 + cg) * V;
   const bool cok = c0 < n;
-  float acc[V], acc2[V];
+  float acc[V], acc2[V], acc3[V], acc4[V];
 #pragma unroll
-  for (int j = 0; j < V; ++j) acc[j] = acc2[j] = 0.f;
+  for (int j = 0; j < V; ++j) acc[j] = acc2[j] = acc3[j] = acc4[j] = 0.f;
   auto ld = [&](const float *p, float (&v)[V]) {
     if constexpr (V == 4) {
       const float4 q = *reinterpret_cast<const float4 *>(p);
@@ -86,6 +89,21 @@ PG_DEVICE void col_reduce_body(const float *__restrict__ part, int R, long long 
   const int r0 = by * rch, r1 = min(R, r0 + rch);
   if (cok) {
     int r = r0 + stripe;
+    // PGDIST_RED_ROWS4 (build define, default off): four rows in flight per thread instead of
+    // two.  Measured (profiles/r3c_reduce_ab.txt): ResNet-50 11.81-11.83 -> 11.93-12.00 ms/step,
+    // MobileNetV2 within noise -- the side-stream reduction then takes HBM bandwidth from the
+    // main stream's convolutions; larger reduction grids (PGDIST_WRED_WGS 1024 / 2048) likewise
+#if PGDIST_RED_ROWS4
+    for (; r + 48 < r1; r += 64) {
+      float a[V], b[V], c[V], d[V];
+      ld(part + (size_t)r * n + c0, a);
+      ld(part + (size_t)(r + 16) * n + c0, b);
+      ld(part + (size_t)(r + 32) * n + c0, c);
+      ld(part + (size_t)(r + 48) * n + c0, d);
+#pragma unroll
+      for (int j = 0; j < V; ++j) { acc[j] += a[j]; acc2[j] += b[j]; acc3[j] += c[j]; acc4[j] += d[j]; }
+    }
+#endif
     for (; r + 16 < r1; r += 32) {   // two rows in flight per thread, fixed order
       float a[V], b[V];
       ld(part + (size_t)r * n + c0, a);
@@ -101,7 +119,7 @@ PG_DEVICE void col_reduce_body(const float *__restrict__ part, int R, long long 
     }
   }
 #pragma unroll
-  for (int j = 0; j < V; ++j) sh[stripe][cg * V + j] = acc[j] + acc2[j];
+  for (int j = 0; j < V; ++j) sh[stripe][cg * V + j] = (acc[j] + acc2[j]) + (acc3[j] + acc4[j]);
   __syncthreads();
   const int col = threadIdx.x;   // < 16 * V: one output column per thread
   const long long oc = (long long)bx * 16 * V + col;
@@ -214,7 +232,11 @@ void wgrad_reduce_flush(hipStream_t st) {
   for (size_t b = 0; b < segs.size(); b += kRedMaxSeg) {
     RedSegs a{};
     a.nseg = (int)std::min<size_t>(kRedMaxSeg, segs.size() - b);
-    const int target = std::max(64, (is_side_stream(st) ? kWredSideWgs : kWredTargetWgs) / a.nseg);
+    static const int env_t = [] {   // PGDIST_WRED_WGS: grid-size target of every reduction
+      const char *e = getenv("PGDIST_WRED_WGS");
+      return e && atoi(e) > 0 ? atoi(e) : 0;
+    }();
+    const int target = std::max(64, (env_t > 0 ? env_t : is_side_stream(st) ? kWredSideWgs : kWredTargetWgs) / a.nseg);
     int wg = 0, ctrs = 0;
     for (int k = 0; k < a.nseg; ++k) {
       const PendingRed &r = segs[b + k];
