@@ -1743,9 +1743,10 @@ struct WgDmaCfg {
 };
 WgDmaCfg wg_dma_cfg(int N, int Ci, int M, int taps) {
   static const int e_t = env_int("PGDIST_WGD_TARGET", 0), e_mk = env_int("PGDIST_WG_DMA_MK", 0),
-                   e_nb = env_int("PGDIST_WG_DMA_NBUF", 0);
+                   e_nb = env_int("PGDIST_WG_DMA_NBUF", 0), e_t1 = env_int("PGDIST_WGD_T1", 512);
   const int TN = N % 128 == 0 ? 128 : 64, TK = Ci % 128 == 0 ? 128 : 64;
-  WgDmaCfg c{512, 64, 2};
+  // PGDIST_WGD_T1: grid target of the 1x1 weight gradients (tuning)
+  WgDmaCfg c{taps > 1 ? 512 : e_t1, 64, 2};
   if (taps > 1) {
     if (M <= 8192) { c.mk = 32; c.nbuf = 3; }
     else if (M <= 32768 || (TN == 64 && TK == 64)) c.target = 1024;
