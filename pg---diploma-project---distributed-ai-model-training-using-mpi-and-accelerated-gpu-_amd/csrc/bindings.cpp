@@ -511,6 +511,10 @@ PYBIND11_MODULE(_pgdist_C, m) {
   m.def("comm_join", &pgdist_rt::comm_join, "waiter stream waits for the collectives issued so far");
   m.def("comm_time_allreduce", &pgdist_rt::comm_time_allreduce, py::call_guard<py::gil_scoped_release>());
   m.def("comm_error", &pgdist_rt::comm_error, py::call_guard<py::gil_scoped_release>());
+  m.def("comm_error_string", &pgdist_rt::comm_error_string);
+  m.def("comm_poison", &pgdist_rt::comm_poison, py::call_guard<py::gil_scoped_release>());
+  m.def("comm_clear_error", &pgdist_rt::comm_clear_error, py::call_guard<py::gil_scoped_release>());
+  m.def("comm_rccl_ranks", &pgdist_rt::comm_rccl_ranks);
   m.def("comm_destroy", &pgdist_rt::comm_destroy, py::call_guard<py::gil_scoped_release>());
 
   m.def("cu_masked_stream", &pgdist_rt::cu_masked_stream,

@@ -22,11 +22,15 @@
 //
 // Memory model (p2p.h): staging is UNCACHED device memory; payload stores and loads use
 // system-coherent buffer instructions (sc0 sc1), every storing wave drains its stores
-// (vmcnt(0)) before the block barrier, then ONE lane per peer stores the epoch into the
-// peer's signal slot with a system-scope atomic, and ONE wave polls this rank's slots with
-// relaxed system-scope loads (+ s_sleep).  The poll is bounded by the realtime clock: a rank
-// that never arrives makes the kernel set its error word and exit instead of hanging the GPU
-// (the host checks the word: Comm::check).
+// (vmcnt(0)) before the block barrier, then a system-scope release fence and ONE lane per
+// peer stores {call signature, epoch} into the peer's 8-byte signal slot with a system-scope
+// atomic; ONE wave polls this rank's slots with relaxed system-scope loads (+ s_sleep) and
+// issues a system-scope acquire fence once every peer is there.  The poll is bounded by the
+// realtime clock: a rank that never arrives, or one that is out of step (skipped, added or
+// reordered collectives), makes the kernel set its error word and exit instead of hanging the
+// GPU or reducing mismatched buffers.  A set error word poisons the communicator: every later
+// collective of that rank exits at once without signalling, so its peers time out as well and
+// every rank's host check (Comm::error -> NativeComm.check_all) fails the job.
 //
 // Single-process emulation: the grid holds nlocal * G blocks, block -> (local rank, block),
 // each local rank with its own descriptor, buffer and staging (tests / microbenchmarks of N
@@ -75,36 +79,65 @@ PG_DEVICE uint4 f4u(const float a, const float b, const float c, const float d) 
 }
 
 // Block-wide barrier with the same block of every rank (see the file comment).  Returns false
-// (and sets the error word) if a peer did not arrive within the timeout.
-__device__ bool ar_barrier(const ArDesc &d, int b, unsigned e, int *s_ok) {
+// (and sets this rank's error word) if a peer did not arrive within the timeout (bit 0), a peer
+// is out of step with this rank (bit 1: its epoch for this block is more than one barrier ahead,
+// or it entered the same barrier for a collective with a different signature — a rank that
+// skipped or reordered collectives), or another block of this rank already failed.
+//
+// Ordering: every storing wave drains its payload stores (vmcnt(0)), the block barrier, then the
+// signalling wave issues a SYSTEM-scope release fence (L2 write-back; the explicit vmcnt(0) after
+// it guards against the compiler dropping the fence's own wait) and stores the signal with a
+// system-scope atomic; the polling wave reads the peers' slots with relaxed system-scope loads
+// and, once every peer is there, issues a system-scope acquire fence + vmcnt(0) before the block
+// barrier that releases the payload loads (MI355X_MICROARCH.md, inter-workgroup visibility).
+__device__ bool ar_barrier(const ArDesc &d, int b, unsigned e, unsigned tag, int *s_ok) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's payload stores are done
   __syncthreads();
   if (threadIdx.x < 64) {
     const int p = threadIdx.x;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");       // system scope
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned long long sig = ((unsigned long long)tag << 32) | e;
     if (p < d.world) {
-      unsigned *slot = reinterpret_cast<unsigned *>(d.stage[p]) + b * 32 + d.rank;
-      __hip_atomic_store(slot, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      unsigned long long *slot = reinterpret_cast<unsigned long long *>(d.stage[p]) + b * 32 + d.rank;
+      __hip_atomic_store(slot, sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    const unsigned *mine = reinterpret_cast<const unsigned *>(d.stage[d.rank]) + b * 32;
+    const unsigned long long *mine = reinterpret_cast<const unsigned long long *>(d.stage[d.rank]) + b * 32;
     const unsigned long long t0 = wall_clock64();
-    bool ok = true;
+    unsigned fail = 0;
     for (;;) {
-      const bool here = p >= d.world ||
-                        (int)(__hip_atomic_load(mine + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) >= 0;
+      int here = 1, bad = 0;
+      if (p < d.world) {
+        const unsigned long long v = __hip_atomic_load(mine + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const int dlt = (int)((unsigned)v - e);
+        here = dlt >= 0;
+        bad = dlt > 1 || (dlt == 0 && (unsigned)(v >> 32) != tag);
+      }
+      if (__any(bad)) {
+        fail = kArErrDesync;
+        break;
+      }
       if (__all(here)) break;
       if (wall_clock64() - t0 > (unsigned long long)d.timeout_ticks) {
-        ok = false;
+        fail = kArErrTimeout;
+        break;
+      }
+      if (__hip_atomic_load(d.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {   // poisoned meanwhile
+        fail = kArErrPoisoned;
         break;
       }
       __builtin_amdgcn_s_sleep(2);
     }
+    if (!fail) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");     // system scope
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     if (p == 0) {
-      if (!ok) atomicOr(d.err, 1u);
-      *s_ok = ok ? 1 : 0;
+      if (fail) atomicOr(d.err, fail);
+      *s_ok = fail ? 0 : 1;
     }
   }
   __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the payload loads below the poll
   return *s_ok != 0;
 }
 
@@ -120,6 +153,13 @@ __global__ __launch_bounds__(kArThreads) void p2p_collective_kernel(const ArCall
   const long long n = call.n;
   const int tid = threadIdx.x;
   const long long stride = (long long)G * kArThreads;
+  // a communicator whose error word is set is poisoned: every later collective exits at once,
+  // sends no signal and leaves the buffer untouched (peers then time out too), so no rank can
+  // continue on desynchronised epochs; the host reports the word (Comm::check) and aborts
+  if (tid == 0) s_ok = __hip_atomic_load(d.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
+  __syncthreads();
+  if (!s_ok) return;
+  const unsigned tag = call.tag;
   unsigned e = __hip_atomic_load(d.ctr + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const unsigned calls = __hip_atomic_load(d.ctr + kArMaxBlocks + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const long long offA = kArSigBytes + (long long)(calls & 1) * d.region_bytes;
@@ -136,7 +176,7 @@ __global__ __launch_bounds__(kArThreads) void p2p_collective_kernel(const ArCall
     if (r == call.root)
       for (long long i = (long long)b * kArThreads + tid; i < nv; i += stride)
         st_sys(rs[r], (uint32_t)(offA + i * 16), bld16(rb, (uint32_t)(i * 16)));
-    ok = ar_barrier(d, b, ++e, &s_ok);
+    ok = ar_barrier(d, b, ++e, tag, &s_ok);
     if (ok && r != call.root)
       for (long long i = (long long)b * kArThreads + tid; i < nv; i += stride)
         bst16(rb, (uint32_t)(i * 16), ld_sys(rs[call.root], (uint32_t)(offA + i * 16)));
@@ -163,7 +203,7 @@ __global__ __launch_bounds__(kArThreads) void p2p_collective_kernel(const ArCall
         }
       }
     }
-    ok = ar_barrier(d, b, ++e, &s_ok);
+    ok = ar_barrier(d, b, ++e, tag, &s_ok);
     // ---- reduce: one-shot the whole bucket, two-shot this rank's segment; rank order 0..N-1
     const long long rbase = two ? (long long)r * segv : 0;
     if (ok) {
@@ -205,7 +245,7 @@ __global__ __launch_bounds__(kArThreads) void p2p_collective_kernel(const ArCall
     }
     // ---- two-shot: gather the other ranks' reduced segments
     if (ok && two) {
-      ok = ar_barrier(d, b, ++e, &s_ok);
+      ok = ar_barrier(d, b, ++e, tag, &s_ok);
       if (ok) {
         for (long long j = (long long)b * kArThreads + tid; j < segv; j += stride) {
           for (int s = 0; s < N; ++s) {

@@ -5,13 +5,14 @@
 // no L2 copy of it exists on any GPU, so a peer's load over xGMI always sees memory) that
 // every other rank maps through hipIpcOpenMemHandle:
 //
-//   [0, kArSigBytes)                  signal slots: uint32 sig[block * 32 + src_rank]
+//   [0, kArSigBytes)                  signal slots: uint64 sig[block * 32 + src_rank] =
+//                                     {call signature << 32 | epoch}
 //   A0 = kArSigBytes                  copy-in region, even calls   (region_bytes)
 //   A1 = A0 + region_bytes            copy-in region, odd calls    (region_bytes)
 //   R  = A1 + region_bytes            two-shot reduced segment     (region_bytes)
 //
 // A signal slot is written ONLY by its source rank (system-scope atomic store of a
-// monotonically increasing epoch) and polled only by the slot's owner, so no slot is ever
+// monotonically increasing epoch tagged with the collective's signature) and polled only by the slot's owner, so no slot is ever
 // reset.  A block's epoch / call counters live in the owner's ordinary device memory and are
 // advanced by the kernel itself (never a host argument: a recorded launch replays with frozen
 // arguments).  Every rank issues the same collectives in the same order with the same block
@@ -52,6 +53,13 @@ struct ArCall {
   int algo;
   int bf16_wire;   // all-reduce: stage bf16 (sum in fp32)
   int root;        // broadcast
+  unsigned tag;    // call signature (algo, n, wire, root): peers in one barrier must agree
+  int pad;
 };
+
+// bits of the error word
+constexpr unsigned kArErrTimeout = 1u;   // a peer did not arrive within the timeout
+constexpr unsigned kArErrDesync = 2u;    // a peer is out of step (epoch or call signature)
+constexpr unsigned kArErrPoisoned = 4u;  // another block of this rank had already failed
 
 __host__ __device__ inline long long ar_stage_bytes(long long region_bytes) { return kArSigBytes + 3 * region_bytes; }

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -36,6 +37,7 @@ struct Rccl {
   decltype(&ncclBroadcast) broadcast = nullptr;
   decltype(&ncclGetErrorString) errorString = nullptr;
   decltype(&ncclGetVersion) getVersion = nullptr;
+  decltype(&ncclCommCount) commCount = nullptr;
 };
 
 template <class F>
@@ -63,6 +65,7 @@ Rccl &rccl() {
     sym(x->h, x->broadcast, "ncclBroadcast");
     sym(x->h, x->errorString, "ncclGetErrorString");
     sym(x->h, x->getVersion, "ncclGetVersion");
+    sym(x->h, x->commCount, "ncclCommCount");
     return x;
   }();
   return *r;
@@ -100,6 +103,19 @@ struct Comm {
   unsigned char *stage[kArMaxRanks] = {};
   unsigned int *ctr = nullptr;    // nlocal * (kArCtrWords + 8) words: counters, error word
   bool p2p = false;
+  // sticky host-side failure state: a synchronous RCCL error at launch (record or replay time),
+  // or an error word / RCCL async error seen by comm_error.  Once set the communicator is
+  // poisoned: every later collective (recorded ops included) throws instead of launching.
+  std::atomic<int> host_err{0};
+  std::string what;
+
+  void fail(int code, const std::string &msg) {
+    if (host_err.fetch_or(code) == 0) what = msg;
+  }
+  void ensure_usable() const {
+    if (host_err.load())
+      throw std::runtime_error("native communicator is poisoned after an earlier failure (" + what + ")");
+  }
 
   unsigned int *ctr_of(int l) const { return ctr + (size_t)l * (kArCtrWords + 8); }
   unsigned int *err_of(int l) const { return ctr_of(l) + kArCtrWords; }
@@ -123,6 +139,13 @@ struct Comm {
     c.algo = algo;
     c.bf16_wire = bf16 ? 1 : 0;
     c.root = root;
+    // call signature: every rank entering one barrier must be in the same collective
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)algo;
+    for (uint64_t v : {(uint64_t)n, (uint64_t)(bf16 ? 1 : 0), (uint64_t)(root + 1)}) {
+      h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+      h *= 0xff51afd7ed558ccdull;
+    }
+    c.tag = (unsigned)(h ^ (h >> 32)) | 1u;
     return c;
   }
 };
@@ -164,6 +187,15 @@ void check_p2p_call(const Comm &c, const std::vector<uintptr_t> &bufs, long long
   if (bytes_needed > c.region)
     throw std::invalid_argument("P2P collective of " + std::to_string(bytes_needed) + " bytes exceeds the " +
                                 std::to_string(c.region) + "-byte staging region");
+}
+
+// a synchronous RCCL failure (bad argument, communicator in error, ...) poisons the
+// communicator and throws; plan_replay propagates the exception to the caller
+void rccl_result(Comm *c, ncclResult_t r, const char *what) {
+  if (r == ncclSuccess || r == ncclInProgress) return;
+  const std::string msg = std::string(what) + ": " + rccl().errorString(r);
+  c->fail(kCommErrRccl, msg);
+  throw std::runtime_error(msg);
 }
 
 }  // namespace
@@ -289,9 +321,11 @@ void comm_allreduce(int id, const std::vector<uintptr_t> &bufs, long long n, int
     void *b = reinterpret_cast<void *>(bufs[0]);
     ncclComm_t nc = c.nccl;
     Rccl *r = &rccl();
+    Comm *cp = &c;
     run_op([=] {
+      cp->ensure_usable();
       wait_all(st, wait, ev);
-      (void)r->allReduce(b, b, (size_t)n, ncclFloat32, ncclSum, nc, st);
+      rccl_result(cp, r->allReduce(b, b, (size_t)n, ncclFloat32, ncclSum, nc, st), "ncclAllReduce");
     });
     return;
   }
@@ -301,7 +335,9 @@ void comm_allreduce(int id, const std::vector<uintptr_t> &bufs, long long n, int
   const ArCall call = c.make_call(bufs, n, algo == COMM_ONESHOT ? AR_ONESHOT : AR_TWOSHOT, bf16_wire, 0);
   const int nl = c.nlocal;
   auto cp = std::make_shared<ArCall>(call);
+  Comm *comm = &c;
   run_op([=] {
+    comm->ensure_usable();
     wait_all(st, wait, ev);
     launch_p2p_collective(*cp, nl, st);
   });
@@ -319,9 +355,11 @@ void comm_broadcast(int id, const std::vector<uintptr_t> &bufs, long long n, int
     void *b = reinterpret_cast<void *>(bufs[0]);
     ncclComm_t nc = c.nccl;
     Rccl *r = &rccl();
+    Comm *cp = &c;
     run_op([=] {
+      cp->ensure_usable();
       wait_all(st, wait, ev);
-      (void)r->broadcast(b, b, (size_t)n, ncclFloat32, root, nc, st);
+      rccl_result(cp, r->broadcast(b, b, (size_t)n, ncclFloat32, root, nc, st), "ncclBroadcast");
     });
     return;
   }
@@ -329,7 +367,9 @@ void comm_broadcast(int id, const std::vector<uintptr_t> &bufs, long long n, int
   check_p2p_call(c, bufs, n, n * 4);
   auto cp = std::make_shared<ArCall>(c.make_call(bufs, n, AR_BROADCAST, false, root));
   const int nl = c.nlocal;
+  Comm *comm = &c;
   run_op([=] {
+    comm->ensure_usable();
     wait_all(st, wait, ev);
     launch_p2p_collective(*cp, nl, st);
   });
@@ -344,9 +384,12 @@ void comm_allreduce_f64(int id, uintptr_t buf, long long n, int op, const std::v
   ncclComm_t nc = c.nccl;
   Rccl *r = &rccl();
   void *b = reinterpret_cast<void *>(buf);
+  Comm *cp = &c;
   run_op([=] {
+    cp->ensure_usable();
     wait_all(st, wait, ev);
-    (void)r->allReduce(b, b, (size_t)n, ncclFloat64, op == 0 ? ncclSum : ncclMax, nc, st);
+    rccl_result(cp, r->allReduce(b, b, (size_t)n, ncclFloat64, op == 0 ? ncclSum : ncclMax, nc, st),
+                "ncclAllReduce(f64)");
   });
 }
 
@@ -388,13 +431,51 @@ int comm_error(int id) {
     std::vector<unsigned int> w((size_t)c.nlocal * (kArCtrWords + 8));
     hcheck(hipMemcpy(w.data(), c.ctr, w.size() * 4, hipMemcpyDeviceToHost), "hipMemcpy(error words)");
     for (int l = 0; l < c.nlocal; ++l) err |= (int)(w[(size_t)l * (kArCtrWords + 8) + kArCtrWords] & 0xff);
+    if (err)
+      c.fail(err, std::string("P2P barrier failure:") + ((err & kArErrTimeout) ? " peer timeout" : "") +
+                      ((err & kArErrDesync) ? " peer out of step" : "") +
+                      ((err & kArErrPoisoned) ? " poisoned" : ""));
   }
   if (c.nccl) {
     ncclResult_t ae = ncclSuccess;
-    if (rccl().getAsyncError(c.nccl, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress)
+    if (rccl().getAsyncError(c.nccl, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
       err |= ((int)ae & 0xff) << 8;
+      c.fail(((int)ae & 0xff) << 8, std::string("RCCL async error: ") + rccl().errorString(ae));
+    }
   }
-  return err;
+  return err | (c.host_err.load() & kCommErrRccl);
+}
+
+void comm_poison(int id, const std::string &why) {
+  Comm &c = get(id);
+  c.fail(kCommErrPeer, why);
+  const unsigned w = kArErrPoisoned;
+  for (int l = 0; c.ctr && l < c.nlocal; ++l)
+    hcheck(hipMemcpyAsync(c.err_of(l), &w, 4, hipMemcpyHostToDevice, c.stream), "hipMemcpyAsync(error word)");
+  hcheck(hipStreamSynchronize(c.stream), "hipStreamSynchronize(comm)");
+}
+
+void comm_clear_error(int id) {
+  Comm &c = get(id);
+  hcheck(hipStreamSynchronize(c.stream), "hipStreamSynchronize(comm)");
+  for (int l = 0; c.ctr && l < c.nlocal; ++l)
+    hcheck(hipMemset(c.err_of(l), 0, 4), "hipMemset(error word)");
+  hcheck(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  c.host_err.store(0);
+  c.what.clear();
+}
+
+std::string comm_error_string(int id) {
+  Comm &c = get(id);
+  return c.host_err.load() ? c.what : std::string();
+}
+
+int comm_rccl_ranks(int id) {
+  Comm &c = get(id);
+  if (!c.nccl) return 0;
+  int n = 0;
+  ncheck(rccl().commCount(c.nccl, &n), "ncclCommCount");
+  return n;
 }
 
 void comm_destroy(int id) {

@@ -58,8 +58,19 @@ void comm_join(int id, uintptr_t waiter);
 // microbenchmark: `iters` back-to-back all-reduces on the comm stream, us per call (host-synchronous)
 double comm_time_allreduce(int id, const std::vector<uintptr_t> &bufs, long long n, int algo, bool bf16_wire,
                            int iters);
-// error state: P2P barrier timeout bits | RCCL async error (<< 8); synchronises the comm stream
+// error state (sticky: a nonzero result poisons the communicator, later collectives throw):
+// P2P error-word bits (p2p.h kArErr*) | RCCL async error << 8 | kCommErrRccl for a synchronous
+// RCCL failure at launch; synchronises the comm stream
+constexpr int kCommErrRccl = 1 << 16;
+constexpr int kCommErrPeer = 1 << 17;   // poisoned because ANOTHER rank failed (comm_poison)
 int comm_error(int id);
+// poison this rank's communicator because a peer failed (host flag + device error word)
+void comm_poison(int id, const std::string &why);
+// un-poison after a failure every rank has agreed on and reacted to (the P2P path is then
+// abandoned: its epochs may be out of step) — used only by the start-up P2P validation
+void comm_clear_error(int id);
+std::string comm_error_string(int id);   // what poisoned the communicator ("" if healthy)
+int comm_rccl_ranks(int id);             // ncclCommCount of the RCCL communicator (0: none)
 void comm_destroy(int id);
 
 }  // namespace pgdist_rt

@@ -21,16 +21,17 @@ def _resolve_backend(backend: str, device: torch.device) -> str:
 
 def build_bench_step(model_name: str, batch_size: int, device: torch.device, backend: str = "auto",
                      img_size: int = 224, use_graph: bool = True, world_size: int = 1, rank: int = 0,
-                     side_stream: bool = True, fp8: bool = False):
+                     side_stream: bool = True, fp8: bool = False, bn_broadcast: bool = False):
     backend = _resolve_backend(backend, device)
     if backend == "hip":
         from .native_step import NativeTrainStep
         # use_graph: 0 eager, 1 whole step in one hipGraph, 2 forward in a hipGraph + eager backward
         step = NativeTrainStep.for_benchmark(model_name, batch_size, device, img_size=img_size,
                                              use_graph=int(use_graph) == 1, world_size=world_size, rank=rank,
-                                             side_stream=side_stream, fp8=fp8, graph_forward=int(use_graph) == 2)
+                                             side_stream=side_stream, fp8=fp8, graph_forward=int(use_graph) == 2,
+                                             bn_broadcast=bn_broadcast)
         graph = "forward" if step.graph_forward else step.graph_enabled
-        meta = {"backend": "hip", "graph": graph, "side_stream": side_stream, "fp8": fp8}
+        meta = {"backend": "hip", "graph": graph, "side_stream": side_stream, "fp8": fp8, "_step": step}
         red = step.reducer
         if red is not None:
             meta["allreduce"] = {
@@ -46,10 +47,10 @@ def build_bench_step(model_name: str, batch_size: int, device: torch.device, bac
         return step.bench_step, meta
     if fp8:
         raise NotImplementedError("fp8 runs on the native (hip) backend")
-    return _torch_bench_step(model_name, batch_size, device, img_size, world_size, rank)
+    return _torch_bench_step(model_name, batch_size, device, img_size, world_size, rank, bn_broadcast)
 
 
-def _torch_bench_step(model_name, batch_size, device, img_size, world_size, rank):
+def _torch_bench_step(model_name, batch_size, device, img_size, world_size, rank, bn_broadcast=False):
     torch.manual_seed(42 + rank)
     n_data = 4096
     imgs_np, labels_np = synthetic_cifar(n_data, seed=rank)
@@ -64,7 +65,7 @@ def _torch_bench_step(model_name, batch_size, device, img_size, world_size, rank
     ddp = model
     if world_size > 1:
         ddp = torch.nn.parallel.DistributedDataParallel(
-            model, device_ids=[device.index] if device.type == "cuda" else None)
+            model, device_ids=[device.index] if device.type == "cuda" else None, broadcast_buffers=bn_broadcast)
     opt = torch.optim.Adam(model.parameters(), lr=1e-4, fused=device.type == "cuda")
     crit = torch.nn.CrossEntropyLoss()
     amp_dtype = torch.bfloat16
@@ -89,4 +90,4 @@ def _torch_bench_step(model_name, batch_size, device, img_size, world_size, rank
         opt.step()
         return loss
 
-    return step, {"backend": "torch", "graph": False}
+    return step, {"backend": "torch", "graph": False, "_params": list(model.parameters())}

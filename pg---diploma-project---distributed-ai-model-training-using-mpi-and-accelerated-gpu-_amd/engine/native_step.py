@@ -182,7 +182,8 @@ class NativeTrainStep:
     # ------------------------------------------------------------------ setup
     @classmethod
     def for_benchmark(cls, model_name: str, batch: int, device, img_size=224, use_graph=True,
-                      world_size=1, rank=0, n_data=50000, side_stream=True, fp8=False, graph_forward=False):
+                      world_size=1, rank=0, n_data=50000, side_stream=True, fp8=False, graph_forward=False,
+                      bn_broadcast=False):
         if model_name not in ("mobilenet_v2", "resnet50"):
             raise NotImplementedError(f"native executors: mobilenet_v2, resnet50 (not {model_name}); "
                                       "use --backend torch")
@@ -200,7 +201,8 @@ class NativeTrainStep:
             src = torch.randint(0, 256, (n_data, 32, 32, 3), dtype=torch.uint8, device=device, generator=g)
             labels = torch.randint(0, 10, (n_data,), dtype=torch.int64, device=device, generator=g)
         st = cls(model, batch, device, img_size=img_size, world_size=world_size, rank=rank,
-                 use_graph=use_graph, seed=42, side_stream=side_stream, fp8=fp8, graph_forward=graph_forward)
+                 use_graph=use_graph, seed=42, side_stream=side_stream, fp8=fp8, graph_forward=graph_forward,
+                 bn_broadcast=bn_broadcast)
         st.set_data(src, labels)
         st._perm = torch.randperm(n_data, device=device, generator=g)
         st._pos = 0
@@ -272,7 +274,8 @@ class NativeTrainStep:
                       epoch_ctr=0, out_hw=self.S)
         if self.bn_broadcast:
             if self.comm is not None:   # native: recorded collectives, no Python at replay
-                algo = "rccl" if self.comm.has_rccl else "oneshot"
+                # P2P broadcast (one barrier, all links) when validated, else RCCL
+                algo = "oneshot" if self.comm.has_p2p else "rccl"
                 cur = torch.cuda.current_stream(self.device)
                 self.comm.broadcast(self.bn_flat, 0, algo, wait=[cur])
                 self.comm.broadcast(self.bn_nbt.view(torch.float32), 0, algo, wait=[cur])

@@ -288,6 +288,12 @@ class Trainer:
             lr = step_lr(self.base_lr, epoch, cfg.step_size, cfg.gamma)
             self.set_lr(lr)
             tl, tc, tn = self.train_epoch(epoch)
+            # native communicator health, once per epoch on every rank (collective): a peer
+            # timeout, an out-of-step peer or an RCCL error on ANY rank raises on EVERY rank
+            # instead of training on with un-reduced gradients
+            comm = getattr(self.step, "comm", None) if self.backend == "hip" else None
+            if comm is not None:
+                comm.check_all()
             g_tl, g_tn, g_tc = all_reduce_scalars([tl, tn, tc], self.device)
             train_loss = g_tl / max(g_tn, 1)
             train_acc_local = tc / max(tn, 1)
@@ -358,6 +364,11 @@ class Trainer:
                f"{'identical' if ok_p else 'DIFFER'} (digest {int(dp[0]):x}), BN buffers "
                f"{'identical' if ok_b else 'DIFFER'} (digest {int(db[0]):x}, bn_sync={self.cfg.bn_sync})",
                self.rank)
+        # the verdict is the same on every rank (MIN == MAX of the digests), so every rank raises
+        bn_synced = self.cfg.bn_sync in ("eval", "broadcast") and bool(self.cfg.eval_every)
+        if not ok_p or (bn_synced and not ok_b):
+            raise RuntimeError(f"data-parallel replicas diverged over {self.world} ranks: parameters "
+                               f"{'identical' if ok_p else 'DIFFER'}, BN buffers {'identical' if ok_b else 'DIFFER'}")
 
     # ------------------------------------------------------------------ checkpoint/resume
     def _adam_step(self) -> int:

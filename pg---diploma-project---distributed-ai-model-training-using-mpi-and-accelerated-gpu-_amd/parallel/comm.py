@@ -31,6 +31,10 @@ ALGO_NAMES = {v: k for k, v in ALGOS.items()}
 _SEQ = itertools.count()
 
 
+class CommError(RuntimeError):
+    """A native collective failed (peer timeout, out-of-step peer, RCCL error)."""
+
+
 def _stream_handle(s) -> int:
     return s.cuda_stream if hasattr(s, "cuda_stream") else int(s)
 
@@ -169,13 +173,42 @@ class NativeComm:
         return lib().comm_time_allreduce(self.id, _ptrs(bufs), n, a, bool(bf16_wire), int(iters))
 
     def error(self) -> int:
-        """0, or P2P barrier-timeout bits | RCCL async error << 8 (synchronises the comm stream)."""
+        """0, or this rank's error code: P2P error-word bits (1 peer timeout, 2 peer out of step,
+        4 poisoned) | RCCL async error << 8 | 1 << 16 for a synchronous RCCL failure.  Nonzero
+        poisons the communicator: every later collective raises (synchronises the comm stream)."""
         return lib().comm_error(self.id)
 
+    def error_string(self) -> str:
+        return lib().comm_error_string(self.id)
+
     def check(self):
+        """Raise if THIS rank's communicator failed (local check, no collective)."""
         e = self.error()
         if e:
-            raise RuntimeError(f"native communicator error 0x{e:x} (P2P barrier timeout bits | RCCL error << 8)")
+            raise CommError(f"native communicator error 0x{e:x} on rank {self.rank}: {self.error_string()}")
+
+    def check_all(self, group=None) -> int:
+        """Collective health check (every rank must call it): this rank's error code is
+        all-reduced (MAX) over the default process group, so a failure on ANY rank raises
+        :class:`CommError` on EVERY rank — no rank is left waiting in a later collective for a
+        peer that aborted.  Returns 0 when every rank is healthy."""
+        e = self.error()
+        if self.world > 1 and not self.emulated and dist.is_available() and dist.is_initialized():
+            t = host_allreduce(torch.tensor([float(e), float(self.rank if e else -1)], dtype=torch.float64),
+                               dist.ReduceOp.MAX)
+            worst, who = int(t[0].item()), int(t[1].item())
+        else:
+            worst, who = e, self.rank
+        if worst:
+            mine = f"; this rank: {self.error_string() or 'healthy'}"
+            if not e:   # a peer failed: this rank's communicator is unusable too
+                lib().comm_poison(self.id, f"rank {who} failed with error 0x{worst:x}")
+            raise CommError(f"native communicator failed (error 0x{worst:x}, reported by rank {who}){mine}")
+        return 0
+
+    def rccl_ranks(self) -> int:
+        """Ranks of the RCCL communicator (ncclCommCount), 0 without one."""
+        return lib().comm_rccl_ranks(self.id) if self.has_rccl else 0
 
     def close(self):
         if self.id is not None:
@@ -227,12 +260,17 @@ class NativeComm:
                         self.allreduce(t, algo, bf)
                         self.join()
                         torch.cuda.synchronize(self.device)
-                        ok = self.error() == 0 and torch.equal(t, expect)
+                        err = self.error()
+                        if err:
+                            self.p2p_error = f"error 0x{err:x}: {self.error_string()}"
+                        ok = err == 0 and torch.equal(t, expect)
                     except Exception as e:   # noqa: BLE001 - reported, then P2P is off everywhere
                         self.p2p_error = repr(e)
                         ok = False
                     if not self._agree(ok):
                         self.has_p2p = False
+                        # every rank abandons P2P: un-poison so the RCCL path stays usable
+                        lib().comm_clear_error(self.id)
                         return False
         finally:
             self.set_timeout(keep)

@@ -184,6 +184,13 @@ class NativeBucketReducer(BucketedGradReducer):
             if comm.region > 0 and comm.world > 1 and not comm.validate_p2p():
                 print(f"[pgdist] P2P all-reduce unavailable or failed validation ({comm.p2p_error}): RCCL only",
                       flush=True)
+            if bf16_wire and comm.world > 1 and not comm.has_p2p:
+                if not comm.has_rccl:
+                    raise RuntimeError("bf16 gradient wire format: neither the P2P path nor RCCL is available")
+                # the bf16 wire is a P2P-kernel option; RCCL reduces fp32 (same result up to the
+                # bf16 rounding of the summands; twice the bytes)
+                print("[pgdist] bf16 gradient wire needs the P2P path: reducing fp32 over RCCL instead", flush=True)
+                bf16_wire = self.bf16_wire = False
             choice = comm.autotune(sizes, bf16_wire=bf16_wire) if comm.world > 1 else {}
             self.algos = [choice.get(sz, "rccl" if comm.has_rccl else "oneshot") for sz in sizes]
         else:

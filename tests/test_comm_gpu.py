@@ -157,6 +157,110 @@ def test_p2p_missing_peer_times_out_instead_of_hanging():
     assert res[1] == 0
 
 
+def _mixed_worker(rank, world, port, q):
+    """one communicator, per-bucket one-shot / two-shot all-reduces of different sizes
+    (fp32 and bf16 wire) interleaved with P2P broadcasts, back to back with NO host sync in
+    between (the even/odd staging halves and the two-shot region are reused across kernels),
+    for several 'steps'; every result checked afterwards."""
+    import pgdist  # noqa: F401
+    from pgdist.parallel.comm import NativeComm
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    c = NativeComm.for_process_group(dev, use_rccl=False, p2p_bytes=1 << 22, blocks=16, timeout_s=10.0)
+    plan = [("broadcast", 4096 + 4, False), ("oneshot", 424976, False), ("twoshot", 393216 + 8, False),
+            ("oneshot", 8, True), ("twoshot", 1 << 20, True), ("broadcast", 136, False), ("twoshot", 65536, False)]
+    checks = []
+    for stp in range(4):
+        for k, (algo, n, bf16) in enumerate(plan):
+            xs = [torch.randn(n, device=dev, generator=torch.Generator(device=dev).manual_seed(7919 * stp + 97 * k + p))
+                  for p in range(world)]
+            t = xs[rank].clone()
+            if algo == "broadcast":
+                root = (stp + k) % world
+                c.broadcast(t, root, "oneshot")
+                want = xs[root]
+            else:
+                c.allreduce(t, algo, bf16)
+                want = _expect(xs, bf16)
+            checks.append((stp, algo, n, bf16, t, want))
+    c.join()
+    torch.cuda.synchronize()
+    err = c.error()
+    bad = [(s_, a, n, bf) for s_, a, n, bf, t, w in checks if not torch.equal(t, w)]
+    dist.barrier()
+    c.close()
+    q.put(("ok", rank, err, bad))
+    dist.destroy_process_group()
+
+
+def test_p2p_mixed_algorithms_interleaved_two_processes():
+    world, port = 2, free_port()
+    for _, rank, err, bad in run_ranks(_mixed_worker, world, (world, port), expect=world, timeout=300):
+        assert err == 0, f"rank {rank}: error word {err}"
+        assert not bad, f"rank {rank}: wrong results for {bad}"
+
+
+def _fault_worker(rank, world, port, mode, q):
+    """A data-parallel 'training' sequence (per step: BN-buffer broadcast + 3 gradient buckets of
+    different sizes and algorithms) where rank 1 misbehaves at step 2: ``skip`` (issues none of
+    that step's collectives) or ``size`` (all-reduces a bucket of the wrong size).  Every rank
+    then runs the collective health check, which must raise on EVERY rank (within the timeout,
+    no hang), and the poisoned communicator must refuse later collectives."""
+    import time
+    import pgdist  # noqa: F401
+    from pgdist.parallel.comm import CommError, NativeComm
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    c = NativeComm.for_process_group(dev, use_rccl=False, p2p_bytes=1 << 22, blocks=8, timeout_s=3.0)
+    bn = torch.zeros(1024, device=dev)
+    grads = [torch.ones(n, device=dev) for n in (65536, 262144, 4096)]
+    t0 = time.time()
+    for stp in range(5):
+        if mode == "skip" and rank == 1 and stp == 2:
+            continue
+        c.broadcast(bn, 0, "oneshot")
+        for k, g in enumerate(grads):
+            if mode == "size" and rank == 1 and stp == 2 and k == 1:
+                c.allreduce(g[:131072], "twoshot")
+            else:
+                c.allreduce(g, "oneshot" if k != 1 else "twoshot")
+    c.join()
+    torch.cuda.synchronize()
+    raised, msg = False, ""
+    try:
+        c.check_all()
+    except CommError as e:
+        raised, msg = True, str(e)
+    refused = False
+    try:
+        c.allreduce(grads[0], "oneshot")
+    except Exception:   # noqa: BLE001 - the poisoned communicator refuses
+        refused = True
+    elapsed = time.time() - t0
+    dist.barrier()
+    c.close()
+    q.put(("ok", rank, raised, msg, refused, elapsed))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["skip", "size"])
+def test_p2p_out_of_step_rank_fails_every_rank(mode):
+    world, port = 2, free_port()
+    res = run_ranks(_fault_worker, world, (world, port, mode), expect=world, timeout=300)
+    for _, rank, raised, msg, refused, elapsed in res:
+        assert raised, f"rank {rank}: the health check did not raise ({mode})"
+        assert "native communicator failed" in msg
+        assert elapsed < 60, f"rank {rank}: detection took {elapsed:.1f} s"
+    # every rank's communicator is poisoned: later collectives are refused
+    assert all(refused for *_, refused, _ in res)
+
+
 def test_rccl_world1_collectives_and_join(dev):
     from pgdist.ops._lib import lib
     from pgdist.parallel.comm import NativeComm
