@@ -204,6 +204,8 @@ def main():
                        "allreduce": meta.get("allreduce")},
         }
         out.update(health)
+        if world > 1 and device.type == "cuda" and info.local_world_size > torch.cuda.device_count():
+            out["rehearsal_on_one_gpu"] = True   # ranks share a GPU: not an N-GPU measurement
         print(json.dumps(out), flush=True)
     cleanup()
     if not healthy:

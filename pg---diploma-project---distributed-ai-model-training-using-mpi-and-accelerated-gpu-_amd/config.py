@@ -34,7 +34,7 @@ class TrainConfig:
     gamma: float = 0.1
     scale_lr: bool = False                    # linear LR scaling with world size (off = reference)
     # data
-    data: str = "cifar10"                     # cifar10 | synthetic
+    data: str = "cifar10"                     # cifar10 | synthetic | synthetic-hard
     data_root: str = "./data"
     synthetic_train_size: int = 50000
     synthetic_test_size: int = 10000

@@ -12,9 +12,22 @@
 // a*G + b*Y + c) is applied once per element while staging A.  Workgroup ids
 // put the N tiles of an M tile 8 ids apart (same XCD, dispatched together) so
 // the A tile is fetched from HBM once into that XCD's L2.
+//
+// Split-K (the 7x7 / 14x14 layers with K = 384 .. 1280): one output tile is a chain of
+// K / KSTEP dependent load -> MFMA steps (15-20 at K = 960 / 1280), so on ~300 workgroups
+// the kernel is latency-bound (0.6-1.3 TB/s, profiles/r3c_roofline_mnv2.txt).  With
+// p.sk = SK > 1 the K steps of a tile are split over SK workgroups (ids 8 apart: same XCD);
+// each writes its fp32 accumulator fragments to a workspace slab with write-through (sc1)
+// stores, drains them, and takes a ticket on the tile's counter; the workgroup whose ticket
+// is last sums the SK slabs in split order 0..SK-1 (fixed order: bitwise independent of
+// arrival order) with sc1 loads and runs the fused epilogue; the others only join the BN
+// finalize tail.  Hand-off: MI355X_MICROARCH.md "Valid forms" table, row 1 (every store and
+// load of the slab sc1, each storing wave's vmcnt(0) before the workgroup barrier, one lane's
+// returning agent-scope add, the re-arm by the last arriver).
 #include "../bnfin.h"
 
 #include <cstdlib>
+#include <map>
 
 enum { PRO_BNBWD_T = 3, PRO_BNRES_T = 5 };
 enum { EPI_FWD_T = 0, EPI_BWD_RELU6_T = 1, EPI_BWD_LIN_T = 2 };
@@ -39,7 +52,12 @@ struct PwTArgs {
   int bn_rep;           // BN-statistics replica rows (g_bn_rep)
   const BnFin *fin;     // fused BN finalize in the tail (nullptr: none)
   const BnFin *lz;      // lazy finalize of the prologue parameters (nullptr: materialised pa/pb/pc)
+  int sk;               // K splits per output tile (1: none)
+  float *skbuf;         // [tiles][sk][256][RT*CTW*4] fp32 accumulator slabs (sk > 1)
+  int *skctr;           // [tiles] arrival tickets, 0 between launches (re-armed by the last arriver)
 };
+
+constexpr int kSc1 = 16;   // buffer cache policy bit sc1: agent-coherent (L2 write-through / L1 bypass)
 }  // namespace
 
 // KSTEP: k per pipeline step (32, or 64 for long K: half the steps / barriers, twice the
@@ -75,22 +93,30 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
   const int wm = wave >> 1, wn = wave & 1;
   const int NT = (p.N + BN - 1) / BN;
   const int nmt = (p.M + BM - 1) / BM;
-  // workgroup -> (mt, nt): the NT tiles of one M tile are 8 ids apart (same XCD)
-  int mt, nt;
+  const int SK = p.sk;
+  // workgroup -> (mt, nt, split): the NT x SK workgroups of one M tile are 8 ids apart (same XCD)
+  int mt, nt, ksplit;
   {
-    const int L = blockIdx.x, full = (nmt / 8) * 8 * NT;
+    const int NTS = NT * SK;
+    const int L = blockIdx.x, full = (nmt / 8) * 8 * NTS;
+    int j;
     if (L < full) {
-      mt = (L / (8 * NT)) * 8 + L % 8;
-      nt = (L / 8) % NT;
+      mt = (L / (8 * NTS)) * 8 + L % 8;
+      j = (L / 8) % NTS;
     } else {
       const int rem = nmt % 8, Lr = L - full;
       mt = (nmt / 8) * 8 + Lr % rem;
-      nt = Lr / rem;
+      j = Lr / rem;
     }
+    nt = j / SK;
+    ksplit = j - nt * SK;
   }
   const int m0 = mt * BM, n0 = nt * BN;
   const int Kp = (p.K + KSTEP - 1) / KSTEP * KSTEP;
-  const int nk = Kp / KSTEP;
+  const int nk_all = Kp / KSTEP;
+  const int kper = (nk_all + SK - 1) / SK;
+  const int kb = ksplit * kper;                          // this split's k steps [kb, ke)
+  const int ke = kb + kper < nk_all ? kb + kper : nk_all;
 
   if constexpr (NPAR > 0) {
     for (int i = tid; i < Kp; i += 256) {
@@ -207,13 +233,13 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
 #pragma unroll
     for (int c = 0; c < CTW; ++c) acc[r][c] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  load(0, true);
+  load(kb * KSTEP, kb < ke);
   __syncthreads();   // Ps staged
-  write(0, 0);
+  write(0, kb * KSTEP);
   __syncthreads();
-  for (int ks = 0; ks < nk; ++ks) {
-    const int buf = ks & 1;
-    load((ks + 1) * KSTEP, ks + 1 < nk);
+  for (int ks = kb; ks < ke; ++ks) {
+    const int buf = (ks - kb) & 1;
+    load((ks + 1) * KSTEP, ks + 1 < ke);
     const bf16_t *Ab = As + buf * BM * kLDK;
     const bf16_t *Bb = Bs + buf * BN * kLDK;
 #pragma unroll
@@ -250,10 +276,64 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
                                                               __builtin_bit_cast(bf16x8_t, bf), acc[r][c], 0, 0, 0);
       }
     }
-    if (ks + 1 < nk) write(buf ^ 1, (ks + 1) * KSTEP);
+    if (ks + 1 < ke) write(buf ^ 1, (ks + 1) * KSTEP);
     __syncthreads();
   }
 
+  // ---- split-K: publish this split's accumulators; the last arriver of the tile sums them
+  __shared__ int s_last;
+  if (SK > 1) {
+    constexpr int NF = RT * CTW;                           // f32x4 fragments per thread
+    const int tile = mt * NT + nt;
+    const rsrc_t rS = make_rsrc(p.skbuf, 0x7fffffffu);
+    const uint32_t mine = (uint32_t)((((size_t)tile * SK + ksplit) * 256 + tid) * NF * 16);
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int c = 0; c < CTW; ++c) {
+        u32x4_t v;
+        v.x = __float_as_uint(acc[r][c][0]);
+        v.y = __float_as_uint(acc[r][c][1]);
+        v.z = __float_as_uint(acc[r][c][2]);
+        v.w = __float_as_uint(acc[r][c][3]);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rS, (int)(mine + (r * CTW + c) * 16), 0, kSc1);
+      }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // this wave's slab stores are done
+    __syncthreads();
+    if (tid == 0) {
+      g_int *ctr = (g_int *)(p.skctr + tile);
+      const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = old == SK - 1;
+      if (s_last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (s_last) {
+      f32x4_t tot[RT][CTW];
+#pragma unroll
+      for (int q = 0; q < SK; ++q) {                       // fixed order 0..SK-1
+        const uint32_t base = (uint32_t)((((size_t)tile * SK + q) * 256 + tid) * NF * 16);
+#pragma unroll
+        for (int r = 0; r < RT; ++r)
+#pragma unroll
+          for (int c = 0; c < CTW; ++c) {
+            f32x4_t v = acc[r][c];
+            if (q != ksplit) {
+              const u32x4_t u = __builtin_amdgcn_raw_buffer_load_b128(rS, (int)(base + (r * CTW + c) * 16), 0, kSc1);
+              v = f32x4_t{__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w)};
+            }
+            tot[r][c] = q == 0 ? v : tot[r][c] + v;
+          }
+      }
+#pragma unroll
+      for (int r = 0; r < RT; ++r)
+#pragma unroll
+        for (int c = 0; c < CTW; ++c) acc[r][c] = tot[r][c];
+    }
+  } else {
+    s_last = 1;
+  }
+
+  if (s_last) {   // workgroup-uniform
   // ---- epilogue: bf16 C tile in LDS, then 16-B row chunks (same contract as pw_gemm_kernel)
 #pragma unroll
   for (int c = 0; c < CTW; ++c) {
@@ -334,6 +414,7 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
     }
     __syncthreads();
   }
+  }   // s_last
   bn_fin_tail(p.fin);
 }
 
@@ -342,9 +423,37 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
 // ===========================================================================
 namespace {
 struct TileGeom {
-  int BM, BN, KS, nmt, nt;
+  int BM, BN, KS, nmt, nt, sk;
   size_t lds;
 };
+
+// split-K workspace of one stream (launches on a stream are serialised, so one slab set and
+// one ticket array per stream serve every layer); allocated once, at the first launch, with
+// the counters zeroed; a launch that would not fit runs unsplit
+constexpr size_t kSkBufBytes = 48ull << 20;
+constexpr int kSkTiles = 16384;
+struct SkWs {
+  float *buf = nullptr;
+  int *ctr = nullptr;
+  bool tried = false;
+};
+SkWs &sk_ws(hipStream_t st) {
+  static auto *m = new std::map<hipStream_t, SkWs>();
+  SkWs &w = (*m)[st];
+  if (!w.tried) {
+    w.tried = true;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone &&
+        hipMalloc(reinterpret_cast<void **>(&w.buf), kSkBufBytes) == hipSuccess &&
+        hipMalloc(reinterpret_cast<void **>(&w.ctr), kSkTiles * sizeof(int)) == hipSuccess &&
+        hipMemset(w.ctr, 0, kSkTiles * sizeof(int)) == hipSuccess && hipDeviceSynchronize() == hipSuccess)
+      return w;
+    w.buf = nullptr;
+    w.ctr = nullptr;
+    (void)hipGetLastError();
+  }
+  return w;
+}
 TileGeom tile_geom(int M, int N, int K, int pro) {
   TileGeom g{};
   // largest tile that still gives >= 384 workgroups (~1.5 per CU), else the smallest
@@ -361,6 +470,15 @@ TileGeom tile_geom(int M, int N, int K, int pro) {
   g.nt = (N + g.BN - 1) / g.BN;
   static const int k64 = [] { const char *e = getenv("PGDIST_TILE_K64"); return e ? atoi(e) : 256; }();
   g.KS = K >= k64 ? 64 : 32;
+  // split-K: double SK while the grid is under ~4 workgroups per CU and every split keeps >= 2
+  // k steps (PGDIST_PW_SPLITK: 0 off, else the grid-size target)
+  static const int sk_target = [] { const char *e = getenv("PGDIST_PW_SPLITK"); return e ? atoi(e) : 1024; }();
+  const int nk = (K + g.KS - 1) / g.KS;
+  const long long tiles = (long long)g.nmt * g.nt;
+  g.sk = 1;
+  while (sk_target > 0 && g.sk < 8 && tiles * g.sk < sk_target && nk >= 4 * g.sk &&
+         tiles * g.sk * 2 * g.BM * g.BN * 4 <= (long long)kSkBufBytes && tiles <= kSkTiles)
+    g.sk *= 2;
   const int npar = pro == ACT_NONE ? 0 : (pro == PRO_BNBWD_T ? 3 : 2);
   const size_t kp = (size_t)((K + g.KS - 1) / g.KS * g.KS);
   const size_t ops = (size_t)2 * (g.BM + g.BN) * (g.KS + 8) * 2;
@@ -373,9 +491,19 @@ TileGeom tile_geom(int M, int N, int K, int pro) {
 }
 
 template <int PRO, int EPI, int BM, int BN, bool F8>
-void launch_tile_t(const PwTArgs &a, const TileGeom &g, hipStream_t st) {
-  if (g.KS == 64) hipLaunchKernelGGL((pw_tile_kernel<PRO, EPI, BM, BN, 64, F8>), dim3(g.nmt * g.nt), dim3(256), g.lds, st, a);
-  else hipLaunchKernelGGL((pw_tile_kernel<PRO, EPI, BM, BN, 32, F8>), dim3(g.nmt * g.nt), dim3(256), g.lds, st, a);
+void launch_tile_t(PwTArgs a, const TileGeom &g, hipStream_t st) {
+  a.sk = 1;
+  if (g.sk > 1) {
+    SkWs &w = sk_ws(st);
+    if (w.buf) {
+      a.sk = g.sk;
+      a.skbuf = w.buf;
+      a.skctr = w.ctr;
+    }
+  }
+  const dim3 grid(g.nmt * g.nt * a.sk);
+  if (g.KS == 64) hipLaunchKernelGGL((pw_tile_kernel<PRO, EPI, BM, BN, 64, F8>), grid, dim3(256), g.lds, st, a);
+  else hipLaunchKernelGGL((pw_tile_kernel<PRO, EPI, BM, BN, 32, F8>), grid, dim3(256), g.lds, st, a);
 }
 
 template <int PRO, int EPI, bool F8 = false>

@@ -100,4 +100,9 @@ def load_dataset(name: str, root: str, train: bool, synthetic_size: Optional[int
         n = synthetic_size or (50000 if train else 10000)
         imgs, labels = synthetic_cifar(n, seed=seed + (0 if train else 1))
         return CIFAR10Arrays(imgs, labels)
+    if name == "synthetic-hard":   # weak, spatially spread class signal + 10 % label noise
+        from .synthetic import synthetic_cifar_hard
+        n = synthetic_size or (50000 if train else 10000)
+        imgs, labels = synthetic_cifar_hard(n, seed=seed, split="train" if train else "test")
+        return CIFAR10Arrays(imgs, labels)
     raise ValueError(f"unknown dataset {name!r}")

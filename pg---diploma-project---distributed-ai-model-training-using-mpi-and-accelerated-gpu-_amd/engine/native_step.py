@@ -92,6 +92,11 @@ class NativeTrainStep:
         self.src = None
         self.src_labels = None
         self.epoch_ctr = 0
+        # fault injection (tests of the end-to-end evidence): the gradients of
+        # the named parameters (PGDIST_FAULT_ZERO_GRAD, comma-separated) are zeroed after every
+        # backward, i.e. a planted "broken weight gradient" bug whose effect a run must expose
+        names = [x for x in os.environ.get("PGDIST_FAULT_ZERO_GRAD", "").split(",") if x]
+        self.fault_zero = [self.flat.range_of(n) for n in names]
         # ---- data parallel
         # PGDIST_COMM: auto (native communicator when the process group is RCCL's, c10d with gloo)
         # | rccl | p2p (IPC xGMI kernels only; also over a gloo default group) | native (both) | c10d
@@ -308,6 +313,8 @@ class NativeTrainStep:
             self.reducer.finish()
         elif self.reducer is not None:
             K.plan_py(self.reducer.finish)
+        for a, b in self.fault_zero:
+            K.memset(self.flat.grad[a:b])
         K.adam_flat(self.flat.master, self.flat.grad, self.flat.exp_avg, self.flat.exp_avg_sq,
                     self.flat.shadow, self.hyper, self.betas[0], self.betas[1], self.eps, self.wd,
                     1.0 / self.world)

@@ -277,6 +277,41 @@ def test_pw_fwd(dev, M, K_, N, pro):
     assert rel(st[1], (ref * ref).sum(0)) < 1e-2
 
 
+@pytest.mark.parametrize("M,K_,N,epi", [(6272, 960, 160, K.EPI_FWD), (6272, 1280, 320, K.EPI_BWD_LIN),
+                                        (25088, 576, 96, K.EPI_FWD), (1111, 1216, 200, K.EPI_BWD_RELU6)])
+def test_pw_splitk_bitwise_repeatable(dev, M, K_, N, epi):
+    """Small-M / long-K GEMMs split K over workgroups (pwtile.hip split-K): the last arriver sums
+    the fp32 slabs in split order, so repeated launches (different arrival orders) are bitwise
+    equal, the ticket counters re-arm (a second launch on the same workspace is correct), and the
+    result matches the fp32 reference."""
+    A = bf(rnd(M, K_, dev=dev, seed=M))
+    W = bf(rnd(N, K_, dev=dev, seed=5) / math.sqrt(K_))
+    P = K.pw_num_partials(M, N, K_)
+    outs, parts = [], []
+    for _ in range(3):
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        part = torch.zeros(P * 2 * N, device=dev)
+        if epi == K.EPI_FWD:
+            K.pw_gemm(K.ACT_NONE, epi, A, W, out, part, M, N, K_)
+        else:
+            ones, zeros = torch.ones(K_, device=dev), torch.zeros(K_, device=dev)
+            Yt = bf(rnd(M, N, dev=dev, seed=6))
+            es, et = torch.ones(N, device=dev), torch.full((N,), 3.0, device=dev)
+            K.pw_gemm(K.PRO_BNBWD, epi, A, W, out, part, M, N, K_, A2=A, pa=ones, pb=zeros, pc=zeros,
+                      Yt=Yt, es=es, et=et, R=torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
+                      if epi == K.EPI_BWD_LIN else None)
+        outs.append(out)
+        parts.append(part)
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+    ref = A.float() @ W.float().t()
+    if epi == K.EPI_BWD_RELU6:
+        a = Yt.float() + 3.0
+        ref = ref * ((a > 0) & (a < 6)).float()
+    assert rel(outs[0], ref) < 8e-3
+
+
 def e4m3(x):
     """fp32 -> OCP e4m3fn (saturating) -> fp32, PyTorch's conversion as the reference."""
     return x.clamp(-448.0, 448.0).to(torch.float8_e4m3fn).float()
