@@ -466,45 +466,47 @@ constexpr int kWLD = kWMK + 8;        // transposed tile row pitch (elements): 1
 // bf16 operand; it is loaded raw into registers one step ahead (prefetch) and
 // written transposed into LDS as T[col][m] (4 rows of m packed per 8-B store)
 // after the current step's MFMAs, with the BN transform applied on the way.
+// Loads are bounds-checked buffer loads issued unconditionally (rows past M / columns past
+// ncols read 0 through the out-of-range offset): no branch around a memory instruction, so
+// hipcc does not drain the one-step-ahead prefetch with a vmcnt(0) at a join.
 struct WgItem {
   uint4 a[4];   // rows of G (dy items) or X (x items)
   uint4 b[4];   // rows of Y (dy items only)
 };
 
 template <bool DY>
-PG_DEVICE void wg_load(WgItem &it, const bf16_t *__restrict__ src, const bf16_t *__restrict__ src2,
-                       int ld, int ncols, int c, int m0, int M) {
+PG_DEVICE void wg_load(WgItem &it, rsrc_t r1, rsrc_t r2, int ld, int ncols, int c, int m0, int M) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int m = m0 + q;
-    if (m < M && c < ncols) {
-      const size_t off = (size_t)m * ld + c;
-      it.a[q] = ldg16(src + off);
-      if constexpr (DY) it.b[q] = ldg16(src2 + off);
-    } else {
-      it.a[q] = make_uint4(0, 0, 0, 0);
-      if constexpr (DY) it.b[q] = make_uint4(0, 0, 0, 0);
-    }
+    const uint32_t off = (m < M && c < ncols) ? (uint32_t)(((size_t)m * ld + c) * 2) : kOOB;
+    it.a[q] = bld16(r1, off);
+    if constexpr (DY) it.b[q] = bld16(r2, off);
   }
 }
 
-// rows beyond M or columns beyond ncols must contribute exactly 0 after the transform
+// rows beyond M must contribute exactly 0 after the transform (columns beyond ncols read 0 and
+// have zero parameters).  P: this item's 8 per-column parameters (a | b | c, stride ldp) in LDS,
+// staged once per workgroup (loop-invariant: the former per-step global loads of pa / pb / pc
+// were 16-24 dword loads per item per step behind branches).
 template <int PRO>
-PG_DEVICE void wg_write(const WgItem &it, const float *pa, const float *pb, const float *pc, int ncols,
-                        int c, int m0, int M, bf16_t *T, int tcol, int tm) {
+PG_DEVICE void wg_write(const WgItem &it, const float *P, int ldp, int m0, int M, bf16_t *T, int tcol, int tm) {
   float v[4][8];
   float aa[8], bb[8], cc[8];
-  const bool cvalid = c < ncols;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    aa[j] = (PRO != ACT_NONE && cvalid) ? pa[c + j] : 0.f;
-    bb[j] = (PRO != ACT_NONE && cvalid) ? pb[c + j] : 0.f;
-    cc[j] = (PRO == PRO_BNBWD && cvalid) ? pc[c + j] : 0.f;
+  if constexpr (PRO != ACT_NONE) {
+    const float4 a0 = *reinterpret_cast<const float4 *>(P), a1 = *reinterpret_cast<const float4 *>(P + 4);
+    const float4 b0 = *reinterpret_cast<const float4 *>(P + ldp), b1 = *reinterpret_cast<const float4 *>(P + ldp + 4);
+    aa[0] = a0.x; aa[1] = a0.y; aa[2] = a0.z; aa[3] = a0.w; aa[4] = a1.x; aa[5] = a1.y; aa[6] = a1.z; aa[7] = a1.w;
+    bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w; bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
+  }
+  if constexpr (PRO == PRO_BNBWD) {
+    const float4 c0 = *reinterpret_cast<const float4 *>(P + 2 * ldp), c1 = *reinterpret_cast<const float4 *>(P + 2 * ldp + 4);
+    cc[0] = c0.x; cc[1] = c0.y; cc[2] = c0.z; cc[3] = c0.w; cc[4] = c1.x; cc[5] = c1.y; cc[6] = c1.z; cc[7] = c1.w;
   }
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     unpack8(it.a[q], v[q]);
-    const bool valid = (m0 + q < M) && cvalid;
+    const bool valid = m0 + q < M;
     if constexpr (PRO == PRO_BNBWD) {
       float y[8];
       unpack8(it.b[q], y);
@@ -557,11 +559,30 @@ __global__ __launch_bounds__(256) void pw_wgrad_kernel(PwWgArgs p) {
   constexpr int IPT = (ITEMS + 255) / 256;           // items per thread
   __shared__ __attribute__((aligned(16))) bf16_t Tdy[2][TN * kWLD];
   __shared__ __attribute__((aligned(16))) bf16_t Tx[2][TK * kWLD];
+  __shared__ __attribute__((aligned(16))) float Pdy[3 * TN];   // a | b | c of this tile's columns n
+  __shared__ __attribute__((aligned(16))) float Px[2 * TK];    // s | t of this tile's columns k
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave >> 1, wk = wave & 1;
   const int n0 = blockIdx.x * TN, k0 = blockIdx.y * TK;
   const int mbeg = blockIdx.z * p.rows_per_split;
   const int mend = min(p.M, mbeg + p.rows_per_split);
+  for (int i = tid; i < TN; i += 256) {
+    const bool ok = n0 + i < p.N;
+    Pdy[i] = ok ? p.ga[n0 + i] : 0.f;
+    Pdy[TN + i] = ok ? p.gb[n0 + i] : 0.f;
+    Pdy[2 * TN + i] = ok ? p.gc[n0 + i] : 0.f;
+  }
+  if constexpr (XPRO == ACT_BN_RELU6) {
+    for (int i = tid; i < TK; i += 256) {
+      const bool ok = k0 + i < p.K;
+      Px[i] = ok ? p.xs[k0 + i] : 0.f;
+      Px[TK + i] = ok ? p.xt[k0 + i] : 0.f;
+    }
+  }
+  const rsrc_t rG = make_rsrc(p.G, (uint32_t)((size_t)p.M * p.N * 2));
+  const rsrc_t rY = make_rsrc(p.Y, (uint32_t)((size_t)p.M * p.N * 2));
+  const rsrc_t rX = make_rsrc(p.X, XPRO == IM2COL_STEM ? 0u : (uint32_t)((size_t)p.M * p.K * 2));
+  __syncthreads();
 
   f32x4_t acc[RN][RK];
 #pragma unroll
@@ -576,12 +597,12 @@ __global__ __launch_bounds__(256) void pw_wgrad_kernel(PwWgArgs p) {
       const int it = tid + i * 256;
       if (it < ITEMS_DY) {
         const int m4 = it % M4, chunk = it / M4;
-        wg_load<true>(items[i], p.G, p.Y, p.N, p.N, n0 + chunk * 8, m0 + m4 * 4, mend);
+        wg_load<true>(items[i], rG, rY, p.N, p.N, n0 + chunk * 8, m0 + m4 * 4, mend);
       } else if (it < ITEMS) {
         const int xi = it - ITEMS_DY;
         const int m4 = xi % M4, chunk = xi / M4;
         if constexpr (XPRO == IM2COL_STEM) wg_load_im2col(items[i], p, chunk, m0 + m4 * 4, mend);
-        else wg_load<false>(items[i], p.X, nullptr, p.K, p.K, k0 + chunk * 8, m0 + m4 * 4, mend);
+        else wg_load<false>(items[i], rX, rX, p.K, p.K, k0 + chunk * 8, m0 + m4 * 4, mend);
       }
     }
   };
@@ -591,17 +612,14 @@ __global__ __launch_bounds__(256) void pw_wgrad_kernel(PwWgArgs p) {
       const int it = tid + i * 256;
       if (it < ITEMS_DY) {
         const int m4 = it % M4, chunk = it / M4;
-        wg_write<PRO_BNBWD>(items[i], p.ga, p.gb, p.gc, p.N, n0 + chunk * 8, m0 + m4 * 4, mend, Tdy[buf],
-                            chunk * 8, m4 * 4);
+        wg_write<PRO_BNBWD>(items[i], Pdy + chunk * 8, TN, m0 + m4 * 4, mend, Tdy[buf], chunk * 8, m4 * 4);
       } else if (it < ITEMS) {
         const int xi = it - ITEMS_DY;
         const int m4 = xi % M4, chunk = xi / M4;
         if constexpr (XPRO == IM2COL_STEM)
-          wg_write<ACT_NONE>(items[i], nullptr, nullptr, nullptr, 36, chunk * 8 < 36 ? 0 : 36, m0 + m4 * 4,
-                             mend, Tx[buf], chunk * 8, m4 * 4);
+          wg_write<ACT_NONE>(items[i], nullptr, 0, m0 + m4 * 4, mend, Tx[buf], chunk * 8, m4 * 4);
         else
-          wg_write<XPRO>(items[i], p.xs, p.xt, nullptr, p.K, k0 + chunk * 8, m0 + m4 * 4, mend, Tx[buf],
-                         chunk * 8, m4 * 4);
+          wg_write<XPRO>(items[i], Px + chunk * 8, TK, m0 + m4 * 4, mend, Tx[buf], chunk * 8, m4 * 4);
       }
     }
   };
@@ -921,11 +939,21 @@ void launch_stem_wgrad(const bf16_t *G, const bf16_t *Y, const float *ga, const 
   hipLaunchKernelGGL(stem_wgrad_permute_kernel, dim3((O * 27 + 255) / 256), dim3(256), 0, st, tmp, grad, O);
 }
 
+bool pw_wgrad_dma_supported(int N, int K);
+void launch_pw_wgrad_dma(const bf16_t *G, const bf16_t *Y, const float *ga, const float *gb, const float *gc,
+                         const bf16_t *X, const float *xs, const float *xt, int xact, float *part, int M, int N,
+                         int K, int rps, int S, hipStream_t st);
+
 void launch_pw_wgrad(const bf16_t *G, const bf16_t *Y, const float *ga, const float *gb,
                      const float *gc, const bf16_t *X, const float *xs, const float *xt, int xact,
                      float *part, float *grad, int M, int N, int K, hipStream_t st) {
   int TN, TK, S, rps;
   wgrad_geom(M, N, K, TN, TK, S, rps);
+  if (pw_wgrad_dma_supported(N, K)) {   // LDS-DMA ring (pwwgrad.hip), same split geometry / partials
+    launch_pw_wgrad_dma(G, Y, ga, gb, gc, X, xs, xt, xact, part, M, N, K, rps, S, st);
+    launch_wgrad_reduce(part, S, (long long)N * K, grad, st);
+    return;
+  }
   PwWgArgs a{G, Y, ga, gb, gc, X, xs, xt, part, M, N, K, rps, 0, 0, 0, 0};
   if (xact == ACT_BN_RELU6) launch_wg_x<ACT_BN_RELU6>(a, TN, TK, S, st);
   else launch_wg_x<ACT_NONE>(a, TN, TK, S, st);

@@ -97,6 +97,8 @@ class NativeTrainStep:
         # backward, i.e. a planted "broken weight gradient" bug whose effect a run must expose
         names = [x for x in os.environ.get("PGDIST_FAULT_ZERO_GRAD", "").split(",") if x]
         self.fault_zero = [self.flat.range_of(n) for n in names]
+        self.main_stream = (torch.cuda.Stream(device, priority=-1)
+                            if device.type == "cuda" and os.environ.get("PGDIST_MAIN_PRIO", "0") == "1" else None)
         # ---- data parallel
         # PGDIST_COMM: auto (native communicator when the process group is RCCL's, c10d with gloo)
         # | rccl | p2p (IPC xGMI kernels only; also over a gloo default group) | native (both) | c10d
@@ -321,6 +323,19 @@ class NativeTrainStep:
         K.reduce_metrics(exe.loss, exe.correct, self.B, self.metrics)
 
     def run(self, idx: torch.Tensor, next_idx: Optional[torch.Tensor] = None):
+        """One training step (on the high-priority critical-path stream when PGDIST_MAIN_PRIO=1:
+        the hardware queue arbiter then dispatches its workgroups ahead of the weight-gradient
+        side stream's; the caller's stream is joined on both sides)."""
+        ms = self.main_stream
+        if ms is None:
+            return self._run(idx, next_idx)
+        cur = torch.cuda.current_stream(self.device)
+        ms.wait_stream(cur)
+        with torch.cuda.stream(ms):
+            self._run(idx, next_idx)
+        cur.wait_stream(ms)
+
+    def _run(self, idx: torch.Tensor, next_idx: Optional[torch.Tensor] = None):
         """One training step on the batch ``src[idx]`` (idx: int64 [B] on device).  With
         ``next_idx`` (the next step's full batch) and prefetch enabled, that batch is augmented
         during this step's backward on the side stream (the next ``run`` then ignores its idx
