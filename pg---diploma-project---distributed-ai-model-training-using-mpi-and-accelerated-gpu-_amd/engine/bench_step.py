@@ -39,7 +39,10 @@ def build_bench_step(model_name: str, batch_size: int, device: torch.device, bac
                 "buckets_kib": [round((e - s) * 4 / 1024, 1) for s, e, _ in red.buckets],
                 "algos": list(getattr(red, "algos", ["c10d"] * len(red.buckets))),
                 "launch_plan": bool(step.use_plan),
+                "bucket_cap_mb": getattr(red, "bucket_cap_mb", None),
             }
+            if getattr(red, "bucket_tuning", None):
+                meta["allreduce"]["bucket_cost_us"] = red.bucket_tuning
             tuning = getattr(step.comm, "tuning", None) if step.comm is not None else None
             if tuning:
                 meta["allreduce"]["tuned_us"] = {str(k): {a: round(v, 1) for a, v in d.items()}

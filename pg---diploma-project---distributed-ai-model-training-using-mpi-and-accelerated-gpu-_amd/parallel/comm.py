@@ -277,15 +277,16 @@ class NativeComm:
         return True
 
     def autotune(self, sizes: Sequence[int], candidates: Optional[Sequence[str]] = None, bf16_wire=False,
-                 iters: int = 10) -> Dict[int, str]:
+                 iters: int = 10, measure: bool = False) -> Dict[int, str]:
         """Fastest algorithm per all-reduce size (elements), by the MAX over ranks of the measured
-        time, identical on every rank."""
+        time, identical on every rank (``self.tuning``: the times; with a single candidate they
+        are measured only when ``measure``)."""
         cands = [c for c in (candidates or self.available_algos()) if c in self.available_algos()]
         if bf16_wire:
             cands = [c for c in cands if c != "rccl"]
         if not cands:
             raise RuntimeError("autotune: no algorithm available")
-        if len(cands) == 1:
+        if len(cands) == 1 and not measure:
             return {int(s): cands[0] for s in sizes}
         uniq = sorted({int(s) for s in sizes})
         scratch = torch.zeros(max(uniq), dtype=torch.float32, device=self.device)

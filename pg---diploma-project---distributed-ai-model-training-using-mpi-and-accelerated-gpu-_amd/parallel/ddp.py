@@ -24,6 +24,7 @@ Re-design for MI355X:
 
 The same class works with the ``gloo`` backend on CPU (multi-process tests).
 """
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -69,9 +70,13 @@ class BucketedGradReducer:
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.reduce_dtype = reduce_dtype
-        self.buckets = build_buckets(ranges, int(bucket_cap_mb * 2 ** 20), int(first_bucket_mb * 2 ** 20))
+        self.bucket_cap_mb = float(bucket_cap_mb)
+        self._set_buckets(build_buckets(ranges, int(bucket_cap_mb * 2 ** 20), int(first_bucket_mb * 2 ** 20)))
+
+    def _set_buckets(self, buckets):
         # a bucket covers [start, end) of the flat buffer; extend the last bucket to the
         # buffer end so alignment padding is reduced too (it is zero on every rank)
+        self.buckets = buckets
         self.owner: Dict[str, int] = {}
         for bi, (_, _, names) in enumerate(self.buckets):
             for n in names:
@@ -81,9 +86,9 @@ class BucketedGradReducer:
         self._ready = [False] * len(self.buckets)
         self._works = []
         self._casts = {}
-        if reduce_dtype != torch.float32:
+        if self.reduce_dtype != torch.float32:
             for bi, (s, e, _) in enumerate(self.buckets):
-                self._casts[bi] = torch.empty(e - s, dtype=reduce_dtype, device=flat_grad.device)
+                self._casts[bi] = torch.empty(e - s, dtype=self.reduce_dtype, device=self.grad.device)
 
     @property
     def enabled(self) -> bool:
@@ -165,21 +170,17 @@ class NativeBucketReducer(BucketedGradReducer):
     def __init__(self, comm, flat_grad: torch.Tensor, ranges: Sequence[Tuple[str, int, int]],
                  bucket_cap_mb: Optional[float] = None, first_bucket_mb: float = 1.0, algo: str = "auto",
                  bf16_wire: bool = False, force: bool = False):
+        tune_cap = bucket_cap_mb is None
         super().__init__(flat_grad, ranges, bucket_cap_mb, first_bucket_mb)
         self.comm = comm
         self.world = comm.world
         self.force = force   # run the bucket collectives even at world size 1 (tests)
         self.side = None     # the executor's side stream (weight-gradient producers)
         self.bf16_wire = bf16_wire
-        # P2P kernels take multiples of 8 elements: bucket ends move to the next 64-element
-        # boundary (flat-buffer alignment padding, zero on every rank), the last to the end
-        n = flat_grad.numel()
-        b2 = []
-        for i, (s, e, names) in enumerate(self.buckets):
-            e = n if i == len(self.buckets) - 1 else min(n, (e + 63) // 64 * 64)
-            b2.append((s, e, names))
-        self.buckets = b2
+        self._ranges, self._first_mb = list(ranges), first_bucket_mb
+        self._set_buckets(self._aligned(self.buckets))
         sizes = [e - s for s, e, _ in self.buckets]
+        self.bucket_tuning = None
         if algo == "auto":
             if comm.region > 0 and comm.world > 1 and not comm.validate_p2p():
                 print(f"[pgdist] P2P all-reduce unavailable or failed validation ({comm.p2p_error}): RCCL only",
@@ -191,12 +192,42 @@ class NativeBucketReducer(BucketedGradReducer):
                 # bf16 rounding of the summands; twice the bytes)
                 print("[pgdist] bf16 gradient wire needs the P2P path: reducing fp32 over RCCL instead", flush=True)
                 bf16_wire = self.bf16_wire = False
+            if comm.world > 1 and tune_cap and os.environ.get("PGDIST_BUCKET_TUNE", "1") == "1":
+                self._tune_bucket_cap(bf16_wire)
+                sizes = [e - s for s, e, _ in self.buckets]
             choice = comm.autotune(sizes, bf16_wire=bf16_wire) if comm.world > 1 else {}
             self.algos = [choice.get(sz, "rccl" if comm.has_rccl else "oneshot") for sz in sizes]
         else:
             self.algos = [algo] * len(sizes)
         if bf16_wire and "rccl" in self.algos:
             raise ValueError("bf16 wire format: P2P algorithms only")
+
+    def _aligned(self, buckets):
+        """P2P kernels take multiples of 8 elements: bucket ends move to the next 64-element
+        boundary (flat-buffer alignment padding, zero on every rank), the last to the end."""
+        n = self.grad.numel()
+        return [(s, n if i == len(buckets) - 1 else min(n, (e + 63) // 64 * 64), names)
+                for i, (s, e, names) in enumerate(buckets)]
+
+    def _tune_bucket_cap(self, bf16_wire: bool):
+        """Bucket size from measurements on this node (the cap was a heuristic).
+        Candidate caps 0.5 .. 32 MiB (the first bucket keeps ``first_bucket_mb``); every bucket
+        size of every candidate is timed with every algorithm (NativeComm.autotune: MAX over ranks,
+        so every rank scores identically) and a candidate costs the sum of its buckets' best
+        all-reduce times plus its LAST bucket's time once more (that one is exposed after the
+        backward; the others overlap it).  The cheapest candidate wins."""
+        grad_mb = self.grad.numel() * 4 / 2 ** 20
+        caps = sorted({c for c in (0.5, 1.0, 2.0, 4.0, 8.0, 16.0, 32.0, self.bucket_cap_mb) if c <= 2 * grad_mb})
+        cands = {c: self._aligned(build_buckets(self._ranges, int(c * 2 ** 20), int(self._first_mb * 2 ** 20)))
+                 for c in caps}
+        sizes = sorted({e - s for b in cands.values() for s, e, _ in b})
+        self.comm.autotune(sizes, bf16_wire=bf16_wire, iters=5, measure=True)
+        best = {sz: min(t.values()) for sz, t in self.comm.tuning.items()}
+        cost = {c: sum(best[e - s] for s, e, _ in b) + best[b[-1][1] - b[-1][0]] for c, b in cands.items()}
+        cap = min(cost, key=lambda c: (cost[c], c))
+        self.bucket_tuning = {str(c): round(v, 1) for c, v in cost.items()}
+        self.bucket_cap_mb = cap
+        self._set_buckets(cands[cap])
 
     @property
     def enabled(self) -> bool:

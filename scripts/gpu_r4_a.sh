@@ -10,7 +10,7 @@ ab() {
   env "$@" timeout -k 10 200 python -u bench.py --steps 40 --warmup 10 > $O/ab.json 2> $O/ab.err || { tail -20 $O/ab.err; exit 1; }
   python -c "import json; d=json.load(open('$O/ab.json')); print('$t', d['ms_per_step'], d['value'])"
 }
-for i in 1 2; do ab new X=1; ab nosplitk PGDIST_PW_SPLITK=0; ab nodma PGDIST_PWWG_DMA=0; ab prio PGDIST_MAIN_PRIO=1; done
+for i in 1 2; do ab new X=1; ab nosplitk PGDIST_PW_SPLITK=0; ab nodma PGDIST_PWWG_DMA=0; ab prio PGDIST_MAIN_PRIO=1; ab wgs512 PGDIST_PWWG_WGS=512; ab narrow PGDIST_PWWG_DMA_WIDE=0; done
 timeout -k 10 600 python -u -m pytest tests/test_comm_gpu.py tests/test_bench_gpu.py -x -v --timeout 300 --timeout-method thread > $O/pytest_comm.log 2>&1
 rc=$?; grep -E "PASS|FAIL|ERROR" $O/pytest_comm.log | tail -40; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python -u -m pytest tests/test_executor_gpu.py tests/test_ddp_gpu.py -x -q --timeout 300 --timeout-method thread > $O/pytest_exe.log 2>&1

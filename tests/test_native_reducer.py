@@ -19,8 +19,10 @@ class FakeComm:
         self.log.append(("validate",))
         return self.has_p2p
 
-    def autotune(self, sizes, bf16_wire=False):
+    def autotune(self, sizes, bf16_wire=False, iters=10, measure=False):
         self.tuned = list(sizes)
+        # latency-dominated model: 20 us per call + 1 us per 64 KiB
+        self.tuning = {s: {"rccl": 20.0 + s * 4 / 65536, "oneshot": 30.0 + s * 4 / 16384} for s in sizes}
         return {s: ("oneshot" if s * 4 <= 64 * 1024 else "rccl") for s in sizes}
 
     def allreduce(self, t, algo, bf16, wait=()):
@@ -96,3 +98,27 @@ def test_world1_reducer_only_runs_when_forced(monkeypatch):
     red.mark_ready([r[0] for r in ranges])
     red.finish()
     assert [x[0] for x in comm.log] == ["ar"] * len(red.buckets) + ["join"]
+
+
+def test_bucket_cap_tuned_from_measured_times(monkeypatch):
+    """bucket_cap_mb=None: candidate caps are scored by the measured all-reduce times (sum of
+    the buckets' best times + the exposed last bucket) and the cheapest wins; with a
+    latency-dominated cost model the choice is neither the smallest nor the largest cap."""
+    monkeypatch.setattr(torch.cuda, "current_stream", _FakeStreamModule.current_stream)
+    big, o = [], 0
+    for i in range(30):                                                # ~ 1.7e7 elements (~66 MB)
+        n_i = 200000 * (1 + i % 5) + (i % 3)
+        big.append((f"p{i}", o, o + n_i))
+        o = (o + n_i + 63) // 64 * 64
+    n = o
+    comm = FakeComm()
+    red = NativeBucketReducer(comm, torch.zeros(n), big, bucket_cap_mb=None, first_bucket_mb=1.0)
+    assert red.bucket_tuning and len(red.bucket_tuning) >= 4
+    costs = {float(c): v for c, v in red.bucket_tuning.items()}
+    assert costs[red.bucket_cap_mb] == min(costs.values())
+    assert min(costs) < red.bucket_cap_mb < max(costs)
+    prev = 0
+    for s, e, _ in red.buckets:
+        assert s == prev and s % 64 == 0
+        prev = e
+    assert prev == n
