@@ -470,9 +470,12 @@ TileGeom tile_geom(int M, int N, int K, int pro) {
   g.nt = (N + g.BN - 1) / g.BN;
   static const int k64 = [] { const char *e = getenv("PGDIST_TILE_K64"); return e ? atoi(e) : 256; }();
   g.KS = K >= k64 ? 64 : 32;
-  // split-K: double SK while the grid is under ~4 workgroups per CU and every split keeps >= 2
-  // k steps (PGDIST_PW_SPLITK: 0 off, else the grid-size target)
-  static const int sk_target = [] { const char *e = getenv("PGDIST_PW_SPLITK"); return e ? atoi(e) : 1024; }();
+  // split-K (opt-in, PGDIST_PW_SPLITK = grid-size target, e.g. 1024): double SK while the grid is
+  // under the target and every split keeps >= 2 k steps.  Measured OFF by default: MobileNetV2
+  // bs128 5.30 ms/step with it vs 4.70 without (same box, profiles/r4_ab_splitk_dma.txt) -- the
+  // fp32 slab traffic (8-10x the bf16 output of these small-M GEMMs, written through to memory
+  // and read back across XCDs) costs more than the shorter k chains save.
+  static const int sk_target = [] { const char *e = getenv("PGDIST_PW_SPLITK"); return e ? atoi(e) : 0; }();
   const int nk = (K + g.KS - 1) / g.KS;
   const long long tiles = (long long)g.nmt * g.nt;
   g.sk = 1;

@@ -262,8 +262,13 @@ __global__ __launch_bounds__(256) void pw_wgrad_dma_kernel(PwWgDmaArgs p, int gx
 // tiles: 128 wide for dimensions above 64 (fewer re-reads and re-transforms), else 64;
 // ring depth 3 (two stages in flight, one barrier per stage).  Returns false (caller keeps the
 // register-staged kernel) for shapes outside the DMA contract.
+// Opt-in (PGDIST_PWWG_DMA=1): measured SLOWER than the register-staged kernel on every MobileNetV2
+// shape (profiles/r4_roofline_pwwg_dma.txt: 22 launches 677 us at 128-wide tiles, 627 us at 64-wide,
+// vs 548 us; bench 4.71 vs 4.64-4.65 ms/step): with 4-8 stages per split the ring never reaches
+// steady state, and the per-fragment BN transforms (done once per (k tile, wave column) here instead
+// of once per element) cost more VALU than the staging they replace.
 bool pw_wgrad_dma_supported(int N, int K) {
-  static const int on = [] { const char *e = getenv("PGDIST_PWWG_DMA"); return e ? atoi(e) : 1; }();
+  static const int on = [] { const char *e = getenv("PGDIST_PWWG_DMA"); return e ? atoi(e) : 0; }();
   return on && N >= 64 && K >= 64 && N % 8 == 0 && K % 8 == 0;
 }
 
