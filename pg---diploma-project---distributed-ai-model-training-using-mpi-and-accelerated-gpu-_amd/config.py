@@ -38,6 +38,7 @@ class TrainConfig:
     data_root: str = "./data"
     synthetic_train_size: int = 50000
     synthetic_test_size: int = 10000
+    synthetic_signal: Optional[float] = None  # synthetic-hard: class-template strength (None: generator default)
     augment: str = "gpu"                      # gpu (fused HIP kernel) | torch (reference-semantics torch ops) | none
     num_workers: int = 2
     # execution

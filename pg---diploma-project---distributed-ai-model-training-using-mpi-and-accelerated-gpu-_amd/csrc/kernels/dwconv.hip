@@ -253,6 +253,21 @@ __global__ __launch_bounds__(256) void dw_fwd_lds_kernel(
   const int lcol = active ? col * S : 0;            // segment column of tap 0 (clamped when inactive)
   const rsrc_t ry = make_rsrc(y, (uint32_t)g.B * g.Ho * g.Wo * g.C * 2);
 
+
+  const int oh_end = min(tl.r0 + g.R, g.Ho);
+  const int j0 = tl.r0 * S - 1;                     // input rows j0 .. j0 + nrows - 1
+  const int nrows = (oh_end - 1) * S + 1 - j0 + 1;
+  const int iw0 = ow * S - 1;
+  // column validity of the 3 taps (rows are checked per step)
+  bool cok[3];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) cok[d] = active && iw0 + d >= 0 && iw0 + d < g.W;
+  Stream sx;
+  sx.init(make_rsrc(x, (uint32_t)g.B * g.H * g.W * g.C * 2), g.H, g.W, g.C, tl.b, tl.w0 * S - 1,
+          ((g.TWc - 1) * S + 3) * CC8, CC8, cbase);
+#pragma unroll
+  for (int q = 0; q < kDepth; ++q) sx.issue(ring, kSlot, q, j0 + q, dummy);
+  // BN / weight parameters staged while the first kDepth rows are in flight
   float s[CPT], t[CPT], stats[2][CPT], wt[9][CPT];
   const bool lazy = ACT != ACT_NONE && g.lz != nullptr;
   if (lazy) lazy_stage(g, cbase, 2);
@@ -269,21 +284,7 @@ __global__ __launch_bounds__(256) void dw_fwd_lds_kernel(
   }
 #pragma unroll
   for (int q = 0; q < 9; ++q) unpack4(ldg8(w + (size_t)q * g.C + c0), wt[q]);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // parameters in registers before the stream
-
-  const int oh_end = min(tl.r0 + g.R, g.Ho);
-  const int j0 = tl.r0 * S - 1;                     // input rows j0 .. j0 + nrows - 1
-  const int nrows = (oh_end - 1) * S + 1 - j0 + 1;
-  const int iw0 = ow * S - 1;
-  // column validity of the 3 taps (rows are checked per step)
-  bool cok[3];
-#pragma unroll
-  for (int d = 0; d < 3; ++d) cok[d] = active && iw0 + d >= 0 && iw0 + d < g.W;
-  Stream sx;
-  sx.init(make_rsrc(x, (uint32_t)g.B * g.H * g.W * g.C * 2), g.H, g.W, g.C, tl.b, tl.w0 * S - 1,
-          ((g.TWc - 1) * S + 3) * CC8, CC8, cbase);
-#pragma unroll
-  for (int q = 0; q < kDepth; ++q) sx.issue(ring, kSlot, q, j0 + q, dummy);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // parameters in registers (and the first rows in LDS)
   float win[3][3][CPT];   // three input rows x three tap columns (roles rotate with the unroll)
 #pragma unroll
   for (int r = 0; r < 3; ++r)
@@ -388,6 +389,27 @@ __global__ __launch_bounds__(256) PGDIST_DW_DGRAD_ATTR void dw_dgrad_s1_lds_kern
   const uint32_t nbytes = (uint32_t)g.B * g.H * g.W * g.C * 2;   // stride 1: dy grid == input grid
   const rsrc_t ro = make_rsrc(gout, nbytes);
 
+
+  const int ih_end = min(tl.r0 + g.R, g.H);
+  const int j0 = tl.r0 - 1;                         // dy rows j0 .. ih_end (window ih-1..ih+1)
+  const int nrows = ih_end - j0 + 1;
+  bool cok[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) cok[c] = active && iw - 1 + c >= 0 && iw - 1 + c < g.W;
+  Stream sg, sy, sp;
+  sg.init(make_rsrc(gin, nbytes), g.H, g.W, g.C, tl.b, tl.w0 - 1, (g.TWc + 2) * CC8, CC8, cbase);
+  sy = sg;
+  sy.rs = make_rsrc(yself, nbytes);
+  sp.init(make_rsrc(yprev, nbytes), g.H, g.W, g.C, tl.b, tl.w0, g.TWc * CC8, CC8, cbase);
+  auto issue = [&](int slot, int k) {
+    char *base = ring + slot * kStep;
+    sg.issue(base, 0, 0, j0 + k, dummy);
+    sy.issue(base + kSlotHalo, 0, 0, j0 + k, dummy);
+    sp.issue(base + 2 * kSlotHalo, 0, 0, tl.r0 + k - 2, dummy);
+  };
+#pragma unroll
+  for (int q = 0; q < kDepth; ++q) issue(q, q);
+  // BN / weight parameters staged while the first kDepth rows are in flight
   float al[CPT], be[CPT], ga[CPT], s[CPT], t[CPT], stats[2][CPT], wt[9][CPT];
   float accw[WG ? 9 : 1][CPT];
   if (g.lz) lazy_stage(g, cbase, 3);
@@ -410,27 +432,7 @@ __global__ __launch_bounds__(256) PGDIST_DW_DGRAD_ATTR void dw_dgrad_s1_lds_kern
   for (int q = 0; q < (WG ? 9 : 1); ++q) zero4(accw[q]);
 #pragma unroll
   for (int q = 0; q < 9; ++q) unpack4(ldg8(w + (size_t)q * g.C + c0), wt[q]);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-  const int ih_end = min(tl.r0 + g.R, g.H);
-  const int j0 = tl.r0 - 1;                         // dy rows j0 .. ih_end (window ih-1..ih+1)
-  const int nrows = ih_end - j0 + 1;
-  bool cok[3];
-#pragma unroll
-  for (int c = 0; c < 3; ++c) cok[c] = active && iw - 1 + c >= 0 && iw - 1 + c < g.W;
-  Stream sg, sy, sp;
-  sg.init(make_rsrc(gin, nbytes), g.H, g.W, g.C, tl.b, tl.w0 - 1, (g.TWc + 2) * CC8, CC8, cbase);
-  sy = sg;
-  sy.rs = make_rsrc(yself, nbytes);
-  sp.init(make_rsrc(yprev, nbytes), g.H, g.W, g.C, tl.b, tl.w0, g.TWc * CC8, CC8, cbase);
-  auto issue = [&](int slot, int k) {
-    char *base = ring + slot * kStep;
-    sg.issue(base, 0, 0, j0 + k, dummy);
-    sy.issue(base + kSlotHalo, 0, 0, j0 + k, dummy);
-    sp.issue(base + 2 * kSlotHalo, 0, 0, tl.r0 + k - 2, dummy);
-  };
-#pragma unroll
-  for (int q = 0; q < kDepth; ++q) issue(q, q);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // parameters in registers (and the first rows in LDS)
   float win[3][3][CPT];   // three dy rows x three columns iw-1..iw+1 (roles rotate with the unroll)
 #pragma unroll
   for (int r = 0; r < 3; ++r)
@@ -548,6 +550,32 @@ __global__ __launch_bounds__(256) PGDIST_DW_DGRAD_ATTR void dw_dgrad_s2_lds_kern
   const uint32_t nin = (uint32_t)g.B * g.H * g.W * g.C * 2, nout = (uint32_t)g.B * g.Ho * g.Wo * g.C * 2;
   const rsrc_t ro = make_rsrc(gout, nin);
 
+  float accA[WG ? 3 : 1][CPT], accB[WG ? 3 : 1][CPT];
+#pragma unroll
+  for (int r = 0; r < (WG ? 3 : 1); ++r) {
+    zero4(accA[r]);
+    zero4(accB[r]);
+  }
+
+  const int ih_end = min(tl.r0 + g.R, g.H);
+  const int o0 = tl.r0 >> 1;                            // r0 even
+  const int nrows = ((ih_end - 1) >> 1) + 1 - o0 + 1;   // dy rows o0 .. (ih_end-1)/2 + 1
+  Stream sg, sy, sp;
+  sg.init(make_rsrc(gin, nout), g.Ho, g.Wo, g.C, tl.b, dcol0, (dcol1 - dcol0 + 1) * CC8, CC8, cbase);
+  sy = sg;
+  sy.rs = make_rsrc(yself, nout);
+  sp.init(make_rsrc(yprev, nin), g.H, g.W, g.C, tl.b, tl.w0, g.TWc * CC8, CC8, cbase);
+  auto issue = [&](int slot, int k) {
+    char *base = ring + slot * kStep;
+    const int o = o0 + k;
+    sg.issue(base, 0, 0, o, dummy);
+    sy.issue(base + kSlotOwn, 0, 0, o, dummy);
+    sp.issue(base + 2 * kSlotOwn, 0, 0, 2 * (o - 1), dummy);
+    sp.issue(base + 3 * kSlotOwn, 0, 0, 2 * (o - 1) + 1, dummy);
+  };
+#pragma unroll
+  for (int q = 0; q < kDepth; ++q) issue(q, q);
+  // BN / weight parameters staged while the first kDepth rows are in flight
   float al[CPT], be[CPT], ga[CPT], s[CPT], t[CPT], stats[2][CPT];
   if (g.lz) lazy_stage(g, cbase, 3);
 #pragma unroll
@@ -578,32 +606,7 @@ __global__ __launch_bounds__(256) PGDIST_DW_DGRAD_ATTR void dw_dgrad_s2_lds_kern
       wB[r][k] = odd_w ? w2[k] : 0.f;
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  float accA[WG ? 3 : 1][CPT], accB[WG ? 3 : 1][CPT];
-#pragma unroll
-  for (int r = 0; r < (WG ? 3 : 1); ++r) {
-    zero4(accA[r]);
-    zero4(accB[r]);
-  }
-
-  const int ih_end = min(tl.r0 + g.R, g.H);
-  const int o0 = tl.r0 >> 1;                            // r0 even
-  const int nrows = ((ih_end - 1) >> 1) + 1 - o0 + 1;   // dy rows o0 .. (ih_end-1)/2 + 1
-  Stream sg, sy, sp;
-  sg.init(make_rsrc(gin, nout), g.Ho, g.Wo, g.C, tl.b, dcol0, (dcol1 - dcol0 + 1) * CC8, CC8, cbase);
-  sy = sg;
-  sy.rs = make_rsrc(yself, nout);
-  sp.init(make_rsrc(yprev, nin), g.H, g.W, g.C, tl.b, tl.w0, g.TWc * CC8, CC8, cbase);
-  auto issue = [&](int slot, int k) {
-    char *base = ring + slot * kStep;
-    const int o = o0 + k;
-    sg.issue(base, 0, 0, o, dummy);
-    sy.issue(base + kSlotOwn, 0, 0, o, dummy);
-    sp.issue(base + 2 * kSlotOwn, 0, 0, 2 * (o - 1), dummy);
-    sp.issue(base + 3 * kSlotOwn, 0, 0, 2 * (o - 1) + 1, dummy);
-  };
-#pragma unroll
-  for (int q = 0; q < kDepth; ++q) issue(q, q);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // parameters in registers (and the first rows in LDS)
   float dyb[2][2][CPT];   // two dy rows (roles alternate with the unroll) x columns A, B
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
@@ -730,19 +733,6 @@ __global__ __launch_bounds__(256) void dw_wgrad_lds_kernel(
   const int lcol = active ? col * S : 0, lown = active ? col : 0;
   const uint32_t nin = (uint32_t)g.B * g.H * g.W * g.C * 2, nout = (uint32_t)g.B * g.Ho * g.Wo * g.C * 2;
 
-  float al[CPT], be[CPT], ga[CPT], s[CPT], t[CPT];
-  float accw[9][CPT];
-#pragma unroll
-  for (int k = 0; k < CPT; ++k) {
-    al[k] = coef[c0 + k];
-    be[k] = coef[g.C + c0 + k];
-    ga[k] = coef[2 * g.C + c0 + k];
-    s[k] = ps[c0 + k];
-    t[k] = pt[c0 + k];
-  }
-#pragma unroll
-  for (int q = 0; q < 9; ++q) zero4(accw[q]);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const int oh_end = min(tl.r0 + g.R, g.Ho);
   const int j0 = tl.r0 * S - 1;
   const int nrows = (oh_end - 1) * S + 1 - j0 + 1;
@@ -767,6 +757,20 @@ __global__ __launch_bounds__(256) void dw_wgrad_lds_kernel(
   };
 #pragma unroll
   for (int q = 0; q < kDepth; ++q) issue(q, q);
+  // BN / weight parameters staged while the first kDepth rows are in flight
+  float al[CPT], be[CPT], ga[CPT], s[CPT], t[CPT];
+  float accw[9][CPT];
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    al[k] = coef[c0 + k];
+    be[k] = coef[g.C + c0 + k];
+    ga[k] = coef[2 * g.C + c0 + k];
+    s[k] = ps[c0 + k];
+    t[k] = pt[c0 + k];
+  }
+#pragma unroll
+  for (int q = 0; q < 9; ++q) zero4(accw[q]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // parameters in registers (and the first rows in LDS)
   float win[3][3][CPT];
 #pragma unroll
   for (int r = 0; r < 3; ++r)

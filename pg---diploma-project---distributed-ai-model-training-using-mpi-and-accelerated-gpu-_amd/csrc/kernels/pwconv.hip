@@ -163,6 +163,39 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
   float *Cf = reinterpret_cast<float *>(cbase);                                        // [KS][BM][LDF]
   float *Red = reinterpret_cast<float *>(cbase);                                       // [RSTEP][BN] (end)
 
+  using Raw = PwRaw<PRO, SUBS, BDIRECT ? CT : 0>;
+  // Bounds-checked buffer loads, issued unconditionally (masked lanes / the prefetch past the
+  // last tile use an out-of-range offset and read 0): a load behind a branch makes hipcc wait
+  // vmcnt(0) at the join, which drained this one-step-ahead prefetch right after issuing it.
+  const rsrc_t rA = make_rsrc(p.A, (uint32_t)((size_t)p.M * p.K * 2));
+  const rsrc_t rA2 = make_rsrc(HAS_A2 ? p.A2 : p.A, (uint32_t)((size_t)p.M * p.K * 2));
+  const rsrc_t rW = make_rsrc(p.W, (uint32_t)((size_t)p.N * p.K * 2));
+  auto load = [&](Raw &r, int m0, int s, bool valid) {
+#pragma unroll
+    for (int ss = 0; ss < SUBS; ++ss) {
+      const int k = s * KSTEP + ss * 32 + 8 * (lane >> 4);
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {
+        const int row = m0 + rg * 32 + f * 16 + (lane & 15);
+        const bool ok = valid && row < p.M && k < p.K;
+        const uint32_t off = ok ? (uint32_t)(((size_t)row * p.K + k) * 2) : kOOB;
+        r.a[ss][f] = bld16(rA, off);
+        if constexpr (HAS_A2) r.y[ss][f] = bld16(rA2, off);
+      }
+      if constexpr (BDIRECT) {
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+          const int n = n0 + c * 16 + (lane & 15);
+          r.b[ss][c] = bld16(rW, (valid && n < p.N && k < p.K) ? (uint32_t)(((size_t)n * p.K + k) * 2) : kOOB);
+        }
+      }
+    }
+  };
+
+  // the first A fragments are in flight during the weight / prologue-parameter staging below
+  Raw cur, nxt;
+  load(cur, blockIdx.x * BM, kp, blockIdx.x < nmt);
+
   // ---- stage the weight tile (once per workgroup) and the per-k prologue parameters
   if constexpr (F8) {
     const int per_row = Kp / 16;            // W8 rows are zero-padded to ldw8 >= Kp
@@ -215,35 +248,6 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
       et[j] = ncol0 + j < p.N ? p.et[ncol0 + j] : 0.f;
     }
   }
-
-  using Raw = PwRaw<PRO, SUBS, BDIRECT ? CT : 0>;
-  // Bounds-checked buffer loads, issued unconditionally (masked lanes / the prefetch past the
-  // last tile use an out-of-range offset and read 0): a load behind a branch makes hipcc wait
-  // vmcnt(0) at the join, which drained this one-step-ahead prefetch right after issuing it.
-  const rsrc_t rA = make_rsrc(p.A, (uint32_t)((size_t)p.M * p.K * 2));
-  const rsrc_t rA2 = make_rsrc(HAS_A2 ? p.A2 : p.A, (uint32_t)((size_t)p.M * p.K * 2));
-  const rsrc_t rW = make_rsrc(p.W, (uint32_t)((size_t)p.N * p.K * 2));
-  auto load = [&](Raw &r, int m0, int s, bool valid) {
-#pragma unroll
-    for (int ss = 0; ss < SUBS; ++ss) {
-      const int k = s * KSTEP + ss * 32 + 8 * (lane >> 4);
-#pragma unroll
-      for (int f = 0; f < 2; ++f) {
-        const int row = m0 + rg * 32 + f * 16 + (lane & 15);
-        const bool ok = valid && row < p.M && k < p.K;
-        const uint32_t off = ok ? (uint32_t)(((size_t)row * p.K + k) * 2) : kOOB;
-        r.a[ss][f] = bld16(rA, off);
-        if constexpr (HAS_A2) r.y[ss][f] = bld16(rA2, off);
-      }
-      if constexpr (BDIRECT) {
-#pragma unroll
-        for (int c = 0; c < CT; ++c) {
-          const int n = n0 + c * 16 + (lane & 15);
-          r.b[ss][c] = bld16(rW, (valid && n < p.N && k < p.K) ? (uint32_t)(((size_t)n * p.K + k) * 2) : kOOB);
-        }
-      }
-    }
-  };
 
   f32x4_t acc[2][CT];
   int cur_m0 = 0;
@@ -298,8 +302,6 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
   };
 
   // ---- flattened (M tile, k step) stream, prefetching one step ahead (across tiles too)
-  Raw cur, nxt;
-  load(cur, blockIdx.x * BM, kp, blockIdx.x < nmt);
   for (int mt = blockIdx.x; mt < nmt; mt += gridDim.x) {
     const int m0 = mt * BM;
     cur_m0 = m0;

@@ -118,23 +118,6 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
   const int kb = ksplit * kper;                          // this split's k steps [kb, ke)
   const int ke = kb + kper < nk_all ? kb + kper : nk_all;
 
-  if constexpr (NPAR > 0) {
-    for (int i = tid; i < Kp; i += 256) {
-      const bool ok = i < p.K;
-      if (p.lz) {
-        float a = 0.f, b = 0.f, c = 0.f;
-        if (ok) bn_lazy(p.lz, i, a, b, c);
-        Ps[i] = a;
-        Ps[Kp + i] = b;
-        if constexpr (NPAR == 3) Ps[2 * Kp + i] = c;
-      } else {
-        Ps[i] = ok ? p.pa[i] : 0.f;
-        Ps[Kp + i] = ok ? p.pb[i] : 0.f;
-        if constexpr (NPAR == 3) Ps[2 * Kp + i] = ok ? p.pc[i] : 0.f;
-      }
-    }
-  }
-
   constexpr bool HAS_A2 = PRO == PRO_BNBWD_T || PRO == PRO_BNRES_T;
   uint4 ra[ACH], ry[HAS_A2 ? ACH : 1], rb[F8 ? B8PT : BCH];
   // bounds-checked buffer loads issued unconditionally (masked: out-of-range offset, reads 0),
@@ -233,7 +216,23 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
 #pragma unroll
     for (int c = 0; c < CTW; ++c) acc[r][c] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  load(kb * KSTEP, kb < ke);
+  load(kb * KSTEP, kb < ke);   // first operand loads in flight during the prologue-parameter staging
+  if constexpr (NPAR > 0) {
+    for (int i = tid; i < Kp; i += 256) {
+      const bool ok = i < p.K;
+      if (p.lz) {
+        float a = 0.f, b = 0.f, c = 0.f;
+        if (ok) bn_lazy(p.lz, i, a, b, c);
+        Ps[i] = a;
+        Ps[Kp + i] = b;
+        if constexpr (NPAR == 3) Ps[2 * Kp + i] = c;
+      } else {
+        Ps[i] = ok ? p.pa[i] : 0.f;
+        Ps[Kp + i] = ok ? p.pb[i] : 0.f;
+        if constexpr (NPAR == 3) Ps[2 * Kp + i] = ok ? p.pc[i] : 0.f;
+      }
+    }
+  }
   __syncthreads();   // Ps staged
   write(0, kb * KSTEP);
   __syncthreads();

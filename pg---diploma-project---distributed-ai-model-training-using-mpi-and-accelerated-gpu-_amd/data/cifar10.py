@@ -92,7 +92,8 @@ def write_cifar10_bin(path: str, images: np.ndarray, labels: np.ndarray):
     rec.tofile(path)
 
 
-def load_dataset(name: str, root: str, train: bool, synthetic_size: Optional[int] = None, seed: int = 0):
+def load_dataset(name: str, root: str, train: bool, synthetic_size: Optional[int] = None, seed: int = 0,
+                 signal: Optional[float] = None):
     if name == "cifar10":
         return load_cifar10(root, train)
     if name == "synthetic":
@@ -103,6 +104,7 @@ def load_dataset(name: str, root: str, train: bool, synthetic_size: Optional[int
     if name == "synthetic-hard":   # weak, spatially spread class signal + 10 % label noise
         from .synthetic import synthetic_cifar_hard
         n = synthetic_size or (50000 if train else 10000)
-        imgs, labels = synthetic_cifar_hard(n, seed=seed, split="train" if train else "test")
+        kw = {} if signal is None else {"signal": float(signal)}
+        imgs, labels = synthetic_cifar_hard(n, seed=seed, split="train" if train else "test", **kw)
         return CIFAR10Arrays(imgs, labels)
     raise ValueError(f"unknown dataset {name!r}")

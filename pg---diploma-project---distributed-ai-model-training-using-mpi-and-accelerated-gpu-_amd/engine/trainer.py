@@ -84,11 +84,14 @@ class Trainer:
         if self.rank == 0:
             if self.ddp_log and cfg.data == "cifar10":
                 L.emit(L.download_line(), self.rank)
-            self.train_data = load_dataset(cfg.data, cfg.data_root, True, cfg.synthetic_train_size)
+            self.train_data = load_dataset(cfg.data, cfg.data_root, True, cfg.synthetic_train_size,
+                                           signal=cfg.synthetic_signal)
         barrier(self.device if self.device.type == "cuda" else None)
         if self.rank != 0:
-            self.train_data = load_dataset(cfg.data, cfg.data_root, True, cfg.synthetic_train_size)
-        self.test_data = load_dataset(cfg.data, cfg.data_root, False, cfg.synthetic_test_size)
+            self.train_data = load_dataset(cfg.data, cfg.data_root, True, cfg.synthetic_train_size,
+                                           signal=cfg.synthetic_signal)
+        self.test_data = load_dataset(cfg.data, cfg.data_root, False, cfg.synthetic_test_size,
+                                     signal=cfg.synthetic_signal)
         for line in L.samples_lines(len(self.train_data), len(self.test_data)):
             L.emit(line, self.rank)
         self.train_sampler = ShardSampler(len(self.train_data), self.world, self.rank, shuffle=True)

@@ -12,11 +12,12 @@ for s in 1 2; do
     --save-path $O/best_hard_$s.pth > $O/gpu128_hard_${EP}ep_run$s.log 2>&1 || { tail -10 $O/gpu128_hard_${EP}ep_run$s.log; exit 1; }
   grep -E "^Epoch|Best" $O/gpu128_hard_${EP}ep_run$s.log | tail -4
 done
-step planted_bug
-PGDIST_FAULT_ZERO_GRAD=${BUG:-features.18.0.weight,features.17.conv.2.weight,features.16.conv.2.weight} \
-  timeout -k 10 600 python -u train.py --preset gpu128 --data synthetic-hard --epochs $EP --seed 1 \
-  --save-path $O/best_bug.pth > $O/gpu128_hard_${EP}ep_planted_bug.log 2>&1 || { tail -10 $O/gpu128_hard_${EP}ep_planted_bug.log; exit 1; }
-grep -E "^Epoch|Best" $O/gpu128_hard_${EP}ep_planted_bug.log | tail -4
+for bug in features.18.0.weight features.1.conv.0.0.weight; do
+  step planted_bug_$bug
+  PGDIST_FAULT_ZERO_GRAD=$bug timeout -k 10 600 python -u train.py --preset gpu128 --data synthetic-hard --epochs $EP \
+    --seed 1 --save-path $O/best_bug.pth > $O/gpu128_hard_${EP}ep_bug_$bug.log 2>&1 || { tail -10 $O/gpu128_hard_${EP}ep_bug_$bug.log; exit 1; }
+  grep -E "^Epoch|Best" $O/gpu128_hard_${EP}ep_bug_$bug.log | tail -3
+done
 for p in bf16 fp8; do
   step curve_$p
   timeout -k 10 600 python -u train.py --preset gpu128 --data synthetic-hard --epochs ${EP8:-8} --batch-size 512 --precision $p --seed 1 \
