@@ -27,6 +27,7 @@
 #include "../bnfin.h"
 
 #include <cstdlib>
+#include <cstring>
 #include <map>
 
 enum { PRO_BNBWD_T = 3, PRO_BNRES_T = 5 };
@@ -457,12 +458,22 @@ TileGeom tile_geom(int M, int N, int K, int pro) {
   TileGeom g{};
   // largest tile that still gives >= 384 workgroups (~1.5 per CU), else the smallest
   static const int min_wgs = [] { const char *e = getenv("PGDIST_TILE_MINWG"); return e && atoi(e) > 0 ? atoi(e) : 384; }();
-  const int cand[4][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}};
+  static constexpr int cand[4][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}};
   int pick = 3;
   for (int i = 0; i < 4; ++i) {
     const long long wgs = (long long)((M + cand[i][0] - 1) / cand[i][0]) * ((N + cand[i][1] - 1) / cand[i][1]);
     if (wgs >= min_wgs) { pick = i; break; }
   }
+  // PGDIST_TILE_FORCE=<BM>x<BN> (tile sweeps): every launch on that tile
+  static const int force = [] {
+    const char *e = getenv("PGDIST_TILE_FORCE");
+    if (!e) return -1;
+    const int bm = atoi(e), bn = strchr(e, 'x') ? atoi(strchr(e, 'x') + 1) : 0;
+    for (int i = 0; i < 4; ++i)
+      if (bm == cand[i][0] && bn == cand[i][1]) return i;
+    return -1;
+  }();
+  if (force >= 0) pick = force;
   g.BM = cand[pick][0];
   g.BN = cand[pick][1];
   g.nmt = (M + g.BM - 1) / g.BM;
@@ -517,7 +528,8 @@ void launch_tile_pe(const PwTArgs &a, const TileGeom &g, hipStream_t st) {
 }
 }  // namespace
 
-int pw_tile_num_partials(int M, int N, int K) { return tile_geom(M, N, K, ACT_NONE).nmt; }
+// BN partial rows: one per M tile of the smallest tile height any launch may pick (64 rows)
+int pw_tile_num_partials(int M, int N, int K) { return (M + 63) / 64; }
 
 void launch_pw_tile(int pro, int epi, const bf16_t *A, const bf16_t *A2, const float *pa, const float *pb,
                     const float *pc, const bf16_t *W, bf16_t *out, const bf16_t *Yt, const float *es,

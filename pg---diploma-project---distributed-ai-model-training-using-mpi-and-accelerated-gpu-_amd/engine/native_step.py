@@ -93,10 +93,10 @@ class NativeTrainStep:
         self.src_labels = None
         self.epoch_ctr = 0
         # fault injection (tests of the end-to-end evidence): the gradients of
-        # the named parameters (PGDIST_FAULT_ZERO_GRAD, comma-separated) are zeroed after every
-        # backward, i.e. a planted "broken weight gradient" bug whose effect a run must expose
-        names = [x for x in os.environ.get("PGDIST_FAULT_ZERO_GRAD", "").split(",") if x]
-        self.fault_zero = [self.flat.range_of(n) for n in names]
+        # the named parameters (PGDIST_FAULT_ZERO_GRAD, comma-separated names, or @dw / @pw / @bn:
+        # every depthwise / 1x1 conv weight / BatchNorm affine parameter, i.e. a broken kernel
+        # family) are zeroed after every backward: a planted "broken weight gradient" bug
+        self.fault_zero = [self.flat.range_of(n) for n in self._fault_names(model)]
         self.main_stream = (torch.cuda.Stream(device, priority=-1)
                             if device.type == "cuda" and os.environ.get("PGDIST_MAIN_PRIO", "0") == "1" else None)
         # ---- data parallel
@@ -172,6 +172,23 @@ class NativeTrainStep:
             self._labs = [self.exe.labels, torch.empty_like(self.exe.labels)]
             self._idxs = [self.idx, torch.empty_like(self.idx)]
             self._prms = [self.aug_params, torch.empty_like(self.aug_params)]
+
+    @staticmethod
+    def _fault_names(model):
+        out = []
+        params = dict(model.named_parameters())
+        bn = {f"{m}.{k}" for m, mod in model.named_modules() if isinstance(mod, torch.nn.BatchNorm2d)
+              for k in ("weight", "bias")}
+        for tok in [x for x in os.environ.get("PGDIST_FAULT_ZERO_GRAD", "").split(",") if x]:
+            if tok == "@dw":
+                out += [n for n, p in params.items() if p.dim() == 4 and p.shape[1] == 1 and p.shape[2] == 3]
+            elif tok == "@pw":
+                out += [n for n, p in params.items() if p.dim() == 4 and p.shape[2] == 1]
+            elif tok == "@bn":
+                out += [n for n in params if n in bn]
+            else:
+                out.append(tok)
+        return out
 
     def _make_comm(self, mode: str, world_size: int) -> NativeComm:
         """Native communicator of this data-parallel step: RCCL (modes rccl / native) and the P2P
