@@ -473,6 +473,16 @@ TileGeom tile_geom(int M, int N, int K, int pro) {
       if (bm == cand[i][0] && bn == cand[i][1]) return i;
     return -1;
   }();
+  // shape rule (default; PGDIST_TILE_RULE=0: the grid-size heuristic above), from the per-op tile
+  // sweep of the 14x14 / 7x7 MobileNetV2 GEMMs (profiles/r4_pw_tile_sweep.txt):
+  //   N > K (expand-shaped): 128 x 64, or 128 x 128 when N*K >= 300k (1280x320, 960x320);
+  //   N <= K (project / long-K): 64 rows, 128 columns when one tile covers an N of 65..127
+  //   (N = 96), else 64 (N = 64, 160, 320: 64-wide column tiles waste less than 128-wide ones)
+  static const int rule = [] { const char *e = getenv("PGDIST_TILE_RULE"); return e ? atoi(e) : 1; }();
+  if (rule) {
+    if (N > K) pick = (long long)N * K >= 300000 ? 0 : 2;
+    else pick = (N > 64 && N < 128) ? 1 : 3;
+  }
   if (force >= 0) pick = force;
   g.BM = cand[pick][0];
   g.BN = cand[pick][1];
