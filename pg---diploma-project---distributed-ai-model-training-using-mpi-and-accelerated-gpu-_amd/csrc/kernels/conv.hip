@@ -30,6 +30,7 @@
 #include "../common.h"
 
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 namespace {
@@ -1500,13 +1501,23 @@ Geom igemm_geom(int M, int N, int Kmax, int Ci, int ncls) {
   // largest tile that still gives min_wgs workgroups (128 x 128 tiles run at 1.3-1.8x the
   // MFMA rate of the smaller ones on MI355X, so the bar is about one workgroup per CU)
   static const int min_wgs = [] { const char *e = getenv("PGDIST_CONV_MINWG"); return e ? atoi(e) : 256; }();
-  const int cand[4][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}};
+  static constexpr int cand[4][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}};
   int pick = 3;
   for (int i = 0; i < 4; ++i) {
     if (cand[i][1] == 128 && N <= 64) continue;   // no half-empty N tiles
     const long long wgs = (long long)((M + cand[i][0] - 1) / cand[i][0]) * ((N + cand[i][1] - 1) / cand[i][1]) * ncls;
     if (wgs >= min_wgs) { pick = i; break; }
   }
+  // PGDIST_CONV_TILE_FORCE=<BM>x<BN> (tile sweeps): every implicit-GEMM launch on that tile
+  static const int force = [] {
+    const char *e = getenv("PGDIST_CONV_TILE_FORCE");
+    if (!e) return -1;
+    const int bm = atoi(e), bn = strchr(e, 'x') ? atoi(strchr(e, 'x') + 1) : 0;
+    for (int i = 0; i < 4; ++i)
+      if (bm == cand[i][0] && bn == cand[i][1]) return i;
+    return -1;
+  }();
+  if (force >= 0 && !(cand[force][1] == 128 && N <= 64)) pick = force;
   g.BM = cand[pick][0];
   g.BN = cand[pick][1];
   g.nmt = (M + g.BM - 1) / g.BM;
