@@ -530,21 +530,19 @@ PG_DEVICE void wg_write(const WgItem &it, const float *P, int ldp, int m0, int M
 
 // im2col of the stem input (NHWC, 4 channels incl. one zero pad channel, 3x3 s2 p1):
 // X[m][k], m -> (b, oh, ow), k = tap*4 + c, tap = kh*3 + kw;  K = 36.  Item = 4 rows x 2 taps.
-PG_DEVICE void wg_load_im2col(WgItem &it, const PwWgArgs &p, int chunk, int m0, int M) {
+PG_DEVICE void wg_load_im2col(WgItem &it, const PwWgArgs &p, rsrc_t rx, int chunk, int m0, int M) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int m = m0 + q;
     const int b = m / (p.oh * p.ow), rem = m % (p.oh * p.ow);
     const int oh = rem / p.ow, ow = rem % p.ow;
-    uint2 u[2] = {make_uint2(0, 0), make_uint2(0, 0)};
+    uint2 u[2];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < 2; ++h) {   // bounds-checked buffer loads: no branch around the load
       const int tap = chunk * 2 + h;
-      if (m < M && tap < 9) {
-        const int ih = oh * 2 - 1 + tap / 3, iw = ow * 2 - 1 + tap % 3;
-        if (ih >= 0 && ih < p.ih && iw >= 0 && iw < p.iw)
-          u[h] = *reinterpret_cast<const uint2 *>(p.X + (((size_t)b * p.ih + ih) * p.iw + iw) * 4);
-      }
+      const int ih = oh * 2 - 1 + tap / 3, iw = ow * 2 - 1 + tap % 3;
+      const bool ok = m < M && tap < 9 && ih >= 0 && ih < p.ih && iw >= 0 && iw < p.iw;
+      u[h] = bld8(rx, ok ? (uint32_t)((((size_t)b * p.ih + ih) * p.iw + iw) * 8) : kOOB);
     }
     it.a[q] = make_uint4(u[0].x, u[0].y, u[1].x, u[1].y);
   }
@@ -583,7 +581,8 @@ __global__ __launch_bounds__(256) void pw_wgrad_kernel(PwWgArgs p) {
   }
   const rsrc_t rG = make_rsrc(p.G, (uint32_t)((size_t)p.M * p.N * 2));
   const rsrc_t rY = make_rsrc(p.Y, (uint32_t)((size_t)p.M * p.N * 2));
-  const rsrc_t rX = make_rsrc(p.X, XPRO == IM2COL_STEM ? 0u : (uint32_t)((size_t)p.M * p.K * 2));
+  const rsrc_t rX = make_rsrc(p.X, XPRO == IM2COL_STEM ? (uint32_t)((size_t)(p.M / (p.oh * p.ow)) * p.ih * p.iw * 8)
+                                                     : (uint32_t)((size_t)p.M * p.K * 2));
   __syncthreads();
 
   f32x4_t acc[RN][RK];
@@ -603,7 +602,7 @@ __global__ __launch_bounds__(256) void pw_wgrad_kernel(PwWgArgs p) {
       } else if (it < ITEMS) {
         const int xi = it - ITEMS_DY;
         const int m4 = xi % M4, chunk = xi / M4;
-        if constexpr (XPRO == IM2COL_STEM) wg_load_im2col(items[i], p, chunk, m0 + m4 * 4, mend);
+        if constexpr (XPRO == IM2COL_STEM) wg_load_im2col(items[i], p, rX, chunk, m0 + m4 * 4, mend);
         else wg_load<false>(items[i], rX, rX, p.K, p.K, k0 + chunk * 8, m0 + m4 * 4, mend);
       }
     }

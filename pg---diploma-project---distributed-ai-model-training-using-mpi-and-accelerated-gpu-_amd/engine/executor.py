@@ -505,6 +505,14 @@ class MobileNetV2Executor:
         self._check_bn_mode()
         if train:
             K.memset(self.bn_arena)   # every BN statistics accumulator of this step
+        # transposed 1x1 weights for the backward's dgrad GEMMs: on the (idle during the forward)
+        # side stream, off the critical path; the main stream joins it at the end of the forward,
+        # before the step enqueues anything else on the side stream
+        self._wt_pending = train and self.side is not None
+        if self._wt_pending:
+            K.stream_wait(self.side, torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self.side):
+                K.wt_transpose(f.shadow, f.shadow_t, self.wt_tab, self.wt_n)
         if self.fp8:
             K.w8_quant(f.master, self.w8_buf, self.w8_scale, self.w8_tab, self.w8_tab.shape[0])
         # stem
@@ -569,13 +577,18 @@ class MobileNetV2Executor:
                g_out=self.bn_last.g if train else None, part=self.bn_last.acc_b if train else None,
                dW=f.g(self.w_lin) if train else None, db=f.g(self.b_lin) if train else None,
                fin=self.bn_last.fin_b if train else None)
+        if self._wt_pending:
+            K.stream_wait(torch.cuda.current_stream(self.device), self.side)
 
     # ------------------------------------------------------------------ backward
     def backward(self):
         f, B, S = self.flat, self.B, self.S
         self._check_bn_mode()
-        # transposed 1x1 weights for the dgrad GEMMs (one batched launch)
-        K.wt_transpose(f.shadow, f.shadow_t, self.wt_tab, self.wt_n)
+        # transposed 1x1 weights for the dgrad GEMMs (one batched launch; done on the side stream
+        # during a training forward)
+        if not getattr(self, "_wt_pending", False):
+            K.wt_transpose(f.shadow, f.shadow_t, self.wt_tab, self.wt_n)
+        self._wt_pending = False
         self._ready([self.w_lin, self.b_lin])
         # BN of the final conv (g produced by the head kernel)
         bnl = self.bn_last

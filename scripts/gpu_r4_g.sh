@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round 4 G: dgrad weight transposes on the side stream during the forward + branch-free stem
+# wgrad im2col loads: tests, same-box A/B against the previous commit (ab/base)
+cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/r4 && export TMPDIR=/tmp
+O=gpurun_out/r4
+timeout -k 10 600 python -u -m pytest tests/test_kernels_gpu.py tests/test_executor_gpu.py tests/test_executor_teacher_forced_gpu.py tests/test_ddp_gpu.py -x -q --timeout 200 --timeout-method thread > $O/pytest_g.log 2>&1
+rc=$?; tail -2 $O/pytest_g.log; [ $rc -eq 0 ] || { grep -E "FAIL|Error|assert" $O/pytest_g.log | head -30; exit $rc; }
+ab() {
+  t=$1; b=$2
+  timeout -k 10 200 python -u $b --steps 60 --warmup 10 > $O/ab.json 2> $O/ab.err || { tail -20 $O/ab.err; exit 1; }
+  python -c "import json; d=json.load(open('$O/ab.json')); print('$t', d['ms_per_step'], d['value'])"
+}
+for i in 1 2 3; do ab base ab/base/bench.py; ab new bench.py; done
