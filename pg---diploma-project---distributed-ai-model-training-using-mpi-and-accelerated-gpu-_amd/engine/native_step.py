@@ -166,6 +166,10 @@ class NativeTrainStep:
         self.prefetch = (self.use_plan and self.augment_enabled and self.train_augment and self.exe.side is not None
                          and os.environ.get("PGDIST_AUG_PREFETCH", "1") == "1")
         self._cur, self._have, self._next = 0, False, False
+        # PGDIST_AUG_PREFETCH_AT: "backward" (default: beside the weight gradients) | "forward" (beside
+        # this step's forward, where the side stream is otherwise idle: measured 4.556-4.572 vs
+        # 4.553-4.557 ms/step, the augmentation's VALU competes with the bandwidth-bound forward)
+        self.prefetch_in_forward = os.environ.get("PGDIST_AUG_PREFETCH_AT", "backward") == "forward"
         self._plans = {}
         if self.prefetch:
             self._imgs = [self.exe.img, torch.empty_like(self.exe.img)]
@@ -296,6 +300,8 @@ class NativeTrainStep:
                       train=self.train_augment,
                       double_resize=self.double_resize, seed=self.seed + 17 * self.rank, hyper=self.hyper,
                       epoch_ctr=0, out_hw=self.S)
+        if self._next and self.prefetch_in_forward:
+            self._prefetch_next()   # the side stream is otherwise idle during the forward
         if self.bn_broadcast:
             if self.comm is not None:   # native: recorded collectives, no Python at replay
                 # P2P broadcast (one barrier, all links) when validated, else RCCL
@@ -308,19 +314,23 @@ class NativeTrainStep:
                 K.plan_py(lambda: broadcast_parameters([self.bn_flat, self.bn_nbt]))
         exe.forward(train=True)
 
+    def _prefetch_next(self):
+        """Render the next batch into the other buffer on the side stream: after this step's
+        main-stream work so far (the previous step, which last read that buffer, is before it);
+        the backward's final join orders it before the next step's forward."""
+        exe = self.exe
+        nb = 1 - self._cur
+        K.stream_wait(exe.side, torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(exe.side):
+            K.augment(self.src, self._idxs[nb], self.src_labels, self._imgs[nb], self._labs[nb], self._prms[nb],
+                      train=True, double_resize=self.double_resize, seed=self.seed + 17 * self.rank,
+                      hyper=self.hyper, epoch_ctr=AUG_NEXT_STEP, out_hw=self.S)
+
     def _back(self):
         """Backward (+ bucketed all-reduce), Adam and metrics."""
         exe = self.exe
-        if self._next:
-            # render the next batch into the other buffer on the side stream: after this step's
-            # main-stream work so far (the previous step, which last read that buffer, is before it);
-            # the backward's final join orders it before the next step's forward
-            nb = 1 - self._cur
-            K.stream_wait(exe.side, torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(exe.side):
-                K.augment(self.src, self._idxs[nb], self.src_labels, self._imgs[nb], self._labs[nb], self._prms[nb],
-                          train=True, double_resize=self.double_resize, seed=self.seed + 17 * self.rank,
-                          hyper=self.hyper, epoch_ctr=AUG_NEXT_STEP, out_hw=self.S)
+        if self._next and not self.prefetch_in_forward:
+            self._prefetch_next()
         native = getattr(self.reducer, "native", False)
         if native:   # host bookkeeping at record time only; the collectives are native plan ops
             self.reducer.side = exe.side
