@@ -21,6 +21,8 @@
 // distributions, not PIL's intermediate uint8 rounding.
 #include "../common.h"
 
+#include <cstdlib>
+
 namespace {
 constexpr int kNP = 16;  // params per image
 // param slots
@@ -28,14 +30,17 @@ enum { P_I = 0, P_J, P_H, P_W, P_FLIP, P_B, P_C, P_S, P_HUE, P_ORDER, P_ANGLE, P
 // The contrast mean is computed by kMeanSplit workgroups per image; each leaves the partial SUM
 // of its share of the 56x56 grey samples in one slot, the render kernel adds them up.
 constexpr int kMeanSplit = 4;
+constexpr int kMaxS = 512;   // largest output size of the composite-filter render path
 __device__ constexpr int kMeanSlot[kMeanSplit] = {P_MEAN, P_MEAN1, P_MEAN2, P_MEAN3};
 constexpr float kMean[3] = {0.485f, 0.456f, 0.406f};
 constexpr float kStd[3] = {0.229f, 0.224f, 0.225f};
 
+// the per-image draws, precomputed by 64 lanes: u() returns pg_uniform(key, b * 64 + k) for the
+// k-th call (the sampler below consumes at most 10 x 2 + 2 + 1 + 3 + 5 = 31)
 struct Rng {
-  uint64_t key;
-  uint64_t ctr;
-  PG_DEVICE float u() { return pg_uniform(key, ctr++); }
+  const float *d;
+  int k = 0;
+  PG_DEVICE float u() { return d[k++]; }
 };
 
 PG_DEVICE void rgb_to_hsv(float r, float g, float b, float &h, float &s, float &v) {
@@ -150,6 +155,71 @@ PG_DEVICE void jitter(float (&x)[3], const float *prm, float mean, bool stop_bef
   }
 }
 
+// Stage the 32x32x3 uint8 source image into LDS as floats in [0, 1]: 192 lanes x one 16-B load
+// (one round trip) when the image is 16-B aligned, else a byte loop (12 dependent loads per lane
+// in the worst case; the former default, 1/3 of the params kernel and a fixed ~10 us per render
+// workgroup).  C4: 4 floats per pixel (RGB + pad) so a tap is one ds_read_b128.
+template <bool C4>
+PG_DEVICE void stage_image(const unsigned char *__restrict__ src, long long si, float *img) {
+  const int tid = threadIdx.x;
+  const unsigned char *s = src + si * 3072;
+  auto put = [&](int i, float v) {
+    if constexpr (C4) img[(i / 3) * 4 + i % 3] = v;
+    else img[i] = v;
+  };
+  if ((reinterpret_cast<uintptr_t>(s) & 15) == 0) {
+    if (tid < 192) {
+      const uint4 v = reinterpret_cast<const uint4 *>(s)[tid];
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 16; ++q) put(tid * 16 + q, (float)((w[q >> 2] >> (8 * (q & 3))) & 0xffu) * (1.f / 255.f));
+    }
+  } else {
+    for (int i = tid; i < 3072; i += 256) put(i, s[i] * (1.f / 255.f));
+  }
+  if constexpr (C4)
+    if (tid < 256) {   // pad channel of the 1024 pixels: 4 per lane
+#pragma unroll
+      for (int q = 0; q < 4; ++q) img[(tid * 4 + q) * 4 + 3] = 0.f;
+    }
+}
+
+// Composite separable filter of one output coordinate (a column u or a row v of the flipped,
+// crop-resized frame) onto the 32 source pixels of that axis: F(u, v) = sum_ij wy_i(v) wx_j(u)
+// src(ry(v) + i, cx(u) + j).  dbl: the crop is taken from the bilinear RH-upsample of the source
+// (two bilinear maps composed: 4 weights over <= 3 source pixels when 32 / RH <= 1), else
+// directly from the source (2 weights).  Same arithmetic as f_pixel up to rounding order.
+PG_DEVICE void axis_filter(int u, float c0, float cl, int S, int RN, bool dbl, int &base, float (&w)[3]) {
+  w[0] = w[1] = w[2] = 0.f;
+  float xr = fminf(fmaxf(c0 + (u + 0.5f) * (cl / S) - 0.5f, c0), c0 + cl - 1.f);
+  int idx[4];
+  float wt[4];
+  int n;
+  if (!dbl) {
+    xr = fminf(fmaxf(xr, 0.f), 31.f);
+    const int x0 = (int)xr;
+    idx[0] = x0; idx[1] = min(x0 + 1, 31);
+    wt[1] = xr - x0; wt[0] = 1.f - wt[1];
+    n = 2;
+  } else {
+    xr = fminf(fmaxf(xr, 0.f), (float)(RN - 1));
+    const int x0 = (int)xr, x1 = min(x0 + 1, RN - 1);
+    const float fx = xr - x0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int q = h ? x1 : x0;
+      const float x = fminf(fmaxf((q + 0.5f) * (32.f / RN) - 0.5f, 0.f), 31.f);
+      const int s0 = (int)x;
+      const float sf = x - s0, ww = h ? fx : 1.f - fx;
+      idx[2 * h] = s0; idx[2 * h + 1] = min(s0 + 1, 31);
+      wt[2 * h] = ww * (1.f - sf); wt[2 * h + 1] = ww * sf;
+    }
+    n = 4;
+  }
+  base = min(idx[0], 29);
+  for (int k = 0; k < n; ++k) w[idx[k] - base] += wt[k];
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -163,10 +233,15 @@ __global__ __launch_bounds__(256) void augment_params_kernel(
   __shared__ float img[32 * 32 * 3];
   __shared__ float prm[kNP];
   __shared__ float red[4];
+  __shared__ float rnd[64];   // this image's 64 counter-based draws, made in parallel
   const int b = blockIdx.x, split = blockIdx.y, tid = threadIdx.x;
   const long long si = idx[b];
-  for (int i = tid; i < 32 * 32 * 3; i += 256) img[i] = src[si * 3072 + i] * (1.f / 255.f);
+  stage_image<false>(src, si, img);
   const int RH = dbl ? S : 32, RW = dbl ? S : 32;  // image the crop is taken from
+  const unsigned long long step = hyper ? (unsigned long long)hyper[1] : 0ull;
+  const uint64_t key = pg_mix64(seed ^ pg_mix64(step * 0x100000001B3ull + (unsigned long long)epoch_ctr));
+  if (train && !given && tid < 64) rnd[tid] = pg_uniform(key, (unsigned long long)b * 64 + tid);
+  __syncthreads();
   if (tid == 0) {
     float *p = prm;
     for (int k = 0; k < kNP; ++k) p[k] = 0.f;
@@ -177,8 +252,7 @@ __global__ __launch_bounds__(256) void augment_params_kernel(
       p[P_B] = 1.f; p[P_C] = 1.f; p[P_S] = 1.f; p[P_HUE] = 0.f;
       p[P_ORDER] = (float)(0 | (1 << 2) | (2 << 4) | (3 << 6));
     } else {
-      const unsigned long long step = hyper ? (unsigned long long)hyper[1] : 0ull;
-      Rng r{pg_mix64(seed ^ pg_mix64(step * 0x100000001B3ull + (unsigned long long)epoch_ctr)), (unsigned long long)b * 64};
+      Rng r{rnd};   // draw k of image b = pg_uniform(key, b * 64 + k) (<= 31 draws per image)
       // RandomResizedCrop.get_params(scale=(0.7,1), ratio=(3/4,4/3))
       const float area = (float)(RH * RW);
       const float lr0 = logf(3.f / 4.f), lr1 = logf(4.f / 3.f);
@@ -250,13 +324,32 @@ __global__ __launch_bounds__(256) void augment_params_kernel(
 __global__ __launch_bounds__(256) void augment_render_kernel(
     const unsigned char *__restrict__ src, const long long *__restrict__ idx,
     const long long *__restrict__ labels_src, int S, int dbl, const float *__restrict__ params,
-    bf16_t *__restrict__ out, long long *__restrict__ labels_out) {
-  __shared__ float img[32 * 32 * 3];
+    bf16_t *__restrict__ out, long long *__restrict__ labels_out, int allow_comp) {
+  __shared__ __attribute__((aligned(16))) float img4[32 * 32 * 4];   // RGBx (composite path)
   __shared__ float prm[kNP];
+  __shared__ int tb[2][kMaxS];           // composite filters: [0] columns u, [1] rows v
+  __shared__ float tw[2][kMaxS][3];
+  float *img = img4;                     // [32*32*3] view for the exact fallback path
   const int b = blockIdx.x, tid = threadIdx.x;
   const long long si = idx[b];
-  for (int i = tid; i < 32 * 32 * 3; i += 256) img[i] = src[si * 3072 + i] * (1.f / 255.f);
   if (tid < kNP) prm[tid] = params[b * kNP + tid];
+  __syncthreads();
+  const int RHp = (int)prm[P_SRC_HW];
+  // composite separable path: <= 3 source taps per axis (an upsample factor >= 1) and S <= kMaxS
+  const bool comp = allow_comp && S <= kMaxS && (!dbl || RHp >= 32);
+  if (comp) {
+    stage_image<true>(src, si, img4);
+    for (int i = tid; i < 2 * S; i += 256) {
+      const int ax = i >= S, u = ax ? i - S : i;
+      int base;
+      float w[3];
+      axis_filter(u, ax ? prm[P_I] : prm[P_J], ax ? prm[P_H] : prm[P_W], S, RHp, dbl != 0, base, w);
+      tb[ax][u] = base;
+      tw[ax][u][0] = w[0]; tw[ax][u][1] = w[1]; tw[ax][u][2] = w[2];
+    }
+  } else {
+    stage_image<false>(src, si, img);
+  }
   __syncthreads();
   if (tid == 0)   // contrast mean = sum of the kMeanSplit partial sums, fixed order
     prm[P_MEAN] = (((prm[P_MEAN] + prm[P_MEAN1]) + prm[P_MEAN2]) + prm[P_MEAN3]) * (1.f / (56.f * 56.f));
@@ -284,7 +377,22 @@ __global__ __launch_bounds__(256) void augment_render_kernel(
       inside = u >= 0 && u < S && v >= 0 && v < S;
     }
     if (inside) {
-      f_pixel(img, 32, 32, RH, RW, prm, S, u, v, dbl != 0, rgb);
+      if (comp) {
+        const int uf = prm[P_FLIP] > 0.5f ? S - 1 - u : u;
+        const int cx = tb[0][uf], ry = tb[1][v];
+        const float wx0 = tw[0][uf][0], wx1 = tw[0][uf][1], wx2 = tw[0][uf][2];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const float wy = tw[1][v][i];
+          const float4 *row = reinterpret_cast<const float4 *>(img4) + (ry + i) * 32 + cx;
+          const float4 p0 = row[0], p1 = row[1], p2 = row[2];
+          rgb[0] = fmaf(wy, fmaf(wx0, p0.x, fmaf(wx1, p1.x, wx2 * p2.x)), rgb[0]);
+          rgb[1] = fmaf(wy, fmaf(wx0, p0.y, fmaf(wx1, p1.y, wx2 * p2.y)), rgb[1]);
+          rgb[2] = fmaf(wy, fmaf(wx0, p0.z, fmaf(wx1, p1.z, wx2 * p2.z)), rgb[2]);
+        }
+      } else {
+        f_pixel(img, 32, 32, RH, RW, prm, S, u, v, dbl != 0, rgb);
+      }
       jitter(rgb, prm, prm[P_MEAN], false);
     }
     float o[4];
@@ -307,6 +415,8 @@ void launch_augment(const unsigned char *src, const long long *idx, const long l
                      given, seed, hyper, epoch_ctr, params);
   const int rows_per_block = (256 * 8 + S - 1) / S;
   dim3 grid(B, (S + rows_per_block - 1) / rows_per_block);
+  // PGDIST_AUG_EXACT=1: render through the exact double-bilinear f_pixel (A/B and tests)
+  static const int exact = [] { const char *e = getenv("PGDIST_AUG_EXACT"); return e ? atoi(e) : 0; }();
   hipLaunchKernelGGL(augment_render_kernel, grid, dim3(256), 0, st, src, idx, labels_src, S, dbl,
-                     params, out, labels_out);
+                     params, out, labels_out, exact ? 0 : 1);
 }

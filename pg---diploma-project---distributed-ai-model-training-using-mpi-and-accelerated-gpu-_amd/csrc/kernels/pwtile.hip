@@ -458,7 +458,7 @@ TileGeom tile_geom(int M, int N, int K, int pro) {
   TileGeom g{};
   // largest tile that still gives >= 384 workgroups (~1.5 per CU), else the smallest
   static const int min_wgs = [] { const char *e = getenv("PGDIST_TILE_MINWG"); return e && atoi(e) > 0 ? atoi(e) : 384; }();
-  static constexpr int cand[4][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}};
+  static constexpr int cand[6][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}, {32, 128}, {32, 64}};
   int pick = 3;
   for (int i = 0; i < 4; ++i) {
     const long long wgs = (long long)((M + cand[i][0] - 1) / cand[i][0]) * ((N + cand[i][1] - 1) / cand[i][1]);
@@ -469,7 +469,7 @@ TileGeom tile_geom(int M, int N, int K, int pro) {
     const char *e = getenv("PGDIST_TILE_FORCE");
     if (!e) return -1;
     const int bm = atoi(e), bn = strchr(e, 'x') ? atoi(strchr(e, 'x') + 1) : 0;
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 6; ++i)
       if (bm == cand[i][0] && bn == cand[i][1]) return i;
     return -1;
   }();
@@ -479,9 +479,11 @@ TileGeom tile_geom(int M, int N, int K, int pro) {
   //   N <= K (project / long-K): 64 rows, 128 columns when one tile covers an N of 65..127
   //   (N = 96), else 64 (N = 64, 160, 320: 64-wide column tiles waste less than 128-wide ones)
   static const int rule = [] { const char *e = getenv("PGDIST_TILE_RULE"); return e ? atoi(e) : 1; }();
+  //   PGDIST_TILE_RULE=2: the N <= K shapes on 32-row tiles (twice the workgroups of a
+  //   latency-bound long-K chain: ~300 -> ~600 on the 7x7 layers)
   if (rule) {
     if (N > K) pick = (long long)N * K >= 300000 ? 0 : 2;
-    else pick = (N > 64 && N < 128) ? 1 : 3;
+    else pick = (N > 64 && N < 128) ? (rule == 2 ? 4 : 1) : (rule == 2 ? 5 : 3);
   }
   if (force >= 0) pick = force;
   g.BM = cand[pick][0];
@@ -489,7 +491,7 @@ TileGeom tile_geom(int M, int N, int K, int pro) {
   g.nmt = (M + g.BM - 1) / g.BM;
   g.nt = (N + g.BN - 1) / g.BN;
   static const int k64 = [] { const char *e = getenv("PGDIST_TILE_K64"); return e ? atoi(e) : 256; }();
-  g.KS = K >= k64 ? 64 : 32;
+  g.KS = (K >= k64 || g.BM == 32) ? 64 : 32;   // 32-row tiles: 64-wide k steps (one 16-B chunk per thread)
   // split-K (opt-in, PGDIST_PW_SPLITK = grid-size target, e.g. 1024): double SK while the grid is
   // under the target and every split keeps >= 2 k steps.  Measured OFF by default: MobileNetV2
   // bs128 5.30 ms/step with it vs 4.70 without (same box, profiles/r4_ab_splitk_dma.txt) -- the
@@ -525,21 +527,25 @@ void launch_tile_t(PwTArgs a, const TileGeom &g, hipStream_t st) {
     }
   }
   const dim3 grid(g.nmt * g.nt * a.sk);
-  if (g.KS == 64) hipLaunchKernelGGL((pw_tile_kernel<PRO, EPI, BM, BN, 64, F8>), grid, dim3(256), g.lds, st, a);
+  if constexpr (BM == 32) hipLaunchKernelGGL((pw_tile_kernel<PRO, EPI, BM, BN, 64, F8>), grid, dim3(256), g.lds, st, a);
+  else if (g.KS == 64) hipLaunchKernelGGL((pw_tile_kernel<PRO, EPI, BM, BN, 64, F8>), grid, dim3(256), g.lds, st, a);
   else hipLaunchKernelGGL((pw_tile_kernel<PRO, EPI, BM, BN, 32, F8>), grid, dim3(256), g.lds, st, a);
 }
 
 template <int PRO, int EPI, bool F8 = false>
 void launch_tile_pe(const PwTArgs &a, const TileGeom &g, hipStream_t st) {
-  if (g.BM == 128 && g.BN == 128) launch_tile_t<PRO, EPI, 128, 128, F8>(a, g, st);
+  if (g.BM == 32) {
+    if (g.BN == 128) launch_tile_t<PRO, EPI, 32, 128, F8>(a, g, st);
+    else launch_tile_t<PRO, EPI, 32, 64, F8>(a, g, st);
+  } else if (g.BM == 128 && g.BN == 128) launch_tile_t<PRO, EPI, 128, 128, F8>(a, g, st);
   else if (g.BM == 64 && g.BN == 128) launch_tile_t<PRO, EPI, 64, 128, F8>(a, g, st);
   else if (g.BM == 128 && g.BN == 64) launch_tile_t<PRO, EPI, 128, 64, F8>(a, g, st);
   else launch_tile_t<PRO, EPI, 64, 64, F8>(a, g, st);
 }
 }  // namespace
 
-// BN partial rows: one per M tile of the smallest tile height any launch may pick (64 rows)
-int pw_tile_num_partials(int M, int N, int K) { return (M + 63) / 64; }
+// BN partial rows: one per M tile of the smallest tile height any launch may pick (32 rows)
+int pw_tile_num_partials(int M, int N, int K) { return (M + 31) / 32; }
 
 void launch_pw_tile(int pro, int epi, const bf16_t *A, const bf16_t *A2, const float *pa, const float *pb,
                     const float *pc, const bf16_t *W, bf16_t *out, const bf16_t *Yt, const float *es,

@@ -180,6 +180,11 @@ class MobileNetV2Executor:
     # block outputs materialised by the consumer GEMM instead of a BN-apply pass: measured neutral
     # on MI355X (the consumer reads y_p and the residual per N tile), so off by default
     FUSE_BLOCK_OUTPUT = os.environ.get("PGDIST_FUSE_BLOCK_OUT", "0") == "1"
+    # ... or only for the blocks whose output map has at most this many pixels per image: the
+    # latency-bound 14x14 / 7x7 stages (196, default), where the BN-apply pass is a ~4 us launch
+    # on a few MB: bs128 4.517-4.530 vs 4.540-4.581 ms/step; 28x28 too (784): 4.527-4.559
+    # (scripts/gpu_r4_aug.sh); 0: none
+    FUSE_BLOCK_OUTPUT_HW = int(os.environ.get("PGDIST_FUSE_BLOCK_OUT_HW", "196"))
     STEM_WGRAD_SIDE = os.environ.get("PGDIST_STEM_WGRAD_SIDE", "0") == "1"
     # fp8 mode: every forward 1x1 conv runs on e4m3 MFMA (weights per output channel, activations
     # scaled by ops.kernels.FP8_ASC), backward and depthwise/BN stay bf16/fp32
@@ -550,7 +555,7 @@ class MobileNetV2Executor:
             self._pw_fwd(K.ACT_BN_RELU6, bp.bn_d.y, bp.w_p, bp.bn_p.y, bp.bn_p.acc_f, Mout, bp.cout, bp.hidden,
                          pa=bp.bn_d.scale, pb=bp.bn_d.shift, fin=F(bp.bn_p), lz=L(bp.bn_d))
             self._fin_fwd(bp.bn_p, K.pw_num_partials(Mout, bp.cout, bp.hidden), train)
-            if self.FUSE_BLOCK_OUTPUT and not self.fp8:
+            if (self.FUSE_BLOCK_OUTPUT or bp.Ho * bp.Wo <= self.FUSE_BLOCK_OUTPUT_HW) and not self.fp8:
                 pend = (bp.bn_p, inp_t if bp.residual else None, bp.o)
             else:
                 K.bn_apply(bp.bn_p.y, bp.bn_p.scale, bp.bn_p.shift, bp.o, relu6=False,

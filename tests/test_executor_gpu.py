@@ -94,6 +94,43 @@ def test_executor_step_matches_autograd(dev, B, S):
     assert _rel(exe.model.features[0][1].running_mean, ref.features[0][1].running_mean) < 0.01
 
 
+@pytest.mark.parametrize("hw", [16, 10 ** 9])
+def test_block_output_fusion_matches_bn_apply(dev, hw, monkeypatch):
+    """Block outputs materialised by the consumer GEMM's prologue (PGDIST_FUSE_BLOCK_OUT_HW:
+    the small-map blocks only, or every block) give the step of the separate BN-apply pass.
+    Deterministic BN mode (fixed-order statistics), so the two schedules see the same BN
+    parameters and the block outputs must agree to rounding."""
+    from pgdist.ops import kernels as K
+    B, S = 16, 64
+    torch.manual_seed(0)
+    model = mobilenet_v2(10)
+    model.classifier[0].p = 0.0
+    img = torch.randn(B, S, S, 3, device=dev).to(torch.bfloat16)
+    labels = torch.randint(0, 10, (B,), device=dev)
+    was = K.deterministic()
+    K.set_deterministic(True)
+    try:
+        res = []
+        for m in (0, 0, hw):
+            monkeypatch.setattr(MobileNetV2Executor, "FUSE_BLOCK_OUTPUT_HW", m)
+            exe = MobileNetV2Executor(copy.deepcopy(model), B, S, dev)
+            exe.img.zero_()
+            exe.img[..., :3] = img
+            exe.labels.copy_(labels)
+            exe.forward(train=True)
+            exe.backward()
+            torch.cuda.synchronize()
+            res.append((exe.logits.clone(), exe.flat.grad.clone(), [bp.o.clone() for bp in exe.blocks]))
+    finally:
+        K.set_deterministic(was)
+    (l0, g0, o0), (l0b, g0b, _), (l1, g1, o1) = res
+    assert torch.equal(l0, l0b) and torch.equal(g0, g0b)   # the reference schedule is reproducible
+    for k, (a, b) in enumerate(zip(o1, o0)):
+        assert _rel(a, b) < 1e-3, k
+    assert _rel(l1, l0) < 1e-2
+    assert _cos(g1, g0) > 0.999
+
+
 def test_native_train_step_loss_decreases(dev):
     from pgdist.engine.native_step import NativeTrainStep
     torch.manual_seed(0)

@@ -664,6 +664,30 @@ def test_augment_flip_identity(dev):
     assert rel(tr, ev.flip(2)) < 1e-3
 
 
+@pytest.mark.parametrize("train", [False, True])
+def test_augment_unaligned_source_matches_aligned(dev, train):
+    """The render / params kernels stage the 32x32x3 source with 16-B loads when the image is
+    16-B aligned and with a byte loop otherwise: both must give identical output."""
+    N, B, S = 6, 5, 224
+    src = torch.randint(0, 256, (N, 32, 32, 3), dtype=torch.uint8, device=dev)
+    buf = torch.empty(N * 3072 + 1, dtype=torch.uint8, device=dev)
+    mis = buf[1:].view(N, 32, 32, 3)
+    mis.copy_(src)
+    assert mis.data_ptr() % 16 != 0
+    labels = torch.arange(N, device=dev)
+    idx = torch.tensor([5, 0, 3, 3, 1], device=dev)
+    hyper = torch.tensor([0.0, 7.0], device=dev)
+    outs = []
+    for s_ in (src, mis):
+        out = torch.empty(B, S, S, 4, dtype=torch.bfloat16, device=dev)
+        lab = torch.empty(B, dtype=torch.int64, device=dev)
+        prm = torch.empty(B, K.AUG_NPARAMS, device=dev)
+        K.augment(s_, idx, labels, out, lab, prm, train=train, seed=11, hyper=hyper)
+        outs.append((out, prm))
+    assert torch.equal(outs[0][1], outs[1][1])
+    assert torch.equal(outs[0][0], outs[1][0])
+
+
 def test_head_dropout_consistent(dev):
     """Dropout in the split head: the pool launch draws the mask, the backward launch redraws
     the same one (same seed / step counter), so g is zero exactly on dropped channels and
