@@ -270,6 +270,9 @@ __global__ __launch_bounds__(256) void dw_fwd_lds_kernel(
   // BN / weight parameters staged while the first kDepth rows are in flight
   float s[CPT], t[CPT], stats[2][CPT], wt[9][CPT];
   const bool lazy = ACT != ACT_NONE && g.lz != nullptr;
+  uint2 wraw[9];   // weight loads in flight across the lazy-finalize round trips
+#pragma unroll
+  for (int q = 0; q < 9; ++q) wraw[q] = ldg8(w + (size_t)q * g.C + c0);
   if (lazy) lazy_stage(g, cbase, 2);
 #pragma unroll
   for (int k = 0; k < CPT; ++k) {
@@ -283,7 +286,7 @@ __global__ __launch_bounds__(256) void dw_fwd_lds_kernel(
     stats[0][k] = stats[1][k] = 0.f;
   }
 #pragma unroll
-  for (int q = 0; q < 9; ++q) unpack4(ldg8(w + (size_t)q * g.C + c0), wt[q]);
+  for (int q = 0; q < 9; ++q) unpack4(wraw[q], wt[q]);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // parameters in registers (and the first rows in LDS)
   float win[3][3][CPT];   // three input rows x three tap columns (roles rotate with the unroll)
 #pragma unroll
@@ -412,6 +415,15 @@ __global__ __launch_bounds__(256) PGDIST_DW_DGRAD_ATTR void dw_dgrad_s1_lds_kern
   // BN / weight parameters staged while the first kDepth rows are in flight
   float al[CPT], be[CPT], ga[CPT], s[CPT], t[CPT], stats[2][CPT], wt[9][CPT];
   float accw[WG ? 9 : 1][CPT];
+  // weight and producer-BN loads in flight across the lazy-finalize round trips
+  uint2 wraw[9];
+#pragma unroll
+  for (int q = 0; q < 9; ++q) wraw[q] = ldg8(w + (size_t)q * g.C + c0);
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    s[k] = ps[c0 + k];
+    t[k] = pt[c0 + k];
+  }
   if (g.lz) lazy_stage(g, cbase, 3);
 #pragma unroll
   for (int k = 0; k < CPT; ++k) {
@@ -424,14 +436,12 @@ __global__ __launch_bounds__(256) PGDIST_DW_DGRAD_ATTR void dw_dgrad_s1_lds_kern
       be[k] = coef[g.C + c0 + k];
       ga[k] = coef[2 * g.C + c0 + k];
     }
-    s[k] = ps[c0 + k];
-    t[k] = pt[c0 + k];
     stats[0][k] = stats[1][k] = 0.f;
   }
 #pragma unroll
   for (int q = 0; q < (WG ? 9 : 1); ++q) zero4(accw[q]);
 #pragma unroll
-  for (int q = 0; q < 9; ++q) unpack4(ldg8(w + (size_t)q * g.C + c0), wt[q]);
+  for (int q = 0; q < 9; ++q) unpack4(wraw[q], wt[q]);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // parameters in registers (and the first rows in LDS)
   float win[3][3][CPT];   // three dy rows x three columns iw-1..iw+1 (roles rotate with the unroll)
 #pragma unroll
@@ -577,6 +587,15 @@ __global__ __launch_bounds__(256) PGDIST_DW_DGRAD_ATTR void dw_dgrad_s2_lds_kern
   for (int q = 0; q < kDepth; ++q) issue(q, q);
   // BN / weight parameters staged while the first kDepth rows are in flight
   float al[CPT], be[CPT], ga[CPT], s[CPT], t[CPT], stats[2][CPT];
+  // weight and producer-BN loads in flight across the lazy-finalize round trips
+  uint2 wraw[9];
+#pragma unroll
+  for (int q = 0; q < 9; ++q) wraw[q] = ldg8(w + (size_t)q * g.C + c0);
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    s[k] = ps[c0 + k];
+    t[k] = pt[c0 + k];
+  }
   if (g.lz) lazy_stage(g, cbase, 3);
 #pragma unroll
   for (int k = 0; k < CPT; ++k) {
@@ -589,17 +608,15 @@ __global__ __launch_bounds__(256) PGDIST_DW_DGRAD_ATTR void dw_dgrad_s2_lds_kern
       be[k] = coef[g.C + c0 + k];
       ga[k] = coef[2 * g.C + c0 + k];
     }
-    s[k] = ps[c0 + k];
-    t[k] = pt[c0 + k];
     stats[0][k] = stats[1][k] = 0.f;
   }
   float wA[3][CPT], wB[3][CPT];
 #pragma unroll
   for (int r = 0; r < 3; ++r) {
     float w0[CPT], w1[CPT], w2[CPT];
-    unpack4(ldg8(w + (size_t)(r * 3 + 0) * g.C + c0), w0);
-    unpack4(ldg8(w + (size_t)(r * 3 + 1) * g.C + c0), w1);
-    unpack4(ldg8(w + (size_t)(r * 3 + 2) * g.C + c0), w2);
+    unpack4(wraw[r * 3 + 0], w0);
+    unpack4(wraw[r * 3 + 1], w1);
+    unpack4(wraw[r * 3 + 2], w2);
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
       wA[r][k] = odd_w ? w0[k] : w1[k];

@@ -9,6 +9,12 @@ grep -E "FAILED|ERROR" $O/tests.log | head -20; tail -2 $O/tests.log
 [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
+ab() {
+  t=$1; b=$2
+  timeout -k 10 200 python -u $b --steps 60 --warmup 10 > $O/ab.json 2> $O/ab.err || { tail -20 $O/ab.err; exit 1; }
+  python -c "import json; d=json.load(open('$O/ab.json')); print('$t', d['ms_per_step'], d['value'])"
+}
+[ -f ab/base/bench.py ] && for i in 1 2 3; do ab base ab/base/bench.py; ab new bench.py; done
 for i in 1 2; do
   timeout -k 10 200 python -u bench.py > $O/mnv2_$i.json 2> $O/mnv2.err || { tail -20 $O/mnv2.err; exit 1; }
   cat $O/mnv2_$i.json
