@@ -48,7 +48,15 @@ int *reduce_counters(int n, hipStream_t st) {
 #define PGDIST_RED_ROWS4 0
 #endif
 constexpr int kWredMaxChunks = 128;
-constexpr int kWredTargetWgs = 2048;
+constexpr int kWredTargetWgs = 512;
+// main-stream grid target (PGDIST_WRED_MAIN_WGS; default kWredTargetWgs).  512 vs the former
+// 2048, same box (scripts/gpu_r4_wred3.sh): MobileNetV2 4.498-4.509 vs 4.510-4.522 ms/step,
+// ResNet-50 11.688 / 11.708 vs 11.712 / 11.733 (small: these reductions are short, but a
+// 2k-workgroup grid delays the side stream's dispatches behind it)
+static int wred_main_wgs() {
+  static const int v = [] { const char *e = getenv("PGDIST_WRED_MAIN_WGS"); return e && atoi(e) > 0 ? atoi(e) : kWredTargetWgs; }();
+  return v;
+}
 constexpr int kWredSideWgs = 384;
 
 bool is_side_stream(hipStream_t st) {
@@ -236,7 +244,7 @@ void wgrad_reduce_flush(hipStream_t st) {
       const char *e = getenv("PGDIST_WRED_WGS");
       return e && atoi(e) > 0 ? atoi(e) : 0;
     }();
-    const int target = std::max(64, (env_t > 0 ? env_t : is_side_stream(st) ? kWredSideWgs : kWredTargetWgs) / a.nseg);
+    const int target = std::max(64, (env_t > 0 ? env_t : is_side_stream(st) ? kWredSideWgs : wred_main_wgs()) / a.nseg);
     int wg = 0, ctrs = 0;
     for (int k = 0; k < a.nseg; ++k) {
       const PendingRed &r = segs[b + k];
@@ -273,7 +281,7 @@ void launch_wgrad_reduce(float *part, int S, long long n, float *grad, hipStream
     const char *e = getenv("PGDIST_WRED_WGS");
     return e && atoi(e) > 0 ? atoi(e) : 0;
   }();
-  const int target = env_t > 0 ? env_t : (is_side_stream(st) ? kWredSideWgs : kWredTargetWgs);
+  const int target = env_t > 0 ? env_t : (is_side_stream(st) ? kWredSideWgs : wred_main_wgs());
   long long want = target / (nb > 0 ? nb : 1);
   int nch = (int)(want < 1 ? 1 : want);
   const int cap = colsum_rows(S);
