@@ -334,17 +334,20 @@ class MobileNetV2Executor:
         # re-quantised from the fp32 master at the start of each forward (one batched launch)
         self.w8 = {}
         if fp8:
-            qtab, dst, sc = [], 0, 0
-            for off, n, k in tab:
+            names = [n for bp in self.blocks for n in ((bp.w_e, bp.w_p) if bp.expand else (bp.w_p,))]
+            names.append(self.w_last)
+            qtab, qnames, dst, sc = [], [], 0, 0
+            for name, (off, n, k) in zip(names, tab):
+                if k < self.FP8_MIN_K:   # bf16 layer (see FP8_MIN_K)
+                    continue
                 qtab.append((off, n, k, dst, sc))
+                qnames.append(name)
                 dst += n * K.fp8_pitch(k)
                 sc += n
             self.w8_buf = torch.zeros(dst + 64, dtype=torch.uint8, device=device)
-            self.w8_scale = torch.ones(sc, dtype=torch.float32, device=device)
+            self.w8_scale = torch.ones(sc + 1, dtype=torch.float32, device=device)
             self.w8_tab = torch.tensor(qtab, dtype=torch.int32, device=device).contiguous()
-            names = [n for bp in self.blocks for n in ((bp.w_e, bp.w_p) if bp.expand else (bp.w_p,))]
-            names.append(self.w_last)
-            for name, (off, n, k, d0, c0) in zip(names, qtab):
+            for name, (off, n, k, d0, c0) in zip(qnames, qtab):
                 self.w8[name] = (self.w8_buf[d0:d0 + n * K.fp8_pitch(k)], self.w8_scale[c0:c0 + n])
 
     # ------------------------------------------------------------------ helpers
@@ -472,9 +475,19 @@ class MobileNetV2Executor:
             K.pw_gemm(K.ACT_BN, K.EPI_FWD, bn.y, W, out, ws, M, N, K_, pa=bn.scale, pb=bn.shift, Aout=o, fin=fin,
                       lz=lz)
 
+    # fp8 mode: the e4m3 GEMM only for reduction depths >= this (PGDIST_FP8_MIN_K; 0: every
+    # forward 1x1 conv).  The K = 16 / 24 / 32 expand convs of the 112 / 56 / 28 maps are pure
+    # bandwidth (A read, C write) with nothing for the e4m3 MFMA to save, and on the e4m3 path
+    # they lose the whole-row bf16 expand tiles: bs512 roofline 112x112 K=16 359 -> 518 us,
+    # 56x56 K=24 280 -> 549 us (profiles/r4_roofline_bs512_fp8_vs_bf16.txt)
+    FP8_MIN_K = int(os.environ.get("PGDIST_FP8_MIN_K", "64"))
+
+    def _fp8_layer(self, K_):
+        return self.fp8 and K_ >= self.FP8_MIN_K
+
     def _pw_fwd(self, pro, A, wname, out, ws, M, N, K_, pa=None, pb=None, fin=None, lz=None):
-        """Forward 1x1 conv: bf16 MFMA GEMM, or the e4m3 one in fp8 mode."""
-        if self.fp8:
+        """Forward 1x1 conv: bf16 MFMA GEMM, or the e4m3 one in fp8 mode (K >= FP8_MIN_K)."""
+        if self._fp8_layer(K_):
             W8, wsc = self.w8[wname]
             K.pw_gemm_f8(pro, A, W8, wsc, out, ws, M, N, K_, pa=pa, pb=pb, fin=fin, lz=lz)
         else:
@@ -555,9 +568,12 @@ class MobileNetV2Executor:
             self._pw_fwd(K.ACT_BN_RELU6, bp.bn_d.y, bp.w_p, bp.bn_p.y, bp.bn_p.acc_f, Mout, bp.cout, bp.hidden,
                          pa=bp.bn_d.scale, pb=bp.bn_d.shift, fin=F(bp.bn_p), lz=L(bp.bn_d))
             self._fin_fwd(bp.bn_p, K.pw_num_partials(Mout, bp.cout, bp.hidden), train)
-            if (self.FUSE_BLOCK_OUTPUT or bp.Ho * bp.Wo <= self.FUSE_BLOCK_OUTPUT_HW) and not self.fp8:
+            # (the consumer -- next expand conv or the final conv, K = bp.cout -- must be a bf16
+            # GEMM: the e4m3 one has no BN + residual prologue)
+            if (self.FUSE_BLOCK_OUTPUT or bp.Ho * bp.Wo <= self.FUSE_BLOCK_OUTPUT_HW) and not self._fp8_layer(bp.cout):
                 pend = (bp.bn_p, inp_t if bp.residual else None, bp.o)
             else:
+                pend = None   # (a previous block's output was consumed by this block's expand)
                 K.bn_apply(bp.bn_p.y, bp.bn_p.scale, bp.bn_p.shift, bp.o, relu6=False,
                            res=inp_t if bp.residual else None, lz=L(bp.bn_p))
             inp_bn, inp_t = bp.bn_p, bp.o

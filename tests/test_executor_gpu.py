@@ -151,18 +151,22 @@ def test_native_train_step_loss_decreases(dev):
     assert st.graph is not None
 
 
-def test_executor_fp8_step_close_to_autograd(dev):
-    """fp8 mode (BASELINE config 5): e4m3 forward 1x1 GEMMs.  The step must still track the
-    fp32 autograd step: loss within 0.1, logits and the classifier gradient direction
-    preserved.  (Per-layer gradient cosines are no criterion at random init: the bf16 step
-    itself only reaches a median of ~0.5 against fp32 there, scripts/diag_fp8.py.)"""
+@pytest.mark.parametrize("min_k,n_e4m3", [(64, 27), (0, 34)])
+def test_executor_fp8_step_close_to_autograd(dev, min_k, n_e4m3, monkeypatch):
+    """fp8 mode (BASELINE config 5): e4m3 forward 1x1 GEMMs (every one, or those with K >= 64:
+    the default layer policy keeps the K = 16 / 24 / 32 expand convs in bf16).  The step must
+    still track the fp32 autograd step: loss within 0.1, logits and the classifier gradient
+    direction preserved.  (Per-layer gradient cosines are no criterion at random init: the
+    bf16 step itself only reaches a median of ~0.5 against fp32 there, scripts/diag_fp8.py.)"""
     B, S = 8, 64
     torch.manual_seed(0)
     model = mobilenet_v2(10)
     model.classifier[0].p = 0.0
     ref = copy.deepcopy(model).to(dev).train()
+    monkeypatch.setattr(MobileNetV2Executor, "FP8_MIN_K", min_k)
     exe = MobileNetV2Executor(model, B, S, dev, fp8=True)
-    assert exe.fp8 and len(exe.w8) == 34   # 16 expand + 17 project + final 1x1
+    # 16 expand + 17 project + final 1x1 in all; K >= 64: 10 expand + 16 project + final
+    assert exe.fp8 and len(exe.w8) == n_e4m3
     img = torch.randn(B, S, S, 3, device=dev).to(torch.bfloat16)
     labels = torch.randint(0, 10, (B,), device=dev)
     exe.img.zero_()
