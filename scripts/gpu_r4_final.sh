@@ -14,7 +14,7 @@ ab() {
   timeout -k 10 200 python -u $b --steps 60 --warmup 10 > $O/ab.json 2> $O/ab.err || { tail -20 $O/ab.err; exit 1; }
   python -c "import json; d=json.load(open('$O/ab.json')); print('$t', d['ms_per_step'], d['value'])"
 }
-[ -f ab/base/bench.py ] && for i in 1 2 3; do ab base ab/base/bench.py; ab new bench.py; done
+[ -f ab/base/bench.py ] && [ -n "$PGDIST_AB" ] && for i in 1 2 3; do ab base ab/base/bench.py; ab new bench.py; done
 for i in 1 2; do
   timeout -k 10 200 python -u bench.py > $O/mnv2_$i.json 2> $O/mnv2.err || { tail -20 $O/mnv2.err; exit 1; }
   cat $O/mnv2_$i.json
