@@ -60,6 +60,7 @@ FWD_SHAPES = [
     (2, 6, 512, 2048, 1, 1, 0),
     (8, 64, 64, 128, 3, 1, 1),     # 128 x 128 tiles (>= 256 workgroups)
     (4, 30, 128, 200, 3, 2, 1),    # N not a multiple of the N tile, M tail
+    (4, 7, 512, 256, 3, 1, 1),     # K = 4608 (72 k steps): split-K with PGDIST_CONV_SPLITK
 ]
 
 
@@ -124,6 +125,7 @@ DGRAD_SHAPES = [
     (2, 7, 2048, 512, 1, 1, 0),
     (8, 64, 128, 64, 3, 1, 1),     # 128 x 128 tiles
     (8, 64, 64, 128, 3, 2, 1),     # 128 x 64 tiles over 4 parity classes
+    (4, 7, 512, 256, 3, 1, 1),     # K = 2304 per class: split-K with PGDIST_CONV_SPLITK
 ]
 
 
