@@ -43,6 +43,10 @@ void launch_f32_to_bf16(const float *, bf16_t *, long long, hipStream_t);
 int dw_fwd_num_partials(int, int, int, int, int);
 void dw_set_geom_mode(int);
 int dw_geom_mode();
+void dw_set_tall_rows(int);
+void dw_set_small_dgrad(int);
+int dw_small_dgrad();
+int dw_tall_rows();
 int bn_rep();
 void bn_fin_arm(const void *desc);
 void bn_lz_arm(const void *desc);
@@ -205,6 +209,10 @@ PYBIND11_MODULE(_pgdist_C, m) {
   m.def("dw_fwd_num_partials", &dw_fwd_num_partials);
   m.def("dw_set_geom_mode", &dw_set_geom_mode);
   m.def("dw_geom_mode", &dw_geom_mode);
+  m.def("dw_set_tall_rows", &dw_set_tall_rows);
+  m.def("dw_set_small_dgrad", &dw_set_small_dgrad);
+  m.def("dw_small_dgrad", &dw_small_dgrad);
+  m.def("dw_tall_rows", &dw_tall_rows);
   m.def("bn_rep", &bn_rep, "replica rows of the atomic BN-statistics accumulators");
   m.def("bn_fin_arm", [](P d) { pgdist_rt::run_op([=] { bn_fin_arm(reinterpret_cast<const void *>(d)); }); },
         "arm a device BnFin descriptor for the next BN-statistics producer launch (finalize fused in its tail)");

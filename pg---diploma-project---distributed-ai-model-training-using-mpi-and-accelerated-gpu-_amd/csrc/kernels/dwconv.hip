@@ -44,6 +44,8 @@ struct DwGeom {
   int TWc;    // columns per workgroup
   int R;      // rows per workgroup
   int tiles_w, tiles_h;
+  int Hi;     // image height (stride 1: rows of the 3x3 window masked at image edges); a "tall"
+              // geometry stacks the batch as one B*Hi-row image (B = 1, H = Ho = B*Hi)
   int bn_rep;         // BN-statistics replica rows (g_bn_rep)
   const BnFin *fin;   // fused BN finalize in the tail (nullptr: none)
   const BnFin *lz;    // lazy finalize (fwd: the input BN's scale / shift; dgrad: this layer's coef)
@@ -294,6 +296,10 @@ __global__ __launch_bounds__(256) void dw_fwd_lds_kernel(
 #pragma unroll
     for (int d = 0; d < 3; ++d) zero4(win[r][d]);
   int slot = 0;
+  // image-local row of input row j0 + k (stride 1): the taps above an image's first output row
+  // and below its last are zero padding even where the strip continues into the next image
+  int ihl = j0 % g.Hi;
+  if (ihl < 0) ihl += g.Hi;
   // one input row: wait for its slot, refill the ring, load it into window row `into`;
   // emit an output row from window rows (ra, rb, rc) when `emit`
   auto step = [&](int k, int into, bool emit, int ra, int rb, int rc) {
@@ -318,16 +324,26 @@ __global__ __launch_bounds__(256) void dw_fwd_lds_kernel(
       }
     }
     const int oh = S == 1 ? ih - 1 : (ih - 1) >> 1;
-    float acc[CPT];
-    zero4(acc);
+    float m0 = 1.f, m2 = 1.f;   // tap rows 0 / 2 inside this output row's image
+    if constexpr (S == 1) {
+      const int ohl = ihl == 0 ? g.Hi - 1 : ihl - 1;
+      m0 = ohl != 0 ? 1.f : 0.f;
+      m2 = ohl != g.Hi - 1 ? 1.f : 0.f;
+      ihl = ihl + 1 == g.Hi ? 0 : ihl + 1;
+    }
+    float ar[3][CPT];
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
       const int wr = r == 0 ? ra : r == 1 ? rb : rc;
+      zero4(ar[r]);
 #pragma unroll
       for (int dw = 0; dw < 3; ++dw)
 #pragma unroll
-        for (int kk = 0; kk < CPT; ++kk) acc[kk] = fmaf(win[wr][dw][kk], wt[r * 3 + dw][kk], acc[kk]);
+        for (int kk = 0; kk < CPT; ++kk) ar[r][kk] = fmaf(win[wr][dw][kk], wt[r * 3 + dw][kk], ar[r][kk]);
     }
+    float acc[CPT];
+#pragma unroll
+    for (int kk = 0; kk < CPT; ++kk) acc[kk] = fmaf(m2, ar[2][kk], fmaf(m0, ar[0][kk], ar[1][kk]));
     bst8(ry, (emit && active) ? nhwc_off(tl.b, g.Ho, g.Wo, g.C, oh, ow, c0) : kOOB, pack4(acc));
     const float e = emit ? 1.f : 0.f;
 #pragma unroll
@@ -449,6 +465,10 @@ __global__ __launch_bounds__(256) PGDIST_DW_DGRAD_ATTR void dw_dgrad_s1_lds_kern
 #pragma unroll
     for (int d = 0; d < 3; ++d) zero4(win[r][d]);
   int slot = 0;
+  // image-local row of input row ih = j0 + k - 1: its dy taps ih-1 / ih+1 are zero padding
+  // across an image edge even where a tall strip continues into the next image
+  int ihl = (j0 - 1) % g.Hi;
+  if (ihl < 0) ihl += g.Hi;
   // dy row j0+k -> window row `into`; rows (ra, rb, rc) = dy rows ih-1, ih, ih+1 of input row
   // ih = j0+k-1, emitted when `emit`
   auto step = [&](int k, int into, bool emit, int ra, int rb, int rc) {
@@ -476,16 +496,21 @@ __global__ __launch_bounds__(256) PGDIST_DW_DGRAD_ATTR void dw_dgrad_s1_lds_kern
     const int ih = oh - 1;
     float yp[CPT];
     unpack4(lds8(sl + 2 * kSlotHalo, lcol, g.CC, c4 * CPT), yp);
-    float acc[CPT];
-    zero4(acc);
+    const float mk[3] = {ihl != g.Hi - 1 ? 1.f : 0.f, 1.f, ihl != 0 ? 1.f : 0.f};   // dy rows ih+1, ih, ih-1
+    ihl = ihl + 1 == g.Hi ? 0 : ihl + 1;
+    float ar[3][CPT];
 #pragma unroll
     for (int dh = 0; dh < 3; ++dh) {   // dx[ih][iw] += dy[ih+1-dh][iw+1-dw] * w[dh][dw]
       const int wr = dh == 0 ? rc : dh == 1 ? rb : ra;
+      zero4(ar[dh]);
 #pragma unroll
       for (int dw = 0; dw < 3; ++dw)
 #pragma unroll
-        for (int kk = 0; kk < CPT; ++kk) acc[kk] = fmaf(win[wr][2 - dw][kk], wt[dh * 3 + dw][kk], acc[kk]);
+        for (int kk = 0; kk < CPT; ++kk) ar[dh][kk] = fmaf(win[wr][2 - dw][kk], wt[dh * 3 + dw][kk], ar[dh][kk]);
     }
+    float acc[CPT];
+#pragma unroll
+    for (int kk = 0; kk < CPT; ++kk) acc[kk] = fmaf(mk[2], ar[2][kk], fmaf(mk[0], ar[0][kk], ar[1][kk]));
     const float e = emit ? 1.f : 0.f;
     if constexpr (WG) {
       float z[CPT];
@@ -498,7 +523,7 @@ __global__ __launch_bounds__(256) PGDIST_DW_DGRAD_ATTR void dw_dgrad_s1_lds_kern
         for (int dw = 0; dw < 3; ++dw)
 #pragma unroll
           for (int kk = 0; kk < CPT; ++kk)
-            accw[WG ? dh * 3 + dw : 0][kk] = fmaf(z[kk], win[wr][2 - dw][kk], accw[WG ? dh * 3 + dw : 0][kk]);
+            accw[WG ? dh * 3 + dw : 0][kk] = fmaf(mk[dh] * z[kk], win[wr][2 - dw][kk], accw[WG ? dh * 3 + dw : 0][kk]);
       }
     }
 #pragma unroll
@@ -918,6 +943,35 @@ int g_dw_geom_mask = [] {
   const char *e = getenv("PGDIST_DW_GEOM");
   return e ? atoi(e) : PGDIST_DW_GEOM_DEFAULT;
 }();
+// Tall geometry for the stride-1 forward / dgrad on small maps (<= 14 rows): the batch is
+// stacked into one B*H-row image and a workgroup walks a strip of g_dw_tall rows across image
+// boundaries (the window taps that would cross an image edge are masked per row), so the DMA
+// ring fill, the parameter staging and the statistics epilogue are paid per strip instead of
+// per 7- or 14-row image.  PGDIST_DW_TALL = strip rows, 0: off.  Measured (scripts/dw_bench.py,
+// profiles/r4_dw_tall_sweep.txt): 14-row strips (two 7x7 images) take 7x7x960 forward 18.8 -> 17.7
+// and dgrad 35.4 -> 30.2 us (bench 4.525 / 4.530 vs 4.535 / 4.551 ms/step); longer strips are
+// slower (21 / 28 / 42 / 56 rows: fewer workgroups, and a strip row costs ~0.2 us of DMA latency
+// per workgroup), 14 leaves the 14x14 tiling unchanged.
+int g_dw_tall = [] {
+  const char *e = getenv("PGDIST_DW_TALL");
+  return e ? atoi(e) : 14;
+}();
+// Small-map stride-1 dgrad (tall geometry on): slab width and strip length chosen together so
+// the launch fits one round of resident workgroups (3 per CU) where it can -- e.g. 14x14x384:
+// 64-channel slabs of all 14 columns (768 workgroups) instead of 96-channel slabs of 10 columns
+// (1024, two rounds).  Cost = rounds x (strip rows + g_dw_fix), ties to more active lanes.
+// PGDIST_DW_SMALL_DGRAD=0: off; PGDIST_DW_FIX: the fixed per-strip cost in rows.  Measured
+// (profiles/r4_dw_small_dgrad.txt): 14x14x576 59.7 -> 52.6-54.8 us (21-row strips of 72-channel
+// slabs, 688 workgroups); 14x14x384 unchanged at 37.1 us although it now fits one round;
+// bench 4.506-4.516 vs 4.507-4.526 ms/step.
+int g_dw_small_dgrad = [] {
+  const char *e = getenv("PGDIST_DW_SMALL_DGRAD");
+  return e ? atoi(e) : 1;
+}();
+static int g_dw_fix = [] {
+  const char *e = getenv("PGDIST_DW_FIX");
+  return e ? atoi(e) : 12;
+}();
 static int dw_occ(int kind, int stride, int gh) {
   return kind == 0 ? 4 : kind == 2 ? 3 : (stride == 1 && gh >= 56 ? 2 : 3);
 }
@@ -945,7 +999,13 @@ DwGeom dw_geom(int kind, int B, int H, int W, int C, int stride) {
   g.C = C;
   g.Ho = (H - 1) / stride + 1;
   g.Wo = (W - 1) / stride + 1;
-  const int gw = kind == 1 ? W : g.Wo, gh = kind == 1 ? H : g.Ho;
+  g.Hi = H;
+  const bool tall = g_dw_tall > 0 && kind <= 1 && stride == 1 && H <= 14 && B > 1;
+  if (tall) {
+    g.B = 1;
+    g.H = g.Ho = B * H;
+  }
+  const int gw = kind == 1 ? W : g.Wo, gh = kind == 1 ? g.H : g.Ho;
   g.CC = dw_cc_narrow(C, gw, kind, stride, dw_cc(C));
   int twc = dw_twc_max(g.CC, kind, stride);
   if (twc > gw) twc = gw;
@@ -958,11 +1018,30 @@ DwGeom dw_geom(int kind, int B, int H, int W, int C, int stride) {
     const char *e = getenv("PGDIST_DW_WROWS");
     return e ? atoi(e) : 0;
   }();
-  int R = env_rows > 0 ? env_rows : kRows;
+  int R = tall ? g_dw_tall : env_rows > 0 ? env_rows : kRows;
   if (kind == 2) R = env_wrows > 0 ? env_wrows : kWRows;
   // (PGDIST_DW_ROWS / PGDIST_DW_WROWS override the strip length for tuning experiments)
   R = dw_fix_rows(kind, stride, R, gh);
-  if ((g_dw_geom_mask & (1 << kind)) && ((g_dw_geom_mask & 8) || (kind <= 1 && stride == 1 && gh >= 56))) {
+  if (tall && kind == 1 && g_dw_small_dgrad) {
+    long long best = -1;
+    int best_act = 0;
+    const int rcand[3] = {g_dw_tall, 21, 28};
+    for (int i = 0; i < 3; ++i) {
+      const int r = rcand[i] < gh ? rcand[i] : gh;
+      for (int cc = 8; cc <= 128; cc += 8) {
+        if (C % cc) continue;
+        int t = dw_twc_max(cc, kind, stride);
+        if (t < 1) continue;
+        if (t > gw) t = gw;
+        const long long nwg = (long long)((gh + r - 1) / r) * ((gw + t - 1) / t) * (C / cc);
+        const long long cost = ((nwg + 767) / 768) * (r + g_dw_fix);
+        const int act = (cc / CPT) * gw / ((gw + t - 1) / t);   // active lanes per workgroup, on average
+        if (best < 0 || cost < best || (cost == best && act > best_act))
+          best = cost, best_act = act, g.CC = cc, g.TWc = t, R = r;
+      }
+    }
+  }
+  if (!tall && (g_dw_geom_mask & (1 << kind)) && ((g_dw_geom_mask & 8) || (kind <= 1 && stride == 1 && gh >= 56))) {
     const long long cur = dw_cost(kind, stride, B, gh, gw, C, g.CC, g.TWc, R);
     long long best = cur;
     int bcc = g.CC, btw = g.TWc, bR = R;
@@ -993,6 +1072,10 @@ int dw_grid_x(const DwGeom &g) { return g.B * g.tiles_h * g.tiles_w; }
 // *_workspace_floats of another mode are in use
 void dw_set_geom_mode(int mask) { g_dw_geom_mask = mask; }
 int dw_geom_mode() { return g_dw_geom_mask; }
+void dw_set_tall_rows(int rows) { g_dw_tall = rows; }
+void dw_set_small_dgrad(int on) { g_dw_small_dgrad = on; }
+int dw_small_dgrad() { return g_dw_small_dgrad; }
+int dw_tall_rows() { return g_dw_tall; }
 
 int dw_fwd_num_partials(int B, int H, int W, int C, int stride) { return dw_grid_x(dw_geom(0, B, H, W, C, stride)); }
 int dw_dgrad_num_partials(int B, int H, int W, int C, int stride) { return dw_grid_x(dw_geom(1, B, H, W, C, stride)); }

@@ -230,6 +230,27 @@ def dw_geom_mode():
     return lib().dw_geom_mode()
 
 
+def dw_set_tall_rows(rows):
+    """Tall depthwise geometry (stride-1 forward / dgrad, maps <= 14 rows): the batch is walked
+    as one B*H-row image in strips of `rows` rows (0: off; default from PGDIST_DW_TALL).  Like
+    dw_set_geom_mode it changes partial counts: switch only before sizing workspaces."""
+    lib().dw_set_tall_rows(int(rows))
+
+
+def dw_tall_rows():
+    return lib().dw_tall_rows()
+
+
+def dw_set_small_dgrad(on):
+    """Round-aware slab / strip choice of the small-map stride-1 dgrad (tall geometry on;
+    default from PGDIST_DW_SMALL_DGRAD).  Changes partial counts like dw_set_tall_rows."""
+    lib().dw_set_small_dgrad(int(on))
+
+
+def dw_small_dgrad():
+    return lib().dw_small_dgrad()
+
+
 def _dw_check(B, H, W, C, stride):
     if C % 8 or C // 8 > 256:
         raise ValueError(f"depthwise: C={C} must be a multiple of 8 and <= 2048")

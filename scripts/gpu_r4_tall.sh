@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round 4: tall depthwise geometry (stride-1 fwd / dgrad on <= 14-row maps walked as one
+# B*H-row image): numerics, isolated per-layer times per strip length, bench A/B
+cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/tall && export TMPDIR=/tmp
+O=gpurun_out/tall
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k "dw_" -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
+for r in 0 14 21 28 42 56; do
+  echo "== tall $r" >> $O/dw.txt
+  PGDIST_DW_TALL=$r timeout -k 10 200 python -u scripts/dw_bench.py --kinds fwd,dgrad --reps 20 >> $O/dw.txt 2>&1 || { tail -20 $O/dw.txt; exit 1; }
+done
+grep -E "==|H= +(7|14) s=1|network" $O/dw.txt
+for i in 1 2; do
+  for r in 0 28 14; do
+    PGDIST_DW_TALL=$r timeout -k 10 200 python -u bench.py --steps 60 --warmup 10 > $O/b.json 2> $O/b.err || { tail -20 $O/b.err; exit 1; }
+    python -c "import json; d=json.load(open('$O/b.json')); print('tall $r', d['ms_per_step'], d['value'])"
+  done
+done

@@ -252,6 +252,36 @@ def test_dw_occupancy_geometry(dev, H, C, stride):
         assert out[6] != ref[6]   # the model re-tiles these layers
 
 
+@pytest.mark.parametrize("B,H,C,rows,small", [(128, 7, 960, 28, 0), (128, 14, 384, 28, 0), (128, 14, 576, 21, 0),
+                                              (5, 7, 960, 10, 0), (3, 14, 384, 9, 0), (128, 14, 384, 14, 1),
+                                              (128, 14, 576, 14, 1), (128, 7, 960, 14, 1)])
+def test_dw_tall_geometry(dev, B, H, C, rows, small):
+    """Tall geometry (dw_set_tall_rows: the batch walked as one B*H-row image in strips that
+    cross image boundaries, here also strips starting mid-image and a partial last strip):
+    the window taps across an image edge are masked, so forward activations and dgrad are
+    identical to the per-image tiling and the BN sums / weight gradients (fused and separate)
+    equal up to float summation order."""
+    old, old_small = K.dw_tall_rows(), K.dw_small_dgrad()
+    try:
+        K.dw_set_tall_rows(0)
+        K.dw_set_small_dgrad(0)
+        ref = _dw_all(B, H, C, 1, dev)
+        K.dw_set_tall_rows(rows)
+        K.dw_set_small_dgrad(small)   # round-aware dgrad slab / strip choice
+        out = _dw_all(B, H, C, 1, dev)
+    finally:
+        K.dw_set_tall_rows(old)
+        K.dw_set_small_dgrad(old_small)
+    assert torch.equal(out[0], ref[0]) and torch.equal(out[2], ref[2])
+    for a, b in zip(out[1:6], ref[1:6]):
+        if a.dtype != torch.bfloat16:
+            assert rel(a, b) < 1e-4
+    tiles_w = ref[6][0] // B   # column tiles per image row (unchanged)
+    assert out[6][0] == -(-B * H // rows) * tiles_w and out[6][2] == ref[6][2]
+    if small:   # the dgrad tiling differs where one round of workgroups is reachable
+        assert out[6][1] != ref[6][1] or C == 960
+
+
 # ----------------------------------------------------------------------------- pointwise
 # small M -> L2-direct weights with the K split over waves (KS 1/2/4); M >= 65536 -> LDS-resident weights
 PW_CASES = [(1000, 16, 96), (4096, 24, 144), (777, 96, 24), (3000, 320, 1280), (2048, 160, 960),
