@@ -44,6 +44,8 @@ int dw_fwd_num_partials(int, int, int, int, int);
 void dw_set_geom_mode(int);
 int dw_geom_mode();
 void dw_set_tall_rows(int);
+void dw_set_tall_wrows(int);
+int dw_tall_wrows();
 void dw_set_small_dgrad(int);
 int dw_small_dgrad();
 int dw_tall_rows();
@@ -210,6 +212,8 @@ PYBIND11_MODULE(_pgdist_C, m) {
   m.def("dw_set_geom_mode", &dw_set_geom_mode);
   m.def("dw_geom_mode", &dw_geom_mode);
   m.def("dw_set_tall_rows", &dw_set_tall_rows);
+  m.def("dw_set_tall_wrows", &dw_set_tall_wrows);
+  m.def("dw_tall_wrows", &dw_tall_wrows);
   m.def("dw_set_small_dgrad", &dw_set_small_dgrad);
   m.def("dw_small_dgrad", &dw_small_dgrad);
   m.def("dw_tall_rows", &dw_tall_rows);

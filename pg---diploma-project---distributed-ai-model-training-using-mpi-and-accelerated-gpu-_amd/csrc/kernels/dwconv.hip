@@ -753,8 +753,10 @@ __global__ __launch_bounds__(256) PGDIST_DW_DGRAD_ATTR void dw_dgrad_s2_lds_kern
 
 // wgrad: dW[tap][c] partials per workgroup [P][9][C]; thread = one output column.  Streams per
 // step k: input row j0+k (z = relu6(BN(yprev)), halo columns) and the dy rows (g, y; own
-// columns) of the output row the step may complete.  Per step: 3 DMA.
-template <int S>
+// columns) of the output row the step may complete.  Per step: 3 DMA.  T: tall strips (masks
+// for the taps across an image edge; a separate instantiation, the masks cost the plain kernel
+// its 4th wave per SIMD: 126 -> 130 VGPRs).
+template <int S, bool T = false>
 __global__ __launch_bounds__(256) void dw_wgrad_lds_kernel(
     const bf16_t *__restrict__ gin, const bf16_t *__restrict__ yself, const float *__restrict__ coef,
     const bf16_t *__restrict__ yprev, const float *__restrict__ ps, const float *__restrict__ pt,
@@ -819,6 +821,9 @@ __global__ __launch_bounds__(256) void dw_wgrad_lds_kernel(
 #pragma unroll
     for (int d = 0; d < 3; ++d) zero4(win[r][d]);
   int slot = 0;
+  // image-local row of input row j0 + k (stride 1, tall strips: see the forward)
+  int ihl = j0 % g.Hi;
+  if (ihl < 0) ihl += g.Hi;
   auto step = [&](int k, int into, bool emit, int ra, int rb, int rc) {
     ring_sync<(kDepth - 1) * 3>();
     issue(slot + kDepth < kRing ? slot + kDepth : slot + kDepth - kRing, k + kDepth);
@@ -840,6 +845,13 @@ __global__ __launch_bounds__(256) void dw_wgrad_lds_kernel(
         if (into == 2) win[2][d][kk] = a;
       }
     }
+    float mr[3] = {1.f, 1.f, 1.f};   // tap rows 0 / 2 inside the output row's image (stride 1)
+    if constexpr (T) {
+      const int ohl = ihl == 0 ? g.Hi - 1 : ihl - 1;
+      mr[0] = ohl != 0 ? 1.f : 0.f;
+      mr[2] = ohl != g.Hi - 1 ? 1.f : 0.f;
+      ihl = ihl + 1 == g.Hi ? 0 : ihl + 1;
+    }
     if (emit) {
       float dy[CPT], gv[CPT], yv[CPT];
       unpack4(lds8(sl + kSlotX, lown, g.CC, c4 * CPT), gv);
@@ -853,7 +865,8 @@ __global__ __launch_bounds__(256) void dw_wgrad_lds_kernel(
 #pragma unroll
         for (int dw = 0; dw < 3; ++dw)
 #pragma unroll
-          for (int kk = 0; kk < CPT; ++kk) accw[r * 3 + dw][kk] = fmaf(dy[kk], win[wr][dw][kk], accw[r * 3 + dw][kk]);
+          for (int kk = 0; kk < CPT; ++kk)
+            accw[r * 3 + dw][kk] = fmaf(T ? mr[r] * dy[kk] : dy[kk], win[wr][dw][kk], accw[r * 3 + dw][kk]);
       }
     }
   };
@@ -968,6 +981,12 @@ int g_dw_small_dgrad = [] {
   const char *e = getenv("PGDIST_DW_SMALL_DGRAD");
   return e ? atoi(e) : 1;
 }();
+// tall strips for the stride-1 weight gradient on <= 14-row maps (side stream): PGDIST_DW_TALL_W
+// = strip rows, 0: off
+int g_dw_tall_w = [] {
+  const char *e = getenv("PGDIST_DW_TALL_W");
+  return e ? atoi(e) : 0;
+}();
 static int g_dw_fix = [] {
   const char *e = getenv("PGDIST_DW_FIX");
   return e ? atoi(e) : 12;
@@ -1000,7 +1019,7 @@ DwGeom dw_geom(int kind, int B, int H, int W, int C, int stride) {
   g.Ho = (H - 1) / stride + 1;
   g.Wo = (W - 1) / stride + 1;
   g.Hi = H;
-  const bool tall = g_dw_tall > 0 && kind <= 1 && stride == 1 && H <= 14 && B > 1;
+  const bool tall = (kind <= 1 ? g_dw_tall : g_dw_tall_w) > 0 && stride == 1 && H <= 14 && B > 1;
   if (tall) {
     g.B = 1;
     g.H = g.Ho = B * H;
@@ -1019,7 +1038,7 @@ DwGeom dw_geom(int kind, int B, int H, int W, int C, int stride) {
     return e ? atoi(e) : 0;
   }();
   int R = tall ? g_dw_tall : env_rows > 0 ? env_rows : kRows;
-  if (kind == 2) R = env_wrows > 0 ? env_wrows : kWRows;
+  if (kind == 2) R = tall ? g_dw_tall_w : env_wrows > 0 ? env_wrows : kWRows;
   // (PGDIST_DW_ROWS / PGDIST_DW_WROWS override the strip length for tuning experiments)
   R = dw_fix_rows(kind, stride, R, gh);
   if (tall && kind == 1 && g_dw_small_dgrad) {
@@ -1073,6 +1092,8 @@ int dw_grid_x(const DwGeom &g) { return g.B * g.tiles_h * g.tiles_w; }
 void dw_set_geom_mode(int mask) { g_dw_geom_mask = mask; }
 int dw_geom_mode() { return g_dw_geom_mask; }
 void dw_set_tall_rows(int rows) { g_dw_tall = rows; }
+void dw_set_tall_wrows(int rows) { g_dw_tall_w = rows; }
+int dw_tall_wrows() { return g_dw_tall_w; }
 void dw_set_small_dgrad(int on) { g_dw_small_dgrad = on; }
 int dw_small_dgrad() { return g_dw_small_dgrad; }
 int dw_tall_rows() { return g_dw_tall; }
@@ -1154,7 +1175,9 @@ void launch_dw_wgrad(const bf16_t *gin, const bf16_t *yself, const float *coef, 
   const DwGeom g = dw_geom(2, B, H, W, C, stride);
   const int P = dw_grid_x(g);
   const dim3 grid(P * (C / g.CC)), block(256);
-  if (stride == 1)
+  if (stride == 1 && g.H != g.Hi)   // tall strips
+    hipLaunchKernelGGL((dw_wgrad_lds_kernel<1, true>), grid, block, 0, st, gin, yself, coef, yprev, ps, pt, part, g);
+  else if (stride == 1)
     hipLaunchKernelGGL((dw_wgrad_lds_kernel<1>), grid, block, 0, st, gin, yself, coef, yprev, ps, pt, part, g);
   else
     hipLaunchKernelGGL((dw_wgrad_lds_kernel<2>), grid, block, 0, st, gin, yself, coef, yprev, ps, pt, part, g);

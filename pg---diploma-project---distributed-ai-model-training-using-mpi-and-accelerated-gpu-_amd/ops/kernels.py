@@ -241,6 +241,16 @@ def dw_tall_rows():
     return lib().dw_tall_rows()
 
 
+def dw_set_tall_wrows(rows):
+    """Tall strips (`rows` rows, 0: off) for the stride-1 depthwise weight gradient on maps <= 14
+    rows (default from PGDIST_DW_TALL_W); changes its partial count."""
+    lib().dw_set_tall_wrows(int(rows))
+
+
+def dw_tall_wrows():
+    return lib().dw_tall_wrows()
+
+
 def dw_set_small_dgrad(on):
     """Round-aware slab / strip choice of the small-map stride-1 dgrad (tall geometry on;
     default from PGDIST_DW_SMALL_DGRAD).  Changes partial counts like dw_set_tall_rows."""
