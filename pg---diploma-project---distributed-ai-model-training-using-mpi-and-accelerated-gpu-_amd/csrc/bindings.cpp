@@ -44,6 +44,8 @@ int dw_fwd_num_partials(int, int, int, int, int);
 void dw_set_geom_mode(int);
 int dw_geom_mode();
 void dw_set_tall_rows(int);
+void pw_f8_set_mx(int);
+int pw_f8_mx();
 void dw_set_tall_wrows(int);
 int dw_tall_wrows();
 void dw_set_small_dgrad(int);
@@ -212,6 +214,8 @@ PYBIND11_MODULE(_pgdist_C, m) {
   m.def("dw_set_geom_mode", &dw_set_geom_mode);
   m.def("dw_geom_mode", &dw_geom_mode);
   m.def("dw_set_tall_rows", &dw_set_tall_rows);
+  m.def("pw_f8_set_mx", &pw_f8_set_mx);
+  m.def("pw_f8_mx", &pw_f8_mx);
   m.def("dw_set_tall_wrows", &dw_set_tall_wrows);
   m.def("dw_tall_wrows", &dw_tall_wrows);
   m.def("dw_set_small_dgrad", &dw_set_small_dgrad);

@@ -15,6 +15,7 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef short s16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef int i32x8_t __attribute__((ext_vector_type(8)));
 
 #define PG_DEVICE __device__ __forceinline__
 

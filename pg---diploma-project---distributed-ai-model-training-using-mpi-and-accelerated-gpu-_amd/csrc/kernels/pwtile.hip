@@ -65,7 +65,11 @@ constexpr int kSc1 = 16;   // buffer cache policy bit sc1: agent-coherent (L2 wr
 // bytes in flight per step)
 // F8: forward in e4m3 (v_mfma_f32_16x16x32_fp8_fp8): A is converted to e4m3 after the
 // prologue while it is staged, B is staged from the e4m3 weight copy; both LDS tiles are
-// half the bytes of the bf16 ones.
+// half the bytes of the bf16 ones.  F8 with KSTEP = 128: one block-scaled
+// v_mfma_scale_f32_16x16x128_f8f6f4 per 16x16 fragment and k step (e4m3 x e4m3, unit E8M0
+// scales: the per-channel scales stay in the epilogue), the gfx950 double-rate fp8 form; lane l
+// holds A[row l & 15][k 32 (l >> 4) .. +31] and B[k 32 (l >> 4) .. +31][col l & 15], 32
+// contiguous bytes of a staged row each.
 template <int PRO, int EPI, int BM, int BN, int KSTEP, bool F8 = false>
 __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
   static_assert(!F8 || (EPI == EPI_FWD_T && PRO != PRO_BNBWD_T && PRO != PRO_BNRES_T), "fp8: forward only");
@@ -242,6 +246,29 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
     load((ks + 1) * KSTEP, ks + 1 < ke);
     const bf16_t *Ab = As + buf * BM * kLDK;
     const bf16_t *Bb = Bs + buf * BN * kLDK;
+    if constexpr (F8 && KSTEP == 128) {
+      const uint8_t *A8 = As8 + buf * BM * kLDK8, *B8 = Bs8 + buf * BN * kLDK8;
+      i32x8_t af[RT];
+#pragma unroll
+      for (int r = 0; r < RT; ++r) {
+        const uint4 *q = reinterpret_cast<const uint4 *>(A8 + (wm * (BM / 2) + r * 16 + (lane & 15)) * kLDK8 +
+                                                         32 * (lane >> 4));
+        const uint4 lo = q[0], hi = q[1];
+        af[r] = i32x8_t{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+      }
+#pragma unroll
+      for (int c = 0; c < CTW; ++c) {
+        const uint4 *q = reinterpret_cast<const uint4 *>(B8 + (wn * (BN / 2) + c * 16 + (lane & 15)) * kLDK8 +
+                                                         32 * (lane >> 4));
+        const uint4 lo = q[0], hi = q[1];
+        const i32x8_t bf = i32x8_t{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w,
+                                   (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+#pragma unroll
+        for (int r = 0; r < RT; ++r)   // formats 0 / 0: e4m3 x e4m3; scales 0x7f = 2^0 in every byte
+          acc[r][c] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[r], bf, acc[r][c], 0, 0, 0, 0x7f7f7f7f,
+                                                                       0, 0x7f7f7f7f);
+      }
+    } else
 #pragma unroll
     for (int sub = 0; sub < KSTEP / 32; ++sub) {
       if constexpr (F8) {
@@ -527,6 +554,12 @@ void launch_tile_t(PwTArgs a, const TileGeom &g, hipStream_t st) {
     }
   }
   const dim3 grid(g.nmt * g.nt * a.sk);
+  if constexpr (F8) {
+    if (g.KS == 128) {
+      hipLaunchKernelGGL((pw_tile_kernel<PRO, EPI, BM, BN, 128, F8>), grid, dim3(256), g.lds, st, a);
+      return;
+    }
+  }
   if constexpr (BM == 32) hipLaunchKernelGGL((pw_tile_kernel<PRO, EPI, BM, BN, 64, F8>), grid, dim3(256), g.lds, st, a);
   else if (g.KS == 64) hipLaunchKernelGGL((pw_tile_kernel<PRO, EPI, BM, BN, 64, F8>), grid, dim3(256), g.lds, st, a);
   else hipLaunchKernelGGL((pw_tile_kernel<PRO, EPI, BM, BN, 32, F8>), grid, dim3(256), g.lds, st, a);
@@ -567,12 +600,29 @@ void launch_pw_tile(int pro, int epi, const bf16_t *A, const bf16_t *A2, const f
 #undef PT_CASE
 }
 
+// the double-rate block-scaled fp8 MFMA in the tile path (128-wide k steps); PGDIST_F8_MX=0: the
+// 16x16x32 fp8 MFMA
+static int g_f8_mx = [] { const char *e = getenv("PGDIST_F8_MX"); return e ? atoi(e) : 1; }();
+void pw_f8_set_mx(int on) { g_f8_mx = on; }
+int pw_f8_mx() { return g_f8_mx; }
+
 void launch_pw_tile_f8(int pro, const bf16_t *A, const float *pa, const float *pb, const uint8_t *W8, int ldw8,
                        const float *wsc, float asc, bf16_t *out, float *part, int M, int N, int K,
                        hipStream_t st) {
   PwTArgs a{A, nullptr, pa, pb, nullptr, nullptr, out, nullptr, nullptr, nullptr, nullptr, part, M, N, K,
             nullptr, W8, wsc, asc, ldw8, g_bn_rep, take_bn_fin(), take_bn_lz()};
-  TileGeom g = tile_geom(M, N, K, pro);   // the bf16 LDS size bounds the e4m3 one
+  TileGeom g = tile_geom(M, N, K, pro);   // the bf16 LDS size bounds the e4m3 one at KS <= 64
+  if (g_f8_mx && g.sk == 1) {
+    g.KS = 128;
+    const int npar = pro == ACT_NONE ? 0 : 2;
+    const size_t kp = (size_t)((K + 127) / 128 * 128);
+    const size_t ops = (size_t)2 * (g.BM + g.BN) * (128 + 16);
+    const size_t ctile = (size_t)g.BM * (g.BN + 8) * 2;
+    const size_t red = (size_t)(256 / (g.BN / 8)) * g.BN * 4;
+    size_t body = ops > ctile ? ops : ctile;
+    if (red > body) body = red;
+    g.lds = body + npar * kp * 4;
+  }
   if (pro == ACT_NONE) launch_tile_pe<ACT_NONE, EPI_FWD_T, true>(a, g, st);
   else if (pro == ACT_BN_RELU6) launch_tile_pe<ACT_BN_RELU6, EPI_FWD_T, true>(a, g, st);
   else if (pro == ACT_BN) launch_tile_pe<ACT_BN, EPI_FWD_T, true>(a, g, st);

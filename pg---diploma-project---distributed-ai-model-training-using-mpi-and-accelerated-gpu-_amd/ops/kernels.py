@@ -395,6 +395,16 @@ def pw_gemm_f8(pro, A, W8, wsc, out, part, M, N, K, pa=None, pb=None, asc=None, 
     lib().pw_gemm_f8(int(pro), _p(A), _p(pa), _p(pb), _p(W8), ld, _p(wsc), a, _p(out), _p(part), M, N, K, _s())
 
 
+def pw_f8_set_mx(on):
+    """fp8 tile GEMMs (small M or K > 192) on the block-scaled double-rate
+    v_mfma_scale_f32_16x16x128_f8f6f4 (1, default from PGDIST_F8_MX) or the 16x16x32 fp8 MFMA (0)."""
+    lib().pw_f8_set_mx(int(on))
+
+
+def pw_f8_mx():
+    return lib().pw_f8_mx()
+
+
 def w8_quant(src, dst, wsc, tab, n):
     """Per-output-channel e4m3 quantisation of fp32 1x1 weights, batched over the int32
     table ``tab`` [n,5] = (src offset, N, K, dst byte offset, scale offset)."""
