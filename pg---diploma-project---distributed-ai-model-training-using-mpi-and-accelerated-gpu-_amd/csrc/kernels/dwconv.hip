@@ -982,7 +982,7 @@ int g_dw_small_dgrad = [] {
   return e ? atoi(e) : 1;
 }();
 // tall strips for the stride-1 weight gradient on <= 14-row maps (side stream): PGDIST_DW_TALL_W
-// = strip rows, 0: off
+// = strip rows, 0: off (measured neutral at 28 rows, slower at 14: profiles/r4_dw_tall_wgrad.txt)
 int g_dw_tall_w = [] {
   const char *e = getenv("PGDIST_DW_TALL_W");
   return e ? atoi(e) : 0;
