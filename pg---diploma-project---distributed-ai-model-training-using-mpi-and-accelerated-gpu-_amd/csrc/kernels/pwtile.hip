@@ -600,9 +600,11 @@ void launch_pw_tile(int pro, int epi, const bf16_t *A, const bf16_t *A2, const f
 #undef PT_CASE
 }
 
-// the double-rate block-scaled fp8 MFMA in the tile path (128-wide k steps); PGDIST_F8_MX=0: the
-// 16x16x32 fp8 MFMA
-static int g_f8_mx = [] { const char *e = getenv("PGDIST_F8_MX"); return e ? atoi(e) : 1; }();
+// the double-rate block-scaled fp8 MFMA in the tile path (128-wide k steps): PGDIST_F8_MX=2
+// (default) on the <= 64-row tiles, 1 on every tile, 0: the 16x16x32 fp8 MFMA.  bs512, one box:
+// 14.889-14.900 (2) vs 14.923-14.967 (1) vs 14.896-14.940 (0) vs bf16 14.906-14.919 ms/step
+// (profiles/r4_fp8_mx_bs512_ab.txt)
+static int g_f8_mx = [] { const char *e = getenv("PGDIST_F8_MX"); return e ? atoi(e) : 2; }();
 void pw_f8_set_mx(int on) { g_f8_mx = on; }
 int pw_f8_mx() { return g_f8_mx; }
 
@@ -612,7 +614,8 @@ void launch_pw_tile_f8(int pro, const bf16_t *A, const float *pa, const float *p
   PwTArgs a{A, nullptr, pa, pb, nullptr, nullptr, out, nullptr, nullptr, nullptr, nullptr, part, M, N, K,
             nullptr, W8, wsc, asc, ldw8, g_bn_rep, take_bn_fin(), take_bn_lz()};
   TileGeom g = tile_geom(M, N, K, pro);   // the bf16 LDS size bounds the e4m3 one at KS <= 64
-  if (g_f8_mx && g.sk == 1) {
+  // PGDIST_F8_MX=2: only the <= 64-row tiles (the 128-row ones need 157-202 VGPRs at KSTEP 128)
+  if (g_f8_mx && g.sk == 1 && (g_f8_mx == 1 || g.BM <= 64)) {
     g.KS = 128;
     const int npar = pro == ACT_NONE ? 0 : 2;
     const size_t kp = (size_t)((K + 127) / 128 * 128);

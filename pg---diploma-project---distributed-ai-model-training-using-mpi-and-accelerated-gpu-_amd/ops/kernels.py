@@ -397,7 +397,8 @@ def pw_gemm_f8(pro, A, W8, wsc, out, part, M, N, K, pa=None, pb=None, asc=None, 
 
 def pw_f8_set_mx(on):
     """fp8 tile GEMMs (small M or K > 192) on the block-scaled double-rate
-    v_mfma_scale_f32_16x16x128_f8f6f4 (1, default from PGDIST_F8_MX) or the 16x16x32 fp8 MFMA (0)."""
+    v_mfma_scale_f32_16x16x128_f8f6f4: 2 (default from PGDIST_F8_MX) on the <= 64-row tiles,
+    1 on every tile, 0: the 16x16x32 fp8 MFMA everywhere."""
     lib().pw_f8_set_mx(int(on))
 
 

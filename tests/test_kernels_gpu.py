@@ -380,13 +380,15 @@ def test_w8_quant_matches_torch_e4m3(dev):
 @pytest.mark.parametrize("M,K_,N,mx", [(70001, 16, 96, 1), (100352, 24, 144, 1), (66000, 192, 64, 1),
                                        (6272, 960, 160, 1), (6272, 960, 160, 0), (25088, 64, 384, 1),
                                        (25088, 64, 384, 0), (3000, 320, 1280, 1), (3000, 320, 1280, 0),
-                                       (777, 96, 24, 1), (777, 96, 24, 0), (25088, 160, 960, 1), (4096, 576, 96, 1)])
+                                       (777, 96, 24, 1), (777, 96, 24, 0), (25088, 160, 960, 1), (4096, 576, 96, 1),
+                                       (25088, 160, 960, 2), (6272, 960, 160, 2)])
 @pytest.mark.parametrize("pro", [K.ACT_NONE, K.ACT_BN_RELU6, K.ACT_BN])
 def test_pw_fwd_fp8(dev, M, K_, N, mx, pro):
     """fp8 forward GEMM: equals the fp32 GEMM of the e4m3-rounded operands (PyTorch
     float8_e4m3fn conversion) up to the bf16 output rounding.  mx = 1: the tile-path launches
     (M < 65536 or K > 192) on the block-scaled v_mfma_scale_f32_16x16x128_f8f6f4 (128-wide k
-    steps, K zero-padded: K = 960 / 320 / 96 / 160 / 576); mx = 0: v_mfma_f32_16x16x32_fp8_fp8."""
+    steps, K zero-padded: K = 960 / 320 / 96 / 160 / 576); mx = 2: only the <= 64-row tiles
+    (the default); mx = 0: v_mfma_f32_16x16x32_fp8_fp8."""
     old = K.pw_f8_mx()
     K.pw_f8_set_mx(mx)
     try:
