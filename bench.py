@@ -190,7 +190,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(imgs_per_s / ref_for(world), 3) if headline else None,
-            "dtype": "fp8-e4m3 1x1 GEMMs / bf16" if args.fp8 else "bf16",
+            "dtype": "fp8-e4m3 forward 1x1 GEMMs (K>=64) / bf16" if args.fp8 else "bf16",
             "data": ("synthetic (device-resident uint8 32x32x3 CIFAR-shaped images, GPU-augmented to 224x224; "
                      "random-init weights)" if args.model == "mobilenet_v2" else
                      "synthetic (device-resident uint8 224x224x3 ImageNet-shaped images, GPU flip + normalise; "

@@ -64,6 +64,8 @@ class TrainConfig:
     eval_every: int = 1
     profile: bool = False                     # roctx ranges + per-step HIP-event timing summary per epoch
     watchdog_s: float = 0.0                   # >0: abort a rank that makes no progress for this long (s)
+    #                                           (the native communicator's collective watchdog is separate:
+    #                                           on for every multi-rank run, PGDIST_COMM_TIMEOUT)
     dist_timeout_s: float = 1800.0            # collective timeout (init_process_group)
 
     def replace(self, **kw) -> "TrainConfig":
@@ -81,10 +83,11 @@ PRESETS = {
     # (bn_sync="broadcast": the reference DDP's broadcast_buffers=True, rank 0's BN running statistics
     #  sent before every training forward; --bn-sync eval is the faster option: sync before eval/save)
     "mpi": dict(batch_size=128, save_path="best_mobilenetv2_cifar10_224_mpi.pth", log_format="ddp", seed=42,
-                bn_sync="broadcast"),
+                bn_sync="broadcast", watchdog_s=1800.0),
     # BASELINE.json config 5: MobileNetV2 fp8 (e4m3 forward GEMMs), bs 512 per GPU, DDP
     "mpi_fp8": dict(batch_size=512, precision="fp8", backend="hip",
-                    save_path="best_mobilenetv2_cifar10_224_mpi_fp8.pth", log_format="ddp", seed=42),
+                    save_path="best_mobilenetv2_cifar10_224_mpi_fp8.pth", log_format="ddp", seed=42,
+                    watchdog_s=1800.0),
 }
 
 

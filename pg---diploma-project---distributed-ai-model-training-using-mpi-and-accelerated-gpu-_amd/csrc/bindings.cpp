@@ -38,7 +38,7 @@ void launch_bn_bwd_finalize(const float *, int, int, float, const float *, const
 void launch_bn_apply(const bf16_t *, const bf16_t *, const float *, const float *, bf16_t *,
                      long long, int, bool, hipStream_t);
 void launch_adam_flat(float *, const float *, float *, float *, bf16_t *, long long, const float *,
-                      float, float, float, float, float, hipStream_t);
+                      float, float, float, float, float, const unsigned *, hipStream_t);
 void launch_f32_to_bf16(const float *, bf16_t *, long long, hipStream_t);
 int dw_fwd_num_partials(int, int, int, int, int);
 void dw_set_geom_mode(int);
@@ -71,6 +71,10 @@ long long dw_dgrad_wgrad_workspace_floats(int, int, int, int, int);
 void launch_dw_wgrad(const bf16_t *, const bf16_t *, const float *, const bf16_t *, const float *,
                      const float *, float *, float *, int, int, int, int, int, hipStream_t);
 int pw_gemm_num_partials(int, int, int);
+int ir_fwd_grid(int, int, int, int, int);
+void launch_ir_fwd(const bf16_t *, const bf16_t *, const void *, bf16_t *, const bf16_t *, const bf16_t *,
+                   const bf16_t *, bf16_t *, bf16_t *, bf16_t *, const void *, const void *, const void *, unsigned *,
+                   unsigned *, int, int, int, int, int, hipStream_t);
 bool pw_bwd_supported(int, int, int);
 int pw_bwd_num_partials(int, int, int);
 long long pw_bwd_wgrad_workspace_floats(int, int, int);
@@ -190,10 +194,10 @@ PYBIND11_MODULE(_pgdist_C, m) {
   });
   // ---- optimizer ----
   m.def("adam_flat", [](P p, P g, P mm, P v, P pb, long long n, P hyper, float b1, float b2,
-                        float eps, float wd, float gscale, P s) {
+                        float eps, float wd, float gscale, P skip, P s) {
     pgdist_rt::run_op([=] {
       launch_adam_flat(ptr<float>(p), ptr<float>(g), ptr<float>(mm), ptr<float>(v), ptr<bf16_t>(pb),
-                       n, ptr<float>(hyper), b1, b2, eps, wd, gscale, S(s));
+                       n, ptr<float>(hyper), b1, b2, eps, wd, gscale, ptr<unsigned>(skip), S(s));
     });
   });
   m.def("f32_to_bf16", [](P x, P y, long long n, P s) {
@@ -268,6 +272,18 @@ PYBIND11_MODULE(_pgdist_C, m) {
   });
   // ---- pointwise ----
   m.def("pw_gemm_num_partials", &pw_gemm_num_partials);
+  // ---- fused inverted-residual block forward (irblock.hip) ----
+  m.def("ir_fwd_grid", &ir_fwd_grid, "workgroups of the fused block forward (0: unsupported / not co-resident)");
+  m.def("ir_fwd", [](P xin, P res, P lz_in, P xout, P we, P wd, P wp, P h1, P h2, P y, P de, P dd, P dp, P bar,
+                     P err, int B, int H, int cin, int ch, int cout, P s) {
+    pgdist_rt::run_op([=] {
+      launch_ir_fwd(ptr<bf16_t>(xin), ptr<bf16_t>(res), reinterpret_cast<const void *>(lz_in), ptr<bf16_t>(xout),
+                    ptr<bf16_t>(we), ptr<bf16_t>(wd), ptr<bf16_t>(wp), ptr<bf16_t>(h1), ptr<bf16_t>(h2),
+                    ptr<bf16_t>(y), reinterpret_cast<const void *>(de), reinterpret_cast<const void *>(dd),
+                    reinterpret_cast<const void *>(dp), ptr<unsigned>(bar), ptr<unsigned>(err), B, H, cin, ch, cout,
+                    S(s));
+    });
+  });
   m.def("pw_gemm", [](int pro, int epi, P A, P A2, P pa, P pb, P pc, P W, P out, P Yt, P es, P et,
                       P R, P part, int M, int N, int K, P Aout, P s) {
     pgdist_rt::run_op([=] {
@@ -531,6 +547,11 @@ PYBIND11_MODULE(_pgdist_C, m) {
   m.def("comm_poison", &pgdist_rt::comm_poison, py::call_guard<py::gil_scoped_release>());
   m.def("comm_clear_error", &pgdist_rt::comm_clear_error, py::call_guard<py::gil_scoped_release>());
   m.def("comm_rccl_ranks", &pgdist_rt::comm_rccl_ranks);
+  m.def("comm_set_watchdog", &pgdist_rt::comm_set_watchdog, py::call_guard<py::gil_scoped_release>());
+  m.def("comm_watchdog", &pgdist_rt::comm_watchdog);
+  m.def("comm_inject_stall", &pgdist_rt::comm_inject_stall);
+  m.def("comm_error_word", &pgdist_rt::comm_error_word);
+  m.def("comm_error_async", &pgdist_rt::comm_error_async);
   m.def("comm_destroy", &pgdist_rt::comm_destroy, py::call_guard<py::gil_scoped_release>());
 
   m.def("cu_masked_stream", &pgdist_rt::cu_masked_stream,

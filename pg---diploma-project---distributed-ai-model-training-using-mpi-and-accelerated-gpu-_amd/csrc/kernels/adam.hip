@@ -10,12 +10,17 @@
 // master weights, and writes the bf16 shadow copy the conv kernels read.
 // lr and the step counter are read from DEVICE memory so the launch can be
 // captured in a hipGraph and replayed while StepLR changes lr.
+// `skip`: the data-parallel communicator's error word (comm_error_word) or null; while it is
+// nonzero (a gradient collective failed or the communicator was poisoned) the update is
+// skipped, so un-reduced gradients never reach the replicas' weights.
 #include "../common.h"
 
 __global__ __launch_bounds__(256) void adam_flat_kernel(
     float *__restrict__ p, const float *__restrict__ g, float *__restrict__ m,
     float *__restrict__ v, bf16_t *__restrict__ pb, long long n4, const float *__restrict__ hyper,
-    float beta1, float beta2, float eps, float weight_decay, float grad_scale) {
+    float beta1, float beta2, float eps, float weight_decay, float grad_scale,
+    const unsigned *__restrict__ skip) {
+  if (skip && __hip_atomic_load(skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
   // hyper[0] = lr, hyper[1] = step (already incremented for this update)
   const float lr = hyper[0];
   const float t = hyper[1];
@@ -62,12 +67,12 @@ __global__ __launch_bounds__(256) void f32_to_bf16_kernel(const float *__restric
 
 void launch_adam_flat(float *p, const float *g, float *m, float *v, bf16_t *pb, long long n,
                       const float *hyper, float beta1, float beta2, float eps, float wd,
-                      float grad_scale, hipStream_t st) {
+                      float grad_scale, const unsigned *skip, hipStream_t st) {
   const long long n4 = n / 4;  // caller pads the flat buffer to a multiple of 4
   int grid = (int)((n4 + 255) / 256);
   if (grid > 4096) grid = 4096;
   hipLaunchKernelGGL(adam_flat_kernel, dim3(grid), dim3(256), 0, st, p, g, m, v, pb, n4, hyper,
-                     beta1, beta2, eps, wd, grad_scale);
+                     beta1, beta2, eps, wd, grad_scale, skip);
 }
 
 void launch_f32_to_bf16(const float *x, bf16_t *y, long long n, hipStream_t st) {

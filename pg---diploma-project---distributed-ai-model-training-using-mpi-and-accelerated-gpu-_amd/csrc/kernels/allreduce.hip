@@ -284,3 +284,18 @@ void launch_p2p_collective(const ArCall &call, int nlocal, hipStream_t st) {
     p2p_collective_kernel<false><<<grid, kArThreads, 0, st>>>(call);
   PG_CHECK_LAUNCH();
 }
+
+// Fault injection for the communicator watchdog tests (comm_inject_stall): one lane spins on
+// the realtime clock for `ticks` (100 MHz) on the comm stream, between a collective's start
+// marker and the collective itself -- a peer that never arrives, as the watchdog sees it.
+// Bounded by construction (the host caps it at 30 s).
+__global__ void comm_stall_kernel(long long ticks) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long t0 = wall_clock64();
+  while ((long long)(wall_clock64() - t0) < ticks) __builtin_amdgcn_s_sleep(127);
+}
+
+void launch_comm_stall(double seconds, hipStream_t st) {
+  const double s = seconds < 30.0 ? seconds : 30.0;
+  hipLaunchKernelGGL(comm_stall_kernel, dim3(1), dim3(64), 0, st, (long long)(s * 1e8));
+}

@@ -24,7 +24,9 @@
 constexpr int kArMaxRanks = 8;
 constexpr int kArMaxBlocks = 64;                    // blocks per rank of one collective
 constexpr int kArThreads = 256;                     // 4 waves
-constexpr long long kArSigBytes = 64 * 1024;        // kArMaxBlocks * 128 B slots, padded
+constexpr long long kArSigBytes = 64 * 1024;        // kArMaxBlocks blocks x 32 source slots x 8 B, padded
+static_assert(kArMaxBlocks * 32 * sizeof(uint64_t) <= kArSigBytes, "signal slots exceed their region");
+static_assert(kArMaxRanks <= 32, "32 source slots per block");
 constexpr int kArCtrWords = 2 * kArMaxBlocks;       // [epoch][calls] per block
 
 enum ArAlgo : int {

@@ -6,17 +6,24 @@
 #include <rccl/rccl.h>
 
 #include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../p2p.h"
 #include "plan.h"
 
 void launch_p2p_collective(const ArCall &call, int nlocal, hipStream_t st);
+void launch_comm_stall(double seconds, hipStream_t st);
 
 namespace pgdist_rt {
 namespace {
@@ -91,6 +98,27 @@ struct Event {
   Event &operator=(const Event &) = delete;
 };
 
+// ---------------------------------------------------------------- watchdog
+// A collective that has STARTED on the comm stream (its start marker completed: every
+// producer it waited for is done) but not finished within the deadline means a peer is dead
+// or out of step.  The P2P kernels time out by themselves (error word); an RCCL kernel waits
+// forever.  The watchdog thread polls the oldest outstanding collective's two events
+// (hipEventQuery, no synchronisation) and, past the deadline, prints the stalled collective,
+// poisons the communicator, calls ncclCommAbort and -- by default -- ends the process with a
+// nonzero status, so a data-parallel job fails on every rank instead of hanging (the peers'
+// own watchdogs fire the same way).
+struct Tracked {
+  std::shared_ptr<Event> start, done;
+  std::string label;
+  double seen = -1.0;   // host time the start marker was first seen complete
+  double limit = 0.0;
+};
+
+double now_s() {
+  using namespace std::chrono;
+  return duration<double>(steady_clock::now().time_since_epoch()).count();
+}
+
 // ---------------------------------------------------------------- communicator
 struct Comm {
   int rank = 0, world = 1, device = 0, nlocal = 1, blocks = 32;
@@ -107,14 +135,71 @@ struct Comm {
   // or an error word / RCCL async error seen by comm_error.  Once set the communicator is
   // poisoned: every later collective (recorded ops included) throws instead of launching.
   std::atomic<int> host_err{0};
+  mutable std::mutex what_mu;   // `what` is written by the op / replay / watchdog threads
   std::string what;
 
+  // watchdog state (mu guards q / pool; the thread runs while wd_s > 0)
+  std::mutex mu;
+  std::deque<Tracked> q;
+  std::vector<std::pair<std::shared_ptr<Event>, std::shared_ptr<Event>>> pool;
+  double wd_s = 0.0;        // deadline after a collective started (0: watchdog off)
+  int wd_exit = 0;          // process exit status on a stall (0: poison + abort only)
+  std::thread wd;
+  std::atomic<bool> wd_stop{false};
+  std::atomic<long long> stall_ms{0};   // fault injection: stall the next collective this long
+
   void fail(int code, const std::string &msg) {
+    std::lock_guard<std::mutex> g(what_mu);
     if (host_err.fetch_or(code) == 0) what = msg;
+  }
+  std::string what_str() const {
+    std::lock_guard<std::mutex> g(what_mu);
+    return what;
   }
   void ensure_usable() const {
     if (host_err.load())
-      throw std::runtime_error("native communicator is poisoned after an earlier failure (" + what + ")");
+      throw std::runtime_error("native communicator is poisoned after an earlier failure (" + what_str() + ")");
+  }
+
+  // called by a collective op on the comm stream (op / replay thread): start marker, the
+  // injected stall if one is armed, then the collective, then end_track's done marker
+  Tracked begin_track(hipStream_t st, const std::string &label, double limit_mult = 1.0) {
+    Tracked t;
+    const long long ms = stall_ms.exchange(0);
+    if (wd_s <= 0.0 && ms == 0) return t;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      if (!pool.empty()) {
+        t.start = pool.back().first;
+        t.done = pool.back().second;
+        pool.pop_back();
+      }
+    }
+    if (!t.start) {
+      t.start = std::make_shared<Event>();
+      t.done = std::make_shared<Event>();
+    }
+    t.label = label;
+    t.limit = wd_s * limit_mult;
+    (void)hipEventRecord(t.start->e, st);
+    if (ms > 0) launch_comm_stall(ms * 1e-3, st);
+    return t;
+  }
+  void end_track(Tracked &&t, hipStream_t st) {
+    if (!t.start) return;
+    (void)hipEventRecord(t.done->e, st);
+    if (wd_s <= 0.0) {
+      std::lock_guard<std::mutex> g(mu);
+      pool.emplace_back(t.start, t.done);
+      return;
+    }
+    std::lock_guard<std::mutex> g(mu);
+    q.push_back(std::move(t));
+  }
+  void watchdog_loop();
+  void stop_watchdog() {
+    wd_stop.store(true);
+    if (wd.joinable()) wd.join();
   }
 
   unsigned int *ctr_of(int l) const { return ctr + (size_t)l * (kArCtrWords + 8); }
@@ -198,6 +283,51 @@ void rccl_result(Comm *c, ncclResult_t r, const char *what) {
   throw std::runtime_error(msg);
 }
 
+void Comm::watchdog_loop() {
+  (void)hipSetDevice(device);
+  while (!wd_stop.load()) {
+    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    std::string stalled;
+    double waited = 0.0;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      while (!q.empty()) {
+        Tracked &f = q.front();
+        if (hipEventQuery(f.done->e) == hipSuccess) {
+          pool.emplace_back(f.start, f.done);
+          q.pop_front();
+          continue;
+        }
+        if (hipEventQuery(f.start->e) == hipSuccess) {
+          const double t = now_s();
+          if (f.seen < 0.0) f.seen = t;
+          else if (t - f.seen > f.limit) {
+            stalled = f.label;
+            waited = t - f.seen;
+          }
+        }
+        break;   // collectives complete in order on the comm stream
+      }
+      (void)hipGetLastError();
+    }
+    if (stalled.empty()) continue;
+    char msg[512];
+    std::snprintf(msg, sizeof(msg),
+                  "[pgdist] comm watchdog: rank %d of %d: %s started %.1f s ago and has not completed "
+                  "(limit %.1f s): a peer is dead or out of step; aborting the communicator",
+                  rank, world, stalled.c_str(), waited, wd_s);
+    std::fprintf(stderr, "%s\n", msg);
+    std::fflush(stderr);
+    fail(kCommErrStall, msg);
+    if (nccl && rccl().commAbort) (void)rccl().commAbort(nccl);
+    if (wd_exit) {
+      std::fflush(stdout);
+      std::_Exit(wd_exit);
+    }
+    return;   // poisoned: every later collective throws
+  }
+}
+
 }  // namespace
 
 bool rccl_available() { return rccl().h != nullptr; }
@@ -246,10 +376,12 @@ int comm_create(int rank, int world, int device, const std::string &uid, long lo
     std::memcpy(id.internal, uid.data(), sizeof(id.internal));
     ncheck(r.commInitRank(&c->nccl, world, id, rank), "ncclCommInitRank");
   }
-  if (region_bytes > 0) {
+  {   // counters + error word (also without P2P: the optimizer skips its update while it is set)
     const size_t words = (size_t)nlocal * (kArCtrWords + 8);
     hcheck(hipMalloc(reinterpret_cast<void **>(&c->ctr), words * 4), "hipMalloc(counters)");
     hcheck(hipMemset(c->ctr, 0, words * 4), "hipMemset(counters)");
+  }
+  if (region_bytes > 0) {
     for (int l = 0; l < nlocal; ++l) {
       void *p = nullptr;
       hcheck(hipExtMallocWithFlags(&p, (size_t)ar_stage_bytes(region_bytes), hipDeviceMallocUncached),
@@ -322,10 +454,13 @@ void comm_allreduce(int id, const std::vector<uintptr_t> &bufs, long long n, int
     ncclComm_t nc = c.nccl;
     Rccl *r = &rccl();
     Comm *cp = &c;
+    const std::string label = "RCCL all-reduce of " + std::to_string(n) + " floats";
     run_op([=] {
       cp->ensure_usable();
       wait_all(st, wait, ev);
+      Tracked t = cp->begin_track(st, label);
       rccl_result(cp, r->allReduce(b, b, (size_t)n, ncclFloat32, ncclSum, nc, st), "ncclAllReduce");
+      cp->end_track(std::move(t), st);
     });
     return;
   }
@@ -336,10 +471,15 @@ void comm_allreduce(int id, const std::vector<uintptr_t> &bufs, long long n, int
   const int nl = c.nlocal;
   auto cp = std::make_shared<ArCall>(call);
   Comm *comm = &c;
+  const std::string label = std::string(algo == COMM_ONESHOT ? "one-shot" : "two-shot") + " P2P all-reduce of " +
+                            std::to_string(n) + " floats";
   run_op([=] {
     comm->ensure_usable();
     wait_all(st, wait, ev);
+    // the P2P kernels time out by themselves (error word); the watchdog is the backstop
+    Tracked t = comm->begin_track(st, label, 2.0);
     launch_p2p_collective(*cp, nl, st);
+    comm->end_track(std::move(t), st);
   });
 }
 
@@ -356,10 +496,13 @@ void comm_broadcast(int id, const std::vector<uintptr_t> &bufs, long long n, int
     ncclComm_t nc = c.nccl;
     Rccl *r = &rccl();
     Comm *cp = &c;
+    const std::string label = "RCCL broadcast of " + std::to_string(n) + " floats";
     run_op([=] {
       cp->ensure_usable();
       wait_all(st, wait, ev);
+      Tracked t = cp->begin_track(st, label);
       rccl_result(cp, r->broadcast(b, b, (size_t)n, ncclFloat32, root, nc, st), "ncclBroadcast");
+      cp->end_track(std::move(t), st);
     });
     return;
   }
@@ -368,10 +511,13 @@ void comm_broadcast(int id, const std::vector<uintptr_t> &bufs, long long n, int
   auto cp = std::make_shared<ArCall>(c.make_call(bufs, n, AR_BROADCAST, false, root));
   const int nl = c.nlocal;
   Comm *comm = &c;
+  const std::string label = "P2P broadcast of " + std::to_string(n) + " floats";
   run_op([=] {
     comm->ensure_usable();
     wait_all(st, wait, ev);
+    Tracked t = comm->begin_track(st, label, 2.0);
     launch_p2p_collective(*cp, nl, st);
+    comm->end_track(std::move(t), st);
   });
 }
 
@@ -385,11 +531,14 @@ void comm_allreduce_f64(int id, uintptr_t buf, long long n, int op, const std::v
   Rccl *r = &rccl();
   void *b = reinterpret_cast<void *>(buf);
   Comm *cp = &c;
+  const std::string label = "RCCL fp64 all-reduce of " + std::to_string(n) + " doubles";
   run_op([=] {
     cp->ensure_usable();
     wait_all(st, wait, ev);
+    Tracked t = cp->begin_track(st, label);
     rccl_result(cp, r->allReduce(b, b, (size_t)n, ncclFloat64, op == 0 ? ncclSum : ncclMax, nc, st),
                 "ncclAllReduce(f64)");
+    cp->end_track(std::move(t), st);
   });
 }
 
@@ -443,7 +592,7 @@ int comm_error(int id) {
       c.fail(((int)ae & 0xff) << 8, std::string("RCCL async error: ") + rccl().errorString(ae));
     }
   }
-  return err | (c.host_err.load() & kCommErrRccl);
+  return err | (c.host_err.load() & (kCommErrRccl | kCommErrPeer | kCommErrStall));
 }
 
 void comm_poison(int id, const std::string &why) {
@@ -462,12 +611,46 @@ void comm_clear_error(int id) {
     hcheck(hipMemset(c.err_of(l), 0, 4), "hipMemset(error word)");
   hcheck(hipDeviceSynchronize(), "hipDeviceSynchronize");
   c.host_err.store(0);
+  std::lock_guard<std::mutex> g(c.what_mu);
   c.what.clear();
 }
 
 std::string comm_error_string(int id) {
   Comm &c = get(id);
-  return c.host_err.load() ? c.what : std::string();
+  return c.host_err.load() ? c.what_str() : std::string();
+}
+
+namespace {
+void stop_all_watchdogs() {   // before static destruction / HIP teardown at process exit
+  for (auto &kv : comms()) kv.second->stop_watchdog();
+}
+}  // namespace
+
+void comm_set_watchdog(int id, double seconds, int exit_status) {
+  static const bool registered = (std::atexit(stop_all_watchdogs), true);
+  (void)registered;
+  Comm &c = get(id);
+  if (seconds < 0) throw std::invalid_argument("comm_set_watchdog: seconds >= 0");
+  c.stop_watchdog();
+  c.wd_stop.store(false);
+  c.wd_s = seconds;
+  c.wd_exit = exit_status;
+  if (seconds > 0) c.wd = std::thread([cp = &c] { cp->watchdog_loop(); });
+}
+
+double comm_watchdog(int id) { return get(id).wd_s; }
+
+void comm_inject_stall(int id, double seconds) {
+  if (!(seconds > 0) || seconds > 30) throw std::invalid_argument("comm_inject_stall: 0 < seconds <= 30");
+  get(id).stall_ms.store((long long)(seconds * 1e3));
+}
+
+uintptr_t comm_error_word(int id) { return reinterpret_cast<uintptr_t>(get(id).err_of(0)); }
+
+void comm_error_async(int id, uintptr_t host_dst) {
+  Comm &c = get(id);
+  hcheck(hipMemcpyAsync(reinterpret_cast<void *>(host_dst), c.err_of(0), 4, hipMemcpyDeviceToHost, c.stream),
+         "hipMemcpyAsync(error word)");
 }
 
 int comm_rccl_ranks(int id) {
@@ -482,6 +665,7 @@ void comm_destroy(int id) {
   auto it = comms().find(id);
   if (it == comms().end()) return;
   Comm &c = *it->second;
+  c.stop_watchdog();
   (void)hipSetDevice(c.device);
   if (c.stream) (void)hipStreamSynchronize(c.stream);
   if (c.nccl) (void)rccl().commDestroy(c.nccl);

@@ -63,6 +63,7 @@ double comm_time_allreduce(int id, const std::vector<uintptr_t> &bufs, long long
 // RCCL failure at launch; synchronises the comm stream
 constexpr int kCommErrRccl = 1 << 16;
 constexpr int kCommErrPeer = 1 << 17;   // poisoned because ANOTHER rank failed (comm_poison)
+constexpr int kCommErrStall = 1 << 18;  // the watchdog saw a started collective miss its deadline
 int comm_error(int id);
 // poison this rank's communicator because a peer failed (host flag + device error word)
 void comm_poison(int id, const std::string &why);
@@ -71,6 +72,20 @@ void comm_poison(int id, const std::string &why);
 void comm_clear_error(int id);
 std::string comm_error_string(int id);   // what poisoned the communicator ("" if healthy)
 int comm_rccl_ranks(int id);             // ncclCommCount of the RCCL communicator (0: none)
+// watchdog: a collective that started on the comm stream but has not completed `seconds` later
+// (P2P: twice that; their kernels time out by themselves) poisons the communicator, aborts the
+// RCCL communicator and, with exit_status != 0, ends the process with that status (0 s: off)
+void comm_set_watchdog(int id, double seconds, int exit_status);
+double comm_watchdog(int id);
+// fault injection (tests): the next collective's kernel is preceded on the comm stream, after its
+// start marker, by a kernel that spins `seconds` (<= 30)
+void comm_inject_stall(int id, double seconds);
+// device address of this rank's error word (nonzero once a P2P collective failed or the
+// communicator was poisoned): the fused Adam skips its update while it is set
+uintptr_t comm_error_word(int id);
+// copy the error word to pinned host memory on the comm stream, after the collectives issued so
+// far (no synchronisation: the caller reads it one step later)
+void comm_error_async(int id, uintptr_t host_dst);
 void comm_destroy(int id);
 
 }  // namespace pgdist_rt

@@ -186,8 +186,13 @@ class MobileNetV2Executor:
     # (scripts/gpu_r4_aug.sh); 0: none
     FUSE_BLOCK_OUTPUT_HW = int(os.environ.get("PGDIST_FUSE_BLOCK_OUT_HW", "196"))
     STEM_WGRAD_SIDE = os.environ.get("PGDIST_STEM_WGRAD_SIDE", "0") == "1"
-    # fp8 mode: every forward 1x1 conv runs on e4m3 MFMA (weights per output channel, activations
-    # scaled by ops.kernels.FP8_ASC), backward and depthwise/BN stay bf16/fp32
+    # fused inverted-residual block forward (csrc/kernels/irblock.hip) for the stride-1 14x14 /
+    # 7x7 blocks: one persistent launch per block instead of expand GEMM + depthwise + project
+    # GEMM (PGDIST_IR_FUSE=0: the three-launch path)
+    IR_FUSE = os.environ.get("PGDIST_IR_FUSE", "1") == "1"
+    # fp8 mode: the forward 1x1 convs with K >= FP8_MIN_K run on e4m3 MFMA (weights per output
+    # channel, activations scaled by ops.kernels.FP8_ASC); the K = 16 / 24 / 32 expand convs, the
+    # backward and depthwise / BN stay bf16 / fp32
 
     def __init__(self, model: MobileNetV2, batch: int, img_size: int, device: torch.device,
                  flat: Optional[FlatParams] = None, dropout_seed: int = 0,
@@ -267,6 +272,22 @@ class MobileNetV2Executor:
         # BN statistics: one accumulator pair per BN ([rows][2][C] forward and backward, rows =
         # min(producer partial rows, bn_rep)), all in one arena so a training step zeroes them
         # with a single memset
+        # blocks whose training forward runs as one fused launch: stride 1 with expansion on a
+        # <= 14x14 map, input = the previous block's pending output (BN_p (+ residual) applied by
+        # the fused kernel), lazy BN descriptors, bf16, and a co-resident grid on this device
+        self.ir_grid = {}
+        lazy_possible = (not K.deterministic() and os.environ.get("PGDIST_BN_FUSED", "0") != "1"
+                         and os.environ.get("PGDIST_BN_LAZY", "1") == "1")
+        if self.IR_FUSE and lazy_possible and not fp8:
+            for bi, bp in enumerate(self.blocks):
+                prev = self.blocks[bi - 1] if bi > 0 else None
+                if (bp.stride == 1 and bp.expand and bp.H <= 14 and prev is not None
+                        and prev.Ho * prev.Wo <= self.FUSE_BLOCK_OUTPUT_HW):
+                    n = K.ir_fwd_grid(B, bp.H, bp.cin, bp.hidden, bp.cout)
+                    if n > 0:
+                        self.ir_grid[bp.idx] = n
+        self.ir_bar = {i: torch.zeros(96, dtype=torch.int32, device=device) for i in self.ir_grid}
+        self.ir_err = torch.zeros(4, dtype=torch.int32, device=device)
         o, spans = 0, []
         self.bn_rep = K.bn_rep()   # the producers' replica rows the arena is sized for
         for bn, (pf, pb) in self._bn_producer_rows().items():
@@ -375,14 +396,15 @@ class MobileNetV2Executor:
             prev = self.blocks[bi - 1] if bi > 0 else None
             Min, Mout = B * bp.H * bp.H, B * bp.Ho * bp.Wo
             dw_in = bp.bn_e if bp.expand else self.bn0
+            nfused = getattr(self, "ir_grid", {}).get(bp.idx, 0)
             if bp.expand:
-                rows[bp.bn_e][0] = K.pw_num_partials(Min, bp.hidden, bp.cin)
+                rows[bp.bn_e][0] = max(K.pw_num_partials(Min, bp.hidden, bp.cin), nfused)
                 rows[prev.bn_p][1] = (K.pw_bwd_num_partials(Min, bp.hidden, bp.cin)
                                       if self._pw_bwd_ok(Min, bp.hidden, bp.cin)
                                       else K.pw_num_partials(Min, bp.cin, bp.hidden))
-            rows[bp.bn_d][0] = K.dw_num_partials("fwd", B, bp.H, bp.H, bp.hidden, bp.stride)
+            rows[bp.bn_d][0] = max(K.dw_num_partials("fwd", B, bp.H, bp.H, bp.hidden, bp.stride), nfused)
             rows[dw_in][1] = K.dw_num_partials("dgrad", B, bp.H, bp.H, bp.hidden, bp.stride)
-            rows[bp.bn_p][0] = K.pw_num_partials(Mout, bp.cout, bp.hidden)
+            rows[bp.bn_p][0] = max(K.pw_num_partials(Mout, bp.cout, bp.hidden), nfused)
             rows[bp.bn_d][1] = (K.pw_bwd_num_partials(Mout, bp.cout, bp.hidden)
                                 if self._pw_bwd_ok(Mout, bp.cout, bp.hidden)
                                 else K.pw_num_partials(Mout, bp.hidden, bp.cout))
@@ -546,6 +568,15 @@ class MobileNetV2Executor:
         for bp in self.blocks:
             Hin = bp.H
             Min = B * Hin * Hin
+            if train and pend is not None and bp.idx in self.ir_grid:
+                # expand -> dw -> project in one launch (its P0 materialises the pending input o)
+                pbn, pres, po = pend
+                K.ir_fwd(pbn.y, pres, pbn.lz_f, po, f.b(bp.w_e), f.b(bp.w_d), f.b(bp.w_p), bp.bn_e.y, bp.bn_d.y,
+                         bp.bn_p.y, bp.bn_e.desc_f, bp.bn_d.desc_f, bp.bn_p.desc_f, self.ir_bar[bp.idx], self.ir_err,
+                         B, Hin, bp.cin, bp.hidden, bp.cout)
+                pend = (bp.bn_p, inp_t if bp.residual else None, bp.o)
+                inp_bn, inp_t = bp.bn_p, bp.o
+                continue
             if bp.expand:
                 if pend is not None:
                     self._consume_output(pend, f.b(bp.w_e), bp.bn_e.y, bp.bn_e.acc_f, Min, bp.hidden, bp.cin,
@@ -737,6 +768,10 @@ class MobileNetV2Executor:
         self._flush_side()
         if self.side is not None:   # join: the optimizer (main stream) needs every gradient
             K.stream_wait(torch.cuda.current_stream(self.device), self.side)
+
+    def ir_error(self) -> int:
+        """Sticky error word of the fused block kernels (bit 0: a grid barrier timed out)."""
+        return int(self.ir_err[0].item())
 
     # ------------------------------------------------------------------ eval
     def eval_prepare(self):

@@ -17,7 +17,7 @@ import torch.distributed as dist
 from ..models import build_model
 from ..ops import kernels as K
 from ..parallel.comm import NativeComm
-from ..parallel.ddp import BucketedGradReducer, NativeBucketReducer, broadcast_parameters
+from ..parallel.ddp import BucketedGradReducer, NativeBucketReducer, broadcast_parameters, estimate_ready_times
 from .executor import MobileNetV2Executor
 
 
@@ -104,6 +104,8 @@ class NativeTrainStep:
         # | rccl | p2p (IPC xGMI kernels only; also over a gloo default group) | native (both) | c10d
         self.reducer = None
         self.comm = None
+        self._measure_ready = False
+        self.bucket_ready_us = None   # measured gradient ready times (us into the backward)
         self.comm_mode = comm or os.environ.get("PGDIST_COMM", "auto")
         force_ddp = force_ddp or os.environ.get("PGDIST_FORCE_DDP", "0") == "1"
         if world_size > 1 or force_ddp:
@@ -117,9 +119,14 @@ class NativeTrainStep:
             else:
                 self.comm = self._make_comm(mode, world_size)
                 algo = allreduce_algo or os.environ.get("PGDIST_AR_ALGO", "auto")
+                # bucket layout: modelled gradient ready times first, re-chosen from the times
+                # measured on the second warm-up step (_back) before the step is recorded
+                ready = (estimate_ready_times(model, img_size, 3000.0)
+                         if bucket_mb is None and algo == "auto" and world_size > 1 else None)
                 self.reducer = NativeBucketReducer(self.comm, self.flat.grad, ranges, bucket_mb, first_bucket_mb,
                                                    algo=algo, bf16_wire=reduce_dtype == torch.bfloat16,
-                                                   force=force_ddp)
+                                                   force=force_ddp, ready_us=ready, t_bwd_us=3000.0)
+                self._measure_ready = getattr(self.reducer, "tunable", False)
                 self.exe.ready_native = True
             self.exe.on_params_ready = self.reducer.mark_ready
             self.exe.ready_probe = self.reducer.would_launch
@@ -132,6 +139,7 @@ class NativeTrainStep:
             self.bn_flat, self.bn_nbt = coalesce_bn_buffers(self.exe.model)
             if hasattr(self.exe, "refresh_bn_fin"):
                 self.exe.refresh_bn_fin()   # fused BN finalize: descriptors point at the re-homed buffers
+        self._validate_collectives()
         # RCCL collectives are issued eagerly between graph segments; a single-graph
         # capture is used on one GPU
         self.use_graph = use_graph and world_size == 1
@@ -176,6 +184,13 @@ class NativeTrainStep:
             self._labs = [self.exe.labels, torch.empty_like(self.exe.labels)]
             self._idxs = [self.idx, torch.empty_like(self.idx)]
             self._prms = [self.aug_params, torch.empty_like(self.aug_params)]
+
+    def _validate_collectives(self):
+        """The step's P2P collectives at their real sizes, back to back with the per-step BN
+        broadcast (collective: every rank), before any training step (and again after a retune)."""
+        if isinstance(self.reducer, NativeBucketReducer) and self.world > 1:
+            bcast = self.bn_flat.numel() if getattr(self, "bn_broadcast", False) else 0
+            self.reducer.validate_layout(bcast)
 
     @staticmethod
     def _fault_names(model):
@@ -337,17 +352,62 @@ class NativeTrainStep:
             self.reducer.begin()
         elif self.reducer is not None:
             K.plan_py(self.reducer.begin)
-        exe.backward()
+        probe = self._measure_ready and self._eager_runs == 2 and not K.plan_recording()
+        if probe:
+            t_ready, orig = [], exe.on_params_ready
+            cur = torch.cuda.current_stream(self.device)
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev0.record(cur)
+
+            def on_ready(names, orig=orig, cur=cur):
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record(cur)
+                t_ready.append((list(names), ev))
+                orig(names)
+            exe.on_params_ready = on_ready
+        try:
+            exe.backward()
+        finally:
+            if probe:
+                exe.on_params_ready = orig
+        if probe:
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev1.record(torch.cuda.current_stream(self.device))
         if native:
             self.reducer.finish()
         elif self.reducer is not None:
             K.plan_py(self.reducer.finish)
         for a, b in self.fault_zero:
             K.memset(self.flat.grad[a:b])
+        # a failed / poisoned gradient collective leaves its error word set: Adam then skips the
+        # update, so no replica applies un-reduced gradients (the job fails at the next check)
         K.adam_flat(self.flat.master, self.flat.grad, self.flat.exp_avg, self.flat.exp_avg_sq,
                     self.flat.shadow, self.hyper, self.betas[0], self.betas[1], self.eps, self.wd,
-                    1.0 / self.world)
+                    1.0 / self.world, skip=self.comm.error_word if self.comm is not None else 0)
         K.reduce_metrics(exe.loss, exe.correct, self.B, self.metrics)
+        if probe:
+            self._retune_buckets(t_ready, ev0, ev1)
+
+    def _retune_buckets(self, t_ready, ev0, ev1):
+        """Gradient ready times measured on this (eager warm-up) step -> the bucket layout of the
+        recorded step: MAX over ranks (every rank must choose the same buckets), then
+        NativeBucketReducer.retune (collective)."""
+        from ..parallel.comm import host_allreduce
+        torch.cuda.synchronize(self.device)
+        names = [n for n, _, _ in self.reducer._ranges]
+        at = {}
+        for ns, ev in t_ready:
+            t = ev0.elapsed_time(ev) * 1e3
+            for n in ns:
+                at[n] = t
+        t_bwd = ev0.elapsed_time(ev1) * 1e3
+        vec = torch.tensor([at.get(n, t_bwd) for n in names] + [t_bwd], dtype=torch.float64)
+        vec = host_allreduce(vec, dist.ReduceOp.MAX)
+        ready = {n: float(v) for n, v in zip(names, vec[:-1].tolist())}
+        self.bucket_ready_us = ready
+        self.reducer.retune(ready, float(vec[-1]))
+        self._measure_ready = False
+        self._validate_collectives()
 
     def run(self, idx: torch.Tensor, next_idx: Optional[torch.Tensor] = None):
         """One training step (on the high-priority critical-path stream when PGDIST_MAIN_PRIO=1:

@@ -198,8 +198,17 @@ class Trainer:
         if self.backend == "hip":
             didx = torch.from_numpy(idx).to(self.device)
             self.step.metrics.zero_()
+            comm = getattr(self.step, "comm", None)
             with trace_range(f"train_epoch_{epoch}", prof):
                 for b in range(nb):
+                    # per-step failure check without a host sync: the communicator's error word
+                    # copied one step earlier (a failed step's Adam update was skipped on device)
+                    if comm is not None and comm.world > 1:
+                        err = comm.poll_error()
+                        if err:
+                            from ..parallel.comm import CommError
+                            raise CommError(f"native communicator error 0x{err:x} on rank {self.rank} before "
+                                            f"epoch {epoch + 1} batch {b}: {comm.error_string() or 'P2P failure'}")
                     sl = didx[b * bs:(b + 1) * bs]
                     # the next batch (augmented during this step's backward when it is full-size)
                     nxt = didx[(b + 1) * bs:(b + 2) * bs] if b + 1 < nb else None

@@ -184,14 +184,16 @@ def bn_apply(y, scale, shift, out, relu6=False, res=None, lz=None):
 
 
 # --------------------------------------------------------------------------- optimizer
-def adam_flat(p, g, m, v, pb, hyper, beta1, beta2, eps, weight_decay=0.0, grad_scale=1.0):
+def adam_flat(p, g, m, v, pb, hyper, beta1, beta2, eps, weight_decay=0.0, grad_scale=1.0, skip=0):
+    """Fused Adam over the flat buffers.  ``skip``: device address of a data-parallel
+    communicator's error word (NativeComm.error_word) -- the update is skipped while it is set."""
     n = p.numel()
     assert n % 4 == 0 and g.numel() == n and m.numel() == n and v.numel() == n
     for t, nm in ((p, "p"), (g, "g"), (m, "m"), (v, "v")):
         _chk(t, F32, n, nm)
     _chk(pb, BF16, n, "pb")
     lib().adam_flat(_p(p), _p(g), _p(m), _p(v), _p(pb), n, _p(hyper), float(beta1), float(beta2),
-                    float(eps), float(weight_decay), float(grad_scale), _s())
+                    float(eps), float(weight_decay), float(grad_scale), int(skip), _s())
 
 
 def f32_to_bf16(x, y):
@@ -356,6 +358,43 @@ def pw_gemm(pro, epi, A, W, out, part, M, N, K, A2=None, pa=None, pb=None, pc=No
     _arm_lz(lz)
     lib().pw_gemm(int(pro), int(epi), _p(A), _p(A2), _p(pa), _p(pb), _p(pc), _p(W), _p(out), _p(Yt),
                   _p(es), _p(et), _p(R), _p(part), M, N, K, _p(Aout), _s())
+
+
+# --------------------------------------------------------------------------- fused block
+def ir_fwd_grid(B, H, cin, ch, cout):
+    """Workgroups of the fused inverted-residual block forward (csrc/kernels/irblock.hip) for B
+    images of an HxH map, or 0 when the shape has no fused kernel or its grid would not be
+    co-resident on this device (the kernel's grid barriers need every workgroup resident)."""
+    return lib().ir_fwd_grid(int(B), int(H), int(cin), int(ch), int(cout))
+
+
+def ir_fwd(xin, res, lz_in, xout, we, wd, wp, h1, h2, y, de, dd, dp, bar, err, B, H, cin, ch, cout):
+    """One training-mode MobileNetV2 inverted-residual block forward (stride 1, expand 6) in one
+    launch: input = BN_p(xin) (+ res) via the lazy descriptor ``lz_in`` (materialised into
+    ``xout``), expand -> BN_e -> ReLU6 -> dw 3x3 -> BN_d -> ReLU6 -> project; raw h1 / h2 / y
+    and the statistics of BN_e / BN_d / BN_p (descriptors ``de`` / ``dd`` / ``dp``, whose
+    accumulators must be zero and have ``rows`` = min(grid, bn_rep())) exactly as the unfused
+    kernels write them.  ``bar``: 96 int32, zero before the first launch (the kernel re-arms them), ``err``: sticky
+    error word (bit 0: a grid barrier timed out)."""
+    M = B * H * H
+    _chk(xin, BF16, M * cin, "xin")
+    _chk(res, BF16, M * cin, "res")
+    _chk(xout, BF16, M * cin, "xout")
+    _chk(we, BF16, ch * cin, "we")
+    _chk(wd, BF16, 9 * ch, "wd")
+    _chk(wp, BF16, cout * ch, "wp")
+    _chk(h1, BF16, M * ch, "h1")
+    _chk(h2, BF16, M * ch, "h2")
+    _chk(y, BF16, M * cout, "y")
+    _chk(bar, torch.int32, 96, "bar")
+    _chk(err, torch.int32, 1, "err")
+    for d in (lz_in, de, dd, dp):
+        if d is None or not (d.is_cuda and d.dtype == torch.uint8):
+            raise TypeError("ir_fwd: BN descriptors from bn_fin_desc")
+    if ir_fwd_grid(B, H, cin, ch, cout) <= 0:
+        raise ValueError(f"ir_fwd: no co-resident fused kernel for B={B} H={H} {cin}->{ch}->{cout}")
+    lib().ir_fwd(_p(xin), _p(res), _p(lz_in), _p(xout), _p(we), _p(wd), _p(wp), _p(h1), _p(h2), _p(y),
+                 _p(de), _p(dd), _p(dp), _p(bar), _p(err), B, H, cin, ch, cout, _s())
 
 
 FP8 = torch.uint8   # raw OCP e4m3fn bytes (torch.float8_e4m3fn views share the encoding)
@@ -1073,7 +1112,7 @@ def _logged(fn):
 
 for _name in ("bn_fwd_finalize", "bn_bwd_finalize", "bn_apply", "bn_finalize_batch", "adam_flat", "f32_to_bf16",
               "step_begin", "reduce_metrics", "dw_fwd", "dw_dgrad", "dw_wgrad", "pw_gemm", "pw_gemm_f8", "w8_quant",
-              "wt_transpose", "pw_bwd", "wgrad_reduce", "wgrad_reduce_flush", "pw_wgrad", "stem_fwd", "stem_wgrad",
+              "wt_transpose", "pw_bwd", "ir_fwd", "wgrad_reduce", "wgrad_reduce_flush", "pw_wgrad", "stem_fwd", "stem_wgrad",
               "head", "augment", "conv_fwd", "conv_dgrad", "conv_wgrad", "bn_mat", "conv_wt", "res_out", "maxpool_fwd",
               "maxpool_bwd", "avgpool", "head_bwd", "softmax_ce", "fc_gemm", "col_sum", "image_prep", "memset"):
     globals()[_name] = _logged(globals()[_name])

@@ -76,14 +76,19 @@ class NativeComm:
     must be on this node).  ``nlocal == world`` builds the single-process emulation of
     ``world`` ranks on one GPU (P2P only)."""
 
+    # process exit status when the watchdog finds a stalled collective (EX_TEMPFAIL)
+    STALL_EXIT = 75
+
     def __init__(self, rank: int, world: int, device: torch.device, store=None, use_rccl: bool = True,
                  p2p_bytes: int = 0, blocks: Optional[int] = None, timeout_s: Optional[float] = None,
-                 emulate: bool = False, tag: Optional[str] = None):
+                 emulate: bool = False, tag: Optional[str] = None, watchdog_s: Optional[float] = None):
         self.rank, self.world, self.device = rank, world, device
         self.emulated = emulate
         self.nlocal = world if emulate else 1
         blocks = blocks or int(os.environ.get("PGDIST_P2P_BLOCKS", "32"))
-        timeout_s = timeout_s or float(os.environ.get("PGDIST_P2P_TIMEOUT", "60"))
+        # PGDIST_COMM_TIMEOUT (s): a P2P barrier gives up after it; the watchdog aborts an RCCL
+        # collective that has not completed that long after it started (P2P ones: twice that)
+        timeout_s = timeout_s or float(os.environ.get("PGDIST_COMM_TIMEOUT", "60"))
         region = (int(p2p_bytes) + 255) // 256 * 256
         tag = tag or f"pgdist/comm/{next(_SEQ)}"
         uid = b""
@@ -127,6 +132,13 @@ class NativeComm:
                 elif self.p2p_error is None:
                     self.p2p_error = "a peer could not export its staging buffer"
         self.stream = torch.cuda.ExternalStream(lib().comm_stream(self.id), device=device)
+        # the comm watchdog: on by default for a real multi-rank job (a dead peer inside an RCCL
+        # collective would otherwise hang every rank), off for world 1 / the one-process emulation
+        if watchdog_s is None:
+            watchdog_s = self.timeout_s if (world > 1 and not emulate) else 0.0
+        self.set_watchdog(watchdog_s)
+        self._err_host = torch.zeros(1, dtype=torch.int32).pin_memory() if device.type == "cuda" else None
+        self._err_polled = False
 
     # ------------------------------------------------------------------ factory
     @classmethod
@@ -206,6 +218,38 @@ class NativeComm:
             raise CommError(f"native communicator failed (error 0x{worst:x}, reported by rank {who}){mine}")
         return 0
 
+    # ------------------------------------------------------------------ failure detection
+    def set_watchdog(self, seconds: float, exit_status: Optional[int] = None):
+        """Watchdog deadline (s; 0 = off): a collective that started on the comm stream and has not
+        completed ``seconds`` later (P2P: twice that) prints which one, poisons the communicator,
+        calls ncclCommAbort and ends the process with ``exit_status`` (default STALL_EXIT; 0:
+        poison and abort only)."""
+        code = self.STALL_EXIT if exit_status is None else int(exit_status)
+        lib().comm_set_watchdog(self.id, float(seconds), code)
+
+    @property
+    def watchdog_s(self) -> float:
+        return lib().comm_watchdog(self.id)
+
+    def inject_stall(self, seconds: float):
+        """Fault injection: the next collective is preceded on the comm stream (after its start
+        marker) by a kernel that spins ``seconds`` -- what a dead peer looks like to the watchdog."""
+        lib().comm_inject_stall(self.id, float(seconds))
+
+    @property
+    def error_word(self) -> int:
+        """Device address of this rank's error word (the fused Adam skips its update while set)."""
+        return lib().comm_error_word(self.id)
+
+    def poll_error(self) -> int:
+        """Cheap per-step failure check, no synchronisation: returns the error word copied
+        asynchronously by the PREVIOUS call (0 on the first) and enqueues the next copy on the comm
+        stream behind the collectives issued so far."""
+        v = int(self._err_host[0]) if self._err_polled else 0
+        lib().comm_error_async(self.id, self._err_host.data_ptr())
+        self._err_polled = True
+        return v
+
     def rccl_ranks(self) -> int:
         """Ranks of the RCCL communicator (ncclCommCount), 0 without one."""
         return lib().comm_rccl_ranks(self.id) if self.has_rccl else 0
@@ -275,6 +319,50 @@ class NativeComm:
         finally:
             self.set_timeout(keep)
         return True
+
+    def validate_layout(self, sizes: Sequence[int], algos: Sequence[str], bf16_wire: bool = False,
+                        bcast_n: int = 0, timeout_s: float = 5.0) -> bool:
+        """The training step's own collectives at their real sizes, issued back to back as the
+        step issues them: one all-reduce per bucket (``sizes`` / ``algos``; P2P buckets only --
+        RCCL validates itself) followed by the per-step BN-buffer broadcast of ``bcast_n`` floats,
+        each checked against an exact integer pattern.  True on every rank iff every result is
+        exact on every rank (agreement over the default process group)."""
+        p2p = [(n, a) for n, a in zip(sizes, algos) if a in ("oneshot", "twoshot")]
+        if self.emulated or not self.has_p2p or (not p2p and not bcast_n):
+            return True
+        keep = self.timeout_s
+        self.set_timeout(timeout_s)
+        ok = True
+        try:
+            bufs, exps = [], []
+            for n, a in p2p:
+                base = torch.arange(n, device=self.device, dtype=torch.float32).remainder_(7)
+                t = base + (self.rank + 1)
+                self.allreduce(t, a, bf16_wire)
+                bufs.append(t)
+                exps.append(base * self.world + self.world * (self.world + 1) / 2)
+            if bcast_n:
+                pat = torch.arange(bcast_n, device=self.device, dtype=torch.float32).remainder_(11)
+                t = pat + 1 if self.rank == 0 else torch.full_like(pat, -1.0)
+                self.broadcast(t, 0, "oneshot")
+                bufs.append(t)
+                exps.append(pat + 1)
+            self.join()
+            torch.cuda.synchronize(self.device)
+            err = self.error()
+            if err:
+                self.p2p_error = f"error 0x{err:x}: {self.error_string()}"
+            ok = err == 0 and all(torch.equal(b, e) for b, e in zip(bufs, exps))
+            if not ok and self.p2p_error is None:
+                self.p2p_error = "a bucket-sized P2P collective miscomputed"
+        except Exception as e:   # noqa: BLE001 - reported, then agreed on
+            self.p2p_error, ok = repr(e), False
+        finally:
+            self.set_timeout(keep)
+        ok = self._agree(ok)
+        if not ok:
+            lib().comm_clear_error(self.id)
+        return ok
 
     def autotune(self, sizes: Sequence[int], candidates: Optional[Sequence[str]] = None, bf16_wire=False,
                  iters: int = 10, measure: bool = False) -> Dict[int, str]:

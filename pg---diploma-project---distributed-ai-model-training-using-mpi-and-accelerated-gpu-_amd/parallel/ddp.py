@@ -32,8 +32,19 @@ import torch.distributed as dist
 
 
 def build_buckets(ranges: Sequence[Tuple[str, int, int]], cap_bytes: int, first_cap_bytes: int,
-                  elem_size: int = 4) -> List[Tuple[int, int, List[str]]]:
-    """Greedy contiguous bucketing of (name, start, end) ranges given in buffer order."""
+                  elem_size: int = 4, last_cap_bytes: int = 0) -> List[Tuple[int, int, List[str]]]:
+    """Greedy contiguous bucketing of (name, start, end) ranges given in buffer order.
+
+    ``last_cap_bytes`` > 0: the trailing ranges that fit in it (at least one) form a last bucket
+    of their own -- the stem side of the network, whose gradients are final only at the very
+    end of the backward, so that bucket's all-reduce is exposed and should be small."""
+    ranges = list(ranges)
+    tail: List[Tuple[str, int, int]] = []
+    if last_cap_bytes > 0 and len(ranges) > 1:
+        k = len(ranges) - 1
+        while k > 1 and (ranges[-1][2] - ranges[k - 1][1]) * elem_size <= last_cap_bytes:
+            k -= 1
+        ranges, tail = ranges[:k], ranges[k:]
     buckets: List[Tuple[int, int, List[str]]] = []
     cur_names: List[str] = []
     cur_start: Optional[int] = None
@@ -49,7 +60,82 @@ def build_buckets(ranges: Sequence[Tuple[str, int, int]], cap_bytes: int, first_
             cur_names, cur_start = [], None
     if cur_names:
         buckets.append((cur_start, cur_end, cur_names))
+    if tail:
+        buckets.append((tail[0][1], tail[-1][2], [n for n, _, _ in tail]))
     return buckets
+
+
+# main-stream cost of one bucket launch (us): the side-stream join and the event waits of the
+# collective put barrier packets on the main stream (~5-8 us of idle each, docs/PERF_NOTES.md)
+BUCKET_JOIN_US = 8.0
+
+
+def simulate_buckets(buckets, ready_us: Dict[str, float], t_bwd_us: float, t_ar,
+                     join_us: float = BUCKET_JOIN_US) -> float:
+    """Exposed data-parallel cost (us) of a bucket layout: bucket b's all-reduce starts when its
+    last gradient is final (``ready_us``: offset from the backward's start) and the comm stream is
+    free, and takes ``t_ar(elements)``; what runs past the end of the backward (``t_bwd_us``) is
+    exposed, and every bucket launch costs the main stream ``join_us``.  This is the quantity
+    the bucket size trades off: small buckets start early (overlap) but each pays a launch."""
+    t = 0.0
+    for s, e, names in buckets:
+        r = max((ready_us.get(n, t_bwd_us) for n in names), default=t_bwd_us)
+        t = max(r, t) + join_us + t_ar(e - s)
+    return max(0.0, t - t_bwd_us) + join_us * len(buckets)
+
+
+BUCKET_CAPS_MB = (0.25, 0.5, 1.0, 2.0, 4.0, 8.0, 16.0, 32.0)
+LAST_CAPS_MB = (0.0, 0.125, 0.25, 0.5, 1.0, 1.5)
+
+
+def candidate_layouts(ranges, first_mb: float, grad_mb: float, aligned=lambda b: b):
+    """{(cap MiB, last cap MiB): buckets} over the candidate grid (caps up to twice the gradient)."""
+    out = {}
+    for c in BUCKET_CAPS_MB:
+        if c > 2 * max(grad_mb, 0.25):
+            continue
+        for lc in LAST_CAPS_MB:
+            out[(c, lc)] = aligned(build_buckets(ranges, int(c * 2 ** 20), int(first_mb * 2 ** 20),
+                                                 last_cap_bytes=int(lc * 2 ** 20)))
+    return out
+
+
+def choose_layout(cands, ready_us, t_bwd_us, t_ar, join_us: float = BUCKET_JOIN_US):
+    """(cost table, best key): the candidate with the least simulated exposed cost (ties: fewer
+    buckets, then the larger cap)."""
+    cost = {k: simulate_buckets(b, ready_us, t_bwd_us, t_ar, join_us) for k, b in cands.items()}
+    best = min(cost, key=lambda k: (round(cost[k], 3), len(cands[k]), -k[0], -k[1]))
+    return cost, best
+
+
+def estimate_ready_times(model: torch.nn.Module, img_size: int, t_bwd_us: float) -> Dict[str, float]:
+    """Model of when every parameter's gradient becomes final during the backward (us after its
+    start), used to size the gradient buckets before the step can be measured: the backward
+    visits the layers in reverse forward order and a layer costs ~ its input + output activation
+    elements (the network is memory-bound on MI355X).  Shapes from one forward of
+    a CPU copy at a quarter of the resolution (every map scales alike)."""
+    import copy
+    m = copy.deepcopy(model).cpu().float().eval()
+    order: List[Tuple[str, float]] = []
+    hooks = []
+    for name, mod in m.named_modules():
+        if any(True for _ in mod.parameters(recurse=False)):
+            def hook(mod_, inp, out, name=name):
+                n_in = sum(t.numel() for t in inp if torch.is_tensor(t))
+                order.append((name, float(n_in + out.numel())))
+            hooks.append(mod.register_forward_hook(hook))
+    S = max(32, (img_size // 4 + 31) // 32 * 32)
+    with torch.no_grad():
+        m(torch.zeros(1, 3, S, S))
+    for h in hooks:
+        h.remove()
+    total = sum(c for _, c in order) or 1.0
+    ready, acc = {}, 0.0
+    for name, c in reversed(order):
+        acc += c
+        for pn, _ in dict(m.named_modules())[name].named_parameters(recurse=False):
+            ready[f"{name}.{pn}" if name else pn] = acc / total * t_bwd_us
+    return ready
 
 
 def auto_bucket_mb(grad_bytes: int) -> float:
@@ -169,8 +255,10 @@ class NativeBucketReducer(BucketedGradReducer):
 
     def __init__(self, comm, flat_grad: torch.Tensor, ranges: Sequence[Tuple[str, int, int]],
                  bucket_cap_mb: Optional[float] = None, first_bucket_mb: float = 1.0, algo: str = "auto",
-                 bf16_wire: bool = False, force: bool = False):
+                 bf16_wire: bool = False, force: bool = False, ready_us: Optional[Dict[str, float]] = None,
+                 t_bwd_us: Optional[float] = None):
         tune_cap = bucket_cap_mb is None
+        self.last_bucket_mb = 0.0
         super().__init__(flat_grad, ranges, bucket_cap_mb, first_bucket_mb)
         self.comm = comm
         self.world = comm.world
@@ -192,12 +280,14 @@ class NativeBucketReducer(BucketedGradReducer):
                 # bf16 rounding of the summands; twice the bytes)
                 print("[pgdist] bf16 gradient wire needs the P2P path: reducing fp32 over RCCL instead", flush=True)
                 bf16_wire = self.bf16_wire = False
-            if comm.world > 1 and tune_cap and os.environ.get("PGDIST_BUCKET_TUNE", "1") == "1":
-                self._tune_bucket_cap(bf16_wire)
+            self.tunable = comm.world > 1 and tune_cap and os.environ.get("PGDIST_BUCKET_TUNE", "1") == "1"
+            if self.tunable:
+                self._tune_bucket_cap(bf16_wire, ready_us, t_bwd_us)
                 sizes = [e - s for s, e, _ in self.buckets]
             choice = comm.autotune(sizes, bf16_wire=bf16_wire) if comm.world > 1 else {}
             self.algos = [choice.get(sz, "rccl" if comm.has_rccl else "oneshot") for sz in sizes]
         else:
+            self.tunable = False
             self.algos = [algo] * len(sizes)
         if bf16_wire and "rccl" in self.algos:
             raise ValueError("bf16 wire format: P2P algorithms only")
@@ -209,25 +299,57 @@ class NativeBucketReducer(BucketedGradReducer):
         return [(s, n if i == len(buckets) - 1 else min(n, (e + 63) // 64 * 64), names)
                 for i, (s, e, names) in enumerate(buckets)]
 
-    def _tune_bucket_cap(self, bf16_wire: bool):
-        """Bucket size from measurements on this node (the cap was a heuristic).
-        Candidate caps 0.5 .. 32 MiB (the first bucket keeps ``first_bucket_mb``); every bucket
-        size of every candidate is timed with every algorithm (NativeComm.autotune: MAX over ranks,
-        so every rank scores identically) and a candidate costs the sum of its buckets' best
-        all-reduce times plus its LAST bucket's time once more (that one is exposed after the
-        backward; the others overlap it).  The cheapest candidate wins."""
+    def _tune_bucket_cap(self, bf16_wire: bool, ready_us: Optional[Dict[str, float]] = None,
+                         t_bwd_us: Optional[float] = None):
+        """Bucket layout from measurements on this node, scored by EXPOSED communication
+        (:func:`simulate_buckets`): every bucket size of every candidate
+        layout (cap x last-bucket cap, :func:`candidate_layouts`) is timed with every algorithm
+        (NativeComm.autotune: MAX over ranks, so every rank scores identically), the layouts are
+        simulated against the gradients' ready times (``ready_us``: measured by
+        NativeTrainStep on a warm-up step, else :func:`estimate_ready_times` or a uniform model)
+        and the one with the least exposed time wins."""
         grad_mb = self.grad.numel() * 4 / 2 ** 20
-        caps = sorted({c for c in (0.5, 1.0, 2.0, 4.0, 8.0, 16.0, 32.0, self.bucket_cap_mb) if c <= 2 * grad_mb})
-        cands = {c: self._aligned(build_buckets(self._ranges, int(c * 2 ** 20), int(self._first_mb * 2 ** 20)))
-                 for c in caps}
+        cands = candidate_layouts(self._ranges, self._first_mb, grad_mb, self._aligned)
         sizes = sorted({e - s for b in cands.values() for s, e, _ in b})
-        self.comm.autotune(sizes, bf16_wire=bf16_wire, iters=5, measure=True)
-        best = {sz: min(t.values()) for sz, t in self.comm.tuning.items()}
-        cost = {c: sum(best[e - s] for s, e, _ in b) + best[b[-1][1] - b[-1][0]] for c, b in cands.items()}
-        cap = min(cost, key=lambda c: (cost[c], c))
-        self.bucket_tuning = {str(c): round(v, 1) for c, v in cost.items()}
-        self.bucket_cap_mb = cap
-        self._set_buckets(cands[cap])
+        missing = [sz for sz in sizes if sz not in getattr(self.comm, "tuning", {}) or {}]
+        if missing:
+            self.comm.autotune(sizes, bf16_wire=bf16_wire, iters=5, measure=True)
+        best_t = {sz: min(t.values()) for sz, t in self.comm.tuning.items()}
+        if ready_us is None:
+            # uniform model: parameters become ready evenly over a backward of 3 ms
+            n = max(1, len(self._ranges))
+            t_bwd_us = 3000.0
+            ready_us = {name: (i + 1) / n * t_bwd_us for i, (name, _, _) in enumerate(self._ranges)}
+        cost, key = choose_layout(cands, ready_us, float(t_bwd_us), lambda n: best_t[n])
+        self.bucket_tuning = {f"{c}/{lc}": round(v, 1) for (c, lc), v in cost.items()}
+        self.bucket_cap_mb, self.last_bucket_mb = key
+        self._set_buckets(cands[key])
+
+    def retune(self, ready_us: Dict[str, float], t_bwd_us: float):
+        """Re-choose the bucket layout from MEASURED gradient ready times (collective: every
+        rank calls it with the same, rank-agreed values) and re-pick the algorithms."""
+        self._tune_bucket_cap(self.bf16_wire, ready_us, t_bwd_us)
+        sizes = [e - s for s, e, _ in self.buckets]
+        choice = self.comm.autotune(sizes, bf16_wire=self.bf16_wire) if self.comm.world > 1 else {}
+        self.algos = [choice.get(sz, "rccl" if self.comm.has_rccl else "oneshot") for sz in sizes]
+
+    def validate_layout(self, bcast_n: int = 0):
+        """Check the chosen buckets' P2P collectives (and the BN broadcast) at their real sizes on
+        every rank; on a failure every rank falls back to RCCL for every bucket (or raises
+        without RCCL)."""
+        if not (self.comm.world > 1 and getattr(self.comm, "has_p2p", False)):
+            return True
+        sizes = [e - s for s, e, _ in self.buckets]
+        if self.comm.validate_layout(sizes, self.algos, self.bf16_wire, bcast_n):
+            return True
+        if not self.comm.has_rccl or self.bf16_wire:
+            raise RuntimeError(f"P2P collectives failed validation at the bucket sizes ({self.comm.p2p_error}) "
+                               "and RCCL cannot take over")
+        print(f"[pgdist] P2P collectives failed validation at the bucket sizes ({self.comm.p2p_error}): "
+              "RCCL for every bucket", flush=True)
+        self.comm.has_p2p = False
+        self.algos = ["rccl"] * len(sizes)
+        return False
 
     @property
     def enabled(self) -> bool:

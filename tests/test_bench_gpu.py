@@ -25,7 +25,7 @@ def _port():
 
 
 def _bench(extra_env, steps=4, timeout=240):
-    env = dict(os.environ, PGDIST_DIST_BACKEND="gloo", PGDIST_COMM="p2p", PGDIST_P2P_TIMEOUT="4")
+    env = dict(os.environ, PGDIST_DIST_BACKEND="gloo", PGDIST_COMM="p2p", PGDIST_COMM_TIMEOUT="4")
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE"):
         env.pop(k, None)
     env.update(extra_env)

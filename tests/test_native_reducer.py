@@ -100,10 +100,10 @@ def test_world1_reducer_only_runs_when_forced(monkeypatch):
     assert [x[0] for x in comm.log] == ["ar"] * len(red.buckets) + ["join"]
 
 
-def test_bucket_cap_tuned_from_measured_times(monkeypatch):
-    """bucket_cap_mb=None: candidate caps are scored by the measured all-reduce times (sum of
-    the buckets' best times + the exposed last bucket) and the cheapest wins; with a
-    latency-dominated cost model the choice is neither the smallest nor the largest cap."""
+def test_bucket_layout_minimises_simulated_exposed_time(monkeypatch):
+    """bucket_cap_mb=None: every (cap, last-bucket cap) layout is scored by the simulated exposed
+    communication (parallel/ddp.py simulate_buckets) from the measured all-reduce times and the
+    gradients' ready times; the cheapest wins and the buckets still tile the buffer."""
     monkeypatch.setattr(torch.cuda, "current_stream", _FakeStreamModule.current_stream)
     big, o = [], 0
     for i in range(30):                                                # ~ 1.7e7 elements (~66 MB)
@@ -113,12 +113,59 @@ def test_bucket_cap_tuned_from_measured_times(monkeypatch):
     n = o
     comm = FakeComm()
     red = NativeBucketReducer(comm, torch.zeros(n), big, bucket_cap_mb=None, first_bucket_mb=1.0)
-    assert red.bucket_tuning and len(red.bucket_tuning) >= 4
-    costs = {float(c): v for c, v in red.bucket_tuning.items()}
-    assert costs[red.bucket_cap_mb] == min(costs.values())
-    assert min(costs) < red.bucket_cap_mb < max(costs)
+    assert red.bucket_tuning and len(red.bucket_tuning) >= 8
+    key = f"{red.bucket_cap_mb}/{red.last_bucket_mb}"
+    assert red.bucket_tuning[key] == min(red.bucket_tuning.values())
     prev = 0
     for s, e, _ in red.buckets:
         assert s == prev and s % 64 == 0
         prev = e
     assert prev == n
+
+
+def _mnv2_ranges():
+    from pgdist.engine.flat import FlatParams
+    from pgdist.models import mobilenet_v2
+    torch.manual_seed(0)
+    model = mobilenet_v2(10)
+    flat = FlatParams(model, torch.device("cpu"))
+    return model, flat, [(nm,) + flat.range_of(nm) for nm in flat.order]
+
+
+def test_mobilenet_layout_overlaps_the_backward():
+    """with a latency-dominated all-reduce (25 us + 60 GB/s) and a 3 ms backward
+    whose gradients become ready as the MobileNetV2 backward visits its layers, the chosen
+    layout has >= 3 buckets and a last (exposed) bucket <= 1.5 MiB -- the old objective (sum of
+    all bucket times + the last) chose 2 buckets, the second holding ~80 % of the gradient and
+    ready only at the very end of the backward."""
+    from pgdist.parallel.ddp import (build_buckets, candidate_layouts, choose_layout, estimate_ready_times,
+                                     simulate_buckets)
+    model, flat, ranges = _mnv2_ranges()
+    ready = estimate_ready_times(model, 224, 3000.0)
+    assert set(ready) == {nm for nm, _, _ in ranges}
+    assert ready["classifier.1.weight"] < ready["features.18.0.weight"] < ready["features.0.0.weight"]
+    t_ar = lambda n: 25.0 + n * 4 / 60e3   # noqa: E731  (us)
+    cands = candidate_layouts(ranges, 1.0, flat.numel * 4 / 2 ** 20)
+    cost, key = choose_layout(cands, ready, 3000.0, t_ar)
+    best = cands[key]
+    assert len(best) >= 3, (key, [(e - s) * 4 / 2 ** 20 for s, e, _ in best])
+    s, e, _ = best[-1]
+    assert (e - s) * 4 <= 1.5 * 2 ** 20
+    # the old objective's pick (8 MiB cap, no tail bucket) exposes more communication
+    old = build_buckets(ranges, 8 << 20, 1 << 20)
+    assert len(old) == 2
+    assert simulate_buckets(old, ready, 3000.0, t_ar) > cost[key] + 50.0
+
+
+def test_retune_from_measured_ready_times(monkeypatch):
+    """A measured ready-time table replaces the model: retune re-chooses the layout and the
+    per-bucket algorithms from it (collective on the real communicator)."""
+    monkeypatch.setattr(torch.cuda, "current_stream", _FakeStreamModule.current_stream)
+    model, flat, ranges = _mnv2_ranges()
+    comm = FakeComm()
+    red = NativeBucketReducer(comm, torch.zeros(flat.numel), ranges, bucket_cap_mb=None, first_bucket_mb=1.0)
+    # everything final only at the end of a 100 us backward: one big bucket is best
+    late = {nm: 100.0 for nm, _, _ in ranges}
+    red.retune(late, 100.0)
+    assert len(red.buckets) <= 2
+    assert len(red.algos) == len(red.buckets)
