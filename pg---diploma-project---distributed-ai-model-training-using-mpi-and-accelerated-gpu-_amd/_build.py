@@ -45,7 +45,7 @@ def _pybind_includes():
 def _flags():
     common = ["-O3", "-std=c++17", "-fPIC", "-I" + CSRC, "-Wno-unused-result"]
     # extra preprocessor defines for same-box A/B builds of a variant copy (e.g.
-    # PGDIST_DEFINES="PGDIST_PACKED_EPI=0"); empty for the in-tree build
+    # PGDIST_DEFINES="NAME=VALUE ..."); empty for the in-tree build
     common += ["-D" + d for d in os.environ.get("PGDIST_DEFINES", "").split()]
     hip = common + [f"--offload-arch={ARCH}", "-x", "hip", "-munsafe-fp-atomics"]
     # host translation units (bindings, runtime) contain no kernels; target gfx950 only as well

@@ -21,10 +21,6 @@
 #include "runtime/plan.h"
 #include "runtime/runtime.h"
 
-namespace pgdist_rt {
-uintptr_t cu_masked_stream(int device, int num, int den);   // runtime/streams.cpp
-}
-
 namespace py = pybind11;
 typedef unsigned short bf16_t;
 typedef uintptr_t P;
@@ -46,8 +42,6 @@ int dw_geom_mode();
 void dw_set_tall_rows(int);
 void pw_f8_set_mx(int);
 int pw_f8_mx();
-void dw_set_tall_wrows(int);
-int dw_tall_wrows();
 void dw_set_small_dgrad(int);
 int dw_small_dgrad();
 int dw_tall_rows();
@@ -72,6 +66,11 @@ void launch_dw_wgrad(const bf16_t *, const bf16_t *, const float *, const bf16_t
                      const float *, float *, float *, int, int, int, int, int, hipStream_t);
 int pw_gemm_num_partials(int, int, int);
 int ir_fwd_grid(int, int, int, int, int);
+int ir_bwd_grid(int, int, int, int, int);
+void launch_ir_bwd(const bf16_t *, const bf16_t *, const void *, const bf16_t *, const bf16_t *, const float *,
+                   const float *, bf16_t *, const void *, const bf16_t *, const bf16_t *, const float *, const float *,
+                   bf16_t *, const void *, const bf16_t *, const bf16_t *, const bf16_t *, bf16_t *, const void *,
+                   unsigned *, unsigned *, int, int, int, int, int, hipStream_t);
 void launch_ir_fwd(const bf16_t *, const bf16_t *, const void *, bf16_t *, const bf16_t *, const bf16_t *,
                    const bf16_t *, bf16_t *, bf16_t *, bf16_t *, const void *, const void *, const void *, unsigned *,
                    unsigned *, int, int, int, int, int, hipStream_t);
@@ -220,8 +219,6 @@ PYBIND11_MODULE(_pgdist_C, m) {
   m.def("dw_set_tall_rows", &dw_set_tall_rows);
   m.def("pw_f8_set_mx", &pw_f8_set_mx);
   m.def("pw_f8_mx", &pw_f8_mx);
-  m.def("dw_set_tall_wrows", &dw_set_tall_wrows);
-  m.def("dw_tall_wrows", &dw_tall_wrows);
   m.def("dw_set_small_dgrad", &dw_set_small_dgrad);
   m.def("dw_small_dgrad", &dw_small_dgrad);
   m.def("dw_tall_rows", &dw_tall_rows);
@@ -274,6 +271,19 @@ PYBIND11_MODULE(_pgdist_C, m) {
   m.def("pw_gemm_num_partials", &pw_gemm_num_partials);
   // ---- fused inverted-residual block forward (irblock.hip) ----
   m.def("ir_fwd_grid", &ir_fwd_grid, "workgroups of the fused block forward (0: unsupported / not co-resident)");
+  m.def("ir_bwd_grid", &ir_bwd_grid, "workgroups of the fused block backward (0: unsupported / not co-resident)");
+  m.def("ir_bwd", [](P G, P y, P lz_p, P wpt, P h2, P sd, P td, P gd, P dd, P wd, P h1, P se, P te, P ge, P de,
+                     P wet, P R, P yprev, P gout, P dprev, P bar, P err, int B, int H, int cin, int ch, int cout,
+                     P s) {
+    pgdist_rt::run_op([=] {
+      launch_ir_bwd(ptr<bf16_t>(G), ptr<bf16_t>(y), reinterpret_cast<const void *>(lz_p), ptr<bf16_t>(wpt),
+                    ptr<bf16_t>(h2), ptr<float>(sd), ptr<float>(td), ptr<bf16_t>(gd),
+                    reinterpret_cast<const void *>(dd), ptr<bf16_t>(wd), ptr<bf16_t>(h1), ptr<float>(se),
+                    ptr<float>(te), ptr<bf16_t>(ge), reinterpret_cast<const void *>(de), ptr<bf16_t>(wet),
+                    ptr<bf16_t>(R), ptr<bf16_t>(yprev), ptr<bf16_t>(gout), reinterpret_cast<const void *>(dprev),
+                    ptr<unsigned>(bar), ptr<unsigned>(err), B, H, cin, ch, cout, S(s));
+    });
+  });
   m.def("ir_fwd", [](P xin, P res, P lz_in, P xout, P we, P wd, P wp, P h1, P h2, P y, P de, P dd, P dp, P bar,
                      P err, int B, int H, int cin, int ch, int cout, P s) {
     pgdist_rt::run_op([=] {
@@ -554,8 +564,6 @@ PYBIND11_MODULE(_pgdist_C, m) {
   m.def("comm_error_async", &pgdist_rt::comm_error_async);
   m.def("comm_destroy", &pgdist_rt::comm_destroy, py::call_guard<py::gil_scoped_release>());
 
-  m.def("cu_masked_stream", &pgdist_rt::cu_masked_stream,
-        "HIP stream whose kernels may use CU i iff i % den < num (returns the stream handle)");
 
   // ---- native runtime (host) ----
   m.def("read_cifar10_bin", &pgdist_rt::read_cifar10_bin, py::arg("paths"), py::arg("num_threads") = 4,

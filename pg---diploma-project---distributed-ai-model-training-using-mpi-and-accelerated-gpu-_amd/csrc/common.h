@@ -44,36 +44,16 @@ PG_DEVICE uint32_t pack2(float a, float b) {
 }
 
 // Store one 16x16 f32 MFMA accumulator fragment (lane: rows row0 + 4*(lane>>4) + j, j = 0..3, of
-// column col0 + (lane & 15)) as bf16 into a row-major LDS tile T (pitch ld elements, ld and col0
-// even).  Default: one ds_write_b16 per element.  PGDIST_PACKED_EPI=1 (build define) completes
-// column pairs across the lane pair (l, l^1) with one DPP move (quad_perm [1,0,3,2]) and writes
-// 4-byte words (2 ds_write_b32 per lane instead of 4 ds_write_b16); measured SLOWER on MI355X in a
-// same-box A/B of two builds (MobileNetV2 4.69-4.70 vs 4.66 ms/step, ResNet-50 11.90-11.94 vs
-// 11.68-11.69, conv fwd 2983 vs 2842 us): the epilogue is not bound by its LDS write count, and
-// the DPP move + repacking VALU sit on its critical path.  Every lane of the wave must execute the
-// packed form (DPP reads the neighbour's register).
-PG_DEVICE uint32_t pack2(float a, float b);
-#ifndef PGDIST_PACKED_EPI
-#define PGDIST_PACKED_EPI 0
-#endif
+// column col0 + (lane & 15)) as bf16 into a row-major LDS tile T (pitch ld elements): one
+// ds_write_b16 per element.  (Completing 4-byte column pairs across lanes with a DPP move was
+// measured slower on MI355X -- MobileNetV2 4.69-4.70 vs 4.66 ms/step, ResNet-50 11.90-11.94 vs
+// 11.68-11.69 -- the epilogue is not bound by its LDS write count; docs/PERF_NOTES.md round 3.)
 PG_DEVICE void frag_store_bf16(bf16_t *T, int ld, int row0, int col0, float v0, float v1, float v2, float v3) {
   const int lane = threadIdx.x & 63;
-  if constexpr (!PGDIST_PACKED_EPI) {   // A/B reference: one 2-byte store per element
-    const float v[4] = {v0, v1, v2, v3};
+  const float v[4] = {v0, v1, v2, v3};
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      T[(row0 + 4 * (lane >> 4) + j) * ld + col0 + (lane & 15)] = __builtin_bit_cast(bf16_t, (__bf16)v[j]);
-    return;
-  }
-  const bool odd = lane & 1;
-  const uint32_t lo = pack2(v0, v1), hi = pack2(v2, v3);
-  const uint32_t recv = (uint32_t)__builtin_amdgcn_mov_dpp((int)(odd ? lo : hi), 0xB1, 0xF, 0xF, false);
-  const uint32_t mine = odd ? hi : lo;
-  const uint32_t a0 = odd ? ((recv & 0xffffu) | (mine << 16)) : ((mine & 0xffffu) | (recv << 16));
-  const uint32_t a1 = odd ? ((recv >> 16) | (mine & 0xffff0000u)) : ((mine >> 16) | (recv & 0xffff0000u));
-  const int row = row0 + 4 * (lane >> 4) + (odd ? 2 : 0), col = col0 + (lane & 14);
-  *reinterpret_cast<uint32_t *>(T + row * ld + col) = a0;
-  *reinterpret_cast<uint32_t *>(T + (row + 1) * ld + col) = a1;
+  for (int j = 0; j < 4; ++j)
+    T[(row0 + 4 * (lane >> 4) + j) * ld + col0 + (lane & 15)] = __builtin_bit_cast(bf16_t, (__bf16)v[j]);
 }
 
 PG_DEVICE uint4 pack8(const float (&f)[8]) {

@@ -72,11 +72,6 @@ struct ConvArgs {
   signed char tr[4][9], ts[4][9], tdh[4][9], tdw[4][9];
 };
 
-int env_int(const char *name, int dflt) {
-  const char *e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
-
 // 16x16x32 bf16 MFMA on raw 8 x bf16 fragments
 PG_DEVICE f32x4_t mfma16(const s16x8_t &a, const s16x8_t &b, const f32x4_t &c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
@@ -1500,7 +1495,7 @@ Geom igemm_geom(int M, int N, int Kmax, int Ci, int ncls) {
   Geom g{};
   // largest tile that still gives min_wgs workgroups (128 x 128 tiles run at 1.3-1.8x the
   // MFMA rate of the smaller ones on MI355X, so the bar is about one workgroup per CU)
-  static const int min_wgs = [] { const char *e = getenv("PGDIST_CONV_MINWG"); return e ? atoi(e) : 256; }();
+  constexpr int min_wgs = 256;   // (512 / 1024: smaller tiles, slower; docs/PERF_NOTES.md round 3)
   static constexpr int cand[4][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}};
   int pick = 3;
   for (int i = 0; i < 4; ++i) {
@@ -1508,16 +1503,6 @@ Geom igemm_geom(int M, int N, int Kmax, int Ci, int ncls) {
     const long long wgs = (long long)((M + cand[i][0] - 1) / cand[i][0]) * ((N + cand[i][1] - 1) / cand[i][1]) * ncls;
     if (wgs >= min_wgs) { pick = i; break; }
   }
-  // PGDIST_CONV_TILE_FORCE=<BM>x<BN> (tile sweeps): every implicit-GEMM launch on that tile
-  static const int force = [] {
-    const char *e = getenv("PGDIST_CONV_TILE_FORCE");
-    if (!e) return -1;
-    const int bm = atoi(e), bn = strchr(e, 'x') ? atoi(strchr(e, 'x') + 1) : 0;
-    for (int i = 0; i < 4; ++i)
-      if (bm == cand[i][0] && bn == cand[i][1]) return i;
-    return -1;
-  }();
-  if (force >= 0 && !(cand[force][1] == 128 && N <= 64)) pick = force;
   g.BM = cand[pick][0];
   g.BN = cand[pick][1];
   g.nmt = (M + g.BM - 1) / g.BM;
@@ -1561,16 +1546,12 @@ void launch_geom(const ConvArgs &a, const Geom &g, hipStream_t st) {
   }
 }
 
-// LDS-DMA kernel (conv_glds_kernel) for operands without a prologue: g_conv_glds = 0 off (the
-// register-staged kernel), 2 or 3 LDS buffers.  Default 2; PGDIST_CONV_GLDS / conv_set_glds().
-int conv_glds_default() {
-  const char *e = getenv("PGDIST_CONV_GLDS");
-  const int v = e ? atoi(e) : 2;
-  return v == 0 || v == 3 || v == 4 ? v : 2;
-}
-int g_conv_glds = conv_glds_default();
+// LDS-DMA kernel (conv_glds_kernel) for operands without a prologue: g_conv_glds = 2 LDS
+// buffers (default), 0 off (the register-staged kernel; conv_set_glds: tests).  (A 3-stage ring
+// at 128x128 -- 96 KB of LDS, one workgroup per CU -- and 32-wide k steps with 2-4 stages
+// measured slower: fwd 3657 / ~2990 vs 2843 us network total, docs/PERF_NOTES.md round 3.)
+int g_conv_glds = 2;
 bool glds_ok(int Ci) { return g_conv_glds != 0 && Ci % 64 == 0; }
-int glds_nbuf() { return g_conv_glds; }
 
 template <int MODE, int EPI, int BM, int BN, int NBUF, int KS, bool MT = false>
 void launch_glds_t(const ConvArgs &a, const Geom &g, hipStream_t st) {
@@ -1580,8 +1561,7 @@ void launch_glds_t(const ConvArgs &a, const Geom &g, hipStream_t st) {
   int kmax = a.K;
   if (MODE == CM_DGRAD)
     for (int c = 0; c < g.ncls; ++c) kmax = a.ntap[c] * a.Ci > kmax ? a.ntap[c] * a.Ci : kmax;
-  static const bool one_stage = env_int("PGDIST_CONV_1STAGE", 1) != 0;
-  const int stages = (one_stage && kmax <= KS) ? 1 : NBUF;
+  const int stages = kmax <= KS ? 1 : NBUF;
   size_t lds = (size_t)stages * (BM + BN) * KS * 2;
   const size_t ctile = (size_t)BM * (BN + 8) * 2, red = (size_t)(256 / (BN / 8)) * BN * 4;
   if (ctile > lds) lds = ctile;
@@ -1590,29 +1570,16 @@ void launch_glds_t(const ConvArgs &a, const Geom &g, hipStream_t st) {
                      st, a);
 }
 
-// LDS-DMA k-step: PGDIST_CONV_KS = 64 (default) | 32; ring depth PGDIST_CONV_GLDS (2..4)
-int glds_ks() {
-  static const int v = [] { const char *e = getenv("PGDIST_CONV_KS"); return e && atoi(e) == 32 ? 32 : 64; }();
-  return v;
-}
 
 // (256 x 128 tiles, one workgroup of 4 waves per CU at 2 or 3 LDS stages, measured slower on
 // every ResNet-50 layer: forward network total 2826 -> 3150 us, dgrad 3875 -> 4533 us; the
 // loop is latency-bound at one wave per SIMD, not operand-bandwidth-bound -- docs/PERF_NOTES.md)
 template <int MODE, int EPI>
 void launch_glds(const ConvArgs &a, const Geom &g, hipStream_t st) {
-  const int nb = glds_nbuf();
-#define LG_GLDS(BM_, BN_)                                                                               \
-  if (g.BM == BM_ && g.BN == BN_) {                                                                     \
-    if (glds_ks() == 32) {                                                                              \
-      if (nb == 4) launch_glds_t<MODE, EPI, BM_, BN_, 4, 32>(a, g, st);                                  \
-      else if (nb == 3) launch_glds_t<MODE, EPI, BM_, BN_, 3, 32>(a, g, st);                             \
-      else launch_glds_t<MODE, EPI, BM_, BN_, 2, 32>(a, g, st);                                          \
-    } else {                                                                                            \
-      if (nb == 3) launch_glds_t<MODE, EPI, BM_, BN_, 3, 64>(a, g, st);                                  \
-      else launch_glds_t<MODE, EPI, BM_, BN_, 2, 64>(a, g, st);                                          \
-    }                                                                                                   \
-    return;                                                                                             \
+#define LG_GLDS(BM_, BN_)                                  \
+  if (g.BM == BM_ && g.BN == BN_) {                        \
+    launch_glds_t<MODE, EPI, BM_, BN_, 2, 64>(a, g, st);   \
+    return;                                                \
   }
   LG_GLDS(128, 128)
   LG_GLDS(128, 64)
@@ -1642,7 +1609,7 @@ void dgrad_classes(ConvArgs &a, int R, int S, int st, int pad) {
 }
 }  // namespace
 
-void conv_set_glds(int mode) { g_conv_glds = mode == 0 || mode == 3 ? mode : 2; }
+void conv_set_glds(int mode) { g_conv_glds = mode == 0 ? 0 : 2; }
 int conv_get_glds() { return g_conv_glds; }
 
 // BN partial rows a forward conv writes (per M tile)
@@ -1736,10 +1703,9 @@ struct WgGeom {
   int TN, TK, nsplit, rows;
 };
 // LDS-DMA weight gradient (conv_wgrad_dma_kernel): materialised dy, x without a prologue,
-// Ci and N multiples of 64.  PGDIST_WG_DMA=0: off.
+// Ci and N multiples of 64 (4584 -> 4029 us of ResNet-50 weight gradients, round 3).
 bool wg_dma_ok(bool dm, int xpro, int Ci, int N) {
-  static const bool on = [] { const char *e = getenv("PGDIST_WG_DMA"); return !e || atoi(e) != 0; }();
-  return on && dm && xpro == CP_NONE && Ci % 64 == 0 && N % 64 == 0;
+  return dm && xpro == CP_NONE && Ci % 64 == 0 && N % 64 == 0;
 }
 // Per-shape configuration of the LDS-DMA weight gradient: split-M grid-size target, m rows per
 // stage and ring depth.  Measured per ResNet-50 layer at bs128 on MI355X (scripts/conv_bench.py
@@ -1748,23 +1714,16 @@ bool wg_dma_ok(bool dm, int xpro, int Ci, int N) {
 // want a 1024-workgroup grid (l1.c2 150 -> 98 us, l3.c2 84 -> 76), the 7x7 maps (3-4 splits) a
 // 3-deep ring of 32-row stages (l4.c2 103 -> 82); the 1x1 layers and the 28x28 3x3 ones keep
 // 512 workgroups and 2 x 64-row stages (network total 4024 -> ~3750 us).
-// PGDIST_WGD_TARGET / PGDIST_WG_DMA_MK / PGDIST_WG_DMA_NBUF override every shape.
 struct WgDmaCfg {
   int target, mk, nbuf;
 };
 WgDmaCfg wg_dma_cfg(int N, int Ci, int M, int taps) {
-  static const int e_t = env_int("PGDIST_WGD_TARGET", 0), e_mk = env_int("PGDIST_WG_DMA_MK", 0),
-                   e_nb = env_int("PGDIST_WG_DMA_NBUF", 0), e_t1 = env_int("PGDIST_WGD_T1", 512);
   const int TN = N % 128 == 0 ? 128 : 64, TK = Ci % 128 == 0 ? 128 : 64;
-  // PGDIST_WGD_T1: grid target of the 1x1 weight gradients (tuning)
-  WgDmaCfg c{taps > 1 ? 512 : e_t1, 64, 2};
+  WgDmaCfg c{512, 64, 2};   // (1x1 grid target 256 / 128: slower, profiles/r3c_resnet50_side_ab.txt)
   if (taps > 1) {
     if (M <= 8192) { c.mk = 32; c.nbuf = 3; }
     else if (M <= 32768 || (TN == 64 && TK == 64)) c.target = 1024;
   }
-  if (e_t > 0) c.target = e_t;
-  if (e_mk == 32 || e_mk == 64) c.mk = e_mk;
-  if (e_nb >= 2 && e_nb <= 4) c.nbuf = e_nb;
   return c;
 }
 
@@ -1778,7 +1737,7 @@ WgGeom wg_geom(int N, int Kw, int M, bool dma = false, int Ci = 0) {
     g.TK = Kw >= 128 ? 128 : 64;
   }
   const long long tiles = (long long)((N + g.TN - 1) / g.TN) * ((Kw + g.TK - 1) / g.TK);
-  static const int target = env_int("PGDIST_WG_TARGET", 1024);
+  constexpr int target = 1024;   // split-M grid target (512 / 2048 / 4096: slower, round 1)
   long long ns = ((dma ? wg_dma_cfg(N, Ci, M, Kw / Ci).target : target) + tiles - 1) / tiles;
   const long long max_ns = (M + 4 * kWgMK - 1) / (4 * kWgMK);   // >= 4 steps per split
   if (ns > max_ns) ns = max_ns;
@@ -1829,13 +1788,10 @@ void launch_conv_wgrad(const bf16_t *G, const bf16_t *Y, const float *ga, const 
     const size_t lds = (size_t)nb * mk * (g.TN + g.TK) * 2;
 #define WGD_K(TN_, TK_, NB_, MK_) \
   hipLaunchKernelGGL((conv_wgrad_dma_kernel<TN_, TK_, NB_, MK_>), dim3(total), dim3(256), lds, stream, a, gx, gy, total)
-#define WGD_L(TN_, TK_)                                                                                         \
-  do {                                                                                                         \
-    if (mk == 32) {                                                                                            \
-      if (nb == 4) WGD_K(TN_, TK_, 4, 32); else if (nb == 3) WGD_K(TN_, TK_, 3, 32); else WGD_K(TN_, TK_, 2, 32); \
-    } else {                                                                                                   \
-      if (nb == 4) WGD_K(TN_, TK_, 4, 64); else if (nb == 3) WGD_K(TN_, TK_, 3, 64); else WGD_K(TN_, TK_, 2, 64); \
-    }                                                                                                          \
+#define WGD_L(TN_, TK_)                                       \
+  do {                                                        \
+    if (mk == 32) WGD_K(TN_, TK_, 3, 32);   /* 7x7 3x3 maps */ \
+    else WGD_K(TN_, TK_, 2, 64);                              \
   } while (0)
     if (g.TN == 128 && g.TK == 128) WGD_L(128, 128);
     else if (g.TN == 128) WGD_L(128, 64);

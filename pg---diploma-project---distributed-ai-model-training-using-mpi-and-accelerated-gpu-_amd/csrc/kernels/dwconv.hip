@@ -34,9 +34,6 @@ constexpr int CPT = 4;        // channels per thread
 // 40 and 14 slower), the side-stream weight gradients keep 28
 constexpr int kRows = 56;
 constexpr int kWRows = 28;
-#ifndef PGDIST_DW_GEOM_DEFAULT
-#define PGDIST_DW_GEOM_DEFAULT 3   // occupancy-aware geometry kinds (see dw_geom); env PGDIST_DW_GEOM
-#endif
 
 struct DwGeom {
   int B, H, W, C, Ho, Wo;
@@ -167,10 +164,7 @@ PG_DEVICE void block_channel_partials(float (&acc)[NV][CPT], float *__restrict__
 // ===========================================================================
 namespace {
 
-#ifndef PGDIST_DW_DEPTH
-#define PGDIST_DW_DEPTH 4
-#endif
-constexpr int kDepth = PGDIST_DW_DEPTH;   // rows in flight per stream
+constexpr int kDepth = 4;   // rows in flight per stream (forward; the dgrad rings use 3)
 constexpr int kRing = kDepth + 1;         // ring slots: the row being read + kDepth in flight
 // per-slot LDS bytes (whole 1 KiB wave pieces): halo row segments (TWc + 2) x CC8 <= 144
 // chunks, own-column segments TWc x CC8 <= 128, stride-2 input segments (2 TWc + 1) x CC8 <= 256
@@ -374,18 +368,11 @@ __global__ __launch_bounds__(256) void dw_fwd_lds_kernel(
 // rows (g, y of this layer's BN backward, halo columns) of dy row r0-1+k and yprev (the
 // producer's pre-BN activation, own columns: ReLU6 mask + fused weight gradient) of input row
 // r0+k-2; step k >= 2 emits input row r0+k-2.  Per step: 3 DMA + 1 store.
-// PGDIST_DW_DGRAD_WPE (build define, A/B only): minimum waves per SIMD for the register
-// allocation.  The fused weight-gradient variant needs 175 VGPRs unconstrained (2 waves per
-// SIMD); waves_per_eu 3 forces <= 168 with 36 B of scratch in the row loop and measured 30-80 %
-// slower (56x56x144: 209.6 -> 277.4 us, 112x112x32: 152.9 -> 271.1 us; waves_per_eu 1 equals
-// the unconstrained build): profiles/r3b_pwwg_sweep.txt.  Unset: no attribute.
-#ifdef PGDIST_DW_DGRAD_WPE
-#define PGDIST_DW_DGRAD_ATTR __attribute__((amdgpu_waves_per_eu(PGDIST_DW_DGRAD_WPE)))
-#else
-#define PGDIST_DW_DGRAD_ATTR
-#endif
+// (The fused weight-gradient variant needs 175 VGPRs: 2 waves per SIMD; forcing 3 with
+// amdgpu_waves_per_eu spilled in the row loop and measured 30-80 % slower: 56x56x144 209.6 ->
+// 277.4 us, 112x112x32 152.9 -> 271.1 us; profiles/r3b_pwwg_sweep.txt.)
 template <bool WG, int D = kDepth>
-__global__ __launch_bounds__(256) PGDIST_DW_DGRAD_ATTR void dw_dgrad_s1_lds_kernel(
+__global__ __launch_bounds__(256) void dw_dgrad_s1_lds_kernel(
     const bf16_t *__restrict__ gin, const bf16_t *__restrict__ yself, const float *__restrict__ coef,
     const bf16_t *__restrict__ w, const bf16_t *__restrict__ yprev, const float *__restrict__ ps,
     const float *__restrict__ pt, bf16_t *__restrict__ gout, float *__restrict__ part, DwGeom g,
@@ -556,7 +543,7 @@ __global__ __launch_bounds__(256) PGDIST_DW_DGRAD_ATTR void dw_dgrad_s1_lds_kern
 // 2(o-1)+1 (own columns); step k >= 1 emits those two input rows (tap dh = 1 with dy row o-1;
 // dh = 2 with row o-1 and dh = 0 with row o).  Per step: 4 DMA + 2 stores.
 template <bool WG, int D = kDepth>
-__global__ __launch_bounds__(256) PGDIST_DW_DGRAD_ATTR void dw_dgrad_s2_lds_kernel(
+__global__ __launch_bounds__(256) void dw_dgrad_s2_lds_kernel(
     const bf16_t *__restrict__ gin, const bf16_t *__restrict__ yself, const float *__restrict__ coef,
     const bf16_t *__restrict__ w, const bf16_t *__restrict__ yprev, const float *__restrict__ ps,
     const float *__restrict__ pt, bf16_t *__restrict__ gout, float *__restrict__ part, DwGeom g,
@@ -919,10 +906,9 @@ static int dw_twc_max(int cc, int kind, int stride) {
 // Channel slab of a narrow map: with the default CC (<= 64) a 7-column map leaves half of
 // the 256 threads without a column (C4 = 16 threads x 7 columns); a wider slab (a multiple
 // of 8 dividing C, <= 128) gives every column more channel lanes: 7x7x960 -> CC = 120,
-// 210 active threads instead of 112 (PGDIST_DW_WIDE=0: off).
+// 210 active threads instead of 112 (MobileNetV2 bs128: 5.17 -> 5.05 ms/step, round 2).
 static int dw_cc_narrow(int C, int gw, int kind, int stride, int cc0) {
-  static const bool on = [] { const char *e = getenv("PGDIST_DW_WIDE"); return !(e && atoi(e) == 0); }();
-  if (!on || dw_twc_max(cc0, kind, stride) <= gw) return cc0;
+  if (dw_twc_max(cc0, kind, stride) <= gw) return cc0;
   int best = cc0, best_act = (cc0 / CPT) * gw;
   for (int cc = 8; cc <= 128; cc += 8) {
     if (C % cc) continue;
@@ -951,46 +937,30 @@ static int dw_cc_narrow(int C, int gw, int kind, int stride, int cc0) {
 // 91 -> 116 us, dgrad 56x56x144: 89 -> 117 us) and the 28x28 dgrad (38 -> 45 us) were slower --
 // rounds are not the whole cost where the kernel is bandwidth-bound or the strip gets short.
 // So by default (mask 3) it applies to the stride-1 forward / dgrad on >= 56-row maps only;
-// bit 8 lifts that restriction (experiments).
-int g_dw_geom_mask = [] {
-  const char *e = getenv("PGDIST_DW_GEOM");
-  return e ? atoi(e) : PGDIST_DW_GEOM_DEFAULT;
-}();
+// bit 8 lifts that restriction (experiments: dw_set_geom_mode).
+int g_dw_geom_mask = 3;
 // Tall geometry for the stride-1 forward / dgrad on small maps (<= 14 rows): the batch is
 // stacked into one B*H-row image and a workgroup walks a strip of g_dw_tall rows across image
 // boundaries (the window taps that would cross an image edge are masked per row), so the DMA
 // ring fill, the parameter staging and the statistics epilogue are paid per strip instead of
-// per 7- or 14-row image.  PGDIST_DW_TALL = strip rows, 0: off.  Measured (scripts/dw_bench.py,
+// per 7- or 14-row image.  g_dw_tall = strip rows, 0: off (dw_set_tall_rows).  Measured (scripts/dw_bench.py,
 // profiles/r4_dw_tall_sweep.txt): 14-row strips (two 7x7 images) take 7x7x960 forward 18.8 -> 17.7
 // and dgrad 35.4 -> 30.2 us (bench 4.525 / 4.530 vs 4.535 / 4.551 ms/step); longer strips are
 // slower (21 / 28 / 42 / 56 rows: fewer workgroups, and a strip row costs ~0.2 us of DMA latency
 // per workgroup), 14 leaves the 14x14 tiling unchanged.
-int g_dw_tall = [] {
-  const char *e = getenv("PGDIST_DW_TALL");
-  return e ? atoi(e) : 14;
-}();
+int g_dw_tall = 14;
 // Small-map stride-1 dgrad (tall geometry on): slab width and strip length chosen together so
 // the launch fits one round of resident workgroups (3 per CU) where it can -- e.g. 14x14x384:
 // 64-channel slabs of all 14 columns (768 workgroups) instead of 96-channel slabs of 10 columns
 // (1024, two rounds).  Cost = rounds x (strip rows + g_dw_fix), ties to more active lanes.
-// PGDIST_DW_SMALL_DGRAD=0: off; PGDIST_DW_FIX: the fixed per-strip cost in rows.  Measured
+// dw_set_small_dgrad(0): off; kDwFix: the fixed per-strip cost in rows.  Measured
 // (profiles/r4_dw_small_dgrad.txt): 14x14x576 59.7 -> 52.6-54.8 us (21-row strips of 72-channel
 // slabs, 688 workgroups); 14x14x384 unchanged at 37.1 us although it now fits one round;
 // bench 4.506-4.516 vs 4.507-4.526 ms/step.
-int g_dw_small_dgrad = [] {
-  const char *e = getenv("PGDIST_DW_SMALL_DGRAD");
-  return e ? atoi(e) : 1;
-}();
-// tall strips for the stride-1 weight gradient on <= 14-row maps (side stream): PGDIST_DW_TALL_W
-// = strip rows, 0: off (measured neutral at 28 rows, slower at 14: profiles/r4_dw_tall_wgrad.txt)
-int g_dw_tall_w = [] {
-  const char *e = getenv("PGDIST_DW_TALL_W");
-  return e ? atoi(e) : 0;
-}();
-static int g_dw_fix = [] {
-  const char *e = getenv("PGDIST_DW_FIX");
-  return e ? atoi(e) : 12;
-}();
+int g_dw_small_dgrad = 1;
+// (tall strips for the side-stream weight gradient measured neutral at 28 rows and slower at 14,
+// profiles/r4_dw_tall_wgrad.txt: the weight gradient keeps per-image strips)
+static constexpr int kDwFix = 12;
 static int dw_occ(int kind, int stride, int gh) {
   return kind == 0 ? 4 : kind == 2 ? 3 : (stride == 1 && gh >= 56 ? 2 : 3);
 }
@@ -1019,7 +989,7 @@ DwGeom dw_geom(int kind, int B, int H, int W, int C, int stride) {
   g.Ho = (H - 1) / stride + 1;
   g.Wo = (W - 1) / stride + 1;
   g.Hi = H;
-  const bool tall = (kind <= 1 ? g_dw_tall : g_dw_tall_w) > 0 && stride == 1 && H <= 14 && B > 1;
+  const bool tall = kind <= 1 && g_dw_tall > 0 && stride == 1 && H <= 14 && B > 1;
   if (tall) {
     g.B = 1;
     g.H = g.Ho = B * H;
@@ -1029,17 +999,7 @@ DwGeom dw_geom(int kind, int B, int H, int W, int C, int stride) {
   int twc = dw_twc_max(g.CC, kind, stride);
   if (twc > gw) twc = gw;
   g.TWc = twc;
-  static const int env_rows = [] {
-    const char *e = getenv("PGDIST_DW_ROWS");
-    return e ? atoi(e) : 0;
-  }();
-  static const int env_wrows = [] {
-    const char *e = getenv("PGDIST_DW_WROWS");
-    return e ? atoi(e) : 0;
-  }();
-  int R = tall ? g_dw_tall : env_rows > 0 ? env_rows : kRows;
-  if (kind == 2) R = tall ? g_dw_tall_w : env_wrows > 0 ? env_wrows : kWRows;
-  // (PGDIST_DW_ROWS / PGDIST_DW_WROWS override the strip length for tuning experiments)
+  int R = tall ? g_dw_tall : (kind == 2 ? kWRows : kRows);
   R = dw_fix_rows(kind, stride, R, gh);
   if (tall && kind == 1 && g_dw_small_dgrad) {
     long long best = -1;
@@ -1053,7 +1013,7 @@ DwGeom dw_geom(int kind, int B, int H, int W, int C, int stride) {
         if (t < 1) continue;
         if (t > gw) t = gw;
         const long long nwg = (long long)((gh + r - 1) / r) * ((gw + t - 1) / t) * (C / cc);
-        const long long cost = ((nwg + 767) / 768) * (r + g_dw_fix);
+        const long long cost = ((nwg + 767) / 768) * (r + kDwFix);
         const int act = (cc / CPT) * gw / ((gw + t - 1) / t);   // active lanes per workgroup, on average
         if (best < 0 || cost < best || (cost == best && act > best_act))
           best = cost, best_act = act, g.CC = cc, g.TWc = t, R = r;
@@ -1092,8 +1052,6 @@ int dw_grid_x(const DwGeom &g) { return g.B * g.tiles_h * g.tiles_w; }
 void dw_set_geom_mode(int mask) { g_dw_geom_mask = mask; }
 int dw_geom_mode() { return g_dw_geom_mask; }
 void dw_set_tall_rows(int rows) { g_dw_tall = rows; }
-void dw_set_tall_wrows(int rows) { g_dw_tall_w = rows; }
-int dw_tall_wrows() { return g_dw_tall_w; }
 void dw_set_small_dgrad(int on) { g_dw_small_dgrad = on; }
 int dw_small_dgrad() { return g_dw_small_dgrad; }
 int dw_tall_rows() { return g_dw_tall; }
@@ -1108,17 +1066,9 @@ void launch_dw_fwd(const bf16_t *x, const float *in_s, const float *in_t, int ac
   g.fin = take_bn_fin();
   g.lz = take_bn_lz();
   const dim3 grid(dw_grid_x(g) * (C / g.CC)), block(256);
-  // ring depth: 4 rows in flight; on small maps (<= 14 rows) PGDIST_DW_FDEPTH_SMALL (6 / 8) rows so
-  // the whole strip is requested up front (one exposed DMA latency instead of ~3); PGDIST_DW_FDEPTH=3
-  // everywhere (tuning experiments)
-  static const int fd_all = [] { const char *e = getenv("PGDIST_DW_FDEPTH"); return e ? atoi(e) : 4; }();
-  static const int fd_small = [] { const char *e = getenv("PGDIST_DW_FDEPTH_SMALL"); return e ? atoi(e) : 0; }();
-  const int D = (fd_small > 0 && H <= 14) ? fd_small : fd_all;
-#define DWF(S_, A_)                                                                                           \
-  if (D == 3) hipLaunchKernelGGL((dw_fwd_lds_kernel<S_, A_, 3>), grid, block, 0, st, x, in_s, in_t, w, y, part, g); \
-  else if (D == 6) hipLaunchKernelGGL((dw_fwd_lds_kernel<S_, A_, 6>), grid, block, 0, st, x, in_s, in_t, w, y, part, g); \
-  else if (D == 8) hipLaunchKernelGGL((dw_fwd_lds_kernel<S_, A_, 8>), grid, block, 0, st, x, in_s, in_t, w, y, part, g); \
-  else hipLaunchKernelGGL((dw_fwd_lds_kernel<S_, A_, 4>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
+  // ring depth 4 rows in flight (3: neutral; 6 / 8 on the small maps: neutral, round 2 / 4 sweeps)
+#define DWF(S_, A_) \
+  hipLaunchKernelGGL((dw_fwd_lds_kernel<S_, A_, 4>), grid, block, 0, st, x, in_s, in_t, w, y, part, g);
   if (stride == 1) {
     if (act == ACT_BN_RELU6) { DWF(1, ACT_BN_RELU6) }
     else { DWF(1, ACT_NONE) }
@@ -1138,19 +1088,11 @@ void launch_dw_dgrad(const bf16_t *gin, const bf16_t *yself, const float *coef, 
   g.fin = take_bn_fin();
   g.lz = take_bn_lz();
   const dim3 grid(dw_grid_x(g) * (C / g.CC)), block(256);
-  // ring depth (rows in flight): 3 by default -- 39 KB of LDS per workgroup, 4 workgroups per CU
-  // instead of 3 at depth 4 (MobileNetV2 bs128: 5.02 -> 4.94 ms/step); PGDIST_DW_DDEPTH=2|3|4
-  // PGDIST_DW_DDEPTH_WG: ring depth of the fused dgrad + wgrad variants (their VGPRs, not LDS,
-  // bound the resident workgroups: 175 -> 2 per CU at stride 1, 139 -> 3 at stride 2)
-  static const int env_d = [] { const char *e = getenv("PGDIST_DW_DDEPTH"); return e ? atoi(e) : 3; }();
-  static const int env_dwg = [] { const char *e = getenv("PGDIST_DW_DDEPTH_WG"); return e ? atoi(e) : 3; }();
-  static const int env_ds1 = [] { const char *e = getenv("PGDIST_DW_DDEPTH_S1"); return e ? atoi(e) : 0; }();
-  const int D = wpart ? env_dwg : (stride == 1 && env_ds1 ? env_ds1 : env_d);
-#define DWD(KER, WGF)                                                                                     \
-  if (D == 2) hipLaunchKernelGGL((KER<WGF, 2>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g, wpart); \
-  else if (D == 4) hipLaunchKernelGGL((KER<WGF, 4>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g, wpart); \
-  else if (D == 5) hipLaunchKernelGGL((KER<WGF, 5>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g, wpart); \
-  else hipLaunchKernelGGL((KER<WGF, 3>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g, wpart);
+  // ring depth (rows in flight) 3: 39 KB of LDS per workgroup, 4 workgroups per CU instead of 3
+  // at depth 4 (MobileNetV2 bs128: 5.02 -> 4.94 ms/step); 2 / 4 / 5 (also for the VGPR-bound fused
+  // dgrad + wgrad variants) measured neutral or slower (profiles/r3c_dw_ddepth_ab.txt)
+#define DWD(KER, WGF) \
+  hipLaunchKernelGGL((KER<WGF, 3>), grid, block, 0, st, gin, yself, coef, w, yprev, ps, pt, gout, part, g, wpart);
   if (wpart) {
     if (stride == 1) { DWD(dw_dgrad_s1_lds_kernel, true) }
     else { DWD(dw_dgrad_s2_lds_kernel, true) }
@@ -1175,9 +1117,7 @@ void launch_dw_wgrad(const bf16_t *gin, const bf16_t *yself, const float *coef, 
   const DwGeom g = dw_geom(2, B, H, W, C, stride);
   const int P = dw_grid_x(g);
   const dim3 grid(P * (C / g.CC)), block(256);
-  if (stride == 1 && g.H != g.Hi)   // tall strips
-    hipLaunchKernelGGL((dw_wgrad_lds_kernel<1, true>), grid, block, 0, st, gin, yself, coef, yprev, ps, pt, part, g);
-  else if (stride == 1)
+  if (stride == 1)
     hipLaunchKernelGGL((dw_wgrad_lds_kernel<1>), grid, block, 0, st, gin, yself, coef, yprev, ps, pt, part, g);
   else
     hipLaunchKernelGGL((dw_wgrad_lds_kernel<2>), grid, block, 0, st, gin, yself, coef, yprev, ps, pt, part, g);

@@ -75,10 +75,8 @@ struct BwdLds {
 // BM = 64 rows per tile (4 waves x 16 rows for the dgrad MFMA) or 32 (2 row groups x
 // 2 column halves; used when KP is large so the prefetched tile fits in registers)
 template <int EPI, int KP, int BN, int BM>
-#ifndef PGDIST_PWB_WPE
-#define PGDIST_PWB_WPE 2   // minimum waves per SIMD for the register allocation (A/B build define)
-#endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PGDIST_PWB_WPE))) void pw_bwd_fused_kernel(PwBwdArgs p) {
+// 2 waves per SIMD for the register allocation (3 would spill 12-328 B per variant)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void pw_bwd_fused_kernel(PwBwdArgs p) {
   constexpr bool RAWX = EPI != EPI_BWD_LIN_ && BN >= 96;
   using L = BwdLds<KP, BN, BM, RAWX>;
   constexpr int LDA = L::LDA, LDX = L::LDX, LDC = L::LDC;
@@ -413,9 +411,8 @@ BwdGeom bwd_geom(int M, int Kg, int Ng) {
   // project convs (small Kg, wide Ng = 96 / 144 / 192): ONE N tile spanning the whole row.
   // With 48- / 64-column tiles each workgroup read and wrote 96- / 128-byte pieces of the
   // 192..384-byte NHWC rows (partial 128-B lines, G and Y re-read per N tile): 1.6-2.0 TB/s
-  // (profiles/r3_roofline_base.txt); PGDIST_PWB_WIDE=0 restores the narrow tiles
-  static const bool wide = [] { const char *e = getenv("PGDIST_PWB_WIDE"); return !(e && atoi(e) == 0); }();
-  if (wide && g.KP <= 32 && (Ng == 96 || Ng == 144 || Ng == 192)) g.BN = Ng;
+  // (profiles/r3_roofline_base.txt; 909 -> 783 us with the wide tiles)
+  if (g.KP <= 32 && (Ng == 96 || Ng == 144 || Ng == 192)) g.BN = Ng;
   // rows per tile: enough 4x8 staging items for all 256 threads, while the prefetched
   // (G, Y) tile stays within 2 waves/SIMD of registers
   const int chunks = (g.KP > g.BN ? g.KP : g.BN) / 8;
@@ -423,8 +420,7 @@ BwdGeom bwd_geom(int M, int Kg, int Ng) {
   g.ok = M >= 65536 && g.KP <= 192 && Kg % 8 == 0 && Ng % 8 == 0 && Kg > 0 && Ng > 0;
   g.nt = (Ng + g.BN - 1) / g.BN;
   const int nmt = (M + g.BM - 1) / g.BM;
-  static const int env_wgs = [] { const char *e = getenv("PGDIST_PWB_WGS"); return e ? atoi(e) : 0; }();
-  int gx = (env_wgs > 0 ? env_wgs : 512) / g.nt;
+  int gx = 512 / g.nt;   // grid target 512 (768 / 1024: slower, docs/PERF_NOTES.md round 2)
   if (gx > nmt) gx = nmt;
   gx = (gx + 7) & ~7;
   if (gx < 8) gx = 8;

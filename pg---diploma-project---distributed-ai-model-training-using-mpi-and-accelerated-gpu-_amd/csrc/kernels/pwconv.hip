@@ -690,14 +690,12 @@ static PwGeom pw_geom(int M, int N, int K, int pro, bool allow_wide = true) {
   const int kstep = g.bdirect ? 32 : 64;
   const int Kp = (K + kstep - 1) / kstep * kstep;
   const int nsteps = Kp / kstep;
-  static const int wide = [] { const char *e = getenv("PGDIST_PW_WIDE_FWD"); return e ? atoi(e) : 1; }();
   if (!g.bdirect) {
     g.BN = N <= 32 ? 32 : 64;     // BN = 128 costs occupancy (1-2 waves/SIMD) for no bandwidth gain
     // N = 96 / 144 (the expand convs at 112x112 / 56x56): one N tile over the whole row (full
     // 192 / 288-B output rows instead of 64 + 32 or 64 + 64 + 16 column slices, no MFMA / LDS
     // work on padding columns, A read once)
-    // PGDIST_PW_WIDE_FWD=2 also N = 192 (the 28x28 expand convs, three exact 64-wide tiles otherwise)
-    if (wide && allow_wide && pro != PRO_BNBWD && (N == 96 || N == 144 || (wide >= 2 && N == 192))) g.BN = N;
+    if (allow_wide && pro != PRO_BNBWD && (N == 96 || N == 144)) g.BN = N;
     g.KS = 1;
   } else {
     g.BN = (N % 64 == 0) ? 64 : 32;
@@ -708,9 +706,9 @@ static PwGeom pw_geom(int M, int N, int K, int pro, bool allow_wide = true) {
   g.nt = (N + g.BN - 1) / g.BN;
   const int BM = 128 / g.KS;
   g.nmt = (M + BM - 1) / BM;
-  static const int env_lds = [] { const char *e = getenv("PGDIST_PW_WGS"); return e ? atoi(e) : 0; }();
-  static const int env_bd = [] { const char *e = getenv("PGDIST_PW_WGS_BD"); return e ? atoi(e) : 0; }();
-  int gx = (g.bdirect ? (env_bd > 0 ? env_bd : 1024) : (env_lds > 0 ? env_lds : 2048)) / g.nt;   // LDS-resident path: 2048 (1024: +0.2-0.5 % step time)
+  // grid-size targets (docs/PERF_NOTES.md round 2 sweeps): LDS-resident path 2048 (1024:
+  // +0.2-0.5 % step time), B-direct path 1024
+  int gx = (g.bdirect ? 1024 : 2048) / g.nt;
   if (gx > g.nmt) gx = g.nmt;
   gx = (gx + 7) & ~7;                  // multiple of 8: the N tiles of one M tile share an XCD L2
   if (gx < 8) gx = 8;
@@ -861,22 +859,11 @@ bool wgrad_reduce_deferring();
 static constexpr int kMinRowsPerSplit = 512, kMinRowsSmallW = 256;
 static constexpr long long kSmallW = 200000;
 static void wgrad_geom(int M, int N, int K, int &TN, int &TK, int &S, int &rps) {
-  static const int env_rows = [] {   // PGDIST_PWWG_MINROWS: rows per split floor, all shapes (tuning)
-    const char *e = getenv("PGDIST_PWWG_MINROWS");
-    return e && atoi(e) >= kWMK ? atoi(e) / kWMK * kWMK : 0;
-  }();
-  static const int env_small = [] {   // PGDIST_PWWG_MINROWS_SMALL: the floor for N*K <= 200k (tuning)
-    const char *e = getenv("PGDIST_PWWG_MINROWS_SMALL");
-    return e && atoi(e) >= kWMK ? atoi(e) / kWMK * kWMK : kMinRowsSmallW;
-  }();
-  const int min_rows = env_rows ? env_rows : ((long long)N * K <= kSmallW ? env_small : kMinRowsPerSplit);
+  const int min_rows = (long long)N * K <= kSmallW ? kMinRowsSmallW : kMinRowsPerSplit;
   TN = N <= 32 ? 32 : (N <= 64 ? 64 : 128);
   TK = K <= 32 ? 32 : (K <= 64 ? 64 : 128);
   const int tiles = ((N + TN - 1) / TN) * ((K + TK - 1) / TK);
-  static const int target = [] {   // PGDIST_PWWG_WGS: split-M grid-size target (tuning experiments)
-    const char *e = getenv("PGDIST_PWWG_WGS");
-    return e && atoi(e) > 0 ? atoi(e) : 1024;
-  }();
+  constexpr int target = 1024;   // split-M grid-size target (512 / 2048: neutral, round 2-3 sweeps)
   S = (target + tiles - 1) / tiles;
   const int max_s = (M + min_rows - 1) / min_rows;
   if (S > max_s) S = max_s;
@@ -940,21 +927,11 @@ void launch_stem_wgrad(const bf16_t *G, const bf16_t *Y, const float *ga, const 
   hipLaunchKernelGGL(stem_wgrad_permute_kernel, dim3((O * 27 + 255) / 256), dim3(256), 0, st, tmp, grad, O);
 }
 
-bool pw_wgrad_dma_supported(int N, int K);
-void launch_pw_wgrad_dma(const bf16_t *G, const bf16_t *Y, const float *ga, const float *gb, const float *gc,
-                         const bf16_t *X, const float *xs, const float *xt, int xact, float *part, int M, int N,
-                         int K, int rps, int S, hipStream_t st);
-
 void launch_pw_wgrad(const bf16_t *G, const bf16_t *Y, const float *ga, const float *gb,
                      const float *gc, const bf16_t *X, const float *xs, const float *xt, int xact,
                      float *part, float *grad, int M, int N, int K, hipStream_t st) {
   int TN, TK, S, rps;
   wgrad_geom(M, N, K, TN, TK, S, rps);
-  if (pw_wgrad_dma_supported(N, K)) {   // LDS-DMA ring (pwwgrad.hip), same split geometry / partials
-    launch_pw_wgrad_dma(G, Y, ga, gb, gc, X, xs, xt, xact, part, M, N, K, rps, S, st);
-    launch_wgrad_reduce(part, S, (long long)N * K, grad, st);
-    return;
-  }
   PwWgArgs a{G, Y, ga, gb, gc, X, xs, xt, part, M, N, K, rps, 0, 0, 0, 0};
   if (xact == ACT_BN_RELU6) launch_wg_x<ACT_BN_RELU6>(a, TN, TK, S, st);
   else launch_wg_x<ACT_NONE>(a, TN, TK, S, st);

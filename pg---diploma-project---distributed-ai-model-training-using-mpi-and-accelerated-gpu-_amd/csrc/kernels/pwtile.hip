@@ -13,22 +13,11 @@
 // put the N tiles of an M tile 8 ids apart (same XCD, dispatched together) so
 // the A tile is fetched from HBM once into that XCD's L2.
 //
-// Split-K (the 7x7 / 14x14 layers with K = 384 .. 1280): one output tile is a chain of
-// K / KSTEP dependent load -> MFMA steps (15-20 at K = 960 / 1280), so on ~300 workgroups
-// the kernel is latency-bound (0.6-1.3 TB/s, profiles/r3c_roofline_mnv2.txt).  With
-// p.sk = SK > 1 the K steps of a tile are split over SK workgroups (ids 8 apart: same XCD);
-// each writes its fp32 accumulator fragments to a workspace slab with write-through (sc1)
-// stores, drains them, and takes a ticket on the tile's counter; the workgroup whose ticket
-// is last sums the SK slabs in split order 0..SK-1 (fixed order: bitwise independent of
-// arrival order) with sc1 loads and runs the fused epilogue; the others only join the BN
-// finalize tail.  Hand-off: MI355X_MICROARCH.md "Valid forms" table, row 1 (every store and
-// load of the slab sc1, each storing wave's vmcnt(0) before the workgroup barrier, one lane's
-// returning agent-scope add, the re-arm by the last arriver).
+// (Split-K over workgroups for the long-K 7x7 / 14x14 layers was built and measured slower --
+// 5.30 vs 4.70 ms/step, the fp32 slab round trip outweighs the shorter k chains -- and removed;
+// docs/PERF_NOTES.md round 4.)
 #include "../bnfin.h"
 
-#include <cstdlib>
-#include <cstring>
-#include <map>
 
 enum { PRO_BNBWD_T = 3, PRO_BNRES_T = 5 };
 enum { EPI_FWD_T = 0, EPI_BWD_RELU6_T = 1, EPI_BWD_LIN_T = 2 };
@@ -53,12 +42,7 @@ struct PwTArgs {
   int bn_rep;           // BN-statistics replica rows (g_bn_rep)
   const BnFin *fin;     // fused BN finalize in the tail (nullptr: none)
   const BnFin *lz;      // lazy finalize of the prologue parameters (nullptr: materialised pa/pb/pc)
-  int sk;               // K splits per output tile (1: none)
-  float *skbuf;         // [tiles][sk][256][RT*CTW*4] fp32 accumulator slabs (sk > 1)
-  int *skctr;           // [tiles] arrival tickets, 0 between launches (re-armed by the last arriver)
 };
-
-constexpr int kSc1 = 16;   // buffer cache policy bit sc1: agent-coherent (L2 write-through / L1 bypass)
 }  // namespace
 
 // KSTEP: k per pipeline step (32, or 64 for long K: half the steps / barriers, twice the
@@ -98,11 +82,10 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
   const int wm = wave >> 1, wn = wave & 1;
   const int NT = (p.N + BN - 1) / BN;
   const int nmt = (p.M + BM - 1) / BM;
-  const int SK = p.sk;
-  // workgroup -> (mt, nt, split): the NT x SK workgroups of one M tile are 8 ids apart (same XCD)
-  int mt, nt, ksplit;
+  // workgroup -> (mt, nt): the NT workgroups of one M tile are 8 ids apart (same XCD)
+  int mt, nt;
   {
-    const int NTS = NT * SK;
+    const int NTS = NT;
     const int L = blockIdx.x, full = (nmt / 8) * 8 * NTS;
     int j;
     if (L < full) {
@@ -113,15 +96,11 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
       mt = (nmt / 8) * 8 + Lr % rem;
       j = Lr / rem;
     }
-    nt = j / SK;
-    ksplit = j - nt * SK;
+    nt = j;
   }
   const int m0 = mt * BM, n0 = nt * BN;
   const int Kp = (p.K + KSTEP - 1) / KSTEP * KSTEP;
-  const int nk_all = Kp / KSTEP;
-  const int kper = (nk_all + SK - 1) / SK;
-  const int kb = ksplit * kper;                          // this split's k steps [kb, ke)
-  const int ke = kb + kper < nk_all ? kb + kper : nk_all;
+  const int kb = 0, ke = Kp / KSTEP;                    // k steps [kb, ke)
 
   constexpr bool HAS_A2 = PRO == PRO_BNBWD_T || PRO == PRO_BNRES_T;
   uint4 ra[ACH], ry[HAS_A2 ? ACH : 1], rb[F8 ? B8PT : BCH];
@@ -307,60 +286,7 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
     __syncthreads();
   }
 
-  // ---- split-K: publish this split's accumulators; the last arriver of the tile sums them
-  __shared__ int s_last;
-  if (SK > 1) {
-    constexpr int NF = RT * CTW;                           // f32x4 fragments per thread
-    const int tile = mt * NT + nt;
-    const rsrc_t rS = make_rsrc(p.skbuf, 0x7fffffffu);
-    const uint32_t mine = (uint32_t)((((size_t)tile * SK + ksplit) * 256 + tid) * NF * 16);
-#pragma unroll
-    for (int r = 0; r < RT; ++r)
-#pragma unroll
-      for (int c = 0; c < CTW; ++c) {
-        u32x4_t v;
-        v.x = __float_as_uint(acc[r][c][0]);
-        v.y = __float_as_uint(acc[r][c][1]);
-        v.z = __float_as_uint(acc[r][c][2]);
-        v.w = __float_as_uint(acc[r][c][3]);
-        __builtin_amdgcn_raw_buffer_store_b128(v, rS, (int)(mine + (r * CTW + c) * 16), 0, kSc1);
-      }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // this wave's slab stores are done
-    __syncthreads();
-    if (tid == 0) {
-      g_int *ctr = (g_int *)(p.skctr + tile);
-      const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_last = old == SK - 1;
-      if (s_last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    if (s_last) {
-      f32x4_t tot[RT][CTW];
-#pragma unroll
-      for (int q = 0; q < SK; ++q) {                       // fixed order 0..SK-1
-        const uint32_t base = (uint32_t)((((size_t)tile * SK + q) * 256 + tid) * NF * 16);
-#pragma unroll
-        for (int r = 0; r < RT; ++r)
-#pragma unroll
-          for (int c = 0; c < CTW; ++c) {
-            f32x4_t v = acc[r][c];
-            if (q != ksplit) {
-              const u32x4_t u = __builtin_amdgcn_raw_buffer_load_b128(rS, (int)(base + (r * CTW + c) * 16), 0, kSc1);
-              v = f32x4_t{__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w)};
-            }
-            tot[r][c] = q == 0 ? v : tot[r][c] + v;
-          }
-      }
-#pragma unroll
-      for (int r = 0; r < RT; ++r)
-#pragma unroll
-        for (int c = 0; c < CTW; ++c) acc[r][c] = tot[r][c];
-    }
-  } else {
-    s_last = 1;
-  }
-
-  if (s_last) {   // workgroup-uniform
+  {
   // ---- epilogue: bf16 C tile in LDS, then 16-B row chunks (same contract as pw_gemm_kernel)
 #pragma unroll
   for (int c = 0; c < CTW; ++c) {
@@ -441,7 +367,7 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
     }
     __syncthreads();
   }
-  }   // s_last
+  }
   bn_fin_tail(p.fin);
 }
 
@@ -450,87 +376,29 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
 // ===========================================================================
 namespace {
 struct TileGeom {
-  int BM, BN, KS, nmt, nt, sk;
+  int BM, BN, KS, nmt, nt;
   size_t lds;
 };
 
-// split-K workspace of one stream (launches on a stream are serialised, so one slab set and
-// one ticket array per stream serve every layer); allocated once, at the first launch, with
-// the counters zeroed; a launch that would not fit runs unsplit
-constexpr size_t kSkBufBytes = 48ull << 20;
-constexpr int kSkTiles = 16384;
-struct SkWs {
-  float *buf = nullptr;
-  int *ctr = nullptr;
-  bool tried = false;
-};
-SkWs &sk_ws(hipStream_t st) {
-  static auto *m = new std::map<hipStream_t, SkWs>();
-  SkWs &w = (*m)[st];
-  if (!w.tried) {
-    w.tried = true;
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone &&
-        hipMalloc(reinterpret_cast<void **>(&w.buf), kSkBufBytes) == hipSuccess &&
-        hipMalloc(reinterpret_cast<void **>(&w.ctr), kSkTiles * sizeof(int)) == hipSuccess &&
-        hipMemset(w.ctr, 0, kSkTiles * sizeof(int)) == hipSuccess && hipDeviceSynchronize() == hipSuccess)
-      return w;
-    w.buf = nullptr;
-    w.ctr = nullptr;
-    (void)hipGetLastError();
-  }
-  return w;
-}
+// Tile shape by a shape rule, from the per-op tile sweep of the 14x14 / 7x7 MobileNetV2 GEMMs
+// (profiles/r4_pw_tile_sweep.txt; the earlier "largest tile with >= 384 workgroups" heuristic,
+// 32-row tiles and 128-wide k steps measured slower, docs/PERF_NOTES.md round 4):
+//   N > K (expand-shaped): 128 x 64, or 128 x 128 when N*K >= 300k (1280x320, 960x320);
+//   N <= K (project / long-K): 64 rows, 128 columns when one tile covers an N of 65..127
+//   (N = 96), else 64 (N = 64, 160, 320: 64-wide column tiles waste less than 128-wide ones);
+// 64-wide k steps from K >= 256.
 TileGeom tile_geom(int M, int N, int K, int pro) {
   TileGeom g{};
-  // largest tile that still gives >= 384 workgroups (~1.5 per CU), else the smallest
-  static const int min_wgs = [] { const char *e = getenv("PGDIST_TILE_MINWG"); return e && atoi(e) > 0 ? atoi(e) : 384; }();
-  static constexpr int cand[6][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}, {32, 128}, {32, 64}};
-  int pick = 3;
-  for (int i = 0; i < 4; ++i) {
-    const long long wgs = (long long)((M + cand[i][0] - 1) / cand[i][0]) * ((N + cand[i][1] - 1) / cand[i][1]);
-    if (wgs >= min_wgs) { pick = i; break; }
+  if (N > K) {
+    g.BM = 128;
+    g.BN = (long long)N * K >= 300000 ? 128 : 64;
+  } else {
+    g.BM = 64;
+    g.BN = (N > 64 && N < 128) ? 128 : 64;
   }
-  // PGDIST_TILE_FORCE=<BM>x<BN> (tile sweeps): every launch on that tile
-  static const int force = [] {
-    const char *e = getenv("PGDIST_TILE_FORCE");
-    if (!e) return -1;
-    const int bm = atoi(e), bn = strchr(e, 'x') ? atoi(strchr(e, 'x') + 1) : 0;
-    for (int i = 0; i < 6; ++i)
-      if (bm == cand[i][0] && bn == cand[i][1]) return i;
-    return -1;
-  }();
-  // shape rule (default; PGDIST_TILE_RULE=0: the grid-size heuristic above), from the per-op tile
-  // sweep of the 14x14 / 7x7 MobileNetV2 GEMMs (profiles/r4_pw_tile_sweep.txt):
-  //   N > K (expand-shaped): 128 x 64, or 128 x 128 when N*K >= 300k (1280x320, 960x320);
-  //   N <= K (project / long-K): 64 rows, 128 columns when one tile covers an N of 65..127
-  //   (N = 96), else 64 (N = 64, 160, 320: 64-wide column tiles waste less than 128-wide ones)
-  static const int rule = [] { const char *e = getenv("PGDIST_TILE_RULE"); return e ? atoi(e) : 1; }();
-  //   PGDIST_TILE_RULE=2: the N <= K shapes on 32-row tiles (twice the workgroups of a
-  //   latency-bound long-K chain: ~300 -> ~600 on the 7x7 layers)
-  if (rule) {
-    if (N > K) pick = (long long)N * K >= 300000 ? 0 : 2;
-    else pick = (N > 64 && N < 128) ? (rule == 2 ? 4 : 1) : (rule == 2 ? 5 : 3);
-  }
-  if (force >= 0) pick = force;
-  g.BM = cand[pick][0];
-  g.BN = cand[pick][1];
   g.nmt = (M + g.BM - 1) / g.BM;
   g.nt = (N + g.BN - 1) / g.BN;
-  static const int k64 = [] { const char *e = getenv("PGDIST_TILE_K64"); return e ? atoi(e) : 256; }();
-  g.KS = (K >= k64 || g.BM == 32) ? 64 : 32;   // 32-row tiles: 64-wide k steps (one 16-B chunk per thread)
-  // split-K (opt-in, PGDIST_PW_SPLITK = grid-size target, e.g. 1024): double SK while the grid is
-  // under the target and every split keeps >= 2 k steps.  Measured OFF by default: MobileNetV2
-  // bs128 5.30 ms/step with it vs 4.70 without (same box, profiles/r4_ab_splitk_dma.txt) -- the
-  // fp32 slab traffic (8-10x the bf16 output of these small-M GEMMs, written through to memory
-  // and read back across XCDs) costs more than the shorter k chains save.
-  static const int sk_target = [] { const char *e = getenv("PGDIST_PW_SPLITK"); return e ? atoi(e) : 0; }();
-  const int nk = (K + g.KS - 1) / g.KS;
-  const long long tiles = (long long)g.nmt * g.nt;
-  g.sk = 1;
-  while (sk_target > 0 && g.sk < 8 && tiles * g.sk < sk_target && nk >= 4 * g.sk &&
-         tiles * g.sk * 2 * g.BM * g.BN * 4 <= (long long)kSkBufBytes && tiles <= kSkTiles)
-    g.sk *= 2;
+  g.KS = K >= 256 ? 64 : 32;
   const int npar = pro == ACT_NONE ? 0 : (pro == PRO_BNBWD_T ? 3 : 2);
   const size_t kp = (size_t)((K + g.KS - 1) / g.KS * g.KS);
   const size_t ops = (size_t)2 * (g.BM + g.BN) * (g.KS + 8) * 2;
@@ -544,41 +412,28 @@ TileGeom tile_geom(int M, int N, int K, int pro) {
 
 template <int PRO, int EPI, int BM, int BN, bool F8>
 void launch_tile_t(PwTArgs a, const TileGeom &g, hipStream_t st) {
-  a.sk = 1;
-  if (g.sk > 1) {
-    SkWs &w = sk_ws(st);
-    if (w.buf) {
-      a.sk = g.sk;
-      a.skbuf = w.buf;
-      a.skctr = w.ctr;
-    }
-  }
-  const dim3 grid(g.nmt * g.nt * a.sk);
+  const dim3 grid(g.nmt * g.nt);
   if constexpr (F8) {
     if (g.KS == 128) {
       hipLaunchKernelGGL((pw_tile_kernel<PRO, EPI, BM, BN, 128, F8>), grid, dim3(256), g.lds, st, a);
       return;
     }
   }
-  if constexpr (BM == 32) hipLaunchKernelGGL((pw_tile_kernel<PRO, EPI, BM, BN, 64, F8>), grid, dim3(256), g.lds, st, a);
-  else if (g.KS == 64) hipLaunchKernelGGL((pw_tile_kernel<PRO, EPI, BM, BN, 64, F8>), grid, dim3(256), g.lds, st, a);
+  if (g.KS == 64) hipLaunchKernelGGL((pw_tile_kernel<PRO, EPI, BM, BN, 64, F8>), grid, dim3(256), g.lds, st, a);
   else hipLaunchKernelGGL((pw_tile_kernel<PRO, EPI, BM, BN, 32, F8>), grid, dim3(256), g.lds, st, a);
 }
 
 template <int PRO, int EPI, bool F8 = false>
 void launch_tile_pe(const PwTArgs &a, const TileGeom &g, hipStream_t st) {
-  if (g.BM == 32) {
-    if (g.BN == 128) launch_tile_t<PRO, EPI, 32, 128, F8>(a, g, st);
-    else launch_tile_t<PRO, EPI, 32, 64, F8>(a, g, st);
-  } else if (g.BM == 128 && g.BN == 128) launch_tile_t<PRO, EPI, 128, 128, F8>(a, g, st);
+  if (g.BM == 128 && g.BN == 128) launch_tile_t<PRO, EPI, 128, 128, F8>(a, g, st);
   else if (g.BM == 64 && g.BN == 128) launch_tile_t<PRO, EPI, 64, 128, F8>(a, g, st);
   else if (g.BM == 128 && g.BN == 64) launch_tile_t<PRO, EPI, 128, 64, F8>(a, g, st);
   else launch_tile_t<PRO, EPI, 64, 64, F8>(a, g, st);
 }
 }  // namespace
 
-// BN partial rows: one per M tile of the smallest tile height any launch may pick (32 rows)
-int pw_tile_num_partials(int M, int N, int K) { return (M + 31) / 32; }
+// BN partial rows: one per M tile of the smallest tile height any launch picks (64 rows)
+int pw_tile_num_partials(int M, int N, int K) { return (M + 63) / 64; }
 
 void launch_pw_tile(int pro, int epi, const bf16_t *A, const bf16_t *A2, const float *pa, const float *pb,
                     const float *pc, const bf16_t *W, bf16_t *out, const bf16_t *Yt, const float *es,
@@ -600,11 +455,11 @@ void launch_pw_tile(int pro, int epi, const bf16_t *A, const bf16_t *A2, const f
 #undef PT_CASE
 }
 
-// the double-rate block-scaled fp8 MFMA in the tile path (128-wide k steps): PGDIST_F8_MX=2
-// (default) on the <= 64-row tiles, 1 on every tile, 0: the 16x16x32 fp8 MFMA.  bs512, one box:
-// 14.889-14.900 (2) vs 14.923-14.967 (1) vs 14.896-14.940 (0) vs bf16 14.906-14.919 ms/step
+// the double-rate block-scaled fp8 MFMA in the tile path (128-wide k steps): 2 (default) on the
+// <= 64-row tiles, 1 on every tile, 0: the 16x16x32 fp8 MFMA (pw_f8_set_mx: tests).  bs512, one
+// box: 14.889-14.900 (2) vs 14.923-14.967 (1) vs 14.896-14.940 (0) vs bf16 14.906-14.919 ms/step
 // (profiles/r4_fp8_mx_bs512_ab.txt)
-static int g_f8_mx = [] { const char *e = getenv("PGDIST_F8_MX"); return e ? atoi(e) : 2; }();
+static int g_f8_mx = 2;
 void pw_f8_set_mx(int on) { g_f8_mx = on; }
 int pw_f8_mx() { return g_f8_mx; }
 
@@ -614,8 +469,8 @@ void launch_pw_tile_f8(int pro, const bf16_t *A, const float *pa, const float *p
   PwTArgs a{A, nullptr, pa, pb, nullptr, nullptr, out, nullptr, nullptr, nullptr, nullptr, part, M, N, K,
             nullptr, W8, wsc, asc, ldw8, g_bn_rep, take_bn_fin(), take_bn_lz()};
   TileGeom g = tile_geom(M, N, K, pro);   // the bf16 LDS size bounds the e4m3 one at KS <= 64
-  // PGDIST_F8_MX=2: only the <= 64-row tiles (the 128-row ones need 157-202 VGPRs at KSTEP 128)
-  if (g_f8_mx && g.sk == 1 && (g_f8_mx == 1 || g.BM <= 64)) {
+  // mode 2: only the <= 64-row tiles (the 128-row ones need 157-202 VGPRs at KSTEP 128)
+  if (g_f8_mx && (g_f8_mx == 1 || g.BM <= 64)) {
     g.KS = 128;
     const int npar = pro == ACT_NONE ? 0 : 2;
     const size_t kp = (size_t)((K + 127) / 128 * 128);

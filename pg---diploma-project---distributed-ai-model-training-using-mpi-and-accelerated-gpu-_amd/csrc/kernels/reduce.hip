@@ -44,19 +44,13 @@ int *reduce_counters(int n, hipStream_t st) {
 // read as 16 x 16-B pieces = 256 contiguous bytes); the rows are split into nch chunks so
 // the grid has ~2k workgroups, and the last-arriving workgroup of a column block sums the
 // nch level-1 rows (<= kWredMaxChunks) the same way.
-#ifndef PGDIST_RED_ROWS4
-#define PGDIST_RED_ROWS4 0
-#endif
 constexpr int kWredMaxChunks = 128;
 constexpr int kWredTargetWgs = 512;
-// main-stream grid target (PGDIST_WRED_MAIN_WGS; default kWredTargetWgs).  512 vs the former
-// 2048, same box (scripts/gpu_r4_wred3.sh): MobileNetV2 4.498-4.509 vs 4.510-4.522 ms/step,
-// ResNet-50 11.688 / 11.708 vs 11.712 / 11.733 (small: these reductions are short, but a
-// 2k-workgroup grid delays the side stream's dispatches behind it)
-static int wred_main_wgs() {
-  static const int v = [] { const char *e = getenv("PGDIST_WRED_MAIN_WGS"); return e && atoi(e) > 0 ? atoi(e) : kWredTargetWgs; }();
-  return v;
-}
+// main-stream grid target kWredTargetWgs: 512 vs the former 2048, same box
+// (scripts/gpu_r4_wred3.sh): MobileNetV2 4.498-4.509 vs 4.510-4.522 ms/step, ResNet-50
+// 11.688 / 11.708 vs 11.712 / 11.733 (small: these reductions are short, but a 2k-workgroup
+// grid delays the side stream's dispatches behind it)
+static int wred_main_wgs() { return kWredTargetWgs; }
 constexpr int kWredSideWgs = 384;
 
 bool is_side_stream(hipStream_t st) {
@@ -83,9 +77,9 @@ PG_DEVICE void col_reduce_body(const float *__restrict__ part, int R, long long 
   const int cg = threadIdx.x & 15, stripe = threadIdx.x >> 4;
   const long long c0 = ((long long)bx * 16 + cg) * V;
   const bool cok = c0 < n;
-  float acc[V], acc2[V], acc3[V], acc4[V];
+  float acc[V], acc2[V];
 #pragma unroll
-  for (int j = 0; j < V; ++j) acc[j] = acc2[j] = acc3[j] = acc4[j] = 0.f;
+  for (int j = 0; j < V; ++j) acc[j] = acc2[j] = 0.f;
   auto ld = [&](const float *p, float (&v)[V]) {
     if constexpr (V == 4) {
       const float4 q = *reinterpret_cast<const float4 *>(p);
@@ -97,21 +91,9 @@ PG_DEVICE void col_reduce_body(const float *__restrict__ part, int R, long long 
   const int r0 = by * rch, r1 = min(R, r0 + rch);
   if (cok) {
     int r = r0 + stripe;
-    // PGDIST_RED_ROWS4 (build define, default off): four rows in flight per thread instead of
-    // two.  Measured (profiles/r3c_reduce_ab.txt): ResNet-50 11.81-11.83 -> 11.93-12.00 ms/step,
-    // MobileNetV2 within noise -- the side-stream reduction then takes HBM bandwidth from the
-    // main stream's convolutions; larger reduction grids (PGDIST_WRED_WGS 1024 / 2048) likewise
-#if PGDIST_RED_ROWS4
-    for (; r + 48 < r1; r += 64) {
-      float a[V], b[V], c[V], d[V];
-      ld(part + (size_t)r * n + c0, a);
-      ld(part + (size_t)(r + 16) * n + c0, b);
-      ld(part + (size_t)(r + 32) * n + c0, c);
-      ld(part + (size_t)(r + 48) * n + c0, d);
-#pragma unroll
-      for (int j = 0; j < V; ++j) { acc[j] += a[j]; acc2[j] += b[j]; acc3[j] += c[j]; acc4[j] += d[j]; }
-    }
-#endif
+    // (four rows in flight per thread measured slower: ResNet-50 11.81-11.83 -> 11.93-12.00
+    // ms/step, the side-stream reduction then takes HBM bandwidth from the main stream's
+    // convolutions; profiles/r3c_reduce_ab.txt)
     for (; r + 16 < r1; r += 32) {   // two rows in flight per thread, fixed order
       float a[V], b[V];
       ld(part + (size_t)r * n + c0, a);
@@ -127,7 +109,7 @@ PG_DEVICE void col_reduce_body(const float *__restrict__ part, int R, long long 
     }
   }
 #pragma unroll
-  for (int j = 0; j < V; ++j) sh[stripe][cg * V + j] = (acc[j] + acc2[j]) + (acc3[j] + acc4[j]);
+  for (int j = 0; j < V; ++j) sh[stripe][cg * V + j] = acc[j] + acc2[j];
   __syncthreads();
   const int col = threadIdx.x;   // < 16 * V: one output column per thread
   const long long oc = (long long)bx * 16 * V + col;
@@ -240,11 +222,7 @@ void wgrad_reduce_flush(hipStream_t st) {
   for (size_t b = 0; b < segs.size(); b += kRedMaxSeg) {
     RedSegs a{};
     a.nseg = (int)std::min<size_t>(kRedMaxSeg, segs.size() - b);
-    static const int env_t = [] {   // PGDIST_WRED_WGS: grid-size target of every reduction
-      const char *e = getenv("PGDIST_WRED_WGS");
-      return e && atoi(e) > 0 ? atoi(e) : 0;
-    }();
-    const int target = std::max(64, (env_t > 0 ? env_t : is_side_stream(st) ? kWredSideWgs : wred_main_wgs()) / a.nseg);
+    const int target = std::max(64, (is_side_stream(st) ? kWredSideWgs : wred_main_wgs()) / a.nseg);
     int wg = 0, ctrs = 0;
     for (int k = 0; k < a.nseg; ++k) {
       const PendingRed &r = segs[b + k];
@@ -277,11 +255,7 @@ void launch_wgrad_reduce(float *part, int S, long long n, float *grad, hipStream
   // on a weight-gradient side stream a smaller grid: the reduction is off the critical path,
   // and a 2k-workgroup launch there holds up the dispatch of the main stream's next kernel
   // (MobileNetV2 bs128 on MI355X: 5.07 ms/step at 2048, 5.00 at 512, 4.98-5.00 at 256)
-  static const int env_t = [] {   // PGDIST_WRED_WGS: grid-size target of every reduction
-    const char *e = getenv("PGDIST_WRED_WGS");
-    return e && atoi(e) > 0 ? atoi(e) : 0;
-  }();
-  const int target = env_t > 0 ? env_t : (is_side_stream(st) ? kWredSideWgs : wred_main_wgs());
+  const int target = is_side_stream(st) ? kWredSideWgs : wred_main_wgs();
   long long want = target / (nb > 0 ? nb : 1);
   int nch = (int)(want < 1 ? 1 : want);
   const int cap = colsum_rows(S);

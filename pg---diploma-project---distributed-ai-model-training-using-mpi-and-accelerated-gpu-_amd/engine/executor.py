@@ -102,8 +102,8 @@ class AtomicBNState(BNState):
       (bnfin.h bn_lazy) -- no finalize launch between producer and consumer.  The side
       outputs are written off the critical path: every forward BN by one batched finalize at
       the end of the forward, the backward ones on the weight-gradient side stream.
-    * ``fused`` (PGDIST_BN_FUSED=1): ``fin_f`` / ``fin_b`` go to the statistics PRODUCERS,
-      whose last workgroup finalizes in the producer's tail; measured slower.
+    * (``fused``: the producers' last workgroup finalizing in their tail -- bnfin.h bn_fin_tail,
+      kept as a kernel feature -- measured 5.93 vs 5.60 ms/step and is not an executor mode.)
     * ``launch`` (deterministic mode, or PGDIST_BN_LAZY=0): a separate finalize launch on
       the main stream after every producer."""
     rows_f = rows_b = 0
@@ -173,23 +173,24 @@ class MobileNetV2Executor:
     PLAN_SAFE = True
     # on_params_ready issues only recordable native ops (NativeBucketReducer): called directly
     ready_native = False
-    # depthwise dgrad+wgrad fused on maps >= this size (measured on MI355X; PGDIST_DW_FUSE_MIN_H)
-    DW_FUSE_MIN_H = int(os.environ.get("PGDIST_DW_FUSE_MIN_H", "56"))
-    # fused 1x1 dgrad+wgrad (pw_bwd) where supported; PGDIST_PW_BWD_FUSE_MIN_M raises the M threshold
-    PW_BWD_FUSE_MIN_M = int(os.environ.get("PGDIST_PW_BWD_FUSE_MIN_M", "0"))
-    # block outputs materialised by the consumer GEMM instead of a BN-apply pass: measured neutral
-    # on MI355X (the consumer reads y_p and the residual per N tile), so off by default
-    FUSE_BLOCK_OUTPUT = os.environ.get("PGDIST_FUSE_BLOCK_OUT", "0") == "1"
-    # ... or only for the blocks whose output map has at most this many pixels per image: the
-    # latency-bound 14x14 / 7x7 stages (196, default), where the BN-apply pass is a ~4 us launch
-    # on a few MB: bs128 4.517-4.530 vs 4.540-4.581 ms/step; 28x28 too (784): 4.527-4.559
-    # (scripts/gpu_r4_aug.sh); 0: none
-    FUSE_BLOCK_OUTPUT_HW = int(os.environ.get("PGDIST_FUSE_BLOCK_OUT_HW", "196"))
-    STEM_WGRAD_SIDE = os.environ.get("PGDIST_STEM_WGRAD_SIDE", "0") == "1"
-    # fused inverted-residual block forward (csrc/kernels/irblock.hip) for the stride-1 14x14 /
-    # 7x7 blocks: one persistent launch per block instead of expand GEMM + depthwise + project
-    # GEMM (PGDIST_IR_FUSE=0: the three-launch path)
-    IR_FUSE = os.environ.get("PGDIST_IR_FUSE", "1") == "1"
+    # depthwise dgrad+wgrad fused on maps >= this size (14 / 28 / 56 / 112 / never: 4.92 / 4.89 /
+    # 4.80-4.85 / 4.85 / 4.94 ms/step, docs/PERF_NOTES.md round 2)
+    DW_FUSE_MIN_H = 56
+    # fused 1x1 dgrad+wgrad (pw_bwd) wherever supported (only M >= 500k / never: 5.06 / 5.27 vs 4.80)
+    PW_BWD_FUSE_MIN_M = 0
+    # block outputs of the maps with at most this many pixels per image (the latency-bound 14x14 /
+    # 7x7 stages) are materialised by their consumer (next GEMM's prologue, or the fused block's
+    # P0) instead of a BN-apply launch: bs128 4.517-4.530 vs 4.540-4.581 ms/step; the 28x28 stage
+    # too (784): 4.527-4.559; every block: neutral (scripts/gpu_r4_aug.sh)
+    FUSE_BLOCK_OUTPUT_HW = 196
+    # side-stream joins batched per this many weight gradients (1 / 2 / 3 / 4 / 6: 5.28 / 5.23 /
+    # 5.15 / 5.22 / 5.21 ms/step, docs/PERF_NOTES.md round 2)
+    SIDE_BATCH = 3
+    # fused inverted-residual blocks (csrc/kernels/irblock.hip) for the stride-1 14x14 / 7x7
+    # blocks: one persistent launch per block forward (expand GEMM + depthwise + project GEMM)
+    # and one for its backward main chain (three dgrads); PGDIST_IR_FUSE = 1 (both) | fwd | bwd |
+    # 0 (the three-launch paths)
+    IR_FUSE = os.environ.get("PGDIST_IR_FUSE", "1")
     # fp8 mode: the forward 1x1 convs with K >= FP8_MIN_K run on e4m3 MFMA (weights per output
     # channel, activations scaled by ops.kernels.FP8_ASC); the K = 16 / 24 / 32 expand convs, the
     # backward and depthwise / BN stay bf16 / fp32
@@ -275,18 +276,24 @@ class MobileNetV2Executor:
         # blocks whose training forward runs as one fused launch: stride 1 with expansion on a
         # <= 14x14 map, input = the previous block's pending output (BN_p (+ residual) applied by
         # the fused kernel), lazy BN descriptors, bf16, and a co-resident grid on this device
-        self.ir_grid = {}
-        lazy_possible = (not K.deterministic() and os.environ.get("PGDIST_BN_FUSED", "0") != "1"
-                         and os.environ.get("PGDIST_BN_LAZY", "1") == "1")
-        if self.IR_FUSE and lazy_possible and not fp8:
+        self.ir_grid, self.irb_grid = {}, {}
+        lazy_possible = not K.deterministic() and os.environ.get("PGDIST_BN_LAZY", "1") == "1"
+        mode = {True: "1", False: "0"}.get(self.IR_FUSE, str(self.IR_FUSE))
+        if mode != "0" and lazy_possible and not fp8:
             for bi, bp in enumerate(self.blocks):
                 prev = self.blocks[bi - 1] if bi > 0 else None
-                if (bp.stride == 1 and bp.expand and bp.H <= 14 and prev is not None
-                        and prev.Ho * prev.Wo <= self.FUSE_BLOCK_OUTPUT_HW):
+                if not (bp.stride == 1 and bp.expand and bp.H <= 14 and prev is not None):
+                    continue
+                if mode in ("1", "fwd") and prev.Ho * prev.Wo <= self.FUSE_BLOCK_OUTPUT_HW:
                     n = K.ir_fwd_grid(B, bp.H, bp.cin, bp.hidden, bp.cout)
                     if n > 0:
                         self.ir_grid[bp.idx] = n
+                if mode in ("1", "bwd"):
+                    n = K.ir_bwd_grid(B, bp.H, bp.cin, bp.hidden, bp.cout)
+                    if n > 0:
+                        self.irb_grid[bp.idx] = n
         self.ir_bar = {i: torch.zeros(96, dtype=torch.int32, device=device) for i in self.ir_grid}
+        self.irb_bar = {i: torch.zeros(96, dtype=torch.int32, device=device) for i in self.irb_grid}
         self.ir_err = torch.zeros(4, dtype=torch.int32, device=device)
         o, spans = 0, []
         self.bn_rep = K.bn_rep()   # the producers' replica rows the arena is sized for
@@ -299,16 +306,14 @@ class MobileNetV2Executor:
         for bn, o, nf, nb in spans:
             bn.acc_f = self.bn_arena[o:o + nf]
             bn.acc_b = self.bn_arena[o + nf:o + nf + nb]
-        # finalize fused into the statistics producers (one arrival-counter pair per BN);
-        # opt-in (PGDIST_BN_FUSED=1): measured on MI355X at bs128 5.93 ms/step fused vs 5.60
-        # with the separate small finalize launches — every producer workgroup must wait for
-        # its statistics atomics to be acknowledged before arriving, which costs more than
-        # the kernel boundary it saves
-        self.fused_bn = not K.deterministic() and os.environ.get("PGDIST_BN_FUSED", "0") == "1"
-        # lazy finalize (default): the consumers compute the BN parameters from the accumulator
-        # rows (bnfin.h bn_lazy); one batched forward finalize, backward finalizes on the side
-        self.lazy_bn = (not K.deterministic() and not self.fused_bn
-                        and os.environ.get("PGDIST_BN_LAZY", "1") == "1")
+        # (finalize fused into the statistics producers' tails: measured on MI355X at bs128 5.93
+        # ms/step vs 5.60 with separate launches -- every producer workgroup must wait for its
+        # statistics atomics before arriving -- so not a mode of the executor)
+        self.fused_bn = False
+        # lazy finalize (default; PGDIST_BN_LAZY=0: a finalize launch after every producer): the
+        # consumers compute the BN parameters from the accumulator rows (bnfin.h bn_lazy); one
+        # batched forward finalize, backward finalizes on the side stream
+        self.lazy_bn = not K.deterministic() and os.environ.get("PGDIST_BN_LAZY", "1") == "1"
         self.bn_mode = "lazy" if self.lazy_bn else ("fused" if self.fused_bn else "launch")
         self.bn_ctr = torch.zeros(8 * len(spans) + 16, dtype=torch.int32, device=device)   # 16-B apart
         self.refresh_bn_fin()
@@ -319,7 +324,7 @@ class MobileNetV2Executor:
         self.ws_wgrad = torch.zeros(max(wg) + 1024, **f32)
         # one split-partial workspace per weight gradient of a flushed side-stream group (their
         # reductions are launched together after the group); ws_wgrad is the first
-        nws = max(1, int(os.environ.get("PGDIST_SIDE_BATCH", "3")))
+        nws = self.SIDE_BATCH
         self.ws_wgrad_pool = [self.ws_wgrad] + [torch.zeros_like(self.ws_wgrad) for _ in range(nws - 1)]
         # the stem weight gradient may run on the main stream concurrently with side-stream
         # weight gradients: its own split-M workspace
@@ -330,8 +335,8 @@ class MobileNetV2Executor:
         self.side = None
         self._side_pending = []   # deferred (BN finalizes, weight-gradient callable) pairs
         self._fin_tabs = {}       # batched backward-finalize descriptor tables by BN group
-        self.side_batch = max(1, int(os.environ.get("PGDIST_SIDE_BATCH", "3")))
-        self.batch_reductions = os.environ.get("PGDIST_RED_BATCH", "1") == "1"
+        self.side_batch = self.SIDE_BATCH
+        self.batch_reductions = True   # a group's split-M reductions in one launch (5.016 -> 5.003 ms)
         if device.type == "cuda" and side_stream:
             self.side = K.side_stream(device)
             K.register_side_stream(self.side)
@@ -397,17 +402,18 @@ class MobileNetV2Executor:
             Min, Mout = B * bp.H * bp.H, B * bp.Ho * bp.Wo
             dw_in = bp.bn_e if bp.expand else self.bn0
             nfused = getattr(self, "ir_grid", {}).get(bp.idx, 0)
+            nfb = getattr(self, "irb_grid", {}).get(bp.idx, 0)
             if bp.expand:
                 rows[bp.bn_e][0] = max(K.pw_num_partials(Min, bp.hidden, bp.cin), nfused)
-                rows[prev.bn_p][1] = (K.pw_bwd_num_partials(Min, bp.hidden, bp.cin)
-                                      if self._pw_bwd_ok(Min, bp.hidden, bp.cin)
-                                      else K.pw_num_partials(Min, bp.cin, bp.hidden))
+                rows[prev.bn_p][1] = max(K.pw_bwd_num_partials(Min, bp.hidden, bp.cin)
+                                         if self._pw_bwd_ok(Min, bp.hidden, bp.cin)
+                                         else K.pw_num_partials(Min, bp.cin, bp.hidden), nfb)
             rows[bp.bn_d][0] = max(K.dw_num_partials("fwd", B, bp.H, bp.H, bp.hidden, bp.stride), nfused)
-            rows[dw_in][1] = K.dw_num_partials("dgrad", B, bp.H, bp.H, bp.hidden, bp.stride)
+            rows[dw_in][1] = max(K.dw_num_partials("dgrad", B, bp.H, bp.H, bp.hidden, bp.stride), nfb)
             rows[bp.bn_p][0] = max(K.pw_num_partials(Mout, bp.cout, bp.hidden), nfused)
-            rows[bp.bn_d][1] = (K.pw_bwd_num_partials(Mout, bp.cout, bp.hidden)
-                                if self._pw_bwd_ok(Mout, bp.cout, bp.hidden)
-                                else K.pw_num_partials(Mout, bp.hidden, bp.cout))
+            rows[bp.bn_d][1] = max(K.pw_bwd_num_partials(Mout, bp.cout, bp.hidden)
+                                   if self._pw_bwd_ok(Mout, bp.cout, bp.hidden)
+                                   else K.pw_num_partials(Mout, bp.hidden, bp.cout), nfb)
         Mf = B * self.Hf * self.Hf
         rows[self.bn_last][0] = K.pw_num_partials(Mf, self.C_last, self.C_last_in)
         rows[self.bn_last][1] = B
@@ -601,7 +607,7 @@ class MobileNetV2Executor:
             self._fin_fwd(bp.bn_p, K.pw_num_partials(Mout, bp.cout, bp.hidden), train)
             # (the consumer -- next expand conv or the final conv, K = bp.cout -- must be a bf16
             # GEMM: the e4m3 one has no BN + residual prologue)
-            if (self.FUSE_BLOCK_OUTPUT or bp.Ho * bp.Wo <= self.FUSE_BLOCK_OUTPUT_HW) and not self._fp8_layer(bp.cout):
+            if bp.Ho * bp.Wo <= self.FUSE_BLOCK_OUTPUT_HW and not self._fp8_layer(bp.cout):
                 pend = (bp.bn_p, inp_t if bp.residual else None, bp.o)
             else:
                 pend = None   # (a previous block's output was consumed by this block's expand)
@@ -669,6 +675,9 @@ class MobileNetV2Executor:
             Hin = bp.H
             Min, Mout = B * Hin * Hin, B * bp.Ho * bp.Wo
             bnp, bnd = bp.bn_p, bp.bn_d
+            if bp.idx in self.irb_grid:
+                self._fused_block_backward(bp, prev)
+                continue
             # bn_p backward coefficients were finalised by whoever produced bp.G
             # project dgrad -> g_d (relu6 mask of BN_d) + BN_d partials
             if self._pw_bwd_ok(Mout, bp.cout, bp.hidden):
@@ -756,18 +765,45 @@ class MobileNetV2Executor:
             else:
                 # t=1 block: its input is relu6(BN0(stem)) -> stem weight gradient.  It is the last
                 # work of the backward: on the main stream it runs beside the side stream's backlog
-                # instead of queueing behind it (PGDIST_STEM_WGRAD_SIDE=1: side stream)
+                # instead of queueing behind it (5.95 vs 5.97 ms/step on the side stream, round 1)
                 bn0 = self.bn0
-                stem_wg = lambda: K.stem_wgrad(bn0.g, bn0.y, bn0.a, bn0.b, bn0.c, self.img, self.ws_stem,  # noqa: E731
-                                               f.g(self.stem_w), B, S, S, 32)
-                if self.STEM_WGRAD_SIDE:
-                    self._wgrad(lambda ws: stem_wg())
-                else:
-                    stem_wg()
+                K.stem_wgrad(bn0.g, bn0.y, bn0.a, bn0.b, bn0.c, self.img, self.ws_stem, f.g(self.stem_w), B, S, S, 32)
                 self._ready([self.stem_w])
         self._flush_side()
         if self.side is not None:   # join: the optimizer (main stream) needs every gradient
             K.stream_wait(torch.cuda.current_stream(self.device), self.side)
+
+    def _fused_block_backward(self, bp: BlockPlan, prev: BlockPlan):
+        """One block's backward main chain as ONE launch (K.ir_bwd: project dgrad -> depthwise dgrad
+        -> expand dgrad with two in-kernel BN-backward barriers); the weight gradients follow on the
+        side stream from the gradients it wrote, exactly as after the three-launch chain."""
+        f, B = self.flat, self.B
+        bnp, bnd, bne = bp.bn_p, bp.bn_d, bp.bn_e
+        Hin = bp.H
+        Min = Mout = B * Hin * Hin
+        K.ir_bwd(bp.G, bnp.y, bnp.lz_b, f.bt(bp.w_p), bnd.y, bnd.scale, bnd.shift, bnd.g, bnd.desc_b, f.b(bp.w_d),
+                 bne.y, bne.scale, bne.shift, bne.g, bne.desc_b, f.bt(bp.w_e), bp.G if bp.residual else None,
+                 prev.bn_p.y, prev.G, prev.bn_p.desc_b, self.irb_bar[bp.idx], self.ir_err, B, Hin, bp.cin, bp.hidden,
+                 bp.cout)
+        P = self.irb_grid[bp.idx]
+
+        def prj_wgrad(ws, bnd=bnd, bnp=bnp, bp=bp):
+            K.pw_wgrad(bp.G, bnp.y, bnp.a, bnp.b, bnp.c, bnd.y, bnd.scale, bnd.shift, K.ACT_BN_RELU6, ws,
+                       f.g(bp.w_p), Mout, bp.cout, bp.hidden)
+        self._wgrad(prj_wgrad, fins=((bnd, P),))
+        self._ready([bp.w_p] + bnd.param_names)
+
+        def dw_wg(ws, bnd=bnd, bne=bne, bp=bp):
+            K.dw_wgrad(bnd.g, bnd.y, bnd.coef, bne.y, bne.scale, bne.shift, ws, f.g(bp.w_d), B, Hin, Hin,
+                       bp.hidden, bp.stride)
+        self._wgrad(dw_wg, fins=((bne, P),))
+        self._ready([bp.w_d] + bne.param_names)
+
+        def exp_wgrad(ws, prev=prev, bne=bne, bp=bp):
+            K.pw_wgrad(bne.g, bne.y, bne.a, bne.b, bne.c, prev.o, None, None, K.ACT_NONE, ws, f.g(bp.w_e), Min,
+                       bp.hidden, bp.cin)
+        self._wgrad(exp_wgrad, fins=((prev.bn_p, P),))
+        self._ready([bp.w_e] + prev.bn_p.param_names)
 
     def ir_error(self) -> int:
         """Sticky error word of the fused block kernels (bit 0: a grid barrier timed out)."""

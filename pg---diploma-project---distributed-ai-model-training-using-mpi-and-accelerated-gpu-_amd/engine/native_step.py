@@ -97,8 +97,6 @@ class NativeTrainStep:
         # every depthwise / 1x1 conv weight / BatchNorm affine parameter, i.e. a broken kernel
         # family) are zeroed after every backward: a planted "broken weight gradient" bug
         self.fault_zero = [self.flat.range_of(n) for n in self._fault_names(model)]
-        self.main_stream = (torch.cuda.Stream(device, priority=-1)
-                            if device.type == "cuda" and os.environ.get("PGDIST_MAIN_PRIO", "0") == "1" else None)
         # ---- data parallel
         # PGDIST_COMM: auto (native communicator when the process group is RCCL's, c10d with gloo)
         # | rccl | p2p (IPC xGMI kernels only; also over a gloo default group) | native (both) | c10d
@@ -174,10 +172,9 @@ class NativeTrainStep:
         self.prefetch = (self.use_plan and self.augment_enabled and self.train_augment and self.exe.side is not None
                          and os.environ.get("PGDIST_AUG_PREFETCH", "1") == "1")
         self._cur, self._have, self._next = 0, False, False
-        # PGDIST_AUG_PREFETCH_AT: "backward" (default: beside the weight gradients) | "forward" (beside
-        # this step's forward, where the side stream is otherwise idle: measured 4.556-4.572 vs
-        # 4.553-4.557 ms/step, the augmentation's VALU competes with the bandwidth-bound forward)
-        self.prefetch_in_forward = os.environ.get("PGDIST_AUG_PREFETCH_AT", "backward") == "forward"
+        # (rendered beside the backward's weight gradients; beside the forward, where the side
+        # stream is otherwise idle, measured 4.556-4.572 vs 4.553-4.557 ms/step: the augmentation's
+        # VALU competes with the bandwidth-bound forward)
         self._plans = {}
         if self.prefetch:
             self._imgs = [self.exe.img, torch.empty_like(self.exe.img)]
@@ -315,8 +312,6 @@ class NativeTrainStep:
                       train=self.train_augment,
                       double_resize=self.double_resize, seed=self.seed + 17 * self.rank, hyper=self.hyper,
                       epoch_ctr=0, out_hw=self.S)
-        if self._next and self.prefetch_in_forward:
-            self._prefetch_next()   # the side stream is otherwise idle during the forward
         if self.bn_broadcast:
             if self.comm is not None:   # native: recorded collectives, no Python at replay
                 # P2P broadcast (one barrier, all links) when validated, else RCCL
@@ -344,7 +339,7 @@ class NativeTrainStep:
     def _back(self):
         """Backward (+ bucketed all-reduce), Adam and metrics."""
         exe = self.exe
-        if self._next and not self.prefetch_in_forward:
+        if self._next:
             self._prefetch_next()
         native = getattr(self.reducer, "native", False)
         if native:   # host bookkeeping at record time only; the collectives are native plan ops
@@ -410,17 +405,9 @@ class NativeTrainStep:
         self._validate_collectives()
 
     def run(self, idx: torch.Tensor, next_idx: Optional[torch.Tensor] = None):
-        """One training step (on the high-priority critical-path stream when PGDIST_MAIN_PRIO=1:
-        the hardware queue arbiter then dispatches its workgroups ahead of the weight-gradient
-        side stream's; the caller's stream is joined on both sides)."""
-        ms = self.main_stream
-        if ms is None:
-            return self._run(idx, next_idx)
-        cur = torch.cuda.current_stream(self.device)
-        ms.wait_stream(cur)
-        with torch.cuda.stream(ms):
-            self._run(idx, next_idx)
-        cur.wait_stream(ms)
+        """One training step on the caller's current stream (a high-priority critical-path stream
+        measured slower: 5.36-5.37 vs 5.30 ms/step, docs/PERF_NOTES.md round 4)."""
+        return self._run(idx, next_idx)
 
     def _run(self, idx: torch.Tensor, next_idx: Optional[torch.Tensor] = None):
         """One training step on the batch ``src[idx]`` (idx: int64 [B] on device).  With

@@ -27,8 +27,8 @@ streamed global -> LDS by buffer_load ... lds, which needs operands without a pr
 every backward conv first materialises its dy = a*G + b*Y + c once (``bn_mat``; read by both
 the dgrad and the side-stream wgrad, which then skip the BN-backward prologue), and the
 forward materialises relu(BN(y)) for the convs where the prologue costs more than the extra
-pass (``mat_dy_pays`` / ``mat_act_pays``, measured per layer with scripts/conv_bench.py;
-PGDIST_RN_DY / PGDIST_RN_ACT = all|none|auto override).
+pass (``mat_dy_pays`` / ``mat_act_pays``, measured per layer with scripts/conv_bench.py; the
+class attributes RN_DY / RN_ACT = all|none|auto select the policy).
 
 Reference call stack for the model forward: SURVEY.md §3.3 (cuDNN conv / BN / ReLU
 launches per layer); this executor replaces all of them.
@@ -91,6 +91,12 @@ class ResNet50Executor:
     PLAN_SAFE = True
     # on_params_ready issues only recordable native ops (NativeBucketReducer): called directly
     ready_native = False
+    # stem form: "s2d" (space-to-depth 4x4 s1 LDS-DMA conv, 12.13 -> 11.95 ms/step) | "direct"
+    STEM = "s2d"
+    # which convs get a materialised dy / relu(BN(y)) (all | none | auto): every dy materialised
+    # 12.48 -> 12.28 ms/step (all wgrads on the LDS-DMA kernel); activations per layer (auto)
+    RN_DY = "all"
+    RN_ACT = "auto"
 
     def __init__(self, model: ResNet, batch: int, img_size: int, device: torch.device,
                  flat: Optional[FlatParams] = None, hyper: Optional[torch.Tensor] = None,
@@ -152,17 +158,16 @@ class ResNet50Executor:
                 self.blocks.append(bp)
                 H, x_in = Ho, bp.out
         # ReLU mask of every block output but the last as bits (res_out writes it, the next block's
-        # conv1 dgrad epilogue reads 1/16 of the bytes of re-reading o; PGDIST_RN_XMASK=0: off)
-        if os.environ.get("PGDIST_RN_XMASK", "1") == "1":
-            for bp in self.blocks[:-1]:
-                bp.out_mask = torch.empty(bp.out.shape[0], bp.cout // 8, dtype=torch.uint8, device=device)
+        # conv1 dgrad epilogue reads 1/16 of the bytes of re-reading o: 12.11 -> 11.98 ms/step)
+        for bp in self.blocks[:-1]:
+            bp.out_mask = torch.empty(bp.out.shape[0], bp.cout // 8, dtype=torch.uint8, device=device)
         # ---------------- materialised operands of the LDS-DMA convs
-        self.mat = K.conv_get_glds() != 0 and os.environ.get("PGDIST_RN_MAT", "1") != "0"
-        act_mode = os.environ.get("PGDIST_RN_ACT", "auto")
+        self.mat = K.conv_get_glds() != 0
+        act_mode = self.RN_ACT
         # every dy materialised: the weight gradients then run on the LDS-DMA kernel
         # (conv_wgrad_dma_kernel), which the extra bn_mat pass more than pays for
         # (bench step 12.48 -> 12.28 ms on MI355X vs the per-layer "auto" policy)
-        dy_mode = os.environ.get("PGDIST_RN_DY", "all")
+        dy_mode = self.RN_DY
         if self.mat:
             for bp in self.blocks:
                 for c in (bp.c1, bp.c2, bp.c3) + ((bp.cd,) if bp.cd else ()):
@@ -205,7 +210,7 @@ class ResNet50Executor:
         for bn, o, nf, nb in spans:
             bn.acc_f = self.bn_arena[o:o + nf]
             bn.acc_b = self.bn_arena[o + nf:o + nf + nb]
-        # lazy BN finalize (default outside deterministic mode; PGDIST_BN_LAZY=0: a finalize launch
+        # lazy BN finalize (opt-in outside deterministic mode, PGDIST_BN_LAZY=1; else a finalize launch
         # after every producer): the consumers that support it -- max-pool, the bn_mat passes
         # (relu(BN(y)) forward, dy = a*G + b*Y + c backward) and the block output res_out --
         # compute the BN parameters they need from the replica rows in their prologue, so no
@@ -244,26 +249,25 @@ class ResNet50Executor:
         self.ws_wgrad = torch.zeros(max(wgs) + 1024, **f32)
         # one split-partial workspace per weight gradient of a flushed side-stream group: the
         # group's split-M reductions then run as one multi-segment launch after its wgrads
-        # (PGDIST_RED_BATCH=0: a reduction launch per wgrad)
-        # opt-in (PGDIST_RED_BATCH=1): measured 11.80 ms/step with a reduction per wgrad vs 11.89-11.93
-        # batched (same reduction time; the batch delays the next group's start on the side stream)
-        self.batch_reductions = os.environ.get("PGDIST_RED_BATCH", "0") == "1"
-        nws = max(1, int(os.environ.get("PGDIST_SIDE_BATCH", "3"))) if self.batch_reductions else 1
+        # -- measured 11.89-11.93 ms/step batched vs 11.80 with a reduction launch per wgrad (the
+        # batch delays the next group's start on the side stream), so per-wgrad reductions here
+        self.batch_reductions = False
+        nws = 1
         self.ws_wgrad_pool = [self.ws_wgrad] + [torch.zeros_like(self.ws_wgrad) for _ in range(nws - 1)]
         self.side = None
         self._side_pending = []
-        self.side_batch = max(1, int(os.environ.get("PGDIST_SIDE_BATCH", "3")))
+        self.side_batch = 3   # side-stream joins per 3 weight gradients (neutral vs per conv here)
         if side_stream:
             self.side = K.side_stream(device)
             K.register_side_stream(self.side)
         self.img = torch.zeros(B, img_size, img_size, 4, **bf16)
-        # space-to-depth stem (default; PGDIST_RN_STEM=direct: the 7x7 implicit GEMM over the
+        # space-to-depth stem (default; STEM = "direct": the 7x7 implicit GEMM over the
         # 4-channel image): the 7x7 s2 conv runs as a 4x4 s1 conv over img2 [B,S/2,S/2,16]
         # (K = 256 in four 64-wide LDS-DMA k-steps of 128 contiguous bytes per row instead of 49
         # 8-byte tap gathers), its weight re-laid out each step (stem_w_s2d) and its gradient
         # permuted back to the 7x7 layout.  img2 is written by image_prep(s2d=True) when the
         # training step renders the batch (img_s2d_external), else converted from img.
-        self.stem_s2d = os.environ.get("PGDIST_RN_STEM", "s2d") == "s2d" and img_size % 2 == 0
+        self.stem_s2d = self.STEM == "s2d" and img_size % 2 == 0
         self.img_s2d_external = False
         if self.stem_s2d:
             self.img2 = torch.zeros(B, img_size // 2, img_size // 2, 16, **bf16)
@@ -570,7 +574,7 @@ class ResNet50Executor:
         if self.stem_s2d:
             stem_wg = lambda ws=None: K.conv_wgrad_s2d(bn0.g, bn0.y, bn0.a, bn0.b, bn0.c, self.img2,  # noqa: E731
                                                        self.ws_stem, f.g(st.name), B, self.S // 2)
-            if bn0.lz_b is None and os.environ.get("PGDIST_RN_STEM_MAIN", "1") == "1":
+            if bn0.lz_b is None:
                 self._flush_side()
                 stem_wg()
             else:

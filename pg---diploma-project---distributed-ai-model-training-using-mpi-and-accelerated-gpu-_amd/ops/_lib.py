@@ -31,8 +31,6 @@ def lib():
                 "(or __graft_entry__.build())") from e
     if os.environ.get("PGDIST_DETERMINISTIC", "0") == "1":
         _LIB.bn_set_rep(1 << 30)   # ops.kernels.set_deterministic(True)
-    elif os.environ.get("PGDIST_BN_REP"):
-        _LIB.bn_set_rep(max(1, min(8, int(os.environ["PGDIST_BN_REP"]))))   # tuning: replica rows 1..8
     return _LIB
 
 

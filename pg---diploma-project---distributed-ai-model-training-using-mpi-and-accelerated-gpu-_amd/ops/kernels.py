@@ -223,7 +223,7 @@ def dw_num_partials(kind, B, H, W, C, stride):
 
 def dw_set_geom_mode(mask):
     """Occupancy-aware depthwise tile geometry per kernel kind (bit 1 fwd, 2 dgrad, 4 wgrad;
-    default from PGDIST_DW_GEOM).  Partial counts and workspaces depend on it: switch only
+    default 3: stride-1 forward / dgrad on >= 56-row maps).  Partial counts and workspaces depend on it: switch only
     before sizing them (tests / tuning)."""
     lib().dw_set_geom_mode(int(mask))
 
@@ -234,7 +234,7 @@ def dw_geom_mode():
 
 def dw_set_tall_rows(rows):
     """Tall depthwise geometry (stride-1 forward / dgrad, maps <= 14 rows): the batch is walked
-    as one B*H-row image in strips of `rows` rows (0: off; default from PGDIST_DW_TALL).  Like
+    as one B*H-row image in strips of `rows` rows (0: off; default 14).  Like
     dw_set_geom_mode it changes partial counts: switch only before sizing workspaces."""
     lib().dw_set_tall_rows(int(rows))
 
@@ -243,19 +243,9 @@ def dw_tall_rows():
     return lib().dw_tall_rows()
 
 
-def dw_set_tall_wrows(rows):
-    """Tall strips (`rows` rows, 0: off) for the stride-1 depthwise weight gradient on maps <= 14
-    rows (default from PGDIST_DW_TALL_W); changes its partial count."""
-    lib().dw_set_tall_wrows(int(rows))
-
-
-def dw_tall_wrows():
-    return lib().dw_tall_wrows()
-
-
 def dw_set_small_dgrad(on):
     """Round-aware slab / strip choice of the small-map stride-1 dgrad (tall geometry on;
-    default from PGDIST_DW_SMALL_DGRAD).  Changes partial counts like dw_set_tall_rows."""
+    default on).  Changes partial counts like dw_set_tall_rows."""
     lib().dw_set_small_dgrad(int(on))
 
 
@@ -397,6 +387,38 @@ def ir_fwd(xin, res, lz_in, xout, we, wd, wp, h1, h2, y, de, dd, dp, bar, err, B
                  _p(de), _p(dd), _p(dp), _p(bar), _p(err), B, H, cin, ch, cout, _s())
 
 
+def ir_bwd_grid(B, H, cin, ch, cout):
+    """Workgroups of the fused inverted-residual block backward (0: no kernel / not co-resident)."""
+    return lib().ir_bwd_grid(int(B), int(H), int(cin), int(ch), int(cout))
+
+
+def ir_bwd(G, y, lz_p, wpt, h2, sd, td, gd, dd, wd, h1, se, te, ge, de, wet, R, yprev, gout, dprev, bar, err,
+           B, H, cin, ch, cout):
+    """One MobileNetV2 inverted-residual block's backward main chain in one launch: project dgrad
+    (BN_p backward from ``lz_p``; ReLU6 mask of BN_d(h2) with the forward ``sd``/``td``) ->
+    ``gd`` + BN_d backward sums (``dd``), depthwise dgrad (BN_d backward) -> ``ge`` + BN_e sums
+    (``de``), expand dgrad (BN_e backward, + skip gradient ``R``) -> ``gout`` + the previous
+    block's BN_p sums (``dprev``).  ``wpt`` / ``wet``: the transposed 1x1 weights; ``bar``: 96
+    int32 zero before the first launch (re-armed by the kernel)."""
+    M = B * H * H
+    for t, n, nm in ((G, M * cout, "G"), (y, M * cout, "y"), (wpt, ch * cout, "wpt"), (h2, M * ch, "h2"),
+                     (gd, M * ch, "gd"), (wd, 9 * ch, "wd"), (h1, M * ch, "h1"), (ge, M * ch, "ge"),
+                     (wet, cin * ch, "wet"), (R, M * cin, "R"), (yprev, M * cin, "yprev"), (gout, M * cin, "gout")):
+        _chk(t, BF16, n, nm)
+    for t, nm in ((sd, "sd"), (td, "td"), (se, "se"), (te, "te")):
+        _chk(t, F32, ch, nm)
+    _chk(bar, torch.int32, 96, "bar")
+    _chk(err, torch.int32, 1, "err")
+    for d in (lz_p, dd, de, dprev):
+        if d is None or not (d.is_cuda and d.dtype == torch.uint8):
+            raise TypeError("ir_bwd: BN descriptors from bn_fin_desc")
+    if ir_bwd_grid(B, H, cin, ch, cout) <= 0:
+        raise ValueError(f"ir_bwd: no co-resident fused kernel for B={B} H={H} {cin}->{ch}->{cout}")
+    lib().ir_bwd(_p(G), _p(y), _p(lz_p), _p(wpt), _p(h2), _p(sd), _p(td), _p(gd), _p(dd), _p(wd), _p(h1), _p(se),
+                 _p(te), _p(ge), _p(de), _p(wet), _p(R), _p(yprev), _p(gout), _p(dprev), _p(bar), _p(err),
+                 B, H, cin, ch, cout, _s())
+
+
 FP8 = torch.uint8   # raw OCP e4m3fn bytes (torch.float8_e4m3fn views share the encoding)
 
 # activation scale applied before the e4m3 conversion of a GEMM's A operand: ReLU6 outputs
@@ -436,7 +458,7 @@ def pw_gemm_f8(pro, A, W8, wsc, out, part, M, N, K, pa=None, pb=None, asc=None, 
 
 def pw_f8_set_mx(on):
     """fp8 tile GEMMs (small M or K > 192) on the block-scaled double-rate
-    v_mfma_scale_f32_16x16x128_f8f6f4: 2 (default from PGDIST_F8_MX) on the <= 64-row tiles,
+    v_mfma_scale_f32_16x16x128_f8f6f4: 2 (default) on the <= 64-row tiles,
     1 on every tile, 0: the 16x16x32 fp8 MFMA everywhere."""
     lib().pw_f8_set_mx(int(on))
 
@@ -551,19 +573,11 @@ def stem_num_partials(B, H, W):
     return lib().stem_fwd_num_partials(B, H, W)
 
 
-def _stem_px_default():
-    # 0: the MFMA implicit GEMM (MobileNetV2 bs128 on MI355X: 4.81 vs 4.88 ms/step with the
-    # best VALU variant, px = 1)
-    v = os.environ.get("PGDIST_STEM_PX", "0")
-    if v not in ("0", "1", "2", "4"):
-        raise ValueError(f"PGDIST_STEM_PX={v!r}: must be 0 (MFMA), 1, 2 or 4")
-    return int(v)
-
-
 def stem_fwd(img, w, y, part, B, H, W, px=None, fin=None):
-    """Stem 3x3 s2 conv forward; ``px``: 0 = MFMA implicit GEMM, else output pixels per thread
-    of the VALU kernel (1, 2 or 4); default from PGDIST_STEM_PX."""
-    px = _stem_px_default() if px is None else int(px)
+    """Stem 3x3 s2 conv forward; ``px``: 0 = MFMA implicit GEMM (default: MobileNetV2 bs128 on
+    MI355X 4.81 vs 4.88 ms/step with the best VALU variant), else output pixels per thread of
+    the VALU kernel (1, 2 or 4)."""
+    px = 0 if px is None else int(px)
     if px not in (0, 1, 2, 4):
         raise ValueError(f"stem_fwd: px={px} must be 0, 1, 2 or 4")
     Ho, Wo = dw_out_hw(H, W, 2)
@@ -638,7 +652,7 @@ CE_BWD_RELU, CE_BWD_RES = 1, 2
 
 def conv_set_glds(mode):
     """Operand staging of the dense convs without a prologue: 0 = register-staged kernel,
-    2 / 3 = LDS-DMA kernel with that many LDS buffers (default 2, env PGDIST_CONV_GLDS)."""
+    2 = LDS-DMA kernel with two LDS buffers (default)."""
     lib().conv_set_glds(int(mode))
 
 
@@ -1050,15 +1064,9 @@ class LaunchPlan:
 
 
 def side_stream(device):
-    """The weight-gradient side stream of an executor.  PGDIST_SIDE_CUS=num/den confines it to
-    that fraction of the CUs (runtime/streams.cpp, hipExtStreamCreateWithCUMask) so its wide
-    launches cannot take every CU slot from the critical-path stream; unset / 0: a plain
-    stream."""
-    spec = os.environ.get("PGDIST_SIDE_CUS", "0")
-    if spec and spec != "0":
-        num, den = (int(x) for x in spec.split("/"))
-        h = lib().cu_masked_stream(device.index or 0, num, den)
-        return torch.cuda.ExternalStream(h, device=device)
+    """The weight-gradient side stream of an executor: a plain stream.  (CU-masked streams
+    (hipExtStreamCreateWithCUMask) measured 1.5-1.9x slower steps with every mask tried, even the
+    full one -- docs/PERF_NOTES.md rounds 2-4 -- and were removed.)"""
     return torch.cuda.Stream(device)
 
 
@@ -1112,7 +1120,7 @@ def _logged(fn):
 
 for _name in ("bn_fwd_finalize", "bn_bwd_finalize", "bn_apply", "bn_finalize_batch", "adam_flat", "f32_to_bf16",
               "step_begin", "reduce_metrics", "dw_fwd", "dw_dgrad", "dw_wgrad", "pw_gemm", "pw_gemm_f8", "w8_quant",
-              "wt_transpose", "pw_bwd", "ir_fwd", "wgrad_reduce", "wgrad_reduce_flush", "pw_wgrad", "stem_fwd", "stem_wgrad",
+              "wt_transpose", "pw_bwd", "ir_fwd", "ir_bwd", "wgrad_reduce", "wgrad_reduce_flush", "pw_wgrad", "stem_fwd", "stem_wgrad",
               "head", "augment", "conv_fwd", "conv_dgrad", "conv_wgrad", "bn_mat", "conv_wt", "res_out", "maxpool_fwd",
               "maxpool_bwd", "avgpool", "head_bwd", "softmax_ce", "fc_gemm", "col_sum", "image_prep", "memset"):
     globals()[_name] = _logged(globals()[_name])

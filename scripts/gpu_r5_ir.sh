@@ -3,7 +3,7 @@
 # fault tests, bench A/B (fused vs three launches), per-op roofline of the fused step
 cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/r5ir && export TMPDIR=/tmp
 O=gpurun_out/r5ir
-timeout -k 10 500 python -u -m pytest tests/test_irblock_gpu.py tests/test_executor_teacher_forced_gpu.py tests/test_comm_watchdog_gpu.py -x -v --timeout 240 --timeout-method thread > $O/tests.log 2>&1
+timeout -k 10 500 python -u -m pytest tests/test_irblock_gpu.py tests/test_executor_teacher_forced_gpu.py tests/test_comm_watchdog_gpu.py -x -v -rP --timeout 240 --timeout-method thread > $O/tests.log 2>&1
 rc=$?; grep -E "PASS|FAIL|ERROR|passed|failed" $O/tests.log | tail -20; [ $rc -ne 0 ] && exit $rc
 for i in 1 2; do
   timeout -k 10 200 python -u bench.py > $O/fused_$i.json 2> $O/b.err || { tail -20 $O/b.err; exit 1; }

@@ -60,7 +60,7 @@ FWD_SHAPES = [
     (2, 6, 512, 2048, 1, 1, 0),
     (8, 64, 64, 128, 3, 1, 1),     # 128 x 128 tiles (>= 256 workgroups)
     (4, 30, 128, 200, 3, 2, 1),    # N not a multiple of the N tile, M tail
-    (4, 7, 512, 256, 3, 1, 1),     # K = 4608 (72 k steps): split-K with PGDIST_CONV_SPLITK
+    (4, 7, 512, 256, 3, 1, 1),     # K = 4608 (72 k steps)
 ]
 
 
@@ -73,7 +73,7 @@ def glds_mode():
 
 
 @pytest.mark.parametrize("shape", FWD_SHAPES)
-@pytest.mark.parametrize("pro,glds", [(K.CP_NONE, 0), (K.CP_NONE, 2), (K.CP_NONE, 3), (K.CP_BN_RELU, 2)])
+@pytest.mark.parametrize("pro,glds", [(K.CP_NONE, 0), (K.CP_NONE, 2), (K.CP_BN_RELU, 2)])
 def test_conv_fwd(dev, shape, pro, glds, glds_mode):
     """CP_NONE with Ci % 64 == 0 runs on the LDS-DMA kernel (2 or 3 LDS buffers) unless glds=0."""
     glds_mode(glds)
@@ -125,7 +125,7 @@ DGRAD_SHAPES = [
     (2, 7, 2048, 512, 1, 1, 0),
     (8, 64, 128, 64, 3, 1, 1),     # 128 x 128 tiles
     (8, 64, 64, 128, 3, 2, 1),     # 128 x 64 tiles over 4 parity classes
-    (4, 7, 512, 256, 3, 1, 1),     # K = 2304 per class: split-K with PGDIST_CONV_SPLITK
+    (4, 7, 512, 256, 3, 1, 1),     # K = 2304 per class
 ]
 
 

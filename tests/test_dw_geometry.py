@@ -2,7 +2,7 @@
 launchers' geometry code in the extension).  The BN-statistics and weight-gradient workspaces
 are sized from these counts, so they must follow every geometry switch: tall strips across
 image boundaries on <= 14-row stride-1 maps (csrc/kernels/dwconv.hip dw_geom), the round-aware
-small-map dgrad choice, and the opt-in tall weight gradient."""
+small-map dgrad choice; the weight gradient keeps per-image strips."""
 import pytest
 
 import pgdist  # noqa: F401
@@ -11,12 +11,11 @@ from pgdist.ops import kernels as K
 
 @pytest.fixture
 def geom():
-    old = (K.dw_tall_rows(), K.dw_small_dgrad(), K.dw_tall_wrows(), K.dw_geom_mode())
+    old = (K.dw_tall_rows(), K.dw_small_dgrad(), K.dw_geom_mode())
     yield
     K.dw_set_tall_rows(old[0])
     K.dw_set_small_dgrad(old[1])
-    K.dw_set_tall_wrows(old[2])
-    K.dw_set_geom_mode(old[3])
+    K.dw_set_geom_mode(old[2])
 
 
 def test_tall_forward_strips_span_images(geom):
@@ -56,9 +55,7 @@ def test_round_aware_small_dgrad(geom):
     assert K.dw_dgrad_wgrad_workspace(128, 14, 14, 576, 1) >= P * 9 * 576
 
 
-def test_tall_weight_gradient_opt_in(geom):
-    K.dw_set_tall_wrows(0)
-    assert K.dw_num_partials("wgrad", 128, 7, 7, 960, 1) == 128
-    K.dw_set_tall_wrows(28)
-    assert K.dw_num_partials("wgrad", 128, 7, 7, 960, 1) == 32
-    assert K.dw_wgrad_workspace(128, 7, 7, 960, 1) >= 32 * 9 * 960
+def test_weight_gradient_keeps_per_image_strips(geom):
+    for rows in (0, 14):
+        K.dw_set_tall_rows(rows)
+        assert K.dw_num_partials("wgrad", 128, 7, 7, 960, 1) == 128

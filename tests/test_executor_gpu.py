@@ -96,7 +96,7 @@ def test_executor_step_matches_autograd(dev, B, S):
 
 @pytest.mark.parametrize("hw", [16, 10 ** 9])
 def test_block_output_fusion_matches_bn_apply(dev, hw, monkeypatch):
-    """Block outputs materialised by the consumer GEMM's prologue (PGDIST_FUSE_BLOCK_OUT_HW:
+    """Block outputs materialised by the consumer GEMM's prologue (MobileNetV2Executor.FUSE_BLOCK_OUTPUT_HW:
     the small-map blocks only, or every block) give the step of the separate BN-apply pass.
     Deterministic BN mode (fixed-order statistics), so the two schedules see the same BN
     parameters and the block outputs must agree to rounding."""

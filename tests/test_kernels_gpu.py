@@ -261,20 +261,17 @@ def test_dw_tall_geometry(dev, B, H, C, rows, small):
     the window taps across an image edge are masked, so forward activations and dgrad are
     identical to the per-image tiling and the BN sums / weight gradients (fused and separate)
     equal up to float summation order."""
-    old, old_small, old_w = K.dw_tall_rows(), K.dw_small_dgrad(), K.dw_tall_wrows()
+    old, old_small = K.dw_tall_rows(), K.dw_small_dgrad()
     try:
         K.dw_set_tall_rows(0)
         K.dw_set_small_dgrad(0)
-        K.dw_set_tall_wrows(0)
         ref = _dw_all(B, H, C, 1, dev)
         K.dw_set_tall_rows(rows)
         K.dw_set_small_dgrad(small)   # round-aware dgrad slab / strip choice
-        K.dw_set_tall_wrows(rows)     # the separate weight gradient in tall strips too
         out = _dw_all(B, H, C, 1, dev)
     finally:
         K.dw_set_tall_rows(old)
         K.dw_set_small_dgrad(old_small)
-        K.dw_set_tall_wrows(old_w)
     assert torch.equal(out[0], ref[0]) and torch.equal(out[2], ref[2])
     for a, b in zip(out[1:6], ref[1:6]):
         if a.dtype != torch.bfloat16:

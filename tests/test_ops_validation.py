@@ -14,13 +14,6 @@ def test_stem_px_rejected(px):
         K.stem_fwd(t, t, t, t, 1, 32, 32, px=px)
 
 
-def test_stem_px_env_rejected(monkeypatch):
-    monkeypatch.setenv("PGDIST_STEM_PX", "3")
-    t = torch.zeros(1)
-    with pytest.raises(ValueError, match="PGDIST_STEM_PX"):
-        K.stem_fwd(t, t, t, t, 1, 32, 32)
-
-
 def test_operands_of_2gib_or_more_rejected():
     """32-bit buffer offsets with the 0x80000000 mask offset: operands must stay below 2 GiB."""
     big = torch.zeros(1, dtype=torch.uint8).expand(1 << 31)        # 2 GiB, no storage behind it

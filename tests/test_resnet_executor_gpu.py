@@ -203,7 +203,8 @@ def test_resnet_lazy_bn_matches_launch(dev, monkeypatch, stem):
     and metrics agree within the float-atomic noise floor of the replica rows (both modes add the
     statistics atomically; estimated by running the launch mode twice)."""
     from pgdist.engine.native_step import NativeTrainStep
-    monkeypatch.setenv("PGDIST_RN_STEM", stem)
+    from pgdist.engine.resnet_executor import ResNet50Executor
+    monkeypatch.setattr(ResNet50Executor, "STEM", stem)
     src = torch.randint(0, 256, (16, 64, 64, 3), dtype=torch.uint8, device=dev,
                         generator=torch.Generator(device=dev).manual_seed(5))
     labels = torch.arange(16, device=dev) % 10
