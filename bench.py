@@ -201,7 +201,7 @@ def main():
                        "hip_graph": meta.get("graph"), "side_stream": meta.get("side_stream"),
                        "fp8": bool(args.fp8), "bn_broadcast": bn_broadcast and world > 1,
                        "dist_backend": backend if world > 1 else None,
-                       "allreduce": meta.get("allreduce")},
+                       "allreduce": meta["allreduce"]() if callable(meta.get("allreduce")) else meta.get("allreduce")},
         }
         out.update(health)
         if world > 1 and device.type == "cuda" and info.local_world_size > torch.cuda.device_count():

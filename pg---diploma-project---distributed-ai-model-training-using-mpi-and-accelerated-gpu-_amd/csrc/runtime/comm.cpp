@@ -319,9 +319,23 @@ void Comm::watchdog_loop() {
     std::fprintf(stderr, "%s\n", msg);
     std::fflush(stderr);
     fail(kCommErrStall, msg);
-    if (nccl && rccl().commAbort) (void)rccl().commAbort(nccl);
+    // ncclCommAbort makes RCCL's own kernels give up, but it can block behind work queued on
+    // the stream (measured: until an injected stall kernel ended): run it beside, and with an
+    // exit status end the process after a bounded grace period whether or not it returned
+    auto done = std::make_shared<std::atomic<bool>>(false);
+    if (nccl && rccl().commAbort) {
+      ncclComm_t nc = nccl;
+      std::thread([nc, done] {
+        (void)rccl().commAbort(nc);
+        done->store(true);
+      }).detach();
+    } else {
+      done->store(true);
+    }
     if (wd_exit) {
+      for (int i = 0; i < 100 && !done->load(); ++i) std::this_thread::sleep_for(std::chrono::milliseconds(20));
       std::fflush(stdout);
+      std::fflush(stderr);
       std::_Exit(wd_exit);
     }
     return;   // poisoned: every later collective throws

@@ -19,6 +19,32 @@ def _resolve_backend(backend: str, device: torch.device) -> str:
     return backend
 
 
+def allreduce_meta(step) -> dict:
+    """Gradient all-reduce layout of a native step: buckets, algorithms, the bucket objective's
+    table (simulated exposed microseconds per candidate "cap/last-cap" layout) and the measured
+    all-reduce times."""
+    red = step.reducer
+    out = {
+        "comm": "native" if getattr(red, "native", False) else "c10d",
+        "buckets_kib": [round((e - s) * 4 / 1024, 1) for s, e, _ in red.buckets],
+        "algos": list(getattr(red, "algos", ["c10d"] * len(red.buckets))),
+        "launch_plan": bool(step.use_plan),
+        "bucket_cap_mb": getattr(red, "bucket_cap_mb", None),
+        "last_bucket_mb": getattr(red, "last_bucket_mb", None),
+        "ready_times": "measured" if getattr(step, "bucket_ready_us", None) else "modelled",
+    }
+    if getattr(red, "bucket_tuning", None):
+        out["bucket_cost_us"] = red.bucket_tuning
+    tuning = getattr(step.comm, "tuning", None) if step.comm is not None else None
+    if tuning:   # the chosen buckets' sizes (every candidate size was timed)
+        sizes = {e - s for s, e, _ in red.buckets}
+        out["tuned_us"] = {str(k): {a: round(v, 1) for a, v in d.items()} for k, d in tuning.items() if k in sizes}
+    ready = getattr(step, "bucket_ready_us", None)
+    if ready:
+        out["bucket_ready_us"] = [round(max(ready.get(n, 0.0) for n in names), 1) for _, _, names in red.buckets]
+    return out
+
+
 def build_bench_step(model_name: str, batch_size: int, device: torch.device, backend: str = "auto",
                      img_size: int = 224, use_graph: bool = True, world_size: int = 1, rank: int = 0,
                      side_stream: bool = True, fp8: bool = False, bn_broadcast: bool = False):
@@ -32,21 +58,10 @@ def build_bench_step(model_name: str, batch_size: int, device: torch.device, bac
                                              bn_broadcast=bn_broadcast)
         graph = "forward" if step.graph_forward else step.graph_enabled
         meta = {"backend": "hip", "graph": graph, "side_stream": side_stream, "fp8": fp8, "_step": step}
-        red = step.reducer
-        if red is not None:
-            meta["allreduce"] = {
-                "comm": "native" if getattr(red, "native", False) else "c10d",
-                "buckets_kib": [round((e - s) * 4 / 1024, 1) for s, e, _ in red.buckets],
-                "algos": list(getattr(red, "algos", ["c10d"] * len(red.buckets))),
-                "launch_plan": bool(step.use_plan),
-                "bucket_cap_mb": getattr(red, "bucket_cap_mb", None),
-            }
-            if getattr(red, "bucket_tuning", None):
-                meta["allreduce"]["bucket_cost_us"] = red.bucket_tuning
-            tuning = getattr(step.comm, "tuning", None) if step.comm is not None else None
-            if tuning:
-                meta["allreduce"]["tuned_us"] = {str(k): {a: round(v, 1) for a, v in d.items()}
-                                                 for k, d in tuning.items()}
+        if step.reducer is not None:
+            # read when the JSON line is written: the bucket layout is re-chosen from the ready times
+            # measured on the second warm-up step (NativeTrainStep._retune_buckets)
+            meta["allreduce"] = lambda step=step: allreduce_meta(step)
         return step.bench_step, meta
     if fp8:
         raise NotImplementedError("fp8 runs on the native (hip) backend")

@@ -190,7 +190,7 @@ class MobileNetV2Executor:
     # blocks: one persistent launch per block forward (expand GEMM + depthwise + project GEMM)
     # and one for its backward main chain (three dgrads); PGDIST_IR_FUSE = 1 (both) | fwd | bwd |
     # 0 (the three-launch paths)
-    IR_FUSE = os.environ.get("PGDIST_IR_FUSE", "1")
+    IR_FUSE = os.environ.get("PGDIST_IR_FUSE", "0")
     # fp8 mode: the forward 1x1 convs with K >= FP8_MIN_K run on e4m3 MFMA (weights per output
     # channel, activations scaled by ops.kernels.FP8_ASC); the K = 16 / 24 / 32 expand convs, the
     # backward and depthwise / BN stay bf16 / fp32
