@@ -59,6 +59,17 @@ struct IrArgs {
   unsigned *err;         // sticky error word (bit 0: a grid barrier timed out)
 };
 
+// phase trace (diagnostics, scripts/ir_phases.py): when set, thread 0 of every workgroup stamps
+// the wall clock (100 MHz) at the phase boundaries into ts[workgroup][16]
+__device__ unsigned long long *g_ir_ts = nullptr;
+#define IR_MARK(k)                                                                                        \
+  do {                                                                                                    \
+    if (threadIdx.x == 0) {                                                                               \
+      unsigned long long *t_ = g_ir_ts;                                                                   \
+      if (t_) t_[(size_t)blockIdx.x * 16 + (k)] = wall_clock64();                                         \
+    }                                                                                                     \
+  } while (0)
+
 PG_DEVICE void ir_grid_sync(unsigned *ctr, unsigned nwg, unsigned *err) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores / float atomics landed
   __syncthreads();
@@ -154,6 +165,7 @@ __global__ __launch_bounds__(kIrThreads) void ir_fwd_kernel(IrArgs p) {
   const int own0 = (r0 - hr0) * W;                 // slot of the first owned pixel
   const size_t gbase = ((size_t)b * H + hr0) * W;  // global row of slot 0
 
+  IR_MARK(0);
   // ---------------- P0: input BN parameters, staged input tile (+ materialised block input)
   for (int c = tid; c < CIN; c += kIrThreads) {
     float s, t, u;
@@ -192,6 +204,7 @@ __global__ __launch_bounds__(kIrThreads) void ir_fwd_kernel(IrArgs p) {
     }
   }
   __syncthreads();
+  IR_MARK(1);
 
   // ---------------- P1: expand GEMM h1[MP][CH] = xs @ We^T, waves over column pairs
   {
@@ -255,6 +268,7 @@ __global__ __launch_bounds__(kIrThreads) void ir_fwd_kernel(IrArgs p) {
     }
   }
   __syncthreads();
+  IR_MARK(2);
   {   // raw h1 of the owned rows -> HBM (16-B rows pieces)
     constexpr int KC = CH / 8;
     for (int q = tid; q < G::NOWN * KC; q += kIrThreads) {
@@ -262,7 +276,9 @@ __global__ __launch_bounds__(kIrThreads) void ir_fwd_kernel(IrArgs p) {
       stg16(p.h1 + (gbase + i) * CH + k, *reinterpret_cast<const uint4 *>(slots + i * LDH + k));
     }
   }
+  IR_MARK(3);
   ir_grid_sync(p.bar, (unsigned)nwg, p.err);
+  IR_MARK(4);
 
   // ---------------- P2: BN_e + ReLU6 in place (bf16 activation, as materialised by the unfused
   // path's consumers), depthwise 3x3 (stride 1, pad 1) from LDS; raw h2 -> HBM only
@@ -275,6 +291,7 @@ __global__ __launch_bounds__(kIrThreads) void ir_fwd_kernel(IrArgs p) {
     st[CH + c] = 0.f;
   }
   __syncthreads();
+  IR_MARK(5);
   {
     constexpr int KC = CH / 8;
     for (int q = tid; q < npix * KC; q += kIrThreads) {
@@ -288,6 +305,7 @@ __global__ __launch_bounds__(kIrThreads) void ir_fwd_kernel(IrArgs p) {
     }
   }
   __syncthreads();
+  IR_MARK(6);
   {
     constexpr int NG = CH / 8, NITEMS = NG * ROWS;
     for (int item = tid; item < NITEMS; item += kIrThreads) {
@@ -364,6 +382,7 @@ __global__ __launch_bounds__(kIrThreads) void ir_fwd_kernel(IrArgs p) {
     }
   }
   __syncthreads();
+  IR_MARK(7);
   {
     const BnFin *dd = p.dd;
     const int rep = dd->rows, rrow = wg % rep;
@@ -372,7 +391,9 @@ __global__ __launch_bounds__(kIrThreads) void ir_fwd_kernel(IrArgs p) {
       atomicAdd(dd->acc + (size_t)(2 * rrow + 1) * CH + c, st[CH + c]);
     }
   }
+  IR_MARK(8);
   ir_grid_sync(p.bar + 32, (unsigned)nwg, p.err);
+  IR_MARK(9);
 
   // ---------------- P3: h2 of the owned rows back from L2 (this workgroup's own stores) with
   // BN_d + ReLU6 applied -> LDS; project GEMM y[NOWN][COUT] = h2' @ Wp^T
@@ -383,6 +404,7 @@ __global__ __launch_bounds__(kIrThreads) void ir_fwd_kernel(IrArgs p) {
     pt[c] = t;
   }
   __syncthreads();
+  IR_MARK(10);
   {
     constexpr int KC = CH / 8, NQ = G::NOWN * KC, NB = 8;
     const rsrc_t rH = make_rsrc(p.h2, 0x7fffffffu);
@@ -407,6 +429,7 @@ __global__ __launch_bounds__(kIrThreads) void ir_fwd_kernel(IrArgs p) {
     }
   }
   __syncthreads();
+  IR_MARK(11);
   {
     constexpr int KS = CH / 32, KCH = 6, NCH = KS / KCH, RT3 = G::RT3, NCP = COUT / 32;
     static_assert(KS % KCH == 0, "k chunks");
@@ -479,6 +502,7 @@ __global__ __launch_bounds__(kIrThreads) void ir_fwd_kernel(IrArgs p) {
   // re-arm: every workgroup has passed both barriers once it arrives here; the last arrival
   // zeroes the three counters, so a launch needs no memset of them (replays, isolated re-runs)
   __syncthreads();
+  IR_MARK(12);
   if (tid == 0) {
     g_u32 *c = (g_u32 *)(p.bar + 64);
     if (__hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)nwg - 1) {
@@ -599,6 +623,7 @@ __global__ __launch_bounds__(kIrThreads) void ir_bwd_kernel(IrBwdArgs p) {
   const int own0 = (r0 - hr0) * W;
   const size_t gbase = ((size_t)b * H + hr0) * W;
 
+  IR_MARK(0);
   // ---------------- B0: BN_p coefficients, h2 and dy of the staged pixels
   for (int c = tid; c < COUT; c += kIrThreads) {
     float a, bb, c2;
@@ -625,6 +650,7 @@ __global__ __launch_bounds__(kIrThreads) void ir_bwd_kernel(IrBwdArgs p) {
     }
   }
   __syncthreads();   // pc staged
+  IR_MARK(1);
   {
     constexpr int KC = COUT / 8, NQ = MP * KC, NIT = (NQ + kIrThreads - 1) / kIrThreads;
     const rsrc_t rG = make_rsrc(p.G, 0x7fffffffu), rY = make_rsrc(p.y, 0x7fffffffu);
@@ -653,6 +679,7 @@ __global__ __launch_bounds__(kIrThreads) void ir_bwd_kernel(IrBwdArgs p) {
     }
   }
   __syncthreads();
+  IR_MARK(2);
 
   // ---------------- B1: g_d = (dy @ Wp) * relu6'(BN_d(h2)) over the staged pixels
   {
@@ -715,7 +742,9 @@ __global__ __launch_bounds__(kIrThreads) void ir_bwd_kernel(IrBwdArgs p) {
       if (cp + 8 < NCP) body(cp + 8, bfb, bfa);
     }
   }
+  IR_MARK(3);
   ir_grid_sync(p.bar, (unsigned)nwg, p.err);
+  IR_MARK(4);
 
   // ---------------- B2: dh2 in LDS, depthwise dgrad -> g_e
   for (int c = tid; c < CH; c += kIrThreads) {
@@ -730,6 +759,7 @@ __global__ __launch_bounds__(kIrThreads) void ir_bwd_kernel(IrBwdArgs p) {
     st[CH + c] = 0.f;
   }
   __syncthreads();
+  IR_MARK(5);
   {   // dh2 = a g_d + b h2 + c over the staged pixels (g_d: this workgroup's own stores)
     constexpr int KC = CH / 8, NB = 8;
     const rsrc_t rD = make_rsrc(p.gd, 0x7fffffffu);
@@ -755,6 +785,7 @@ __global__ __launch_bounds__(kIrThreads) void ir_bwd_kernel(IrBwdArgs p) {
     }
   }
   __syncthreads();
+  IR_MARK(6);
   {
     constexpr int NG = CH / 8, NITEMS = NG * ROWS;
     const rsrc_t rH1 = make_rsrc(p.h1, 0x7fffffffu);
@@ -842,6 +873,7 @@ __global__ __launch_bounds__(kIrThreads) void ir_bwd_kernel(IrBwdArgs p) {
     }
   }
   __syncthreads();
+  IR_MARK(7);
   {
     const BnFin *de = p.de;
     const int rep = de->rows, rrow = wg % rep;
@@ -850,7 +882,9 @@ __global__ __launch_bounds__(kIrThreads) void ir_bwd_kernel(IrBwdArgs p) {
       atomicAdd(de->acc + (size_t)(2 * rrow + 1) * CH + c, st[CH + c]);
     }
   }
+  IR_MARK(8);
   ir_grid_sync(p.bar + 32, (unsigned)nwg, p.err);
+  IR_MARK(9);
 
   // ---------------- B3: dh1 of the owned pixels in LDS, dx = dh1 @ We (+ skip) -> prev.G
   for (int c = tid; c < CH; c += kIrThreads) {
@@ -861,6 +895,7 @@ __global__ __launch_bounds__(kIrThreads) void ir_bwd_kernel(IrBwdArgs p) {
     cc[c] = c2;
   }
   __syncthreads();
+  IR_MARK(10);
   {
     constexpr int KC = CH / 8, NQ = G::NOWN * KC, NB = 8;
     const rsrc_t rE = make_rsrc(p.ge, 0x7fffffffu), rH1 = make_rsrc(p.h1, 0x7fffffffu);
@@ -888,6 +923,7 @@ __global__ __launch_bounds__(kIrThreads) void ir_bwd_kernel(IrBwdArgs p) {
     }
   }
   __syncthreads();
+  IR_MARK(11);
   {
     constexpr int KS = CH / 32, KCH = 6, NCH = KS / KCH, RT3 = G::RT3, NCP = CIN / 32;
     static_assert(KS % KCH == 0, "k chunks");
@@ -958,6 +994,7 @@ __global__ __launch_bounds__(kIrThreads) void ir_bwd_kernel(IrBwdArgs p) {
     }
   }
   __syncthreads();
+  IR_MARK(12);
   if (tid == 0) {
     g_u32 *c = (g_u32 *)(p.bar + 64);
     if (__hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)nwg - 1) {
@@ -1029,6 +1066,10 @@ bool ir_dispatch(int cin, int ch, int cout, int H, F &&f) {
 
 // workgroups of one launch (B images), or 0 when the shape has no fused kernel or the grid
 // would not be co-resident on this device (the grid barriers need every workgroup resident)
+void ir_trace_set(void *ts) {   // nullptr: off (the default)
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_ir_ts), &ts, sizeof(ts));
+}
+
 int ir_fwd_grid(int B, int H, int cin, int ch, int cout) {
   int wgs = 0;
   ir_dispatch(cin, ch, cout, H, [&](auto k) { wgs = co_resident_grid<decltype(k)>(B); });

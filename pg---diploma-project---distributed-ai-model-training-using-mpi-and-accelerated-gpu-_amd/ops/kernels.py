@@ -387,6 +387,14 @@ def ir_fwd(xin, res, lz_in, xout, we, wd, wp, h1, h2, y, de, dd, dp, bar, err, B
                  _p(de), _p(dd), _p(dp), _p(bar), _p(err), B, H, cin, ch, cout, _s())
 
 
+def ir_trace_set(buf):
+    """Diagnostics: the fused block kernels stamp the wall clock (100 MHz) at their phase
+    boundaries into ``buf`` (int64 [grid][16]) from now on; None switches it off."""
+    if buf is not None:
+        _chk(buf, torch.int64, buf.numel(), "buf")
+    lib().ir_trace_set(0 if buf is None else buf.data_ptr())
+
+
 def ir_bwd_grid(B, H, cin, ch, cout):
     """Workgroups of the fused inverted-residual block backward (0: no kernel / not co-resident)."""
     return lib().ir_bwd_grid(int(B), int(H), int(cin), int(ch), int(cout))
