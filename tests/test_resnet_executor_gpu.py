@@ -201,7 +201,8 @@ def test_resnet_lazy_bn_matches_launch(dev, monkeypatch, stem):
     batched at the end of the forward / on the side stream) vs a finalize launch after every
     producer: after 4 replayed training steps the weights, Adam moments, BN running statistics
     and metrics agree within the float-atomic noise floor of the replica rows (both modes add the
-    statistics atomically; estimated by running the launch mode twice)."""
+    statistics atomically; estimated from the spread of three launch-mode runs -- one pair alone
+    can under-estimate this heavy-tailed noise by 10x at batch 8)."""
     from pgdist.engine.native_step import NativeTrainStep
     from pgdist.engine.resnet_executor import ResNet50Executor
     monkeypatch.setattr(ResNet50Executor, "STEM", stem)
@@ -209,7 +210,7 @@ def test_resnet_lazy_bn_matches_launch(dev, monkeypatch, stem):
                         generator=torch.Generator(device=dev).manual_seed(5))
     labels = torch.arange(16, device=dev) % 10
     out = []
-    for lazy in ("0", "0", "1"):
+    for lazy in ("0", "0", "0", "1"):
         monkeypatch.setenv("PGDIST_BN_LAZY", lazy)
         torch.manual_seed(0)
         st = NativeTrainStep(build_model("resnet50", num_classes=10), 8, dev, img_size=64, lr=1e-3,
@@ -226,12 +227,19 @@ def test_resnet_lazy_bn_matches_launch(dev, monkeypatch, stem):
                         if isinstance(m, torch.nn.BatchNorm2d)])
         nbt = [int(m.num_batches_tracked) for m in st.exe.model.modules() if isinstance(m, torch.nn.BatchNorm2d)]
         out.append((st.flat.master.clone(), st.flat.exp_avg.clone(), rs, nbt, losses))
-    (w0, m0, r0, n0, k0), (w1, m1, r1, _, k1), (w2, m2, r2, n2, k2) = out
+    ref, lz = out[:3], out[3]
+    (w0, m0, r0, n0, k0) = ref[0]
+    (w2, m2, r2, n2, k2) = lz
     assert n2 == n0 and set(n2) == {4}
+    pairs = [(a, b) for i, a in enumerate(ref) for b in ref[i + 1:]]
+
+    def spread(f):
+        return max(f(a, b) for a, b in pairs)
     # the first step's forward sees identical weights: its loss agrees to the atomic noise
     # (a consumer reading stale BN parameters would be off by far more)
-    assert abs(k2[0] - k0[0]) <= 1e-3 * abs(k0[0]) + 10 * abs(k1[0] - k0[0]), (k0, k1, k2)
-    noise = max(_rel(w1, w0), 1e-6)
+    lnoise = spread(lambda a, b: abs(a[4][0] - b[4][0]))
+    assert abs(k2[0] - k0[0]) <= 2e-3 * abs(k0[0]) + 10 * lnoise, ([r[4] for r in ref], k2)
+    noise = max(spread(lambda a, b: _rel(a[0], b[0])), 1e-6)
     assert _rel(w2, w0) < max(20 * noise, 1e-4), (_rel(w2, w0), noise)
-    assert _rel(m2, m0) < max(20 * max(_rel(m1, m0), 1e-6), 1e-3)
-    assert _rel(r2, r0) < max(20 * max(_rel(r1, r0), 1e-6), 1e-4)
+    assert _rel(m2, m0) < max(20 * max(spread(lambda a, b: _rel(a[1], b[1])), 1e-6), 1e-3)
+    assert _rel(r2, r0) < max(20 * max(spread(lambda a, b: _rel(a[2], b[2])), 1e-6), 1e-4)
