@@ -120,6 +120,15 @@ struct PwRaw {
   uint4 a[SUBS][2];
   uint4 y[(PRO == PRO_BNBWD || PRO == PRO_BNRES) ? SUBS : 1][2];
   uint4 b[SUBS][CTB > 0 ? CTB : 1];
+  // keep the registers allocated up to here: the epilogue then cannot reuse them, so hipcc has
+  // no write-after-write on registers a load may still target (it would wait vmcnt for the
+  // next tile's prefetch, which is meant to land behind the epilogue)
+  PG_DEVICE void hold() const {
+#pragma unroll
+    for (int i = 0; i < SUBS; ++i)
+#pragma unroll
+      for (int f = 0; f < 2; ++f) asm volatile("" ::"v"(a[i][f].x), "v"(a[i][f].y), "v"(a[i][f].z), "v"(a[i][f].w));
+  }
 };
 
 // F8: e4m3 forward (v_mfma_f32_16x16x32_fp8_fp8): the weight tile is staged as e4m3
@@ -139,6 +148,7 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
   constexpr int NP = (BM + RSTEP - 1) / RSTEP;
   constexpr int NPAR = PRO == ACT_NONE ? 0 : (PRO == PRO_BNBWD ? 3 : 2);
   constexpr bool HAS_A2 = PRO == PRO_BNBWD || PRO == PRO_BNRES;
+  constexpr bool AOUT = PRO == PRO_BNRES || PRO == ACT_BN;   // consumers of a pending block output
   constexpr int SUBS = BDIRECT ? 1 : 2;     // 32-k MFMA sub-steps per pipeline step
   constexpr int KSTEP = 32 * SUBS;
   constexpr int EB = NP < 4 ? NP : 4;       // epilogue rows whose operands are loaded together
@@ -281,7 +291,9 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
       s16x8_t af[2];
 #pragma unroll
       for (int f = 0; f < 2; ++f) af[f] = a_transform<PRO>(r.a[ss][f], r.y[HAS_A2 ? ss : 0][f], Ps, Kp, kl);
-      if (p.Aout && blockIdx.y == 0) {   // materialise the transformed A (block output) once
+      // (only the block-output consumers pass Aout: a possible store here would make hipcc wait
+      // for the next tile's prefetch before it reuses these registers in the epilogue)
+      if (AOUT && p.Aout && blockIdx.y == 0) {   // materialise the transformed A (block output) once
 #pragma unroll
         for (int f = 0; f < 2; ++f) {
           const int row = cur_m0 + rg * 32 + f * 16 + (lane & 15);
@@ -314,7 +326,9 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
       if (ns >= nsteps) { ns = kp; nm = mt + gridDim.x; }
       load(nxt, nm * BM, ns, nm < nmt);
       compute(cur, s);
-      cur = nxt;
+      // the next tile's first fragments are taken over after the epilogue below, so their
+      // load latency hides behind it (a copy here waits vmcnt(0) for them right after issue)
+      if (s + KS < nsteps) cur = nxt;
     }
     // ---- C tile to LDS: acc[f][c][j] = C[rg*32 + f*16 + 4*(lane>>4) + j][c*16 + (lane&15)]
 #pragma unroll
@@ -332,6 +346,10 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(PwArgs p) {
         }
       }
     __syncthreads();
+    // take over the next tile's first fragments before this tile's stores are issued (vmcnt
+    // counts loads and stores in one queue: a wait placed after the stores would drain them too)
+    cur.hold();
+    cur = nxt;
 #pragma unroll
     for (int i0 = 0; i0 < NP; i0 += EB) {
       // bwd epilogue operands of EB rows are loaded together (one latency per batch)
