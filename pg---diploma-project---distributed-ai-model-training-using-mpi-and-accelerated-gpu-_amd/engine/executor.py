@@ -176,8 +176,6 @@ class MobileNetV2Executor:
     # depthwise dgrad+wgrad fused on maps >= this size (14 / 28 / 56 / 112 / never: 4.92 / 4.89 /
     # 4.80-4.85 / 4.85 / 4.94 ms/step, docs/PERF_NOTES.md round 2)
     DW_FUSE_MIN_H = 56
-    # blocks (features.<i>) kept on the lean dgrad + side-stream wgrad even on large maps
-    DW_SIDE = tuple(int(x) for x in os.environ.get("PGDIST_DW_SIDE", "").split(",") if x.strip())
     # fused 1x1 dgrad+wgrad (pw_bwd) wherever supported (only M >= 500k / never: 5.06 / 5.27 vs 4.80)
     PW_BWD_FUSE_MIN_M = 0
     # block outputs of the maps with at most this many pixels per image (the latency-bound 14x14 /
@@ -246,7 +244,7 @@ class MobileNetV2Executor:
                 wg.append(K.pw_wgrad_workspace(Min, blk.hidden, blk.inp))
                 if self._pw_bwd_ok(Min, blk.hidden, blk.inp):
                     wparts[(i, "e")] = K.pw_bwd_wgrad_workspace(Min, blk.hidden, blk.inp)
-            if Hin >= self.DW_FUSE_MIN_H and i not in self.DW_SIDE:
+            if Hin >= self.DW_FUSE_MIN_H:
                 wparts[(i, "d")] = K.dw_dgrad_wgrad_workspace(B, Hin, Hin, blk.hidden, blk.stride)
             else:
                 wg.append(K.dw_wgrad_workspace(B, Hin, Hin, blk.hidden, blk.stride))
