@@ -22,6 +22,21 @@
 enum { PRO_BNBWD_T = 3, PRO_BNRES_T = 5 };
 enum { EPI_FWD_T = 0, EPI_BWD_RELU6_T = 1, EPI_BWD_LIN_T = 2 };
 
+// Phase trace (diagnostics builds only, PGDIST_DEFINES=PGDIST_PWT_TRACE): thread 0 of every
+// workgroup stamps the wall clock (100 MHz) at the phase boundaries into g_pwt_ts[wg][8]
+#ifdef PGDIST_PWT_TRACE
+__device__ unsigned long long *g_pwt_ts = nullptr;
+#define PWT_MARK(k)                                                                              \
+  do {                                                                                           \
+    if (threadIdx.x == 0) {                                                                      \
+      unsigned long long *t_ = g_pwt_ts;                                                         \
+      if (t_) t_[(size_t)blockIdx.x * 8 + (k)] = wall_clock64();                                 \
+    }                                                                                            \
+  } while (0)
+#else
+#define PWT_MARK(k) ((void)0)
+#endif
+
 namespace {
 struct PwTArgs {
   const bf16_t *A;      // [M][K]
@@ -68,6 +83,7 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
   constexpr int CH = BN / 8, RSTEP = 256 / CH, NP = BM / RSTEP;
   constexpr int EB = NP < 4 ? NP : 4;
   static_assert(ACH >= 1 && BCH >= 1 && NP >= 1, "tile too small for 256 threads");
+  PWT_MARK(0);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t *As = reinterpret_cast<bf16_t *>(smem);                         // [2][BM][kLDK]
   bf16_t *Bs = As + 2 * BM * kLDK;                                       // [2][BN][kLDK]
@@ -103,13 +119,20 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
   const int kb = 0, ke = Kp / KSTEP;                    // k steps [kb, ke)
 
   constexpr bool HAS_A2 = PRO == PRO_BNBWD_T || PRO == PRO_BNRES_T;
-  uint4 ra[ACH], ry[HAS_A2 ? ACH : 1], rb[F8 ? B8PT : BCH];
+  constexpr bool AOUT = EPI == EPI_FWD_T && (PRO == PRO_BNRES_T || PRO == ACT_BN);
+  // PF2 (64-row tiles with 64-wide k steps: the long-K project / dgrad GEMMs, K >= 256): two
+  // register sets, the loads of step ks + 2 issued while step ks + 1's land in the other set
+  // (two k steps of global-load latency hidden instead of one).  Elsewhere one set: the
+  // 128-row tiles would double their VGPRs, and K < 256 is at most 8 steps.
+  constexpr bool PF2 = BM == 64 && KSTEP == 64 && !F8;
+  uint4 ra0[ACH], ry0[HAS_A2 ? ACH : 1], rb0[F8 ? B8PT : BCH];
+  uint4 ra1[PF2 ? ACH : 1], ry1[PF2 && HAS_A2 ? ACH : 1], rb1[PF2 ? BCH : 1];
   // bounds-checked buffer loads issued unconditionally (masked: out-of-range offset, reads 0),
   // so the one-step-ahead prefetch is not drained by a vmcnt(0) at a branch join
   const rsrc_t rA = make_rsrc(p.A, (uint32_t)((size_t)p.M * p.K * 2));
   const rsrc_t rA2 = make_rsrc(HAS_A2 ? p.A2 : p.A, (uint32_t)((size_t)p.M * p.K * 2));
   const rsrc_t rW = F8 ? make_rsrc(p.W8, (uint32_t)((size_t)p.N * p.ldw8)) : make_rsrc(p.W, (uint32_t)((size_t)p.N * p.K * 2));
-  auto load = [&](int k0, bool valid) {
+  auto load = [&](auto &ra, auto &ry, auto &rb, int k0, bool valid) {
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
       const int c = tid + i * 256, row = c / KCH, kk = (c % KCH) * 8;
@@ -135,7 +158,7 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
       }
     }
   };
-  auto write = [&](int buf, int k0) {
+  auto write = [&](const auto &ra, const auto &ry, const auto &rb, int buf, int k0) {
     bf16_t *Ab = As + buf * BM * kLDK;
     bf16_t *Bb = Bs + buf * BN * kLDK;
 #pragma unroll
@@ -166,7 +189,10 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
           continue;
         }
         v = pack8(x);
-        if (p.Aout && nt == 0) {   // materialise the block output once (N-tile 0)
+        // materialise the block output once (N-tile 0); compiled only into the consumer forms
+        // that take one (a possibly-issued store in the k loop shares the vmcnt queue with the
+        // prefetch loads, and the waitcnt pass then drains the queue at the loop header)
+        if (AOUT && p.Aout && nt == 0) {
           const int gr = m0 + row;
           if (gr < p.M && k < p.K) stg16(p.Aout + (size_t)gr * p.K + k, v);
         }
@@ -200,7 +226,9 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
 #pragma unroll
     for (int c = 0; c < CTW; ++c) acc[r][c] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  load(kb * KSTEP, kb < ke);   // first operand loads in flight during the prologue-parameter staging
+  // first operand loads (PF2: first two steps) in flight during the prologue-parameter staging
+  load(ra0, ry0, rb0, kb * KSTEP, kb < ke);
+  if constexpr (PF2) load(ra1, ry1, rb1, min(kb + 1, ke - 1) * KSTEP, true);
   if constexpr (NPAR > 0) {
     for (int i = tid; i < Kp; i += 256) {
       const bool ok = i < p.K;
@@ -218,11 +246,11 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
     }
   }
   __syncthreads();   // Ps staged
-  write(0, kb * KSTEP);
+  PWT_MARK(1);
+  write(ra0, ry0, rb0, 0, kb * KSTEP);
   __syncthreads();
-  for (int ks = kb; ks < ke; ++ks) {
-    const int buf = (ks - kb) & 1;
-    load((ks + 1) * KSTEP, ks + 1 < ke);
+  PWT_MARK(2);
+  auto step = [&](int buf) {   // MFMAs of the k step staged in LDS buffer buf
     const bf16_t *Ab = As + buf * BM * kLDK;
     const bf16_t *Bb = Bs + buf * BN * kLDK;
     if constexpr (F8 && KSTEP == 128) {
@@ -282,10 +310,34 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
                                                               __builtin_bit_cast(bf16x8_t, bf), acc[r][c], 0, 0, 0);
       }
     }
-    if (ks + 1 < ke) write(buf ^ 1, (ks + 1) * KSTEP);
-    __syncthreads();
+  };
+  if constexpr (PF2) {
+    // two k steps per iteration so each register set has a static index.  Every load is
+    // issued unconditionally (past the end: the last step again, never used) -- a load under a
+    // wave-uniform branch makes the loop header join paths with different loads in flight,
+    // where the waitcnt pass then drains the queue (vmcnt(0)) and the second stage is lost
+    for (int ks = kb; ks < ke; ks += 2) {
+      load(ra0, ry0, rb0, min(ks + 2, ke - 1) * KSTEP, true);
+      step(0);
+      if (ks + 1 < ke) write(ra1, ry1, rb1, 1, (ks + 1) * KSTEP);
+      __syncthreads();
+      if (ks + 1 >= ke) break;
+      load(ra1, ry1, rb1, min(ks + 3, ke - 1) * KSTEP, true);
+      step(1);
+      if (ks + 2 < ke) write(ra0, ry0, rb0, 0, (ks + 2) * KSTEP);
+      __syncthreads();
+    }
+  } else {
+    for (int ks = kb; ks < ke; ++ks) {   // one step ahead
+      const int buf = (ks - kb) & 1;
+      load(ra0, ry0, rb0, (ks + 1) * KSTEP, ks + 1 < ke);
+      step(buf);
+      if (ks + 1 < ke) write(ra0, ry0, rb0, buf ^ 1, (ks + 1) * KSTEP);
+      __syncthreads();
+    }
   }
 
+  PWT_MARK(3);
   {
   // ---- epilogue: bf16 C tile in LDS, then 16-B row chunks (same contract as pw_gemm_kernel)
 #pragma unroll
@@ -354,6 +406,7 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
     }
   }
   __syncthreads();
+  PWT_MARK(4);
   // ---- BN partials of this tile's columns -> part[mt][2][N]
   for (int s = 0; s < 2; ++s) {
     const int rgrp = tid / CH;
@@ -368,7 +421,9 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
     __syncthreads();
   }
   }
+  PWT_MARK(5);
   bn_fin_tail(p.fin);
+  PWT_MARK(6);
 }
 
 // ===========================================================================
@@ -431,6 +486,14 @@ void launch_tile_pe(const PwTArgs &a, const TileGeom &g, hipStream_t st) {
   else launch_tile_t<PRO, EPI, 64, 64, F8>(a, g, st);
 }
 }  // namespace
+
+void pwt_trace_set(void *ts) {   // nullptr: off; no-op unless built with PGDIST_PWT_TRACE
+#ifdef PGDIST_PWT_TRACE
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pwt_ts), &ts, sizeof(ts));
+#else
+  (void)ts;
+#endif
+}
 
 // BN partial rows: one per M tile of the smallest tile height any launch picks (64 rows)
 int pw_tile_num_partials(int M, int N, int K) { return (M + 63) / 64; }

@@ -337,8 +337,8 @@ def pw_gemm(pro, epi, A, W, out, part, M, N, K, A2=None, pa=None, pb=None, pc=No
         assert A2 is not None and pc is not None
     if pro == PRO_BNRES:
         assert A2 is not None and epi == EPI_FWD
-    if Aout is not None and pro not in (ACT_BN_RELU6, ACT_BN, PRO_BNRES):
-        raise ValueError("pw_gemm: Aout needs a transforming prologue")
+    if Aout is not None and (pro not in (ACT_BN, PRO_BNRES) or epi != EPI_FWD):
+        raise ValueError("pw_gemm: Aout (block output) needs the ACT_BN / PRO_BNRES forward prologue")
     if epi in (EPI_BWD_RELU6, EPI_BWD_LIN):
         assert Yt is not None
     if epi == EPI_BWD_RELU6:
@@ -393,6 +393,14 @@ def ir_trace_set(buf):
     if buf is not None:
         _chk(buf, torch.int64, buf.numel(), "buf")
     lib().ir_trace_set(0 if buf is None else buf.data_ptr())
+
+
+def pwt_trace_set(buf):
+    """Diagnostics (builds with PGDIST_DEFINES=PGDIST_PWT_TRACE): the small-M pointwise GEMM
+    (pw_tile) stamps the wall clock at its phase boundaries into ``buf`` (int64 [grid][8])."""
+    if buf is not None:
+        _chk(buf, torch.int64, buf.numel(), "buf")
+    lib().pwt_trace_set(0 if buf is None else buf.data_ptr())
 
 
 def ir_bwd_grid(B, H, cin, ch, cout):

@@ -9,4 +9,4 @@ PKG=pg---diploma-project---distributed-ai-model-training-using-mpi-and-accelerat
 rm -rf ab/base && mkdir -p ab/base
 git archive "$REV" bench.py pgdist.py __graft_entry__.py $PKG | tar -x -C ab/base
 (cd ab/base && python -c "import __graft_entry__ as g; g.build()" 2>&1 | tail -1)
-rm -rf ab/base/$PKG/build ab/base/$PKG/csrc/*.o
+rm -rf ab/base/build ab/base/$PKG/build ab/base/$PKG/csrc/*.o
