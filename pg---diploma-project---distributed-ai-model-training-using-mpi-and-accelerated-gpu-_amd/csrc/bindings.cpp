@@ -69,6 +69,8 @@ int ir_fwd_grid(int, int, int, int, int);
 int ir_bwd_grid(int, int, int, int, int);
 void ir_trace_set(void *);
 void pwt_trace_set(void *);
+void pwb_trace_set(void *);
+void pwg_trace_set(void *);
 void launch_ir_bwd(const bf16_t *, const bf16_t *, const void *, const bf16_t *, const bf16_t *, const float *,
                    const float *, bf16_t *, const void *, const bf16_t *, const bf16_t *, const float *, const float *,
                    bf16_t *, const void *, const bf16_t *, const bf16_t *, const bf16_t *, bf16_t *, const void *,
@@ -277,6 +279,10 @@ PYBIND11_MODULE(_pgdist_C, m) {
         "phase trace buffer of the fused block kernels ([grid][16] uint64 wall-clock stamps; 0: off)");
   m.def("pwt_trace_set", [](P ts) { pwt_trace_set(reinterpret_cast<void *>(ts)); },
         "phase trace buffer of pw_tile ([grid][8] uint64 wall-clock stamps; 0: off; PGDIST_PWT_TRACE builds)");
+  m.def("pwb_trace_set", [](P ts) { pwb_trace_set(reinterpret_cast<void *>(ts)); },
+        "phase-sum buffer of pw_bwd_fused ([grid][8] uint64; 0: off; PGDIST_PWT_TRACE builds)");
+  m.def("pwg_trace_set", [](P ts) { pwg_trace_set(reinterpret_cast<void *>(ts)); },
+        "phase trace buffer of pw_wgrad ([grid][8] uint64; 0: off; PGDIST_PWT_TRACE builds)");
   m.def("ir_bwd_grid", &ir_bwd_grid, "workgroups of the fused block backward (0: unsupported / not co-resident)");
   m.def("ir_bwd", [](P G, P y, P lz_p, P wpt, P h2, P sd, P td, P gd, P dd, P wd, P h1, P se, P te, P ge, P de,
                      P wet, P R, P yprev, P gout, P dprev, P bar, P err, int B, int H, int cin, int ch, int cout,

@@ -33,6 +33,31 @@ enum { EPI_BWD_RELU6_ = 1, EPI_BWD_LIN_ = 2 };   // same values as pwconv.hip
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
 
+// Phase trace (diagnostics builds only, PGDIST_DEFINES=PGDIST_PWT_TRACE): thread 0 of every
+// workgroup sums the wall clock (100 MHz ticks) spent per phase over its tiles and writes the
+// sums to g_pwb_ts[wg][8]: 0 prologue, 1 staging (incl. the wait for the prefetched tile),
+// 2 MFMAs, 3 C tile, 4 epilogue stores, 5 tail, 6 tiles
+#ifdef PGDIST_PWT_TRACE
+__device__ unsigned long long *g_pwb_ts = nullptr;
+#define PWB_T0() unsigned long long pwb_acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pwb_last_ = wall_clock64()
+#define PWB_MARK(k)                                       \
+  do {                                                    \
+    const unsigned long long n_ = wall_clock64();         \
+    pwb_acc_[k] += n_ - pwb_last_;                        \
+    pwb_last_ = n_;                                       \
+  } while (0)
+#define PWB_DONE()                                                                  \
+  do {                                                                              \
+    unsigned long long *t_ = g_pwb_ts;                                              \
+    if (t_ && threadIdx.x == 0)                                                     \
+      for (int k_ = 0; k_ < 8; ++k_) t_[(size_t)blockIdx.x * 8 + k_] = pwb_acc_[k_]; \
+  } while (0)
+#else
+#define PWB_T0() ((void)0)
+#define PWB_MARK(k) ((void)0)
+#define PWB_DONE() ((void)0)
+#endif
+
 namespace {
 struct PwBwdArgs {
   const bf16_t *G, *Y;          // [M][Kg]
@@ -103,6 +128,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
   float *Red = reinterpret_cast<float *>(smem + L::RED);
   float *Ps = reinterpret_cast<float *>(smem + L::PS);
 
+  PWB_T0();
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int rw = RGS >= 4 ? wave : wave % RGS, cw = RGS >= 4 ? 0 : wave / RGS;   // rows rw + 4*r
   const int n0 = blockIdx.y * BN;
@@ -184,6 +210,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
   };
 
   load_tile(blockIdx.x * BM, blockIdx.x < nmt);
+  PWB_MARK(0);
   for (int mt = blockIdx.x; mt < nmt; mt += gridDim.x) {
     const int m0 = mt * BM;
     __syncthreads();                 // previous tile's epilogue is done with Cs (aliases the staging)
@@ -245,6 +272,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
       }
     }
     __syncthreads();
+    PWB_MARK(1);
     load_tile((mt + gridDim.x) * BM, mt + gridDim.x < nmt);   // next tile in flight from here on
     // ---- dgrad MFMA: wave -> rows rw*16 .. +16, column tiles cw*CTW .. +CTW
     f32x4_t acc[RPW][CTW];
@@ -302,6 +330,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
       }
     }
     __syncthreads();                 // staging reads done: Cs may overwrite it
+    PWB_MARK(2);
     // acc[r][c][j] = C[(rw + 4r)*16 + 4*(lane>>4) + j][(cw*CTW + c)*16 + (lane&15)]
 #pragma unroll
     for (int r = 0; r < RPW; ++r)
@@ -311,6 +340,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
         for (int j = 0; j < 4; ++j)
           Cs[((rw + 4 * r) * 16 + 4 * (lane >> 4) + j) * LDC + (cw * CTW + c) * 16 + (lane & 15)] = f2bf(acc[r][c][j]);
     __syncthreads();
+    PWB_MARK(3);
     // ---- epilogue, item mapping (4 rows x 8 cols, operands already in registers)
 #pragma unroll
     for (int i = 0; i < IX; ++i) {
@@ -350,6 +380,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
         }
       }
     }
+    PWB_MARK(4);
+#ifdef PGDIST_PWT_TRACE
+    pwb_acc_[6] += 1;
+#endif
   }
   __syncthreads();
   // ---- wgrad partial of this workgroup: accW[u][j] = dW[ti*16 + 4*(lane>>4) + j][n0 + tj*16 + (lane&15)]
@@ -388,6 +422,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
     __syncthreads();
   }
   bn_fin_tail(p.fin);
+  PWB_MARK(5);
+  PWB_DONE();
+}
+
+void pwb_trace_set(void *ts) {   // nullptr: off; no-op unless built with PGDIST_PWT_TRACE
+#ifdef PGDIST_PWT_TRACE
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pwb_ts), &ts, sizeof(ts));
+#else
+  (void)ts;
+#endif
 }
 
 // ===========================================================================

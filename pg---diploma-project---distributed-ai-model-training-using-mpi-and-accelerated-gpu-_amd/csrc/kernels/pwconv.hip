@@ -566,8 +566,26 @@ PG_DEVICE void wg_load_im2col(WgItem &it, const PwWgArgs &p, rsrc_t rx, int chun
   }
 }
 
+// Phase trace (diagnostics builds only, PGDIST_DEFINES=PGDIST_PWT_TRACE): thread 0 of every
+// pw_wgrad workgroup stamps the wall clock (100 MHz) into g_pwg_ts[wg][8]: start (0), prologue
+// parameters staged (1), first tile in LDS (2), k loop done (3), partial tile stored (4)
+#ifdef PGDIST_PWT_TRACE
+__device__ unsigned long long *g_pwg_ts = nullptr;
+#define PWG_MARK(k)                                                                                \
+  do {                                                                                             \
+    if (threadIdx.x == 0) {                                                                        \
+      unsigned long long *t_ = g_pwg_ts;                                                           \
+      const size_t wg_ = blockIdx.x + (size_t)gridDim.x * (blockIdx.y + (size_t)gridDim.y * blockIdx.z); \
+      if (t_) t_[wg_ * 8 + (k)] = wall_clock64();                                                  \
+    }                                                                                              \
+  } while (0)
+#else
+#define PWG_MARK(k) ((void)0)
+#endif
+
 template <int XPRO, int TN, int TK>
 __global__ __launch_bounds__(256) void pw_wgrad_kernel(PwWgArgs p) {
+  PWG_MARK(0);
   // output tile TN x TK split over 4 waves as 2 x 2 quadrants
   constexpr int QN = TN / 2, QK = TK / 2;
   constexpr int RN = QN / 16, RK = QK / 16;
@@ -602,6 +620,7 @@ __global__ __launch_bounds__(256) void pw_wgrad_kernel(PwWgArgs p) {
   const rsrc_t rX = make_rsrc(p.X, XPRO == IM2COL_STEM ? (uint32_t)((size_t)(p.M / (p.oh * p.ow)) * p.ih * p.iw * 8)
                                                      : (uint32_t)((size_t)p.M * p.K * 2));
   __syncthreads();
+  PWG_MARK(1);
 
   f32x4_t acc[RN][RK];
 #pragma unroll
@@ -649,6 +668,7 @@ __global__ __launch_bounds__(256) void pw_wgrad_kernel(PwWgArgs p) {
     write_step(mbeg, 0);
   }
   __syncthreads();
+  PWG_MARK(2);
   for (int m0 = mbeg; m0 < mend; m0 += kWMK) {
     const bool has_next = m0 + kWMK < mend;
     if (has_next) load_step(m0 + kWMK);           // global loads in flight during the MFMAs
@@ -673,6 +693,7 @@ __global__ __launch_bounds__(256) void pw_wgrad_kernel(PwWgArgs p) {
     __syncthreads();
     buf ^= 1;
   }
+  PWG_MARK(3);
   // acc[a][b][j] = dW[n0 + wn*QN + a*16 + 4*(lane>>4) + j][k0 + wk*QK + b*16 + (lane&15)]
   float *dst = p.part + (size_t)blockIdx.z * p.N * p.K;
 #pragma unroll
@@ -685,6 +706,15 @@ __global__ __launch_bounds__(256) void pw_wgrad_kernel(PwWgArgs p) {
         const int k = k0 + wk * QK + b * 16 + (lane & 15);
         if (n < p.N && k < p.K) dst[(size_t)n * p.K + k] = acc[a][b][j];
       }
+  PWG_MARK(4);
+}
+
+void pwg_trace_set(void *ts) {   // nullptr: off; no-op unless built with PGDIST_PWT_TRACE
+#ifdef PGDIST_PWT_TRACE
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pwg_ts), &ts, sizeof(ts));
+#else
+  (void)ts;
+#endif
 }
 
 // ===========================================================================

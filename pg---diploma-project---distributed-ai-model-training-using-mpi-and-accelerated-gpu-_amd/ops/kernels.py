@@ -403,6 +403,22 @@ def pwt_trace_set(buf):
     lib().pwt_trace_set(0 if buf is None else buf.data_ptr())
 
 
+def pwb_trace_set(buf):
+    """Diagnostics (PGDIST_PWT_TRACE builds): the fused large-M pointwise backward (pw_bwd) sums
+    its per-phase wall clock over its tiles into ``buf`` (int64 [grid][8])."""
+    if buf is not None:
+        _chk(buf, torch.int64, buf.numel(), "buf")
+    lib().pwb_trace_set(0 if buf is None else buf.data_ptr())
+
+
+def pwg_trace_set(buf):
+    """Diagnostics (PGDIST_PWT_TRACE builds): the 1x1 weight gradient (pw_wgrad) stamps the
+    wall clock at its phase boundaries into ``buf`` (int64 [grid][8])."""
+    if buf is not None:
+        _chk(buf, torch.int64, buf.numel(), "buf")
+    lib().pwg_trace_set(0 if buf is None else buf.data_ptr())
+
+
 def ir_bwd_grid(B, H, cin, ch, cout):
     """Workgroups of the fused inverted-residual block backward (0: no kernel / not co-resident)."""
     return lib().ir_bwd_grid(int(B), int(H), int(cin), int(ch), int(cout))
