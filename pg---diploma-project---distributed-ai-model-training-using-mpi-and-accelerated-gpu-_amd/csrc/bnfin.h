@@ -174,6 +174,108 @@ PG_DEVICE void bn_lazy(const BnFin *d, int c, float &o0, float &o1, float &o2) {
   }
 }
 
+// The prologue parameters of a consumer with K channels staged into LDS: P[j * Kp + i] for
+// i < Kp (zero past K), j < NPAR.  Lazy (lz != nullptr): computed from the producer's replica
+// rows (bn_lazy); else copied from the materialised p0 / p1 / p2.  Thread t handles channels
+// t, t + 256, ... (blockDim 256); up to MAXIT of them with every load of every channel issued
+// before the first use (clamped indices past K: one memory latency for the whole staging
+// instead of one per channel chunk).  Larger Kp falls back to the per-chunk loop.
+template <int NPAR, int MAXIT = 5>
+PG_DEVICE void bn_stage_params(const BnFin *lz, const float *p0, const float *p1, const float *p2, int K,
+                               int Kp, float *P) {
+  const int tid = threadIdx.x;
+  if (Kp > MAXIT * 256) {
+    for (int i = tid; i < Kp; i += 256) {
+      const bool ok = i < K;
+      float a = 0.f, b = 0.f, c = 0.f;
+      if (lz) {
+        if (ok) bn_lazy(lz, i, a, b, c);
+      } else if (ok) {
+        a = p0[i];
+        b = p1[i];
+        if constexpr (NPAR == 3) c = p2[i];
+      }
+      P[i] = a;
+      P[Kp + i] = b;
+      if constexpr (NPAR == 3) P[2 * Kp + i] = c;
+    }
+    return;
+  }
+  const int nit = (Kp - tid + 255) / 256;   // chunks this thread writes (<= MAXIT)
+  if (lz) {
+    const int C = lz->C, rows = lz->rows;
+    const float *acc = lz->acc;
+    const bool bwd = lz->bwd;
+    float v[MAXIT][2 * kBnRep], g[MAXIT], x0[MAXIT], x1[MAXIT];
+#pragma unroll
+    for (int u = 0; u < MAXIT; ++u) {
+      const int c = min(tid + u * 256, K - 1);
+#pragma unroll
+      for (int r = 0; r < kBnRep; ++r) {
+        const int rr = r < rows ? r : 0;
+        v[u][2 * r] = acc[(size_t)(2 * rr) * C + c];
+        v[u][2 * r + 1] = acc[(size_t)(2 * rr + 1) * C + c];
+      }
+      g[u] = lz->gamma ? lz->gamma[c] : 1.f;
+      x0[u] = bwd ? lz->mean[c] : (lz->beta ? lz->beta[c] : 0.f);
+      x1[u] = bwd ? lz->rstd[c] : 0.f;
+    }
+    const double n = (double)lz->count;
+#pragma unroll
+    for (int u = 0; u < MAXIT; ++u) {
+      if (u >= nit) break;
+      const int i = tid + u * 256;
+      float o0 = 0.f, o1 = 0.f, o2 = 0.f;
+      if (i < K) {
+        double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+        for (int r = 0; r < kBnRep; ++r) {
+          const double m = r < rows ? 1.0 : 0.0;
+          s0 += m * (double)v[u][2 * r];
+          s1 += m * (double)v[u][2 * r + 1];
+        }
+        if (bwd) {   // same arithmetic as bn_lazy
+          const float mu = x0[u], rs = x1[u];
+          const double sgx = (s1 - (double)mu * s0) * rs;
+          const double a = (double)g[u] * rs;
+          o0 = (float)a;
+          o1 = (float)(-a * rs * sgx / n);
+          o2 = (float)(-a * s0 / n + a * rs * (double)mu * sgx / n);
+        } else {
+          const double m = s0 / n;
+          double var = s1 / n - m * m;
+          if (var < 0.0) var = 0.0;
+          const float r = (float)(1.0 / sqrt(var + (double)lz->eps));
+          o0 = g[u] * r;
+          o1 = x0[u] - (float)m * g[u] * r;
+        }
+      }
+      P[i] = o0;
+      P[Kp + i] = o1;
+      if constexpr (NPAR == 3) P[2 * Kp + i] = o2;
+    }
+  } else {
+    float a[MAXIT], b[MAXIT], c[MAXIT];
+#pragma unroll
+    for (int u = 0; u < MAXIT; ++u) {
+      const int ci = min(tid + u * 256, K - 1);
+      a[u] = p0[ci];
+      b[u] = p1[ci];
+      c[u] = NPAR == 3 ? p2[ci] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < MAXIT; ++u) {
+      if (u >= nit) break;
+      const int i = tid + u * 256;
+      const bool ok = i < K;
+      P[i] = ok ? a[u] : 0.f;
+      P[Kp + i] = ok ? b[u] : 0.f;
+      if constexpr (NPAR == 3) P[2 * Kp + i] = ok ? c[u] : 0.f;
+    }
+  }
+}
+
+
 // host: the lazy descriptor armed for the next consumer launch (bn_lz_arm); nullptr: the
 // consumer reads materialised parameters
 const BnFin *take_bn_lz();

@@ -229,22 +229,11 @@ __global__ __launch_bounds__(256) void pw_tile_kernel(PwTArgs p) {
   // first operand loads (PF2: first two steps) in flight during the prologue-parameter staging
   load(ra0, ry0, rb0, kb * KSTEP, kb < ke);
   if constexpr (PF2) load(ra1, ry1, rb1, min(kb + 1, ke - 1) * KSTEP, true);
-  if constexpr (NPAR > 0) {
-    for (int i = tid; i < Kp; i += 256) {
-      const bool ok = i < p.K;
-      if (p.lz) {
-        float a = 0.f, b = 0.f, c = 0.f;
-        if (ok) bn_lazy(p.lz, i, a, b, c);
-        Ps[i] = a;
-        Ps[Kp + i] = b;
-        if constexpr (NPAR == 3) Ps[2 * Kp + i] = c;
-      } else {
-        Ps[i] = ok ? p.pa[i] : 0.f;
-        Ps[Kp + i] = ok ? p.pb[i] : 0.f;
-        if constexpr (NPAR == 3) Ps[2 * Kp + i] = ok ? p.pc[i] : 0.f;
-      }
-    }
-  }
+  // parameter chunks staged with one memory latency: K < 256 (32-wide k steps) needs one; the
+  // long-K 64 x 64 tiles take K up to 1280, the 64 x 128 ones (N = 96) up to 576; more would
+  // cost the wider tiles occupancy
+  constexpr int PMAX = KSTEP == 32 ? 1 : (BM == 64 ? (BN == 64 ? 5 : 3) : 2);
+  if constexpr (NPAR > 0) bn_stage_params<NPAR, PMAX>(p.lz, p.pa, p.pb, p.pc, p.K, Kp, Ps);
   __syncthreads();   // Ps staged
   PWT_MARK(1);
   write(ra0, ry0, rb0, 0, kb * KSTEP);
