@@ -140,6 +140,11 @@ constexpr uint32_t kOOB = 0x80000000u;
 PG_DEVICE rsrc_t make_rsrc(const void *base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)bytes, 0x00020000);
 }
+// the same descriptor as raw SGPR words, for inline-asm buffer instructions
+PG_DEVICE u32x4_t make_srd(const void *base, uint32_t bytes) {
+  const size_t a = (size_t)base;
+  return u32x4_t{(uint32_t)a, (uint32_t)(a >> 32) & 0xffffu, bytes, 0x00020000u};
+}
 PG_DEVICE uint4 bld16(rsrc_t r, uint32_t off) {
   const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
   return make_uint4(v.x, v.y, v.z, v.w);

@@ -176,12 +176,18 @@ constexpr int kSlotHalo = 3072, kSlotOwn = 2048, kSlotS2 = 4096;
 // offsets, so that every wave issues the same number of VMEM instructions per step.
 struct Stream {
   rsrc_t rs;
+  u32x4_t srd;         // the same descriptor as raw words (inline-asm DMA)
   int H, W, C, b, col0;
   int lane_col;        // segment column of this lane's chunk (-1: none)
   int lane_coff;       // channel byte offset of this lane's chunk
   bool wave_used;      // wave-uniform
-  PG_DEVICE void init(rsrc_t r, int H_, int W_, int C_, int b_, int col0_, int nchunk, int CC8, int cbase) {
-    rs = r;
+  PG_DEVICE void set(const void *base, uint32_t bytes) {
+    rs = make_rsrc(base, bytes);
+    srd = make_srd(base, bytes);
+  }
+  PG_DEVICE void init(const void *base, uint32_t bytes, int H_, int W_, int C_, int b_, int col0_, int nchunk,
+                      int CC8, int cbase) {
+    set(base, bytes);
     H = H_;
     W = W_;
     C = C_;
@@ -192,13 +198,19 @@ struct Stream {
     lane_coff = (cbase + (t < nchunk ? t % CC8 : 0) * 8) * 2;
     wave_used = (t & ~63) < nchunk;
   }
-  // DMA row ih into `slot` of a ring of `stride`-byte slots at `ring`
+  // DMA row ih into `slot` of a ring of `stride`-byte slots at `ring`.  Issued by inline asm:
+  // hipcc tracks a builtin LDS DMA as a pending write to the ring and waits vmcnt(0) before
+  // the next ring read it cannot prove disjoint, i.e. for the rows just issued kDepth ahead
+  // (one full DMA latency per row).  The ring's own counted ring_sync waits are the ordering.
   PG_DEVICE void issue(char *ring, int stride, int slot, int ih, char *dummy) const {
     const int iw = col0 + lane_col;
     const bool ok = wave_used && lane_col >= 0 && ih >= 0 && ih < H && iw >= 0 && iw < W;
     const uint32_t off = ok ? (uint32_t)(((b * H + ih) * W + iw) * C) * 2u + (uint32_t)lane_coff : kOOB;
     char *dst = wave_used ? ring + slot * stride + (threadIdx.x & ~63) * 16 : dummy;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)dst, 16, off, 0, 0, 0);
+    const uint32_t m0v = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(size_t)((__attribute__((address_space(3))) char *)dst));
+    asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0v), "v"(off), "s"(srd)
+                 : "memory", "m0");
   }
 };
 
@@ -259,7 +271,7 @@ __global__ __launch_bounds__(256) void dw_fwd_lds_kernel(
 #pragma unroll
   for (int d = 0; d < 3; ++d) cok[d] = active && iw0 + d >= 0 && iw0 + d < g.W;
   Stream sx;
-  sx.init(make_rsrc(x, (uint32_t)g.B * g.H * g.W * g.C * 2), g.H, g.W, g.C, tl.b, tl.w0 * S - 1,
+  sx.init(x, (uint32_t)g.B * g.H * g.W * g.C * 2, g.H, g.W, g.C, tl.b, tl.w0 * S - 1,
           ((g.TWc - 1) * S + 3) * CC8, CC8, cbase);
 #pragma unroll
   for (int q = 0; q < kDepth; ++q) sx.issue(ring, kSlot, q, j0 + q, dummy);
@@ -403,10 +415,10 @@ __global__ __launch_bounds__(256) void dw_dgrad_s1_lds_kernel(
 #pragma unroll
   for (int c = 0; c < 3; ++c) cok[c] = active && iw - 1 + c >= 0 && iw - 1 + c < g.W;
   Stream sg, sy, sp;
-  sg.init(make_rsrc(gin, nbytes), g.H, g.W, g.C, tl.b, tl.w0 - 1, (g.TWc + 2) * CC8, CC8, cbase);
+  sg.init(gin, nbytes, g.H, g.W, g.C, tl.b, tl.w0 - 1, (g.TWc + 2) * CC8, CC8, cbase);
   sy = sg;
-  sy.rs = make_rsrc(yself, nbytes);
-  sp.init(make_rsrc(yprev, nbytes), g.H, g.W, g.C, tl.b, tl.w0, g.TWc * CC8, CC8, cbase);
+  sy.set(yself, nbytes);
+  sp.init(yprev, nbytes, g.H, g.W, g.C, tl.b, tl.w0, g.TWc * CC8, CC8, cbase);
   auto issue = [&](int slot, int k) {
     char *base = ring + slot * kStep;
     sg.issue(base, 0, 0, j0 + k, dummy);
@@ -583,10 +595,10 @@ __global__ __launch_bounds__(256) void dw_dgrad_s2_lds_kernel(
   const int o0 = tl.r0 >> 1;                            // r0 even
   const int nrows = ((ih_end - 1) >> 1) + 1 - o0 + 1;   // dy rows o0 .. (ih_end-1)/2 + 1
   Stream sg, sy, sp;
-  sg.init(make_rsrc(gin, nout), g.Ho, g.Wo, g.C, tl.b, dcol0, (dcol1 - dcol0 + 1) * CC8, CC8, cbase);
+  sg.init(gin, nout, g.Ho, g.Wo, g.C, tl.b, dcol0, (dcol1 - dcol0 + 1) * CC8, CC8, cbase);
   sy = sg;
-  sy.rs = make_rsrc(yself, nout);
-  sp.init(make_rsrc(yprev, nin), g.H, g.W, g.C, tl.b, tl.w0, g.TWc * CC8, CC8, cbase);
+  sy.set(yself, nout);
+  sp.init(yprev, nin, g.H, g.W, g.C, tl.b, tl.w0, g.TWc * CC8, CC8, cbase);
   auto issue = [&](int slot, int k) {
     char *base = ring + slot * kStep;
     const int o = o0 + k;
@@ -772,10 +784,10 @@ __global__ __launch_bounds__(256) void dw_wgrad_lds_kernel(
 #pragma unroll
   for (int d = 0; d < 3; ++d) cok[d] = active && iw0 + d >= 0 && iw0 + d < g.W;
   Stream sx, sg, sy;
-  sx.init(make_rsrc(yprev, nin), g.H, g.W, g.C, tl.b, tl.w0 * S - 1, ((g.TWc - 1) * S + 3) * CC8, CC8, cbase);
-  sg.init(make_rsrc(gin, nout), g.Ho, g.Wo, g.C, tl.b, tl.w0, g.TWc * CC8, CC8, cbase);
+  sx.init(yprev, nin, g.H, g.W, g.C, tl.b, tl.w0 * S - 1, ((g.TWc - 1) * S + 3) * CC8, CC8, cbase);
+  sg.init(gin, nout, g.Ho, g.Wo, g.C, tl.b, tl.w0, g.TWc * CC8, CC8, cbase);
   sy = sg;
-  sy.rs = make_rsrc(yself, nout);
+  sy.set(yself, nout);
   // output row completed at step k: S = 1: r0 + k - 2; S = 2 (even k): r0 + (k - 2) / 2
   auto out_row = [&](int k) { return S == 1 ? tl.r0 + k - 2 : tl.r0 + ((k - 2) >> 1); };
   auto issue = [&](int slot, int k) {
