@@ -225,6 +225,15 @@ PG_DEVICE void ring_sync() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 PG_DEVICE void mem_fence_compiler() { asm volatile("" ::: "memory"); }
+// vmcnt(0) as the s_waitcnt builtin (vmcnt 0, expcnt 7, lgkmcnt 15): unlike an asm wait, hipcc's
+// waitcnt pass sees it, so it knows the parameter loads issued before the row loop have landed
+// and does not wait for them again (vmcnt(N) / vmcnt(0) before their first use inside the
+// loop, which then also waits for the ring's in-flight rows)
+PG_DEVICE void params_landed() {
+  mem_fence_compiler();   // no load sinks below the wait
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  mem_fence_compiler();
+}
 
 PG_DEVICE uint2 lds8(const char *slot, int col, int CC, int c) {
   return *reinterpret_cast<const uint2 *>(slot + (col * CC + c) * 2);
@@ -295,7 +304,7 @@ __global__ __launch_bounds__(256) void dw_fwd_lds_kernel(
   }
 #pragma unroll
   for (int q = 0; q < 9; ++q) unpack4(wraw[q], wt[q]);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // parameters in registers (and the first rows in LDS)
+  params_landed();   // parameters in registers (and the first rows in LDS)
   float win[3][3][CPT];   // three input rows x three tap columns (roles rotate with the unroll)
 #pragma unroll
   for (int r = 0; r < 3; ++r)
@@ -457,7 +466,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_s1_lds_kernel(
   for (int q = 0; q < (WG ? 9 : 1); ++q) zero4(accw[q]);
 #pragma unroll
   for (int q = 0; q < 9; ++q) unpack4(wraw[q], wt[q]);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // parameters in registers (and the first rows in LDS)
+  params_landed();   // parameters in registers (and the first rows in LDS)
   float win[3][3][CPT];   // three dy rows x three columns iw-1..iw+1 (roles rotate with the unroll)
 #pragma unroll
   for (int r = 0; r < 3; ++r)
@@ -647,7 +656,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_s2_lds_kernel(
       wB[r][k] = odd_w ? w2[k] : 0.f;
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // parameters in registers (and the first rows in LDS)
+  params_landed();   // parameters in registers (and the first rows in LDS)
   float dyb[2][2][CPT];   // two dy rows (roles alternate with the unroll) x columns A, B
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
@@ -813,7 +822,12 @@ __global__ __launch_bounds__(256) void dw_wgrad_lds_kernel(
   }
 #pragma unroll
   for (int q = 0; q < 9; ++q) zero4(accw[q]);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // parameters in registers (and the first rows in LDS)
+  // a use of every parameter here: hipcc waits for their loads at this point (the restrict
+  // loads may otherwise sink below the wait and be waited for inside the row loop, where the
+  // wait also covers the ring's in-flight rows)
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) asm volatile("" ::"v"(al[k]), "v"(be[k]), "v"(ga[k]), "v"(s[k]), "v"(t[k]));
+  params_landed();   // parameters in registers (and the first rows in LDS)
   float win[3][3][CPT];
 #pragma unroll
   for (int r = 0; r < 3; ++r)
