@@ -145,6 +145,18 @@ PG_DEVICE u32x4_t make_srd(const void *base, uint32_t bytes) {
   const size_t a = (size_t)base;
   return u32x4_t{(uint32_t)a, (uint32_t)(a >> 32) & 0xffffu, bytes, 0x00020000u};
 }
+// LDS DMA by inline asm: one buffer_load_dwordx4 ... lds, 16 B per lane into the wave's
+// 1-KiB piece at `dst` (wave-uniform).  hipcc tracks the builtin form as a pending write to
+// the LDS object and waits for it (vmcnt) before any later read of that object it cannot prove
+// disjoint, i.e. also for stages issued ahead of the one being read: software pipelines over
+// a ring then serialise.  Users order their ring reads with their own counted waits.  Sets M0
+// (no other code in the users' translation units uses it).
+PG_DEVICE void lds_dma16(const u32x4_t &srd, const void *dst, uint32_t voff) {
+  const uint32_t m0v =
+      __builtin_amdgcn_readfirstlane((uint32_t)(size_t)((const __attribute__((address_space(3))) char *)dst));
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0v), "v"(voff), "s"(srd)
+               : "memory", "m0");
+}
 PG_DEVICE uint4 bld16(rsrc_t r, uint32_t off) {
   const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
   return make_uint4(v.x, v.y, v.z, v.w);

@@ -70,6 +70,8 @@ struct ConvArgs {
                         // bn_rep >= P (deterministic mode): one plainly stored row per tile
   int ntap[4];
   signed char tr[4][9], ts[4][9], tdh[4][9], tdw[4][9];
+  int tapx[4][9];       // the same taps packed per dword (dh | dw << 8 | (tr * S + ts) << 16):
+                        // a wave-uniform index then reads them with scalar loads
 };
 
 // 16x16x32 bf16 MFMA on raw 8 x bf16 fragments
@@ -558,8 +560,9 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs p) {
   const int HWc = p.Hc * p.Wc;
   const int lrow = lane / CPR;                          // row of this lane inside a 1-KiB piece
   const int lch = (lane % CPR) ^ glds_sw<KS>(lrow);     // k-chunk this lane fetches (source swizzle)
-  const rsrc_t ra = make_rsrc(p.A, (uint32_t)p.Nb * p.Hi * p.Wi * p.Ci * 2);
-  const rsrc_t rw = make_rsrc(p.W, (uint32_t)p.N * p.Kw * 2);
+  // raw descriptors for the inline-asm DMA (common.h lds_dma16)
+  const u32x4_t ra = make_srd(p.A, (uint32_t)p.Nb * p.Hi * p.Wi * p.Ci * 2);
+  const u32x4_t rw = make_srd(p.W, (uint32_t)p.N * p.Kw * 2);
 
   // A rows of this wave's pieces (fixed across k-steps): image, base h / w; rb < 0: past M
   int rb[APW], rh[APW], rwc[APW];
@@ -596,6 +599,14 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs p) {
     int dh, dw, wt;
     if constexpr (MODE == CM_FWD) {
       dh = j / p.S; dw = j - dh * p.S; wt = j;
+    } else if constexpr (!MT) {
+      // j is wave-uniform here: as a scalar the tap tables are read by scalar loads from the
+      // kernel arguments (lgkmcnt), not by per-lane global loads whose vmcnt wait each k-step
+      // also waited for the DMAs in flight (and put the table latency on every step's path)
+      const int v = p.tapx[cls][__builtin_amdgcn_readfirstlane(j)];
+      dh = (int)(signed char)(v & 0xff);
+      dw = (int)(signed char)((v >> 8) & 0xff);
+      wt = v >> 16;
     } else {
       dh = p.tdh[cls][j]; dw = p.tdw[cls][j];
       wt = p.tr[cls][j] * p.S + p.ts[cls][j];
@@ -607,15 +618,13 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs p) {
       const int ih = rh[i] + dh, iw = rwc[i] + dw;
       const bool ok = rb[i] >= 0 && ih >= 0 && ih < p.Hi && iw >= 0 && iw < p.Wi;
       const uint32_t off = ok ? (uint32_t)((((rb[i] * p.Hi + ih) * p.Wi + iw) * p.Ci + ci) * 2) : kOOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (__attribute__((address_space(3))) void *)(abase + (wave * APW + i) * 1024),
-                                               16, off, 0, 0, 0);
+      lds_dma16(ra, abase + (wave * APW + i) * 1024, off);
     }
     const uint32_t kb = (uint32_t)(wt * p.Ci + ci) * 2;
 #pragma unroll
     for (int i = 0; i < BPW; ++i) {
       const uint32_t off = wrow[i] == kOOB ? kOOB : wrow[i] + kb;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void *)(bbase + (wave * BPW + i) * 1024),
-                                               16, off, 0, 0, 0);
+      lds_dma16(rw, bbase + (wave * BPW + i) * 1024, off);
     }
   };
 
@@ -1042,8 +1051,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_dma_kernel(WgArgs p, int gx, i
   // this k tile lies inside one filter tap (Ci % TK == 0)
   const int tap = k0 / p.Ci, ci0 = k0 - tap * p.Ci;
   const int tr = tap / p.S, ts = tap - tr * p.S;
-  const rsrc_t rg = make_rsrc(p.G, (uint32_t)((size_t)p.M * p.N * 2));
-  const rsrc_t rx = make_rsrc(p.X, (uint32_t)((size_t)(p.M / HWo) * p.Hi * p.Wi * p.Ci * 2));
+  // raw descriptors for the inline-asm DMA (common.h lds_dma16)
+  const u32x4_t rg = make_srd(p.G, (uint32_t)((size_t)p.M * p.N * 2));
+  const u32x4_t rx = make_srd(p.X, (uint32_t)((size_t)(p.M / HWo) * p.Hi * p.Wi * p.Ci * 2));
   // this lane's rows / source chunks in its pieces
   const int drow0 = lane / CPN, dq = lane % CPN;
   const int xrow0 = lane / CPK, xq = lane % CPK;
@@ -1059,8 +1069,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_dma_kernel(WgArgs p, int gx, i
       const int c = dq ^ (2 * wg_sw<RBN>(row));
       const int m = m0 + row;
       const uint32_t off = m < mend ? (uint32_t)(((size_t)m * p.N + n0 + c * 8) * 2) : kOOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rg, (__attribute__((address_space(3))) void *)(dbase + piece * 1024), 16,
-                                               off, 0, 0, 0);
+      lds_dma16(rg, dbase + piece * 1024, off);
     }
 #pragma unroll
     for (int i = 0; i < PKW; ++i) {
@@ -1076,8 +1085,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_dma_kernel(WgArgs p, int gx, i
         if (ih >= 0 && ih < p.Hi && iw >= 0 && iw < p.Wi)
           off = (uint32_t)(((((size_t)b * p.Hi + ih) * p.Wi + iw) * p.Ci + ci0 + c * 8) * 2);
       }
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) void *)(xbase + piece * 1024), 16,
-                                               off, 0, 0, 0);
+      lds_dma16(rx, xbase + piece * 1024, off);
     }
   };
 
@@ -1601,6 +1609,7 @@ void dgrad_classes(ConvArgs &a, int R, int S, int st, int pad) {
         a.ts[cls][n] = (signed char)s;
         a.tdh[cls][n] = (signed char)((ph + pad - r) / st);   // exact division (multiple of st)
         a.tdw[cls][n] = (signed char)((pw + pad - s) / st);
+        a.tapx[cls][n] = (int)(uint8_t)a.tdh[cls][n] | ((int)(uint8_t)a.tdw[cls][n] << 8) | ((r * S + s) << 16);
         ++n;
       }
     }

@@ -198,19 +198,15 @@ struct Stream {
     lane_coff = (cbase + (t < nchunk ? t % CC8 : 0) * 8) * 2;
     wave_used = (t & ~63) < nchunk;
   }
-  // DMA row ih into `slot` of a ring of `stride`-byte slots at `ring`.  Issued by inline asm:
-  // hipcc tracks a builtin LDS DMA as a pending write to the ring and waits vmcnt(0) before
-  // the next ring read it cannot prove disjoint, i.e. for the rows just issued kDepth ahead
-  // (one full DMA latency per row).  The ring's own counted ring_sync waits are the ordering.
+  // DMA row ih into `slot` of a ring of `stride`-byte slots at `ring` (inline asm, common.h
+  // lds_dma16: a builtin DMA made hipcc wait for the rows issued kDepth ahead before every
+  // ring read; the ring's own counted ring_sync waits are the ordering)
   PG_DEVICE void issue(char *ring, int stride, int slot, int ih, char *dummy) const {
     const int iw = col0 + lane_col;
     const bool ok = wave_used && lane_col >= 0 && ih >= 0 && ih < H && iw >= 0 && iw < W;
     const uint32_t off = ok ? (uint32_t)(((b * H + ih) * W + iw) * C) * 2u + (uint32_t)lane_coff : kOOB;
     char *dst = wave_used ? ring + slot * stride + (threadIdx.x & ~63) * 16 : dummy;
-    const uint32_t m0v = __builtin_amdgcn_readfirstlane(
-        (uint32_t)(size_t)((__attribute__((address_space(3))) char *)dst));
-    asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0v), "v"(off), "s"(srd)
-                 : "memory", "m0");
+    lds_dma16(srd, dst, off);
   }
 };
 
