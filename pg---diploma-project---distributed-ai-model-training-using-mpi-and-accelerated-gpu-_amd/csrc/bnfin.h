@@ -177,31 +177,14 @@ PG_DEVICE void bn_lazy(const BnFin *d, int c, float &o0, float &o1, float &o2) {
 // The prologue parameters of a consumer with K channels staged into LDS: P[j * Kp + i] for
 // i < Kp (zero past K), j < NPAR.  Lazy (lz != nullptr): computed from the producer's replica
 // rows (bn_lazy); else copied from the materialised p0 / p1 / p2.  Thread t handles channels
-// t, t + 256, ... (blockDim 256); up to MAXIT of them with every load of every channel issued
-// before the first use (clamped indices past K: one memory latency for the whole staging
-// instead of one per channel chunk).  Larger Kp falls back to the per-chunk loop.
-template <int NPAR, int MAXIT = 5>
-PG_DEVICE void bn_stage_params(const BnFin *lz, const float *p0, const float *p1, const float *p2, int K,
-                               int Kp, float *P) {
+// t, t + 256, ... (blockDim 256) in batches of MAXIT chunks, every load of a batch issued
+// before its first use (clamped indices past K): one memory latency per batch instead of one
+// per 256-channel chunk.
+template <int NPAR, int MAXIT>
+PG_DEVICE void bn_stage_batch(const BnFin *lz, const float *p0, const float *p1, const float *p2, int K, int Kp,
+                              float *P, int base) {
   const int tid = threadIdx.x;
-  if (Kp > MAXIT * 256) {
-    for (int i = tid; i < Kp; i += 256) {
-      const bool ok = i < K;
-      float a = 0.f, b = 0.f, c = 0.f;
-      if (lz) {
-        if (ok) bn_lazy(lz, i, a, b, c);
-      } else if (ok) {
-        a = p0[i];
-        b = p1[i];
-        if constexpr (NPAR == 3) c = p2[i];
-      }
-      P[i] = a;
-      P[Kp + i] = b;
-      if constexpr (NPAR == 3) P[2 * Kp + i] = c;
-    }
-    return;
-  }
-  const int nit = (Kp - tid + 255) / 256;   // chunks this thread writes (<= MAXIT)
+  const int nit = (Kp - base - tid + 255) / 256;   // chunks of this batch this thread writes
   if (lz) {
     const int C = lz->C, rows = lz->rows;
     const float *acc = lz->acc;
@@ -209,7 +192,7 @@ PG_DEVICE void bn_stage_params(const BnFin *lz, const float *p0, const float *p1
     float v[MAXIT][2 * kBnRep], g[MAXIT], x0[MAXIT], x1[MAXIT];
 #pragma unroll
     for (int u = 0; u < MAXIT; ++u) {
-      const int c = min(tid + u * 256, K - 1);
+      const int c = min(base + tid + u * 256, K - 1);
 #pragma unroll
       for (int r = 0; r < kBnRep; ++r) {
         const int rr = r < rows ? r : 0;
@@ -224,7 +207,7 @@ PG_DEVICE void bn_stage_params(const BnFin *lz, const float *p0, const float *p1
 #pragma unroll
     for (int u = 0; u < MAXIT; ++u) {
       if (u >= nit) break;
-      const int i = tid + u * 256;
+      const int i = base + tid + u * 256;
       float o0 = 0.f, o1 = 0.f, o2 = 0.f;
       if (i < K) {
         double s0 = 0.0, s1 = 0.0;
@@ -258,7 +241,7 @@ PG_DEVICE void bn_stage_params(const BnFin *lz, const float *p0, const float *p1
     float a[MAXIT], b[MAXIT], c[MAXIT];
 #pragma unroll
     for (int u = 0; u < MAXIT; ++u) {
-      const int ci = min(tid + u * 256, K - 1);
+      const int ci = min(base + tid + u * 256, K - 1);
       a[u] = p0[ci];
       b[u] = p1[ci];
       c[u] = NPAR == 3 ? p2[ci] : 0.f;
@@ -266,7 +249,7 @@ PG_DEVICE void bn_stage_params(const BnFin *lz, const float *p0, const float *p1
 #pragma unroll
     for (int u = 0; u < MAXIT; ++u) {
       if (u >= nit) break;
-      const int i = tid + u * 256;
+      const int i = base + tid + u * 256;
       const bool ok = i < K;
       P[i] = ok ? a[u] : 0.f;
       P[Kp + i] = ok ? b[u] : 0.f;
@@ -275,6 +258,11 @@ PG_DEVICE void bn_stage_params(const BnFin *lz, const float *p0, const float *p1
   }
 }
 
+template <int NPAR, int MAXIT = 5>
+PG_DEVICE void bn_stage_params(const BnFin *lz, const float *p0, const float *p1, const float *p2, int K,
+                               int Kp, float *P) {
+  for (int base = 0; base < Kp; base += MAXIT * 256) bn_stage_batch<NPAR, MAXIT>(lz, p0, p1, p2, K, Kp, P, base);
+}
 
 // host: the lazy descriptor armed for the next consumer launch (bn_lz_arm); nullptr: the
 // consumer reads materialised parameters

@@ -93,14 +93,10 @@ PG_DEVICE void ld8f(const float *p, float (&v)[8]) {
 // (forward: scale, shift; backward: a, b, c).  Every workgroup reduces the <= 8 replica rows
 // of the producer itself instead of waiting for a finalize launch between the two kernels;
 // the caller synchronises the workgroup before reading sm.
+// (bnfin.h bn_stage_params: loads batched 4 chunks of 256 channels at a time)
 PG_DEVICE void lz_stage(const BnFin *d, float *sm, int C, int npar) {
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float o0, o1, o2;
-    bn_lazy(d, c, o0, o1, o2);
-    sm[c] = o0;
-    sm[C + c] = o1;
-    if (npar == 3) sm[2 * C + c] = o2;
-  }
+  if (npar == 3) bn_stage_params<3, 4>(d, nullptr, nullptr, nullptr, C, C, sm);
+  else bn_stage_params<2, 4>(d, nullptr, nullptr, nullptr, C, C, sm);
 }
 }  // namespace
 
