@@ -173,9 +173,11 @@ class MobileNetV2Executor:
     PLAN_SAFE = True
     # on_params_ready issues only recordable native ops (NativeBucketReducer): called directly
     ready_native = False
-    # depthwise dgrad+wgrad fused on maps >= this size (14 / 28 / 56 / 112 / never: 4.92 / 4.89 /
-    # 4.80-4.85 / 4.85 / 4.94 ms/step, docs/PERF_NOTES.md round 2)
-    DW_FUSE_MIN_H = 56
+    # depthwise dgrad+wgrad fused on maps >= this size.  Round 2: 14 / 28 / 56 / 112 / never =
+    # 4.92 / 4.89 / 4.80-4.85 / 4.85 / 4.94 ms/step.  Round 5, after the fused kernel's ring
+    # pipelined (inline-asm DMA): 28 = 4.365-4.375 vs 56 = 4.382-4.394 (7 / 14: 4.39-4.40),
+    # same box (docs/PERF_NOTES.md round 5)
+    DW_FUSE_MIN_H = 28
     # fused 1x1 dgrad+wgrad (pw_bwd) wherever supported (only M >= 500k / never: 5.06 / 5.27 vs 4.80)
     PW_BWD_FUSE_MIN_M = 0
     # block outputs of the maps with at most this many pixels per image (the latency-bound 14x14 /
