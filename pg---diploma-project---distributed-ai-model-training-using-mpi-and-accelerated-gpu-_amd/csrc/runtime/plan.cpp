@@ -4,6 +4,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <map>
 #include <memory>
 #include <stdexcept>
@@ -35,9 +36,22 @@ void check(hipError_t e, const char *what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// flags of the cross-stream join events (PGDIST_EVENT_FLAGS overrides).  Both streams are on
+// this device and every kernel ends with its own device-scope release, so a join needs no
+// system-scope fence of its own: without it the record costs the main stream less
+// (4.320 vs 4.342 ms/step, docs/PERF_NOTES.md).  Host-visible waits use other events.
+unsigned event_flags() {
+  static const unsigned f = [] {
+    const char *s = std::getenv("PGDIST_EVENT_FLAGS");
+    return s ? static_cast<unsigned>(std::strtoul(s, nullptr, 0))
+             : static_cast<unsigned>(hipEventDisableTiming | hipEventDisableSystemFence);
+  }();
+  return f;
+}
+
 struct Event {
   hipEvent_t e = nullptr;
-  Event() { check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreateWithFlags"); }
+  Event() { check(hipEventCreateWithFlags(&e, event_flags()), "hipEventCreateWithFlags"); }
   ~Event() {
     if (e) (void)hipEventDestroy(e);
   }
