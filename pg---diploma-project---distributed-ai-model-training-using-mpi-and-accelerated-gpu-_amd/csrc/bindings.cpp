@@ -34,7 +34,8 @@ void launch_bn_bwd_finalize(const float *, int, int, float, const float *, const
 void launch_bn_apply(const bf16_t *, const bf16_t *, const float *, const float *, bf16_t *,
                      long long, int, bool, hipStream_t);
 void launch_adam_flat(float *, const float *, float *, float *, bf16_t *, long long, const float *,
-                      float, float, float, float, float, const unsigned *, hipStream_t);
+                      float, float, float, float, float, const unsigned *, const float *, const float *, int,
+                      double *, hipStream_t);
 void launch_f32_to_bf16(const float *, bf16_t *, long long, hipStream_t);
 int dw_fwd_num_partials(int, int, int, int, int);
 void dw_set_geom_mode(int);
@@ -107,7 +108,7 @@ void launch_head(const bf16_t *, const float *, const float *, const float *, co
 void launch_augment(const unsigned char *, const long long *, const long long *, int, int, int,
                     int, int, const float *, unsigned long long, const float *, long long, bf16_t *,
                     long long *, float *, hipStream_t);
-void launch_step_begin(float *, hipStream_t);
+void launch_step_begin(float *, float *, long long, hipStream_t);
 int colsum_rows(int);
 void launch_wgrad_reduce(float *, int, long long, float *, hipStream_t);
 void wgrad_reduce_defer(bool on);
@@ -197,10 +198,11 @@ PYBIND11_MODULE(_pgdist_C, m) {
   });
   // ---- optimizer ----
   m.def("adam_flat", [](P p, P g, P mm, P v, P pb, long long n, P hyper, float b1, float b2,
-                        float eps, float wd, float gscale, P skip, P s) {
+                        float eps, float wd, float gscale, P skip, P loss, P correct, int B, P acc, P s) {
     pgdist_rt::run_op([=] {
       launch_adam_flat(ptr<float>(p), ptr<float>(g), ptr<float>(mm), ptr<float>(v), ptr<bf16_t>(pb),
-                       n, ptr<float>(hyper), b1, b2, eps, wd, gscale, ptr<unsigned>(skip), S(s));
+                       n, ptr<float>(hyper), b1, b2, eps, wd, gscale, ptr<unsigned>(skip), ptr<float>(loss),
+                       ptr<float>(correct), B, ptr<double>(acc), S(s));
     });
   });
   m.def("f32_to_bf16", [](P x, P y, long long n, P s) {
@@ -208,8 +210,8 @@ PYBIND11_MODULE(_pgdist_C, m) {
       launch_f32_to_bf16(ptr<float>(x), ptr<bf16_t>(y), n, S(s));
     });
   });
-  m.def("step_begin", [](P hyper, P s) {
-    pgdist_rt::run_op([=] { launch_step_begin(ptr<float>(hyper), S(s)); });
+  m.def("step_begin", [](P hyper, P zero, long long n, P s) {
+    pgdist_rt::run_op([=] { launch_step_begin(ptr<float>(hyper), ptr<float>(zero), n, S(s)); });
   });
   m.def("reduce_metrics", [](P loss, P correct, int B, P acc, P s) {
     pgdist_rt::run_op([=] {

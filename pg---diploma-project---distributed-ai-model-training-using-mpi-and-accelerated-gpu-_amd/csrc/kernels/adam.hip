@@ -19,7 +19,32 @@ __global__ __launch_bounds__(256) void adam_flat_kernel(
     float *__restrict__ p, const float *__restrict__ g, float *__restrict__ m,
     float *__restrict__ v, bf16_t *__restrict__ pb, long long n4, const float *__restrict__ hyper,
     float beta1, float beta2, float eps, float weight_decay, float grad_scale,
-    const unsigned *__restrict__ skip) {
+    const unsigned *__restrict__ skip, const float *__restrict__ loss,
+    const float *__restrict__ correct, int B, double *__restrict__ acc) {
+  // the step's metrics (acc[0] += sum loss, acc[1] += sum correct, acc[2] += B) in the last
+  // workgroup, instead of a separate reduce_metrics launch after the update
+  if (acc && blockIdx.x == gridDim.x - 1) {
+    __shared__ double sh[2][4];
+    double l = 0.0, c = 0.0;
+    for (int i = threadIdx.x; i < B; i += 256) {
+      l += loss[i];
+      c += correct[i];
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      l += __shfl_down(l, o);
+      c += __shfl_down(c, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      sh[0][threadIdx.x >> 6] = l;
+      sh[1][threadIdx.x >> 6] = c;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      acc[0] += sh[0][0] + sh[0][1] + sh[0][2] + sh[0][3];
+      acc[1] += sh[1][0] + sh[1][1] + sh[1][2] + sh[1][3];
+      acc[2] += (double)B;
+    }
+  }
   if (skip && __hip_atomic_load(skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
   // hyper[0] = lr, hyper[1] = step (already incremented for this update)
   const float lr = hyper[0];
@@ -67,12 +92,13 @@ __global__ __launch_bounds__(256) void f32_to_bf16_kernel(const float *__restric
 
 void launch_adam_flat(float *p, const float *g, float *m, float *v, bf16_t *pb, long long n,
                       const float *hyper, float beta1, float beta2, float eps, float wd,
-                      float grad_scale, const unsigned *skip, hipStream_t st) {
+                      float grad_scale, const unsigned *skip, const float *loss,
+                      const float *correct, int B, double *acc, hipStream_t st) {
   const long long n4 = n / 4;  // caller pads the flat buffer to a multiple of 4
   int grid = (int)((n4 + 255) / 256);
   if (grid > 4096) grid = 4096;
   hipLaunchKernelGGL(adam_flat_kernel, dim3(grid), dim3(256), 0, st, p, g, m, v, pb, n4, hyper,
-                     beta1, beta2, eps, wd, grad_scale, skip);
+                     beta1, beta2, eps, wd, grad_scale, skip, loss, correct, B, acc);
 }
 
 void launch_f32_to_bf16(const float *x, bf16_t *y, long long n, hipStream_t st) {

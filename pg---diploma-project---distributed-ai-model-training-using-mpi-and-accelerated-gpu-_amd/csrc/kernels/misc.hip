@@ -6,9 +6,14 @@
 // folded into fp64 device accumulators and read once per epoch.
 #include "../common.h"
 
-// hyper[1] = optimizer step / RNG step counter
-__global__ void step_begin_kernel(float *hyper) {
-  if (threadIdx.x == 0) hyper[1] += 1.f;
+// hyper[1] = optimizer step / RNG step counter; zero[0, n) = 0: the step's BatchNorm statistics
+// arena, cleared in the same launch instead of a separate fill at the head of every step
+__global__ __launch_bounds__(256) void step_begin_kernel(float *hyper, float *zero, long long n) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) hyper[1] += 1.f;
+  const long long n4 = n >> 2;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += gridDim.x * 256LL)
+    reinterpret_cast<float4 *>(zero)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) zero[n4 * 4 + threadIdx.x] = 0.f;
 }
 
 // acc[0] += sum loss, acc[1] += sum correct, acc[2] += B
@@ -38,8 +43,10 @@ __global__ __launch_bounds__(256) void reduce_metrics_kernel(const float *__rest
   }
 }
 
-void launch_step_begin(float *hyper, hipStream_t st) {
-  hipLaunchKernelGGL(step_begin_kernel, dim3(1), dim3(64), 0, st, hyper);
+void launch_step_begin(float *hyper, float *zero, long long n, hipStream_t st) {
+  long long grid = ((n >> 2) + 255) / 256;
+  grid = grid < 1 ? 1 : (grid > 512 ? 512 : grid);
+  hipLaunchKernelGGL(step_begin_kernel, dim3((unsigned)grid), dim3(256), 0, st, hyper, zero, n);
 }
 
 void launch_reduce_metrics(const float *loss, const float *correct, int B, double *acc,

@@ -551,7 +551,7 @@ class MobileNetV2Executor:
         """Runs the forward pass on ``self.img`` (and, when training, the head backward)."""
         f, B, S = self.flat, self.B, self.S
         self._check_bn_mode()
-        if train:
+        if train and not self.__dict__.pop("arena_cleared", False):   # (else cleared by step_begin)
             K.memset(self.bn_arena)   # every BN statistics accumulator of this step
         # transposed 1x1 weights for the backward's dgrad GEMMs: on the (idle during the forward)
         # side stream, off the critical path; the main stream joins it at the end of the forward,

@@ -8,6 +8,7 @@ loss.backward(); optimizer.step(); torch.max(...); loss.item(); (...).item()``
 — two host syncs per batch and a CPU/PIL data pipeline.  Here the only host
 work per step is one 1 KB index copy and a graph replay.
 """
+import contextlib
 import os
 from typing import Optional
 
@@ -299,7 +300,10 @@ class NativeTrainStep:
     def _front(self):
         """Step counter, augmentation and the training forward (main stream only)."""
         exe = self.exe
-        K.step_begin(self.hyper)
+        # step counter + this step's BatchNorm statistics arena cleared in one launch
+        arena = getattr(exe, "bn_arena", None)
+        K.step_begin(self.hyper, zero=arena)
+        exe.arena_cleared = arena is not None
         if self.augment_enabled and self.src.shape[1] != 32:
             s2d = getattr(exe, "stem_s2d", False)   # ResNet space-to-depth stem: render its input directly
             if s2d:
@@ -378,8 +382,8 @@ class NativeTrainStep:
         # update, so no replica applies un-reduced gradients (the job fails at the next check)
         K.adam_flat(self.flat.master, self.flat.grad, self.flat.exp_avg, self.flat.exp_avg_sq,
                     self.flat.shadow, self.hyper, self.betas[0], self.betas[1], self.eps, self.wd,
-                    1.0 / self.world, skip=self.comm.error_word if self.comm is not None else 0)
-        K.reduce_metrics(exe.loss, exe.correct, self.B, self.metrics)
+                    1.0 / self.world, skip=self.comm.error_word if self.comm is not None else 0,
+                    metrics=(exe.loss, exe.correct, self.B, self.metrics))   # (+ the step's metrics)
         if probe:
             self._retune_buckets(t_ready, ev0, ev1)
 
@@ -465,7 +469,10 @@ class NativeTrainStep:
             self.idx.copy_(idx, non_blocking=True)
         self._next = next_idx is not None and next_idx.numel() == self.B
         if self._next:
-            self._idxs[1 - cur].copy_(next_idx, non_blocking=True)
+            # on the side stream, which reads it (the next batch's augmentation during this step's
+            # backward) and last read that buffer: off the main stream's step head
+            with torch.cuda.stream(self.exe.side) if self.exe.side is not None else contextlib.nullcontext():
+                self._idxs[1 - cur].copy_(next_idx, non_blocking=True)
         if self._have and self._next and self._eager_runs >= 2:
             plan = self._plans.get(cur)
             if plan is None:

@@ -438,7 +438,8 @@ class ResNet50Executor:
     # ------------------------------------------------------------------ forward
     def forward(self, train: bool = True):
         B = self.B
-        K.memset(self.bn_arena)   # every BN statistics accumulator of this step
+        if not self.__dict__.pop("arena_cleared", False):   # (else cleared by the step's step_begin)
+            K.memset(self.bn_arena)   # every BN statistics accumulator of this step
         if self.stem_s2d:
             st, H2 = self.stem, self.S // 2
             if not self.img_s2d_external:

@@ -184,16 +184,26 @@ def bn_apply(y, scale, shift, out, relu6=False, res=None, lz=None):
 
 
 # --------------------------------------------------------------------------- optimizer
-def adam_flat(p, g, m, v, pb, hyper, beta1, beta2, eps, weight_decay=0.0, grad_scale=1.0, skip=0):
+def adam_flat(p, g, m, v, pb, hyper, beta1, beta2, eps, weight_decay=0.0, grad_scale=1.0, skip=0, metrics=None):
     """Fused Adam over the flat buffers.  ``skip``: device address of a data-parallel
-    communicator's error word (NativeComm.error_word) -- the update is skipped while it is set."""
+    communicator's error word (NativeComm.error_word) -- the update is skipped while it is set.
+    ``metrics``: (loss [B], correct [B], B, acc fp64 [3]) -- the same launch also folds the step's
+    metrics into acc, as reduce_metrics would."""
     n = p.numel()
+    loss = correct = acc = None
+    B = 0
+    if metrics is not None:
+        loss, correct, B, acc = metrics
+        _chk(acc, torch.float64, 3, "acc")
+        _chk(loss, F32, B, "loss")
+        _chk(correct, F32, B, "correct")
     assert n % 4 == 0 and g.numel() == n and m.numel() == n and v.numel() == n
     for t, nm in ((p, "p"), (g, "g"), (m, "m"), (v, "v")):
         _chk(t, F32, n, nm)
     _chk(pb, BF16, n, "pb")
     lib().adam_flat(_p(p), _p(g), _p(m), _p(v), _p(pb), n, _p(hyper), float(beta1), float(beta2),
-                    float(eps), float(weight_decay), float(grad_scale), int(skip), _s())
+                    float(eps), float(weight_decay), float(grad_scale), int(skip), _p(loss), _p(correct), int(B),
+                    _p(acc), _s())
 
 
 def f32_to_bf16(x, y):
@@ -201,8 +211,14 @@ def f32_to_bf16(x, y):
     lib().f32_to_bf16(_p(x), _p(y), x.numel(), _s())
 
 
-def step_begin(hyper):
-    lib().step_begin(_p(hyper), _s())
+def step_begin(hyper, zero=None):
+    """hyper[1] += 1 (step counter); with ``zero`` (fp32, 16-byte aligned) the same launch also
+    clears that buffer (a step's BatchNorm statistics arena)."""
+    n = 0
+    if zero is not None:
+        assert zero.dtype == F32 and zero.is_contiguous() and zero.data_ptr() % 16 == 0, "step_begin: zero buffer"
+        n = zero.numel()
+    lib().step_begin(_p(hyper), _p(zero), n, _s())
 
 
 def reduce_metrics(loss, correct, B, acc):
