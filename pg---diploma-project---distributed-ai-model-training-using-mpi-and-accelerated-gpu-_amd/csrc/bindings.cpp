@@ -110,7 +110,7 @@ void launch_augment(const unsigned char *, const long long *, const long long *,
                     long long *, float *, hipStream_t);
 void launch_step_begin(float *, float *, long long, hipStream_t);
 int colsum_rows(int);
-void launch_wgrad_reduce(float *, int, long long, float *, hipStream_t);
+void launch_wgrad_reduce(float *, int, long long, float *, hipStream_t, bool = false);
 void wgrad_reduce_defer(bool on);
 void wgrad_reduce_flush(hipStream_t st);
 long long bn_part_floats(int, int);

@@ -1754,7 +1754,7 @@ WgGeom wg_geom(int N, int Kw, int M, bool dma = false, int Ci = 0) {
 }  // namespace
 
 int colsum_rows(int R);
-void launch_wgrad_reduce(float *part, int S, long long n, float *grad, hipStream_t st);
+void launch_wgrad_reduce(float *part, int S, long long n, float *grad, hipStream_t st, bool stem36 = false);
 
 long long conv_wgrad_workspace_floats(int Nb, int H, int W, int Ci, int N, int R, int S, int st, int pad) {
   const int Ho = (H + 2 * pad - R) / st + 1, Wo = (W + 2 * pad - S) / st + 1;

@@ -1131,7 +1131,7 @@ long long dw_dgrad_wgrad_workspace_floats(int B, int H, int W, int C, int stride
   return (long long)(P + colsum_rows(P)) * 9 * C;
 }
 
-void launch_wgrad_reduce(float *part, int S, long long n, float *grad, hipStream_t st);
+void launch_wgrad_reduce(float *part, int S, long long n, float *grad, hipStream_t st, bool stem36 = false);
 
 void launch_dw_wgrad(const bf16_t *gin, const bf16_t *yself, const float *coef, const bf16_t *yprev,
                      const float *ps, const float *pt, float *part, float *grad, int B, int H, int W,

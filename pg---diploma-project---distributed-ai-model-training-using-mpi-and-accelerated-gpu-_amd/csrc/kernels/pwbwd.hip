@@ -437,7 +437,7 @@ void pwb_trace_set(void *ts) {   // nullptr: off; no-op unless built with PGDIST
 // ===========================================================================
 // host side
 // ===========================================================================
-void launch_wgrad_reduce(float *part, int S, long long n, float *grad, hipStream_t st);
+void launch_wgrad_reduce(float *part, int S, long long n, float *grad, hipStream_t st, bool stem36 = false);
 int colsum_rows(int R);
 
 namespace {

@@ -895,7 +895,7 @@ void launch_wt_transpose(const bf16_t *src, bf16_t *dst, const int *tab, int n, 
 }
 
 int colsum_rows(int R);
-void launch_wgrad_reduce(float *part, int S, long long n, float *grad, hipStream_t st);
+void launch_wgrad_reduce(float *part, int S, long long n, float *grad, hipStream_t st, bool stem36 = false);
 void wgrad_reduce_defer(bool on);
 bool wgrad_reduce_deferring();
 
@@ -942,19 +942,10 @@ static void launch_wg_x(const PwWgArgs &a, int TN, int TK, int S, hipStream_t st
 #undef WG_CASE
 }
 
-// reorder [32][36] (k = tap*4 + c) -> torch [32][3][3][3] (o, c, kh, kw)
-__global__ void stem_wgrad_permute_kernel(const float *__restrict__ src, float *__restrict__ grad,
-                                          int O) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= O * 27) return;
-  const int o = i / 27, r = i % 27, c = r / 9, tap = r % 9;
-  grad[i] = src[o * 36 + tap * 4 + c];
-}
-
 long long stem_wgrad_workspace_floats(int M, int O) {
   int TN, TK, S, rps;
   wgrad_geom(M, O, 36, TN, TK, S, rps);
-  return (long long)(S + colsum_rows(S) + 1) * O * 36;
+  return (long long)(S + colsum_rows(S)) * O * 36;
 }
 
 void launch_stem_wgrad(const bf16_t *G, const bf16_t *Y, const float *ga, const float *gb,
@@ -966,13 +957,8 @@ void launch_stem_wgrad(const bf16_t *G, const bf16_t *Y, const float *ga, const 
   wgrad_geom(M, O, 36, TN, TK, S, rps);
   PwWgArgs a{G, Y, ga, gb, gc, img, nullptr, nullptr, part, M, O, 36, rps, H, W, Ho, Wo};
   launch_wg_x<IM2COL_STEM>(a, TN, TK, S, st);
-  const long long n = (long long)O * 36;
-  float *tmp = part + (size_t)(S + colsum_rows(S)) * n;
-  const bool deferring = wgrad_reduce_deferring();   // the permute below reads tmp right away
-  wgrad_reduce_defer(false);
-  launch_wgrad_reduce(part, S, n, tmp, st);
-  wgrad_reduce_defer(deferring);
-  hipLaunchKernelGGL(stem_wgrad_permute_kernel, dim3((O * 27 + 255) / 256), dim3(256), 0, st, tmp, grad, O);
+  // the split reduction stores straight into the torch [O][3][3][3] layout (no permute launch)
+  launch_wgrad_reduce(part, S, (long long)O * 36, grad, st, /*stem36=*/true);
 }
 
 void launch_pw_wgrad(const bf16_t *G, const bf16_t *Y, const float *ga, const float *gb,

@@ -66,12 +66,20 @@ int colsum_rows(int R) {
   return c < 1 ? 1 : (c > kWredMaxChunks ? kWredMaxChunks : c);
 }
 
+// Output index of reduced column oc.  stem36: the stem weight gradient, reduced as
+// [O][tap*4 + c] (3 channels padded to 4) and stored as torch [O][c][kh][kw]; -1: padding.
+PG_DEVICE long long red_out_index(long long oc, bool stem36) {
+  if (!stem36) return oc;
+  const int o = (int)(oc / 36), r = (int)(oc % 36), tap = r >> 2, c = r & 3;
+  return c == 3 ? -1 : (long long)o * 27 + c * 9 + tap;
+}
+
 // One workgroup's share of a column reduction: column block bx, row chunk by (ctr: the
 // arrival counter of column block bx).
 template <int V>
 PG_DEVICE void col_reduce_body(const float *__restrict__ part, int R, long long n, int rch, int nch,
                                float *__restrict__ lvl1, int *__restrict__ ctr, float *__restrict__ out, int bx,
-                               int by) {
+                               int by, bool stem36 = false) {
   __shared__ float sh[16][16 * V + 1];
   __shared__ int flag;
   const int cg = threadIdx.x & 15, stripe = threadIdx.x >> 4;
@@ -118,8 +126,9 @@ PG_DEVICE void col_reduce_body(const float *__restrict__ part, int R, long long 
 #pragma unroll
     for (int k = 0; k < 16; ++k) s1 += sh[k][col];
   }
+  const long long od = red_out_index(oc, stem36);
   if (nch == 1) {
-    if (col < 16 * V && oc < n) out[oc] = s1;
+    if (col < 16 * V && oc < n && od >= 0) out[od] = s1;
     return;
   }
   if (col < 16 * V && oc < n) st_sc1(lvl1 + (size_t)by * n + oc, s1);
@@ -137,19 +146,20 @@ PG_DEVICE void col_reduce_body(const float *__restrict__ part, int R, long long 
 #pragma unroll
   for (int j = 0; j < V; ++j) sh[stripe][cg * V + j] = b[j];
   __syncthreads();
-  if (col < 16 * V && oc < n) {
+  if (col < 16 * V && oc < n && od >= 0) {
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < 16; ++k) s += sh[k][col];
-    out[oc] = s;
+    out[od] = s;
   }
 }
 
 template <int V>
 __global__ __launch_bounds__(256) void col_reduce_kernel(const float *__restrict__ part, int R, long long n, int rch,
                                                          int nch, float *__restrict__ lvl1, int *__restrict__ ctr,
-                                                         float *__restrict__ out) {
-  col_reduce_body<V>(part, R, n, rch, nch, lvl1, ctr ? ctr + blockIdx.x : nullptr, out, blockIdx.x, blockIdx.y);
+                                                         float *__restrict__ out, int stem36) {
+  col_reduce_body<V>(part, R, n, rch, nch, lvl1, ctr ? ctr + blockIdx.x : nullptr, out, blockIdx.x, blockIdx.y,
+                     stem36 != 0);
 }
 
 // Several independent reductions in ONE launch (the weight gradients of a group of layers
@@ -243,15 +253,17 @@ void wgrad_reduce_flush(hipStream_t st) {
   }
 }
 
-// grad[n] = sum over S split rows of part[S][n] (fixed order); part needs S + colsum_rows(S) rows
-void launch_wgrad_reduce(float *part, int S, long long n, float *grad, hipStream_t st) {
-  if (g_red_defer) {
+// grad[n] = sum over S split rows of part[S][n] (fixed order); part needs S + colsum_rows(S) rows.
+// stem36: grad is the stem weight gradient in torch layout (red_out_index); never deferred.
+void launch_wgrad_reduce(float *part, int S, long long n, float *grad, hipStream_t st, bool stem36) {
+  if (g_red_defer && !stem36) {
     g_red_pending.push_back(PendingRed{part, S, n, grad});
     return;
   }
   const bool vec = (n % 4 == 0) && ((uintptr_t)part % 16 == 0) && ((uintptr_t)grad % 16 == 0);
   const int V = vec ? 4 : 1;
   const long long nb = (n + 16 * V - 1) / (16 * V);
+  const int perm = stem36 ? 1 : 0;
   // on a weight-gradient side stream a smaller grid: the reduction is off the critical path,
   // and a 2k-workgroup launch there holds up the dispatch of the main stream's next kernel
   // (MobileNetV2 bs128 on MI355X: 5.07 ms/step at 2048, 5.00 at 512, 4.98-5.00 at 256)
@@ -265,8 +277,8 @@ void launch_wgrad_reduce(float *part, int S, long long n, float *grad, hipStream
   int *ctr = nch > 1 ? reduce_counters((int)nb, st) : nullptr;
   if (vec)
     hipLaunchKernelGGL(col_reduce_kernel<4>, dim3((unsigned)nb, nch), dim3(256), 0, st, part, S, n, rch, nch,
-                       part + (size_t)S * n, ctr, grad);
+                       part + (size_t)S * n, ctr, grad, perm);
   else
     hipLaunchKernelGGL(col_reduce_kernel<1>, dim3((unsigned)nb, nch), dim3(256), 0, st, part, S, n, rch, nch,
-                       part + (size_t)S * n, ctr, grad);
+                       part + (size_t)S * n, ctr, grad, perm);
 }
