@@ -21,7 +21,7 @@ PG_DEVICE float drop_keep(int train, float drop_p, unsigned long long seed, unsi
 }
 }  // namespace
 
-// The head runs as three launches so the 16 MB feature map is streamed by B x C/256
+// The head runs as three launches (two when training: the CE is recomputed in the backward) so the 16 MB feature map is streamed by B x C/256
 // workgroups (640 at B=128) instead of one workgroup per image (128 workgroups, half the
 // CUs idle, a 49-deep per-thread load chain):
 //   pool:  z = relu6(BN(y)) averaged over HW, dropout -> pd[B][C]      grid (B, C/256)
@@ -76,12 +76,13 @@ __global__ __launch_bounds__(256) void head_pool_kernel(
   }
 }
 
-__global__ __launch_bounds__(256) void head_ce_kernel(
-    const float *__restrict__ pd, const float *__restrict__ Wl, const float *__restrict__ bl,
-    const long long *__restrict__ labels, int C, int NC, float loss_scale, float *__restrict__ logits_out,
-    float *__restrict__ loss_out, float *__restrict__ correct_out, float *__restrict__ dlogits) {
-  __shared__ float red[4][kMaxNC];
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+// Linear + softmax-CE of image b by the whole workgroup (256 threads x 8 channels >= C).  write:
+// store logits / loss / correct / dlogits; dl_sh (optional): dlogits[b][:] into LDS for the caller.
+PG_DEVICE void ce_row(const float *__restrict__ pd, const float *__restrict__ Wl, const float *__restrict__ bl,
+                      const long long *__restrict__ labels, int b, int C, int NC, float loss_scale,
+                      float *__restrict__ logits_out, float *__restrict__ loss_out, float *__restrict__ correct_out,
+                      float *__restrict__ dlogits, bool write, float (*red)[kMaxNC], float *dl_sh) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int c0 = tid * 8;
   const bool active = c0 < C;
   float p[8];
@@ -97,34 +98,55 @@ __global__ __launch_bounds__(256) void head_ce_kernel(
     if (lane == 0) red[wave][j] = a;
   }
   __syncthreads();
-  if (tid != 0) return;
-  float lg[kMaxNC];
-  float mx = -INFINITY;
-  int arg = 0;
-  for (int j = 0; j < NC; ++j) {
-    lg[j] = red[0][j] + red[1][j] + red[2][j] + red[3][j] + bl[j];
-    if (lg[j] > mx) { mx = lg[j]; arg = j; }
-    if (logits_out) logits_out[(size_t)b * NC + j] = lg[j];
+  if (tid == 0) {
+    float lg[kMaxNC];
+    float mx = -INFINITY;
+    int arg = 0;
+    for (int j = 0; j < NC; ++j) {
+      lg[j] = red[0][j] + red[1][j] + red[2][j] + red[3][j] + bl[j];
+      if (lg[j] > mx) { mx = lg[j]; arg = j; }
+      if (write && logits_out) logits_out[(size_t)b * NC + j] = lg[j];
+    }
+    float se = 0.f;
+    for (int j = 0; j < NC; ++j) se += __expf(lg[j] - mx);
+    const float lse = mx + __logf(se);
+    const int lab = labels ? (int)labels[b] : 0;
+    if (write && loss_out) loss_out[b] = lse - lg[lab];
+    if (write && correct_out) correct_out[b] = (arg == lab) ? 1.f : 0.f;
+    for (int j = 0; j < NC; ++j) {
+      const float d = (__expf(lg[j] - lse) - (j == lab ? 1.f : 0.f)) * loss_scale;
+      if (dl_sh) dl_sh[j] = d;
+      if (write && dlogits) dlogits[(size_t)b * NC + j] = d;
+    }
   }
-  float se = 0.f;
-  for (int j = 0; j < NC; ++j) se += __expf(lg[j] - mx);
-  const float lse = mx + __logf(se);
-  const int lab = labels ? (int)labels[b] : 0;
-  if (loss_out) loss_out[b] = lse - lg[lab];
-  if (correct_out) correct_out[b] = (arg == lab) ? 1.f : 0.f;
-  if (dlogits) {
-    for (int j = 0; j < NC; ++j)
-      dlogits[(size_t)b * NC + j] = (__expf(lg[j] - lse) - (j == lab ? 1.f : 0.f)) * loss_scale;
-  }
+  __syncthreads();
 }
 
+__global__ __launch_bounds__(256) void head_ce_kernel(
+    const float *__restrict__ pd, const float *__restrict__ Wl, const float *__restrict__ bl,
+    const long long *__restrict__ labels, int C, int NC, float loss_scale, float *__restrict__ logits_out,
+    float *__restrict__ loss_out, float *__restrict__ correct_out, float *__restrict__ dlogits) {
+  __shared__ float red[4][kMaxNC];
+  ce_row(pd, Wl, bl, labels, blockIdx.x, C, NC, loss_scale, logits_out, loss_out, correct_out, dlogits, true, red,
+         nullptr);
+}
+
+// (training: the CE of image b is recomputed by each of its C/256 workgroups from pd -- 51 KB of
+// L2-resident weights -- instead of a separate launch between pool and backward; the chunk-0
+// workgroup stores logits / loss / correct / dlogits)
 __global__ __launch_bounds__(256) void head_bwd_kernel(
     const bf16_t *__restrict__ y, const float *__restrict__ s, const float *__restrict__ t,
-    const float *__restrict__ Wl, const float *__restrict__ dlogits, int HW, int C, int NC, float drop_p,
-    unsigned long long seed, const float *__restrict__ hyper, bf16_t *__restrict__ g_out,
+    const float *__restrict__ Wl, const float *__restrict__ pd, const float *__restrict__ bl,
+    const long long *__restrict__ labels, float loss_scale, float *__restrict__ logits_out,
+    float *__restrict__ loss_out, float *__restrict__ correct_out, float *__restrict__ dlogits, int HW, int C,
+    int NC, float drop_p, unsigned long long seed, const float *__restrict__ hyper, bf16_t *__restrict__ g_out,
     float *__restrict__ part, int rep, const BnFin *fin) {
   __shared__ float r0[kSlots][kChunk + 4];
   __shared__ float r1[kSlots][kChunk + 4];
+  __shared__ float cred[4][kMaxNC];
+  __shared__ float dls[kMaxNC];
+  ce_row(pd, Wl, bl, labels, blockIdx.x, C, NC, loss_scale, logits_out, loss_out, correct_out, dlogits,
+         blockIdx.y == 0, cred, dls);
   const int b = blockIdx.x, tid = threadIdx.x, cl = tid & 31, slot = tid >> 5;
   const int cbase = blockIdx.y * kChunk;
   const int c0 = cbase + cl * 8;
@@ -143,7 +165,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
       dz[k] = 0.f;
     }
     for (int j = 0; j < NC; ++j) {
-      const float d = dlogits[(size_t)b * NC + j];
+      const float d = dls[j];
 #pragma unroll
       for (int k = 0; k < 8; ++k) dz[k] = fmaf(d, Wl[(size_t)j * C + c0 + k], dz[k]);
     }
@@ -225,11 +247,13 @@ void launch_head(const bf16_t *y, const float *s, const float *t, const float *W
   const dim3 grid2(B, (C + kChunk - 1) / kChunk);
   const BnFin *fin = take_bn_fin();   // backward statistics of the final BN (train only)
   hipLaunchKernelGGL(head_pool_kernel, grid2, dim3(256), 0, st, y, s, t, HW, C, drop_p, seed, hyper, train, pd);
-  hipLaunchKernelGGL(head_ce_kernel, dim3(B), dim3(256), 0, st, pd, Wl, bl, labels, C, NC, loss_scale, logits,
-                     loss, correct, train ? dlogits : nullptr);
-  if (!train) return;
-  hipLaunchKernelGGL(head_bwd_kernel, grid2, dim3(256), 0, st, y, s, t, Wl, dlogits, HW, C, NC, drop_p, seed,
-                     hyper, g_out, part, g_bn_rep, fin);
+  if (!train) {
+    hipLaunchKernelGGL(head_ce_kernel, dim3(B), dim3(256), 0, st, pd, Wl, bl, labels, C, NC, loss_scale, logits,
+                       loss, correct, nullptr);
+    return;
+  }
+  hipLaunchKernelGGL(head_bwd_kernel, grid2, dim3(256), 0, st, y, s, t, Wl, pd, bl, labels, loss_scale, logits,
+                     loss, correct, dlogits, HW, C, NC, drop_p, seed, hyper, g_out, part, g_bn_rep, fin);
   hipLaunchKernelGGL(head_wgrad_kernel, dim3((NC * C + NC + 255) / 256), dim3(256), 0, st, dlogits, pd, B, C,
                      NC, dW, db);
 }
