@@ -66,19 +66,9 @@ long long dw_dgrad_wgrad_workspace_floats(int, int, int, int, int);
 void launch_dw_wgrad(const bf16_t *, const bf16_t *, const float *, const bf16_t *, const float *,
                      const float *, float *, float *, int, int, int, int, int, hipStream_t);
 int pw_gemm_num_partials(int, int, int);
-int ir_fwd_grid(int, int, int, int, int);
-int ir_bwd_grid(int, int, int, int, int);
-void ir_trace_set(void *);
 void pwt_trace_set(void *);
 void pwb_trace_set(void *);
 void pwg_trace_set(void *);
-void launch_ir_bwd(const bf16_t *, const bf16_t *, const void *, const bf16_t *, const bf16_t *, const float *,
-                   const float *, bf16_t *, const void *, const bf16_t *, const bf16_t *, const float *, const float *,
-                   bf16_t *, const void *, const bf16_t *, const bf16_t *, const bf16_t *, bf16_t *, const void *,
-                   unsigned *, unsigned *, int, int, int, int, int, hipStream_t);
-void launch_ir_fwd(const bf16_t *, const bf16_t *, const void *, bf16_t *, const bf16_t *, const bf16_t *,
-                   const bf16_t *, bf16_t *, bf16_t *, bf16_t *, const void *, const void *, const void *, unsigned *,
-                   unsigned *, int, int, int, int, int, hipStream_t);
 bool pw_bwd_supported(int, int, int);
 int pw_bwd_num_partials(int, int, int);
 long long pw_bwd_wgrad_workspace_floats(int, int, int);
@@ -275,39 +265,12 @@ PYBIND11_MODULE(_pgdist_C, m) {
   });
   // ---- pointwise ----
   m.def("pw_gemm_num_partials", &pw_gemm_num_partials);
-  // ---- fused inverted-residual block forward (irblock.hip) ----
-  m.def("ir_fwd_grid", &ir_fwd_grid, "workgroups of the fused block forward (0: unsupported / not co-resident)");
-  m.def("ir_trace_set", [](P ts) { ir_trace_set(reinterpret_cast<void *>(ts)); },
-        "phase trace buffer of the fused block kernels ([grid][16] uint64 wall-clock stamps; 0: off)");
   m.def("pwt_trace_set", [](P ts) { pwt_trace_set(reinterpret_cast<void *>(ts)); },
         "phase trace buffer of pw_tile ([grid][8] uint64 wall-clock stamps; 0: off; PGDIST_PWT_TRACE builds)");
   m.def("pwb_trace_set", [](P ts) { pwb_trace_set(reinterpret_cast<void *>(ts)); },
         "phase-sum buffer of pw_bwd_fused ([grid][8] uint64; 0: off; PGDIST_PWT_TRACE builds)");
   m.def("pwg_trace_set", [](P ts) { pwg_trace_set(reinterpret_cast<void *>(ts)); },
         "phase trace buffer of pw_wgrad ([grid][8] uint64; 0: off; PGDIST_PWT_TRACE builds)");
-  m.def("ir_bwd_grid", &ir_bwd_grid, "workgroups of the fused block backward (0: unsupported / not co-resident)");
-  m.def("ir_bwd", [](P G, P y, P lz_p, P wpt, P h2, P sd, P td, P gd, P dd, P wd, P h1, P se, P te, P ge, P de,
-                     P wet, P R, P yprev, P gout, P dprev, P bar, P err, int B, int H, int cin, int ch, int cout,
-                     P s) {
-    pgdist_rt::run_op([=] {
-      launch_ir_bwd(ptr<bf16_t>(G), ptr<bf16_t>(y), reinterpret_cast<const void *>(lz_p), ptr<bf16_t>(wpt),
-                    ptr<bf16_t>(h2), ptr<float>(sd), ptr<float>(td), ptr<bf16_t>(gd),
-                    reinterpret_cast<const void *>(dd), ptr<bf16_t>(wd), ptr<bf16_t>(h1), ptr<float>(se),
-                    ptr<float>(te), ptr<bf16_t>(ge), reinterpret_cast<const void *>(de), ptr<bf16_t>(wet),
-                    ptr<bf16_t>(R), ptr<bf16_t>(yprev), ptr<bf16_t>(gout), reinterpret_cast<const void *>(dprev),
-                    ptr<unsigned>(bar), ptr<unsigned>(err), B, H, cin, ch, cout, S(s));
-    });
-  });
-  m.def("ir_fwd", [](P xin, P res, P lz_in, P xout, P we, P wd, P wp, P h1, P h2, P y, P de, P dd, P dp, P bar,
-                     P err, int B, int H, int cin, int ch, int cout, P s) {
-    pgdist_rt::run_op([=] {
-      launch_ir_fwd(ptr<bf16_t>(xin), ptr<bf16_t>(res), reinterpret_cast<const void *>(lz_in), ptr<bf16_t>(xout),
-                    ptr<bf16_t>(we), ptr<bf16_t>(wd), ptr<bf16_t>(wp), ptr<bf16_t>(h1), ptr<bf16_t>(h2),
-                    ptr<bf16_t>(y), reinterpret_cast<const void *>(de), reinterpret_cast<const void *>(dd),
-                    reinterpret_cast<const void *>(dp), ptr<unsigned>(bar), ptr<unsigned>(err), B, H, cin, ch, cout,
-                    S(s));
-    });
-  });
   m.def("pw_gemm", [](int pro, int epi, P A, P A2, P pa, P pb, P pc, P W, P out, P Yt, P es, P et,
                       P R, P part, int M, int N, int K, P Aout, P s) {
     pgdist_rt::run_op([=] {

@@ -181,18 +181,12 @@ class MobileNetV2Executor:
     # fused 1x1 dgrad+wgrad (pw_bwd) wherever supported (only M >= 500k / never: 5.06 / 5.27 vs 4.80)
     PW_BWD_FUSE_MIN_M = 0
     # block outputs of the maps with at most this many pixels per image (the latency-bound 14x14 /
-    # 7x7 stages) are materialised by their consumer (next GEMM's prologue, or the fused block's
-    # P0) instead of a BN-apply launch: bs128 4.517-4.530 vs 4.540-4.581 ms/step; the 28x28 stage
+    # 7x7 stages) are materialised by their consumer (next GEMM's prologue) instead of a BN-apply launch: bs128 4.517-4.530 vs 4.540-4.581 ms/step; the 28x28 stage
     # too (784): 4.527-4.559; every block: neutral (scripts/gpu_r4_aug.sh)
     FUSE_BLOCK_OUTPUT_HW = 196
     # side-stream joins batched per this many weight gradients (1 / 2 / 3 / 4 / 6: 5.28 / 5.23 /
     # 5.15 / 5.22 / 5.21 ms/step, docs/PERF_NOTES.md round 2)
     SIDE_BATCH = 3
-    # fused inverted-residual blocks (csrc/kernels/irblock.hip) for the stride-1 14x14 / 7x7
-    # blocks: one persistent launch per block forward (expand GEMM + depthwise + project GEMM)
-    # and one for its backward main chain (three dgrads); PGDIST_IR_FUSE = 1 (both) | fwd | bwd |
-    # 0 (the three-launch paths)
-    IR_FUSE = os.environ.get("PGDIST_IR_FUSE", "0")
     # fp8 mode: the forward 1x1 convs with K >= FP8_MIN_K run on e4m3 MFMA (weights per output
     # channel, activations scaled by ops.kernels.FP8_ASC); the K = 16 / 24 / 32 expand convs, the
     # backward and depthwise / BN stay bf16 / fp32
@@ -275,28 +269,6 @@ class MobileNetV2Executor:
         # BN statistics: one accumulator pair per BN ([rows][2][C] forward and backward, rows =
         # min(producer partial rows, bn_rep)), all in one arena so a training step zeroes them
         # with a single memset
-        # blocks whose training forward runs as one fused launch: stride 1 with expansion on a
-        # <= 14x14 map, input = the previous block's pending output (BN_p (+ residual) applied by
-        # the fused kernel), lazy BN descriptors, bf16, and a co-resident grid on this device
-        self.ir_grid, self.irb_grid = {}, {}
-        lazy_possible = not K.deterministic() and os.environ.get("PGDIST_BN_LAZY", "1") == "1"
-        mode = {True: "1", False: "0"}.get(self.IR_FUSE, str(self.IR_FUSE))
-        if mode != "0" and lazy_possible and not fp8:
-            for bi, bp in enumerate(self.blocks):
-                prev = self.blocks[bi - 1] if bi > 0 else None
-                if not (bp.stride == 1 and bp.expand and bp.H <= 14 and prev is not None):
-                    continue
-                if mode in ("1", "fwd") and prev.Ho * prev.Wo <= self.FUSE_BLOCK_OUTPUT_HW:
-                    n = K.ir_fwd_grid(B, bp.H, bp.cin, bp.hidden, bp.cout)
-                    if n > 0:
-                        self.ir_grid[bp.idx] = n
-                if mode in ("1", "bwd"):
-                    n = K.ir_bwd_grid(B, bp.H, bp.cin, bp.hidden, bp.cout)
-                    if n > 0:
-                        self.irb_grid[bp.idx] = n
-        self.ir_bar = {i: torch.zeros(96, dtype=torch.int32, device=device) for i in self.ir_grid}
-        self.irb_bar = {i: torch.zeros(96, dtype=torch.int32, device=device) for i in self.irb_grid}
-        self.ir_err = torch.zeros(4, dtype=torch.int32, device=device)
         o, spans = 0, []
         self.bn_rep = K.bn_rep()   # the producers' replica rows the arena is sized for
         for bn, (pf, pb) in self._bn_producer_rows().items():
@@ -403,19 +375,17 @@ class MobileNetV2Executor:
             prev = self.blocks[bi - 1] if bi > 0 else None
             Min, Mout = B * bp.H * bp.H, B * bp.Ho * bp.Wo
             dw_in = bp.bn_e if bp.expand else self.bn0
-            nfused = getattr(self, "ir_grid", {}).get(bp.idx, 0)
-            nfb = getattr(self, "irb_grid", {}).get(bp.idx, 0)
             if bp.expand:
-                rows[bp.bn_e][0] = max(K.pw_num_partials(Min, bp.hidden, bp.cin), nfused)
-                rows[prev.bn_p][1] = max(K.pw_bwd_num_partials(Min, bp.hidden, bp.cin)
-                                         if self._pw_bwd_ok(Min, bp.hidden, bp.cin)
-                                         else K.pw_num_partials(Min, bp.cin, bp.hidden), nfb)
-            rows[bp.bn_d][0] = max(K.dw_num_partials("fwd", B, bp.H, bp.H, bp.hidden, bp.stride), nfused)
-            rows[dw_in][1] = max(K.dw_num_partials("dgrad", B, bp.H, bp.H, bp.hidden, bp.stride), nfb)
-            rows[bp.bn_p][0] = max(K.pw_num_partials(Mout, bp.cout, bp.hidden), nfused)
-            rows[bp.bn_d][1] = max(K.pw_bwd_num_partials(Mout, bp.cout, bp.hidden)
-                                   if self._pw_bwd_ok(Mout, bp.cout, bp.hidden)
-                                   else K.pw_num_partials(Mout, bp.hidden, bp.cout), nfb)
+                rows[bp.bn_e][0] = K.pw_num_partials(Min, bp.hidden, bp.cin)
+                rows[prev.bn_p][1] = (K.pw_bwd_num_partials(Min, bp.hidden, bp.cin)
+                                      if self._pw_bwd_ok(Min, bp.hidden, bp.cin)
+                                      else K.pw_num_partials(Min, bp.cin, bp.hidden))
+            rows[bp.bn_d][0] = K.dw_num_partials("fwd", B, bp.H, bp.H, bp.hidden, bp.stride)
+            rows[dw_in][1] = K.dw_num_partials("dgrad", B, bp.H, bp.H, bp.hidden, bp.stride)
+            rows[bp.bn_p][0] = K.pw_num_partials(Mout, bp.cout, bp.hidden)
+            rows[bp.bn_d][1] = (K.pw_bwd_num_partials(Mout, bp.cout, bp.hidden)
+                                if self._pw_bwd_ok(Mout, bp.cout, bp.hidden)
+                                else K.pw_num_partials(Mout, bp.hidden, bp.cout))
         Mf = B * self.Hf * self.Hf
         rows[self.bn_last][0] = K.pw_num_partials(Mf, self.C_last, self.C_last_in)
         rows[self.bn_last][1] = B
@@ -576,15 +546,6 @@ class MobileNetV2Executor:
         for bp in self.blocks:
             Hin = bp.H
             Min = B * Hin * Hin
-            if train and pend is not None and bp.idx in self.ir_grid:
-                # expand -> dw -> project in one launch (its P0 materialises the pending input o)
-                pbn, pres, po = pend
-                K.ir_fwd(pbn.y, pres, pbn.lz_f, po, f.b(bp.w_e), f.b(bp.w_d), f.b(bp.w_p), bp.bn_e.y, bp.bn_d.y,
-                         bp.bn_p.y, bp.bn_e.desc_f, bp.bn_d.desc_f, bp.bn_p.desc_f, self.ir_bar[bp.idx], self.ir_err,
-                         B, Hin, bp.cin, bp.hidden, bp.cout)
-                pend = (bp.bn_p, inp_t if bp.residual else None, bp.o)
-                inp_bn, inp_t = bp.bn_p, bp.o
-                continue
             if bp.expand:
                 if pend is not None:
                     self._consume_output(pend, f.b(bp.w_e), bp.bn_e.y, bp.bn_e.acc_f, Min, bp.hidden, bp.cin,
@@ -677,9 +638,6 @@ class MobileNetV2Executor:
             Hin = bp.H
             Min, Mout = B * Hin * Hin, B * bp.Ho * bp.Wo
             bnp, bnd = bp.bn_p, bp.bn_d
-            if bp.idx in self.irb_grid:
-                self._fused_block_backward(bp, prev)
-                continue
             # bn_p backward coefficients were finalised by whoever produced bp.G
             # project dgrad -> g_d (relu6 mask of BN_d) + BN_d partials
             if self._pw_bwd_ok(Mout, bp.cout, bp.hidden):
@@ -774,42 +732,6 @@ class MobileNetV2Executor:
         self._flush_side()
         if self.side is not None:   # join: the optimizer (main stream) needs every gradient
             K.stream_wait(torch.cuda.current_stream(self.device), self.side)
-
-    def _fused_block_backward(self, bp: BlockPlan, prev: BlockPlan):
-        """One block's backward main chain as ONE launch (K.ir_bwd: project dgrad -> depthwise dgrad
-        -> expand dgrad with two in-kernel BN-backward barriers); the weight gradients follow on the
-        side stream from the gradients it wrote, exactly as after the three-launch chain."""
-        f, B = self.flat, self.B
-        bnp, bnd, bne = bp.bn_p, bp.bn_d, bp.bn_e
-        Hin = bp.H
-        Min = Mout = B * Hin * Hin
-        K.ir_bwd(bp.G, bnp.y, bnp.lz_b, f.bt(bp.w_p), bnd.y, bnd.scale, bnd.shift, bnd.g, bnd.desc_b, f.b(bp.w_d),
-                 bne.y, bne.scale, bne.shift, bne.g, bne.desc_b, f.bt(bp.w_e), bp.G if bp.residual else None,
-                 prev.bn_p.y, prev.G, prev.bn_p.desc_b, self.irb_bar[bp.idx], self.ir_err, B, Hin, bp.cin, bp.hidden,
-                 bp.cout)
-        P = self.irb_grid[bp.idx]
-
-        def prj_wgrad(ws, bnd=bnd, bnp=bnp, bp=bp):
-            K.pw_wgrad(bp.G, bnp.y, bnp.a, bnp.b, bnp.c, bnd.y, bnd.scale, bnd.shift, K.ACT_BN_RELU6, ws,
-                       f.g(bp.w_p), Mout, bp.cout, bp.hidden)
-        self._wgrad(prj_wgrad, fins=((bnd, P),))
-        self._ready([bp.w_p] + bnd.param_names)
-
-        def dw_wg(ws, bnd=bnd, bne=bne, bp=bp):
-            K.dw_wgrad(bnd.g, bnd.y, bnd.coef, bne.y, bne.scale, bne.shift, ws, f.g(bp.w_d), B, Hin, Hin,
-                       bp.hidden, bp.stride)
-        self._wgrad(dw_wg, fins=((bne, P),))
-        self._ready([bp.w_d] + bne.param_names)
-
-        def exp_wgrad(ws, prev=prev, bne=bne, bp=bp):
-            K.pw_wgrad(bne.g, bne.y, bne.a, bne.b, bne.c, prev.o, None, None, K.ACT_NONE, ws, f.g(bp.w_e), Min,
-                       bp.hidden, bp.cin)
-        self._wgrad(exp_wgrad, fins=((prev.bn_p, P),))
-        self._ready([bp.w_e] + prev.bn_p.param_names)
-
-    def ir_error(self) -> int:
-        """Sticky error word of the fused block kernels (bit 0: a grid barrier timed out)."""
-        return int(self.ir_err[0].item())
 
     # ------------------------------------------------------------------ eval
     def eval_prepare(self):

@@ -366,51 +366,6 @@ def pw_gemm(pro, epi, A, W, out, part, M, N, K, A2=None, pa=None, pb=None, pc=No
                   _p(es), _p(et), _p(R), _p(part), M, N, K, _p(Aout), _s())
 
 
-# --------------------------------------------------------------------------- fused block
-def ir_fwd_grid(B, H, cin, ch, cout):
-    """Workgroups of the fused inverted-residual block forward (csrc/kernels/irblock.hip) for B
-    images of an HxH map, or 0 when the shape has no fused kernel or its grid would not be
-    co-resident on this device (the kernel's grid barriers need every workgroup resident)."""
-    return lib().ir_fwd_grid(int(B), int(H), int(cin), int(ch), int(cout))
-
-
-def ir_fwd(xin, res, lz_in, xout, we, wd, wp, h1, h2, y, de, dd, dp, bar, err, B, H, cin, ch, cout):
-    """One training-mode MobileNetV2 inverted-residual block forward (stride 1, expand 6) in one
-    launch: input = BN_p(xin) (+ res) via the lazy descriptor ``lz_in`` (materialised into
-    ``xout``), expand -> BN_e -> ReLU6 -> dw 3x3 -> BN_d -> ReLU6 -> project; raw h1 / h2 / y
-    and the statistics of BN_e / BN_d / BN_p (descriptors ``de`` / ``dd`` / ``dp``, whose
-    accumulators must be zero and have ``rows`` = min(grid, bn_rep())) exactly as the unfused
-    kernels write them.  ``bar``: 96 int32, zero before the first launch (the kernel re-arms them), ``err``: sticky
-    error word (bit 0: a grid barrier timed out)."""
-    M = B * H * H
-    _chk(xin, BF16, M * cin, "xin")
-    _chk(res, BF16, M * cin, "res")
-    _chk(xout, BF16, M * cin, "xout")
-    _chk(we, BF16, ch * cin, "we")
-    _chk(wd, BF16, 9 * ch, "wd")
-    _chk(wp, BF16, cout * ch, "wp")
-    _chk(h1, BF16, M * ch, "h1")
-    _chk(h2, BF16, M * ch, "h2")
-    _chk(y, BF16, M * cout, "y")
-    _chk(bar, torch.int32, 96, "bar")
-    _chk(err, torch.int32, 1, "err")
-    for d in (lz_in, de, dd, dp):
-        if d is None or not (d.is_cuda and d.dtype == torch.uint8):
-            raise TypeError("ir_fwd: BN descriptors from bn_fin_desc")
-    if ir_fwd_grid(B, H, cin, ch, cout) <= 0:
-        raise ValueError(f"ir_fwd: no co-resident fused kernel for B={B} H={H} {cin}->{ch}->{cout}")
-    lib().ir_fwd(_p(xin), _p(res), _p(lz_in), _p(xout), _p(we), _p(wd), _p(wp), _p(h1), _p(h2), _p(y),
-                 _p(de), _p(dd), _p(dp), _p(bar), _p(err), B, H, cin, ch, cout, _s())
-
-
-def ir_trace_set(buf):
-    """Diagnostics: the fused block kernels stamp the wall clock (100 MHz) at their phase
-    boundaries into ``buf`` (int64 [grid][16]) from now on; None switches it off."""
-    if buf is not None:
-        _chk(buf, torch.int64, buf.numel(), "buf")
-    lib().ir_trace_set(0 if buf is None else buf.data_ptr())
-
-
 def pwt_trace_set(buf):
     """Diagnostics (builds with PGDIST_DEFINES=PGDIST_PWT_TRACE): the small-M pointwise GEMM
     (pw_tile) stamps the wall clock at its phase boundaries into ``buf`` (int64 [grid][8])."""
@@ -433,38 +388,6 @@ def pwg_trace_set(buf):
     if buf is not None:
         _chk(buf, torch.int64, buf.numel(), "buf")
     lib().pwg_trace_set(0 if buf is None else buf.data_ptr())
-
-
-def ir_bwd_grid(B, H, cin, ch, cout):
-    """Workgroups of the fused inverted-residual block backward (0: no kernel / not co-resident)."""
-    return lib().ir_bwd_grid(int(B), int(H), int(cin), int(ch), int(cout))
-
-
-def ir_bwd(G, y, lz_p, wpt, h2, sd, td, gd, dd, wd, h1, se, te, ge, de, wet, R, yprev, gout, dprev, bar, err,
-           B, H, cin, ch, cout):
-    """One MobileNetV2 inverted-residual block's backward main chain in one launch: project dgrad
-    (BN_p backward from ``lz_p``; ReLU6 mask of BN_d(h2) with the forward ``sd``/``td``) ->
-    ``gd`` + BN_d backward sums (``dd``), depthwise dgrad (BN_d backward) -> ``ge`` + BN_e sums
-    (``de``), expand dgrad (BN_e backward, + skip gradient ``R``) -> ``gout`` + the previous
-    block's BN_p sums (``dprev``).  ``wpt`` / ``wet``: the transposed 1x1 weights; ``bar``: 96
-    int32 zero before the first launch (re-armed by the kernel)."""
-    M = B * H * H
-    for t, n, nm in ((G, M * cout, "G"), (y, M * cout, "y"), (wpt, ch * cout, "wpt"), (h2, M * ch, "h2"),
-                     (gd, M * ch, "gd"), (wd, 9 * ch, "wd"), (h1, M * ch, "h1"), (ge, M * ch, "ge"),
-                     (wet, cin * ch, "wet"), (R, M * cin, "R"), (yprev, M * cin, "yprev"), (gout, M * cin, "gout")):
-        _chk(t, BF16, n, nm)
-    for t, nm in ((sd, "sd"), (td, "td"), (se, "se"), (te, "te")):
-        _chk(t, F32, ch, nm)
-    _chk(bar, torch.int32, 96, "bar")
-    _chk(err, torch.int32, 1, "err")
-    for d in (lz_p, dd, de, dprev):
-        if d is None or not (d.is_cuda and d.dtype == torch.uint8):
-            raise TypeError("ir_bwd: BN descriptors from bn_fin_desc")
-    if ir_bwd_grid(B, H, cin, ch, cout) <= 0:
-        raise ValueError(f"ir_bwd: no co-resident fused kernel for B={B} H={H} {cin}->{ch}->{cout}")
-    lib().ir_bwd(_p(G), _p(y), _p(lz_p), _p(wpt), _p(h2), _p(sd), _p(td), _p(gd), _p(dd), _p(wd), _p(h1), _p(se),
-                 _p(te), _p(ge), _p(de), _p(wet), _p(R), _p(yprev), _p(gout), _p(dprev), _p(bar), _p(err),
-                 B, H, cin, ch, cout, _s())
 
 
 FP8 = torch.uint8   # raw OCP e4m3fn bytes (torch.float8_e4m3fn views share the encoding)
@@ -1168,7 +1091,7 @@ def _logged(fn):
 
 for _name in ("bn_fwd_finalize", "bn_bwd_finalize", "bn_apply", "bn_finalize_batch", "adam_flat", "f32_to_bf16",
               "step_begin", "reduce_metrics", "dw_fwd", "dw_dgrad", "dw_wgrad", "pw_gemm", "pw_gemm_f8", "w8_quant",
-              "wt_transpose", "pw_bwd", "ir_fwd", "ir_bwd", "wgrad_reduce", "wgrad_reduce_flush", "pw_wgrad", "stem_fwd", "stem_wgrad",
+              "wt_transpose", "pw_bwd", "wgrad_reduce", "wgrad_reduce_flush", "pw_wgrad", "stem_fwd", "stem_wgrad",
               "head", "augment", "conv_fwd", "conv_dgrad", "conv_wgrad", "bn_mat", "conv_wt", "res_out", "maxpool_fwd",
               "maxpool_bwd", "avgpool", "head_bwd", "softmax_ce", "fc_gemm", "col_sum", "image_prep", "memset"):
     globals()[_name] = _logged(globals()[_name])
