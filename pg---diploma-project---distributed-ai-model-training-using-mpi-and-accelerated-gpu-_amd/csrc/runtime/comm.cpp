@@ -88,9 +88,15 @@ void ncheck(ncclResult_t e, const char *what) {
   if (e != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + rccl().errorString(e));
 }
 
+// Device-side join / marker events.  The communicator's events are recorded on the main and
+// side streams before every bucket (the collective's wait) and around every tracked collective
+// (the watchdog polls them from the host with hipEventQuery, which needs no fence): created
+// like the plan's join events, without a system-scope fence.  A kernel's own
+// device-scope release already makes its gradient writes visible to the comm stream's kernels
+// and to RCCL / P2P peers (which read staging written by this device's comm kernels).
 struct Event {
   hipEvent_t e = nullptr;
-  Event() { hcheck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreateWithFlags"); }
+  Event() { hcheck(hipEventCreateWithFlags(&e, join_event_flags()), "hipEventCreateWithFlags"); }
   ~Event() {
     if (e) (void)hipEventDestroy(e);
   }
@@ -147,6 +153,16 @@ struct Comm {
   std::thread wd;
   std::atomic<bool> wd_stop{false};
   std::atomic<long long> stall_ms{0};   // fault injection: stall the next collective this long
+  // the RCCL handle is shared with the watchdog: on a stall the watchdog takes it (nccl_mu),
+  // nulls it and hands it to the aborter thread, so no later comm_error / comm_rccl_ranks / comm_destroy
+  // touches an aborted (freed) communicator; comm_destroy joins the aborter first
+  std::mutex nccl_mu;
+  std::thread aborter;
+  std::atomic<bool> abort_done{false};
+  ncclComm_t rccl_handle() {
+    std::lock_guard<std::mutex> g(nccl_mu);
+    return nccl;
+  }
 
   void fail(int code, const std::string &msg) {
     std::lock_guard<std::mutex> g(what_mu);
@@ -319,21 +335,40 @@ void Comm::watchdog_loop() {
     std::fprintf(stderr, "%s\n", msg);
     std::fflush(stderr);
     fail(kCommErrStall, msg);
+    // poison the device error word too, through a private stream (the comm stream is the one
+    // that is stuck, and the main stream waits for it): the fused Adam of a step whose RCCL
+    // collective was aborted then skips its update instead of applying whatever the aborted
+    // collective left in the gradient buffer
+    {
+      hipStream_t ps = nullptr;
+      if (ctr && hipStreamCreateWithFlags(&ps, hipStreamNonBlocking) == hipSuccess) {
+        const unsigned w = kArErrPoisoned;
+        for (int l = 0; l < nlocal; ++l) (void)hipMemcpyAsync(err_of(l), &w, 4, hipMemcpyHostToDevice, ps);
+        (void)hipStreamSynchronize(ps);
+        (void)hipStreamDestroy(ps);
+      }
+      (void)hipGetLastError();
+    }
     // ncclCommAbort makes RCCL's own kernels give up, but it can block behind work queued on
     // the stream (measured: until an injected stall kernel ended): run it beside, and with an
-    // exit status end the process after a bounded grace period whether or not it returned
-    auto done = std::make_shared<std::atomic<bool>>(false);
-    if (nccl && rccl().commAbort) {
-      ncclComm_t nc = nccl;
-      std::thread([nc, done] {
+    // exit status end the process after a bounded grace period whether or not it returned.
+    // The handle leaves the communicator before the abort starts (nothing else uses it again).
+    ncclComm_t nc = nullptr;
+    {
+      std::lock_guard<std::mutex> g(nccl_mu);
+      nc = nccl;
+      nccl = nullptr;
+    }
+    if (nc && rccl().commAbort) {
+      aborter = std::thread([nc, this] {
         (void)rccl().commAbort(nc);
-        done->store(true);
-      }).detach();
+        abort_done.store(true);
+      });
     } else {
-      done->store(true);
+      abort_done.store(true);
     }
     if (wd_exit) {
-      for (int i = 0; i < 100 && !done->load(); ++i) std::this_thread::sleep_for(std::chrono::milliseconds(20));
+      for (int i = 0; i < 100 && !abort_done.load(); ++i) std::this_thread::sleep_for(std::chrono::milliseconds(20));
       std::fflush(stdout);
       std::fflush(stderr);
       std::_Exit(wd_exit);
@@ -461,11 +496,11 @@ void comm_allreduce(int id, const std::vector<uintptr_t> &bufs, long long n, int
   auto ev = make_events(wait.size());
   hipStream_t st = c.stream;
   if (algo == COMM_RCCL) {
-    if (!c.nccl) throw std::runtime_error("communicator has no RCCL path");
+    if (!c.rccl_handle()) throw std::runtime_error("communicator has no RCCL path");
     if (bufs.size() != 1 || !bufs[0]) throw std::invalid_argument("RCCL all-reduce: one buffer");
     if (bf16_wire) throw std::invalid_argument("RCCL all-reduce: fp32 only (bf16 wire is a P2P option)");
     void *b = reinterpret_cast<void *>(bufs[0]);
-    ncclComm_t nc = c.nccl;
+    ncclComm_t nc = c.rccl_handle();
     Rccl *r = &rccl();
     Comm *cp = &c;
     const std::string label = "RCCL all-reduce of " + std::to_string(n) + " floats";
@@ -504,10 +539,10 @@ void comm_broadcast(int id, const std::vector<uintptr_t> &bufs, long long n, int
   auto ev = make_events(wait.size());
   hipStream_t st = c.stream;
   if (algo == COMM_RCCL) {
-    if (!c.nccl) throw std::runtime_error("communicator has no RCCL path");
+    if (!c.rccl_handle()) throw std::runtime_error("communicator has no RCCL path");
     if (bufs.size() != 1 || !bufs[0]) throw std::invalid_argument("RCCL broadcast: one buffer");
     void *b = reinterpret_cast<void *>(bufs[0]);
-    ncclComm_t nc = c.nccl;
+    ncclComm_t nc = c.rccl_handle();
     Rccl *r = &rccl();
     Comm *cp = &c;
     const std::string label = "RCCL broadcast of " + std::to_string(n) + " floats";
@@ -537,11 +572,11 @@ void comm_broadcast(int id, const std::vector<uintptr_t> &bufs, long long n, int
 
 void comm_allreduce_f64(int id, uintptr_t buf, long long n, int op, const std::vector<uintptr_t> &wait) {
   Comm &c = get(id);
-  if (!c.nccl) throw std::runtime_error("communicator has no RCCL path");
+  if (!c.rccl_handle()) throw std::runtime_error("communicator has no RCCL path");
   if (op != 0 && op != 2) throw std::invalid_argument("comm_allreduce_f64: op 0 (sum) or 2 (max)");
   auto ev = make_events(wait.size());
   hipStream_t st = c.stream;
-  ncclComm_t nc = c.nccl;
+  ncclComm_t nc = c.rccl_handle();
   Rccl *r = &rccl();
   void *b = reinterpret_cast<void *>(buf);
   Comm *cp = &c;
@@ -588,7 +623,8 @@ double comm_time_allreduce(int id, const std::vector<uintptr_t> &bufs, long long
 
 int comm_error(int id) {
   Comm &c = get(id);
-  hcheck(hipStreamSynchronize(c.stream), "hipStreamSynchronize(comm)");
+  // (after a watchdog abort the comm stream may hold a collective that never completes)
+  if (!(c.host_err.load() & kCommErrStall)) hcheck(hipStreamSynchronize(c.stream), "hipStreamSynchronize(comm)");
   int err = 0;
   if (c.ctr) {
     std::vector<unsigned int> w((size_t)c.nlocal * (kArCtrWords + 8));
@@ -599,9 +635,9 @@ int comm_error(int id) {
                       ((err & kArErrDesync) ? " peer out of step" : "") +
                       ((err & kArErrPoisoned) ? " poisoned" : ""));
   }
-  if (c.nccl) {
+  if (ncclComm_t nc = c.rccl_handle()) {   // (null once the watchdog aborted it)
     ncclResult_t ae = ncclSuccess;
-    if (rccl().getAsyncError(c.nccl, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+    if (rccl().getAsyncError(nc, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
       err |= ((int)ae & 0xff) << 8;
       c.fail(((int)ae & 0xff) << 8, std::string("RCCL async error: ") + rccl().errorString(ae));
     }
@@ -669,9 +705,10 @@ void comm_error_async(int id, uintptr_t host_dst) {
 
 int comm_rccl_ranks(int id) {
   Comm &c = get(id);
-  if (!c.nccl) return 0;
+  ncclComm_t nc = c.rccl_handle();
+  if (!nc) return 0;
   int n = 0;
-  ncheck(rccl().commCount(c.nccl, &n), "ncclCommCount");
+  ncheck(rccl().commCount(nc, &n), "ncclCommCount");
   return n;
 }
 
@@ -681,12 +718,15 @@ void comm_destroy(int id) {
   Comm &c = *it->second;
   c.stop_watchdog();
   (void)hipSetDevice(c.device);
-  if (c.stream) (void)hipStreamSynchronize(c.stream);
-  if (c.nccl) (void)rccl().commDestroy(c.nccl);
+  const bool aborted = c.aborter.joinable();
+  if (aborted) c.aborter.join();   // the watchdog's ncclCommAbort has returned
+  // a stalled (aborted) comm stream is not waited for: its collective may never complete
+  if (c.stream && !aborted) (void)hipStreamSynchronize(c.stream);
+  if (ncclComm_t nc = c.rccl_handle()) (void)rccl().commDestroy(nc);
   for (void *p : c.opened) (void)hipIpcCloseMemHandle(p);
   for (void *p : c.own) (void)hipFree(p);
   if (c.ctr) (void)hipFree(c.ctr);
-  if (c.stream) (void)hipStreamDestroy(c.stream);
+  if (c.stream && !aborted) (void)hipStreamDestroy(c.stream);   // (an aborted one is leaked)
   comms().erase(it);
 }
 

@@ -154,6 +154,8 @@ std::size_t plan_size(int id) {
   return it == plans().end() ? 0 : it->second.ops.size();
 }
 
+unsigned join_event_flags() { return event_flags(); }
+
 void stream_wait(hipStream_t waiter, hipStream_t signaler) {
   if (waiter == signaler) return;
   if (!plan_recording()) {

@@ -49,6 +49,9 @@ void run_op(F &&f) {
 // `waiter` waits for the work enqueued so far on `signaler` (event record + stream wait);
 // a recorded wait owns its event, eager waits reuse a small event ring
 void stream_wait(hipStream_t waiter, hipStream_t signaler);
+// flags of device-side join events (no timing, no system-scope fence unless PGDIST_EVENT_FLAGS
+// says otherwise): the events of stream_wait, and the communicator's bucket joins / watchdog markers
+unsigned join_event_flags();
 // hipMemsetAsync(ptr, value, bytes, stream) as a plan op
 void memset_async(void *ptr, int value, std::size_t bytes, hipStream_t st);
 

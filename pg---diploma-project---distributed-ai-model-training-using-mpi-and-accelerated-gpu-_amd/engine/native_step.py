@@ -74,9 +74,13 @@ class NativeTrainStep:
                  double_resize: bool = True, augment: bool = True, train_augment: bool = True,
                  side_stream: bool = True, bn_broadcast: bool = False, fp8: bool = False,
                  graph_forward: bool = False, comm: Optional[str] = None, force_ddp: bool = False,
-                 allreduce_algo: Optional[str] = None):
+                 allreduce_algo: Optional[str] = None, comm_watchdog_s: Optional[float] = None):
         self.device, self.B, self.S = device, batch, img_size
         self.world, self.rank = world_size, rank
+        # deadline of the native communicator's collective watchdog (None: PGDIST_COMM_TIMEOUT);
+        # the trainer passes its dist_timeout_s, so rank-0-only epoch work (checkpoints) that
+        # keeps the peers waiting inside a collective is not mistaken for a dead peer
+        self.comm_watchdog_s = comm_watchdog_s
         self.exe = executor_class(model)(model, batch, img_size, device, dropout_seed=(seed * 7919) ^ rank,
                                          side_stream=side_stream, fp8=fp8)
         self.flat = self.exe.flat
@@ -216,7 +220,8 @@ class NativeTrainStep:
             raise RuntimeError("PGDIST_COMM=p2p needs every rank on this node (at most 8)")
         grad_bytes = self.flat.grad.numel() * 4
         return NativeComm.for_process_group(self.device, use_rccl=mode in ("rccl", "native"),
-                                            p2p_bytes=grad_bytes if use_p2p else 0) \
+                                            p2p_bytes=grad_bytes if use_p2p else 0,
+                                            watchdog_s=self.comm_watchdog_s) \
             if world_size > 1 else NativeComm(0, 1, self.device, use_rccl=mode in ("rccl", "native"),
                                               p2p_bytes=grad_bytes if use_p2p else 0)
 
@@ -378,8 +383,10 @@ class NativeTrainStep:
             K.plan_py(self.reducer.finish)
         for a, b in self.fault_zero:
             K.memset(self.flat.grad[a:b])
-        # a failed / poisoned gradient collective leaves its error word set: Adam then skips the
-        # update, so no replica applies un-reduced gradients (the job fails at the next check)
+        # a failed P2P collective, a poisoned communicator (comm_poison) or an RCCL collective the
+        # watchdog aborted leaves the device error word set: Adam then skips the update, so no
+        # replica applies un-reduced gradients (the job fails at the next check).  An RCCL
+        # asynchronous error is only seen by the host poll (comm_error), one step later.
         K.adam_flat(self.flat.master, self.flat.grad, self.flat.exp_avg, self.flat.exp_avg_sq,
                     self.flat.shadow, self.hyper, self.betas[0], self.betas[1], self.eps, self.wd,
                     1.0 / self.world, skip=self.comm.error_word if self.comm is not None else 0,

@@ -126,7 +126,8 @@ class Trainer:
                                     first_bucket_mb=cfg.first_bucket_mb,
                                     reduce_dtype=torch.bfloat16 if cfg.grad_reduce_dtype == "bf16" else torch.float32,
                                     augment=True, train_augment=cfg.augment != "none",
-                                    bn_broadcast=cfg.bn_sync == "broadcast", fp8=cfg.precision == "fp8")
+                                    bn_broadcast=cfg.bn_sync == "broadcast", fp8=cfg.precision == "fp8",
+                                    comm_watchdog_s=cfg.dist_timeout_s if self.world > 1 else None)
         self.flat = self.step.flat
         self.train_src = torch.from_numpy(self.train_data.images).to(self.device)
         self.train_labels = torch.from_numpy(self.train_data.labels).to(self.device)
@@ -207,6 +208,10 @@ class Trainer:
                         err = comm.poll_error()
                         if err:
                             from ..parallel.comm import CommError
+                            from ..ops._lib import lib
+                            # poison this rank's communicator (device error word included) before
+                            # raising, so nothing later on this rank launches a collective
+                            lib().comm_poison(comm.id, f"rank {self.rank}: error 0x{err:x} seen by the step poll")
                             raise CommError(f"native communicator error 0x{err:x} on rank {self.rank} before "
                                             f"epoch {epoch + 1} batch {b}: {comm.error_string() or 'P2P failure'}")
                     sl = didx[b * bs:(b + 1) * bs]
@@ -344,6 +349,11 @@ class Trainer:
                 self.best_state = ckpt.snapshot_state_dict(self.model)
             if cfg.ckpt_dir and self.rank == 0:
                 self._save_full(epoch + 1, lr)
+            if cfg.ckpt_dir and self.world > 1:
+                # the peers wait here (host barrier, dist_timeout_s) while rank 0 writes the
+                # checkpoint, not inside the next epoch's first collective, where the native
+                # communicator's watchdog would see a stall
+                barrier(self.device if self.device.type == "cuda" else None)
         total = time.time() - total
         if self.world > 1:
             self.replica_check()

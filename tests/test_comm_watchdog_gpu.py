@@ -141,3 +141,44 @@ def test_adam_skips_while_the_error_word_is_set():
     K.adam_flat(p, grad, m, v, pb, hyper, 0.9, 0.999, 1e-8, skip=word.data_ptr())
     torch.cuda.synchronize()
     assert not torch.equal(p, p0) and m.any()
+
+
+def test_poison_only_watchdog_then_error_and_close():
+    """exit_status=0 (poison + abort only): after the stall fires the communicator's
+    RCCL handle is gone, so comm_error and close() must neither use the aborted communicator
+    nor wait for the stalled comm stream; the stalled training step's Adam update is skipped
+    (the watchdog also poisons the device error word)."""
+    r, dt = _run("""
+        import sys, time, torch
+        sys.path.insert(0, '.')
+        import pgdist
+        from pgdist.engine.native_step import NativeTrainStep
+        from pgdist.models import mobilenet_v2
+        dev = torch.device('cuda', 0)
+        torch.manual_seed(0)
+        st = NativeTrainStep(mobilenet_v2(10), 16, dev, img_size=96, force_ddp=True, allreduce_algo='rccl',
+                             comm='rccl', use_graph=False)
+        src = torch.randint(0, 256, (64, 32, 32, 3), dtype=torch.uint8, device=dev)
+        st.set_data(src, torch.randint(0, 10, (64,), device=dev))
+        st.comm.set_watchdog(1.0, exit_status=0)
+        for i in range(3):
+            st.run(torch.arange(16, device=dev))
+        torch.cuda.synchronize()
+        assert st.comm.error() == 0
+        before = st.flat.master.clone()
+        st.comm.inject_stall(4.0)
+        st.run(torch.arange(16, device=dev))
+        torch.cuda.synchronize()   # the stall kernel ends; the aborted collective does not hang
+        err = st.comm.error()
+        assert err != 0, err
+        assert st.comm.rccl_ranks() == 0, 'the aborted RCCL handle must be dropped'
+        assert torch.equal(before, st.flat.master), 'the stalled step must not update the weights'
+        print('error', hex(err), st.comm.error_string()[:60], flush=True)
+        t0 = time.time()
+        st.comm.close()
+        print('closed in %.1f s' % (time.time() - t0), flush=True)
+    """, timeout=180)
+    assert "comm watchdog" in r.stderr, (r.returncode, r.stdout[-1000:], r.stderr[-3000:])
+    assert r.returncode == 0, (r.returncode, r.stdout[-1000:], r.stderr[-3000:])
+    assert "closed in" in r.stdout
+    assert dt < 150

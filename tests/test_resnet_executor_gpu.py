@@ -201,8 +201,8 @@ def test_resnet_lazy_bn_matches_launch(dev, monkeypatch, stem):
     batched at the end of the forward / on the side stream) vs a finalize launch after every
     producer: after 4 replayed training steps the weights, Adam moments, BN running statistics
     and metrics agree within the float-atomic noise floor of the replica rows (both modes add the
-    statistics atomically; estimated from the spread of three launch-mode runs -- one pair alone
-    can under-estimate this heavy-tailed noise by 10x at batch 8)."""
+    statistics atomically; estimated as the median pairwise spread of three launch-mode runs, and
+    the lazy run is compared with its closest launch-mode run)."""
     from pgdist.engine.native_step import NativeTrainStep
     from pgdist.engine.resnet_executor import ResNet50Executor
     monkeypatch.setattr(ResNet50Executor, "STEM", stem)
@@ -233,13 +233,16 @@ def test_resnet_lazy_bn_matches_launch(dev, monkeypatch, stem):
     assert n2 == n0 and set(n2) == {4}
     pairs = [(a, b) for i, a in enumerate(ref) for b in ref[i + 1:]]
 
-    def spread(f):
-        return max(f(a, b) for a, b in pairs)
+    def spread(f):   # median pairwise spread of the three reference runs
+        return sorted(f(a, b) for a, b in pairs)[len(pairs) // 2]
+
+    def dist(f):     # lazy run vs the closest reference run (the same statistic as a pair)
+        return min(f(lz, r) for r in ref)
     # the first step's forward sees identical weights: its loss agrees to the atomic noise
     # (a consumer reading stale BN parameters would be off by far more)
     lnoise = spread(lambda a, b: abs(a[4][0] - b[4][0]))
-    assert abs(k2[0] - k0[0]) <= 2e-3 * abs(k0[0]) + 10 * lnoise, ([r[4] for r in ref], k2)
+    assert dist(lambda a, b: abs(a[4][0] - b[4][0])) <= 1e-3 * abs(k0[0]) + 10 * lnoise, ([r[4] for r in ref], k2)
     noise = max(spread(lambda a, b: _rel(a[0], b[0])), 1e-6)
-    assert _rel(w2, w0) < max(20 * noise, 1e-4), (_rel(w2, w0), noise)
-    assert _rel(m2, m0) < max(20 * max(spread(lambda a, b: _rel(a[1], b[1])), 1e-6), 1e-3)
-    assert _rel(r2, r0) < max(20 * max(spread(lambda a, b: _rel(a[2], b[2])), 1e-6), 1e-4)
+    assert dist(lambda a, b: _rel(a[0], b[0])) < max(20 * noise, 1e-4), (_rel(w2, w0), noise)
+    assert dist(lambda a, b: _rel(a[1], b[1])) < max(20 * max(spread(lambda a, b: _rel(a[1], b[1])), 1e-6), 1e-3)
+    assert dist(lambda a, b: _rel(a[2], b[2])) < max(20 * max(spread(lambda a, b: _rel(a[2], b[2])), 1e-6), 1e-4)
