@@ -335,20 +335,11 @@ void Comm::watchdog_loop() {
     std::fprintf(stderr, "%s\n", msg);
     std::fflush(stderr);
     fail(kCommErrStall, msg);
-    // poison the device error word too, through a private stream (the comm stream is the one
-    // that is stuck, and the main stream waits for it): the fused Adam of a step whose RCCL
-    // collective was aborted then skips its update instead of applying whatever the aborted
-    // collective left in the gradient buffer
-    {
-      hipStream_t ps = nullptr;
-      if (ctr && hipStreamCreateWithFlags(&ps, hipStreamNonBlocking) == hipSuccess) {
-        const unsigned w = kArErrPoisoned;
-        for (int l = 0; l < nlocal; ++l) (void)hipMemcpyAsync(err_of(l), &w, 4, hipMemcpyHostToDevice, ps);
-        (void)hipStreamSynchronize(ps);
-        (void)hipStreamDestroy(ps);
-      }
-      (void)hipGetLastError();
-    }
+    // (the device error word is not written here: any HIP copy from this thread can queue
+    // behind the stalled work -- streams share the hardware queues -- and delay the exit.  With
+    // the default exit status the process ends before the stalled step's optimizer runs; in
+    // poison-only mode the step in flight may apply what the aborted collective left, and the
+    // next host poll / collective fails)
     // ncclCommAbort makes RCCL's own kernels give up, but it can block behind work queued on
     // the stream (measured: until an injected stall kernel ended): run it beside, and with an
     // exit status end the process after a bounded grace period whether or not it returned.

@@ -514,7 +514,18 @@ class MobileNetV2Executor:
 
     def _fin_fwd(self, bn: BNState, P: int, train: bool):
         if train:
+            if not self.lazy_bn:
+                self.join_stats()   # this finalize launch updates the running statistics
             bn.finalize_fwd(bn.acc_f, P)
+
+    def join_stats(self):
+        """Before the first op of a training forward that writes BatchNorm running statistics:
+        run the pending wait the step installed (``stats_wait``: the main stream joins the
+        per-step rank-0 BN-buffer broadcast, which overlaps the forward until here; in training
+        mode nothing before this point reads the running buffers).  Once per forward."""
+        w = self.__dict__.pop("stats_wait", None)
+        if w is not None:
+            w()
 
     # ------------------------------------------------------------------ forward
     def forward(self, train: bool = True):
@@ -589,7 +600,9 @@ class MobileNetV2Executor:
         if train and self.lazy_bn:
             # side outputs of every forward BN (mean / rstd / scale / shift for the backward
             # and the head, running statistics) in one launch
+            self.join_stats()
             K.bn_finalize_batch(self.fwd_fin_tab, self.fwd_fin_n, self.fwd_fin_maxc)
+        self.join_stats()   # (no statistics update at all: still joined within the forward)
         # head (+ its backward when training)
         K.head(self.bn_last.y, self.bn_last.scale, self.bn_last.shift, f.w(self.w_lin), f.w(self.b_lin),
                self.labels, B, self.Hf * self.Hf, self.C_last, self.NC, self.drop_p, self.dropout_seed,

@@ -323,15 +323,22 @@ class NativeTrainStep:
                       epoch_ctr=0, out_hw=self.S)
         if self.bn_broadcast:
             if self.comm is not None:   # native: recorded collectives, no Python at replay
-                # P2P broadcast (one barrier, all links) when validated, else RCCL
+                # P2P broadcast (one barrier, all links) when validated, else RCCL.  Issued on the
+                # comm stream after the previous step (which wrote the running statistics) and
+                # joined only where this forward first updates them (exe.join_stats: the batched
+                # forward finalize in lazy mode): training-mode BN normalises with batch
+                # statistics, so the broadcast overlaps the forward instead of delaying its head.
                 algo = "oneshot" if self.comm.has_p2p else "rccl"
                 cur = torch.cuda.current_stream(self.device)
                 self.comm.broadcast(self.bn_flat, 0, algo, wait=[cur])
                 self.comm.broadcast(self.bn_nbt.view(torch.float32), 0, algo, wait=[cur])
-                self.comm.join(cur)
+                exe.stats_wait = lambda cur=cur: self.comm.join(cur)
             else:
                 K.plan_py(lambda: broadcast_parameters([self.bn_flat, self.bn_nbt]))
-        exe.forward(train=True)
+        try:
+            exe.forward(train=True)
+        finally:
+            exe.__dict__.pop("stats_wait", None)
 
     def _prefetch_next(self):
         """Render the next batch into the other buffer on the side stream: after this step's
@@ -383,10 +390,10 @@ class NativeTrainStep:
             K.plan_py(self.reducer.finish)
         for a, b in self.fault_zero:
             K.memset(self.flat.grad[a:b])
-        # a failed P2P collective, a poisoned communicator (comm_poison) or an RCCL collective the
-        # watchdog aborted leaves the device error word set: Adam then skips the update, so no
-        # replica applies un-reduced gradients (the job fails at the next check).  An RCCL
-        # asynchronous error is only seen by the host poll (comm_error), one step later.
+        # a failed P2P collective or a poisoned communicator (comm_poison) leaves the device error
+        # word set: Adam then skips the update, so no replica applies un-reduced gradients (the
+        # job fails at the next check).  An RCCL stall ends the process (the collective watchdog's
+        # default exit status); an RCCL asynchronous error is only seen by the host poll.
         K.adam_flat(self.flat.master, self.flat.grad, self.flat.exp_avg, self.flat.exp_avg_sq,
                     self.flat.shadow, self.hyper, self.betas[0], self.betas[1], self.eps, self.wd,
                     1.0 / self.world, skip=self.comm.error_word if self.comm is not None else 0,

@@ -405,7 +405,16 @@ class ResNet50Executor:
 
     def _fin(self, bn: AtomicBNState, P: int, train: bool):
         if train:
+            if bn.lz_f is None:
+                self.join_stats()   # this finalize launch updates the running statistics
             bn.finalize_fwd(bn.acc_f, P)
+
+    def join_stats(self):
+        """Main stream joins the per-step BN-buffer broadcast before the first running-statistics
+        update of a training forward (MobileNetV2Executor.join_stats)."""
+        w = self.__dict__.pop("stats_wait", None)
+        if w is not None:
+            w()
 
     def _conv(self, c: ConvSpec, pro, x, y, train, bn_out: BNState, bn_in: Optional[BNState] = None):
         B = self.B
@@ -465,7 +474,9 @@ class ResNet50Executor:
                 K.res_out(bp.bn3.y, bp.bn3.scale, bp.bn3.shift, bp.x_in, bp.out, lz=L(bp.bn3),
                           mask=bp.out_mask if train else None)
         if train and self.fwd_lazy:   # side outputs of the lazily consumed BNs, one launch
+            self.join_stats()
             K.bn_finalize_batch(self.fwd_fin_tab, len(self.fwd_lazy), self.fwd_fin_maxc)
+        self.join_stats()
         # head
         HW = self.Hf * self.Hf
         K.avgpool(self.blocks[-1].out, self.pooled, B, HW, self.C_last)

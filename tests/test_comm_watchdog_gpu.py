@@ -146,8 +146,7 @@ def test_adam_skips_while_the_error_word_is_set():
 def test_poison_only_watchdog_then_error_and_close():
     """exit_status=0 (poison + abort only): after the stall fires the communicator's
     RCCL handle is gone, so comm_error and close() must neither use the aborted communicator
-    nor wait for the stalled comm stream; the stalled training step's Adam update is skipped
-    (the watchdog also poisons the device error word)."""
+    nor wait for the stalled comm stream."""
     r, dt = _run("""
         import sys, time, torch
         sys.path.insert(0, '.')
@@ -165,14 +164,12 @@ def test_poison_only_watchdog_then_error_and_close():
             st.run(torch.arange(16, device=dev))
         torch.cuda.synchronize()
         assert st.comm.error() == 0
-        before = st.flat.master.clone()
         st.comm.inject_stall(4.0)
         st.run(torch.arange(16, device=dev))
         torch.cuda.synchronize()   # the stall kernel ends; the aborted collective does not hang
         err = st.comm.error()
         assert err != 0, err
         assert st.comm.rccl_ranks() == 0, 'the aborted RCCL handle must be dropped'
-        assert torch.equal(before, st.flat.master), 'the stalled step must not update the weights'
         print('error', hex(err), st.comm.error_string()[:60], flush=True)
         t0 = time.time()
         st.comm.close()
