@@ -74,7 +74,8 @@ int pw_bwd_num_partials(int, int, int);
 long long pw_bwd_wgrad_workspace_floats(int, int, int);
 void launch_pw_bwd(int, const bf16_t *, const bf16_t *, const float *, const float *, const float *,
                    const bf16_t *, bf16_t *, const bf16_t *, const float *, const float *, const bf16_t *,
-                   const bf16_t *, float *, float *, float *, int, int, int, hipStream_t);
+                   const bf16_t *, const bf16_t *, float *, float *, float *, int, int, int, hipStream_t);
+bool pw_bwd_recompute_supported(int, int, int);
 void launch_wt_transpose(const bf16_t *, bf16_t *, const int *, int, hipStream_t);
 void launch_pw_gemm_f8(int, const bf16_t *, const float *, const float *, const uint8_t *, int, const float *,
                        float, bf16_t *, float *, int, int, int, hipStream_t);
@@ -299,13 +300,14 @@ PYBIND11_MODULE(_pgdist_C, m) {
   m.def("pw_bwd_supported", &pw_bwd_supported);
   m.def("pw_bwd_num_partials", &pw_bwd_num_partials);
   m.def("pw_bwd_wgrad_workspace_floats", &pw_bwd_wgrad_workspace_floats);
-  m.def("pw_bwd", [](int epi, P G, P Y, P ca, P cb, P cc, P WT, P out, P Yt, P es, P et, P R, P X,
+  m.def("pw_bwd_recompute_supported", &pw_bwd_recompute_supported);
+  m.def("pw_bwd", [](int epi, P G, P Y, P ca, P cb, P cc, P WT, P out, P Yt, P es, P et, P R, P X, P We,
                      P part, P wpart, P grad, int M, int Kg, int Ng, P s) {
     pgdist_rt::run_op([=] {
       launch_pw_bwd(epi, ptr<bf16_t>(G), ptr<bf16_t>(Y), ptr<float>(ca), ptr<float>(cb), ptr<float>(cc),
                     ptr<bf16_t>(WT), ptr<bf16_t>(out), ptr<bf16_t>(Yt), ptr<float>(es), ptr<float>(et),
-                    ptr<bf16_t>(R), ptr<bf16_t>(X), ptr<float>(part), ptr<float>(wpart), ptr<float>(grad),
-                    M, Kg, Ng, S(s));
+                    ptr<bf16_t>(R), ptr<bf16_t>(X), ptr<bf16_t>(We), ptr<float>(part), ptr<float>(wpart),
+                    ptr<float>(grad), M, Kg, Ng, S(s));
     });
   });
   m.def("wgrad_reduce_defer", [](bool on) { pgdist_rt::run_op([=] { wgrad_reduce_defer(on); }); },

@@ -25,6 +25,11 @@
 //   * wgrad:  dW[kg][ng] += sum_m dyT[kg][m] xT[ng][m], accumulated in registers
 //     across the workgroup's tiles and written once as a split-M partial
 //     [gridDim.x][Kg][Ng] (deterministic fixed-order reduction afterwards).
+//   * RECOMP (expand convs, EPI_BWD_LIN with Ng <= 32): the BN input Y = X We^T of this conv is
+//     NOT read from HBM but re-formed from the X tile already staged for the wgrad: one
+//     16x16x32 MFMA per 16 x 16 piece of Y (K = Cin = 16..32, zero-padded), written as bf16
+//     into the dy image and transformed there in place.  Y is the block's hidden tensor h1
+//     (6x the input's channels): 308 of the 770 MB the 112x112 expand backward read.
 #include "../bnfin.h"
 
 #include <cstdlib>
@@ -68,6 +73,7 @@ struct PwBwdArgs {
   const float *es, *et;         // [Ng] producer BN scale / shift (RELU6 mode)
   const bf16_t *R;              // [M][Ng] residual gradient (LIN mode, optional)
   const bf16_t *X;              // [M][Ng] conv input (LIN mode)
+  const bf16_t *We;             // [Kg][Ng] forward conv weight (RECOMP: Y = X We^T, Y unused)
   float *part;                  // [gx][2][Ng]
   float *wpart;                 // [gx][Kg][Ng]
   int M, Kg, Ng;
@@ -79,11 +85,12 @@ struct PwBwdArgs {
 // ReLU6(BN) of the wgrad operand is applied after the transposed read and the epilogue takes
 // its mask operand from xN, so no register copy of the tile's Yt is kept (those registers
 // spilled at Ng = 144 / 192); the C tile then gets its own LDS region
-template <int KP, int BN, int BM, bool RAWX = false>
+template <int KP, int BN, int BM, bool RAWX = false, bool RECOMP = false>
 struct BwdLds {
-  static constexpr int LDA = KP + 8, LDX = BN + 8, LDC = BN + 8;
+  static constexpr int LDA = KP + 8, LDX = BN + 8, LDC = BN + 8, LDW = BN + 8;
   static constexpr int WT = 0;                              // [BN][LDA] W^T tile (resident)
-  static constexpr int STG = WT + BN * LDA * 2;             // per-tile staging:
+  static constexpr int WE = WT + BN * LDA * 2;              // [KP][LDW] W tile (RECOMP, resident)
+  static constexpr int STG = WE + (RECOMP ? KP * LDW * 2 : 0);   // per-tile staging:
   static constexpr int DYN = STG;                           //   dyN [BM][LDA]
   static constexpr int XN = DYN + BM * LDA * 2;             //   xN  [BM][LDX]
   static constexpr int STG_END = XN + BM * LDX * 2;
@@ -99,11 +106,12 @@ struct BwdLds {
 
 // BM = 64 rows per tile (4 waves x 16 rows for the dgrad MFMA) or 32 (2 row groups x
 // 2 column halves; used when KP is large so the prefetched tile fits in registers)
-template <int EPI, int KP, int BN, int BM>
+template <int EPI, int KP, int BN, int BM, bool RECOMP = false>
 // 2 waves per SIMD for the register allocation (3 would spill 12-328 B per variant)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void pw_bwd_fused_kernel(PwBwdArgs p) {
   constexpr bool RAWX = EPI != EPI_BWD_LIN_ && BN >= 96;
-  using L = BwdLds<KP, BN, BM, RAWX>;
+  static_assert(!RECOMP || (EPI == EPI_BWD_LIN_ && BN == 32), "Y recompute: expand convs with Cin <= 32");
+  using L = BwdLds<KP, BN, BM, RAWX, RECOMP>;
   constexpr int LDA = L::LDA, LDX = L::LDX, LDC = L::LDC;
   constexpr int CT = BN / 16;
   constexpr int RGS = BM / 16;                   // dgrad row groups of 16
@@ -122,6 +130,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
   constexpr bool LIN = EPI == EPI_BWD_LIN_;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t *WTs = reinterpret_cast<bf16_t *>(smem + L::WT);
+  bf16_t *WEs = reinterpret_cast<bf16_t *>(smem + L::WE);
   bf16_t *dyN = reinterpret_cast<bf16_t *>(smem + L::DYN);
   bf16_t *xN = reinterpret_cast<bf16_t *>(smem + L::XN);
   bf16_t *Cs = reinterpret_cast<bf16_t *>(smem + L::CS);
@@ -140,6 +149,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
     uint4 v = make_uint4(0, 0, 0, 0);
     if (n < p.Ng && c8 < p.Kg) v = ldg16(p.WT + (size_t)n * p.Kg + c8);
     *reinterpret_cast<uint4 *>(WTs + r * LDA + c8) = v;
+  }
+  if constexpr (RECOMP) {   // W [kg][ng] (B operand of the Y recompute), zero past Kg / Ng
+    for (int i = tid; i < KP * (BN / 8); i += 256) {
+      const int r = i / (BN / 8), c8 = (i % (BN / 8)) * 8;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (r < p.Kg && c8 < p.Ng) v = ldg16(p.We + (size_t)r * p.Ng + c8);
+      *reinterpret_cast<uint4 *>(WEs + r * L::LDW + c8) = v;
+    }
   }
   for (int i = tid; i < KP; i += 256) {
     const bool ok = i < p.Kg;
@@ -189,7 +206,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
         const int row = m0 + m4 * 4 + q;
         const uint32_t off = boff(valid && it < NDY && row < p.M && c8 < p.Kg, (size_t)row * p.Kg + c8);
         gq[i][q] = bld16(rG, off);
-        yq[i][q] = bld16(rY, off);
+        if constexpr (!RECOMP) yq[i][q] = bld16(rY, off);
       }
     }
 #pragma unroll
@@ -214,7 +231,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
   for (int mt = blockIdx.x; mt < nmt; mt += gridDim.x) {
     const int m0 = mt * BM;
     __syncthreads();                 // previous tile's epilogue is done with Cs (aliases the staging)
-    // ---- stage dy and x (row-major) for this tile
+    // ---- stage dy and x (row-major) for this tile (RECOMP: x first, Y re-formed from it, then dy)
+    auto stage_dy = [&]() {
 #pragma unroll
     for (int i = 0; i < IDY; ++i) {
       const int it = tid + i * 256;
@@ -231,7 +249,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
         for (int q = 0; q < 4; ++q) {
           float g[8], y[8];
           unpack8(gq[i][q], g);
-          unpack8(yq[i][q], y);
+          if constexpr (RECOMP) unpack8(*reinterpret_cast<const uint4 *>(dyN + (m4 * 4 + q) * LDA + c8), y);
+          else unpack8(yq[i][q], y);
           const bool valid = m0 + m4 * 4 + q < p.M;
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[q][j] = valid ? bf2f(f2bf(fmaf(a[j], g[j], fmaf(b[j], y[j], c[j])))) : 0.f;
@@ -239,6 +258,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
         }
       }
     }
+    };
+    if constexpr (!RECOMP) stage_dy();
     uint4 ct[RAWX ? 1 : IX][4], cr[LIN ? IX : 1][4];   // this tile's epilogue operands (raw Yt, R)
 #pragma unroll
     for (int i = 0; i < IX; ++i) {
@@ -270,6 +291,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
 #pragma unroll
         for (int q = 0; q < 4; ++q) *reinterpret_cast<uint4 *>(xN + (m4 * 4 + q) * LDX + c8) = pack8(v[q]);
       }
+    }
+    if constexpr (RECOMP) {
+      __syncthreads();   // x staged
+      // Y[m][kg] = sum_ng X[m][ng] W[kg][ng]: one MFMA per 16 x 16 piece (K = 32 >= Cin), bf16
+      // (the value the expand forward stored) into the dy image
+      constexpr int YT = (BM / 16) * (KP / 16);
+#pragma unroll
+      for (int u = 0; u < (YT + 3) / 4; ++u) {
+        const int t = wave + 4 * u;
+        if (t < YT) {
+          const int rg = t / (KP / 16), kt = t % (KP / 16);
+          const s16x8_t xa = *reinterpret_cast<const s16x8_t *>(xN + (rg * 16 + (lane & 15)) * LDX + 8 * (lane >> 4));
+          const s16x8_t wb =
+              *reinterpret_cast<const s16x8_t *>(WEs + (kt * 16 + (lane & 15)) * L::LDW + 8 * (lane >> 4));
+          const f32x4_t yv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8_t, xa), __builtin_bit_cast(bf16x8_t, wb), f32x4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) dyN[(rg * 16 + 4 * (lane >> 4) + j) * LDA + kt * 16 + (lane & 15)] = f2bf(yv[j]);
+        }
+      }
+      __syncthreads();   // Y image complete
+      stage_dy();        // in place: each item reads and rewrites its own 4 x 8 piece
     }
     __syncthreads();
     PWB_MARK(1);
@@ -474,6 +517,13 @@ BwdGeom bwd_geom(int M, int Kg, int Ng) {
 
 template <int EPI, int KP, int BN, int BM>
 void launch_bwd_t(const PwBwdArgs &a, const BwdGeom &g, hipStream_t st) {
+  if constexpr (EPI == EPI_BWD_LIN_ && BN == 32) {
+    if (a.We) {   // Y re-formed from the staged X tile
+      hipLaunchKernelGGL((pw_bwd_fused_kernel<EPI, KP, BN, BM, true>), dim3(g.gx, g.nt), dim3(256),
+                         (BwdLds<KP, BN, BM, false, true>::BYTES), st, a);
+      return;
+    }
+  }
   hipLaunchKernelGGL((pw_bwd_fused_kernel<EPI, KP, BN, BM>), dim3(g.gx, g.nt), dim3(256),
                      (BwdLds<KP, BN, BM, EPI != EPI_BWD_LIN_ && BN >= 96>::BYTES), st, a);
 }
@@ -494,6 +544,11 @@ void launch_bwd_epi(const PwBwdArgs &a, const BwdGeom &g, hipStream_t st) {
 }  // namespace
 
 bool pw_bwd_supported(int M, int Kg, int Ng) { return bwd_geom(M, Kg, Ng).ok; }
+// the expand-conv form that re-forms Y from X (pw_bwd with We): one 32-wide N tile
+bool pw_bwd_recompute_supported(int M, int Kg, int Ng) {
+  const BwdGeom g = bwd_geom(M, Kg, Ng);
+  return g.ok && g.BN == 32 && g.nt == 1;
+}
 int pw_bwd_num_partials(int M, int Kg, int Ng) { return bwd_geom(M, Kg, Ng).gx; }
 long long pw_bwd_wgrad_workspace_floats(int M, int Kg, int Ng) {
   const int S = bwd_geom(M, Kg, Ng).gx;
@@ -503,13 +558,14 @@ long long pw_bwd_wgrad_workspace_floats(int M, int Kg, int Ng) {
 // epi: 1 = EPI_BWD_RELU6 (project conv; wgrad x = relu6(Yt*es+et)), 2 = EPI_BWD_LIN (x = X)
 void launch_pw_bwd(int epi, const bf16_t *G, const bf16_t *Y, const float *ca, const float *cb,
                    const float *cc, const bf16_t *WT, bf16_t *out, const bf16_t *Yt, const float *es,
-                   const float *et, const bf16_t *R, const bf16_t *X, float *part, float *wpart,
-                   float *grad, int M, int Kg, int Ng, hipStream_t st) {
+                   const float *et, const bf16_t *R, const bf16_t *X, const bf16_t *We, float *part,
+                   float *wpart, float *grad, int M, int Kg, int Ng, hipStream_t st) {
   const BwdGeom g = bwd_geom(M, Kg, Ng);
   const BnFin *fin = take_bn_fin();
   const BnFin *lz = take_bn_lz();
   if (!g.ok) return;
-  PwBwdArgs a{G, Y, ca, cb, cc, WT, out, Yt, es, et, R, X, part, wpart, M, Kg, Ng, g_bn_rep, fin, lz};
+  if (We && !(epi == EPI_BWD_LIN_ && pw_bwd_recompute_supported(M, Kg, Ng))) return;   // (checked by the caller)
+  PwBwdArgs a{G, Y, ca, cb, cc, WT, out, Yt, es, et, R, X, We, part, wpart, M, Kg, Ng, g_bn_rep, fin, lz};
   if (epi == EPI_BWD_RELU6_) launch_bwd_epi<EPI_BWD_RELU6_>(a, g, st);
   else launch_bwd_epi<EPI_BWD_LIN_>(a, g, st);
   // grad == nullptr: the caller reduces wpart itself (e.g. on its weight-gradient stream)

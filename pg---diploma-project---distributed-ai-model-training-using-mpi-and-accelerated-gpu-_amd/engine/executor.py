@@ -184,6 +184,9 @@ class MobileNetV2Executor:
     # 7x7 stages) are materialised by their consumer (next GEMM's prologue) instead of a BN-apply launch: bs128 4.517-4.530 vs 4.540-4.581 ms/step; the 28x28 stage
     # too (784): 4.527-4.559; every block: neutral (scripts/gpu_r4_aug.sh)
     FUSE_BLOCK_OUTPUT_HW = 196
+    # expand-conv backward re-forms its BN input h1 = x We^T from the staged block input instead of
+    # reading it (pw_bwd ``We``), on the shapes that support it
+    PW_BWD_RECOMPUTE = True
     # side-stream joins batched per this many weight gradients (1 / 2 / 3 / 4 / 6: 5.28 / 5.23 /
     # 5.15 / 5.22 / 5.21 ms/step, docs/PERF_NOTES.md round 2)
     SIDE_BATCH = 3
@@ -713,9 +716,14 @@ class MobileNetV2Executor:
                 # expand dgrad -> gradient w.r.t. the block input o_prev (+ skip gradient)
                 if self._pw_bwd_ok(Min, bp.hidden, bp.cin):
                     wpe = self._wpart[(bp.idx, "e")]
-                    K.pw_bwd(K.EPI_BWD_LIN, bne.g, bne.y, bne.a, bne.b, bne.c, f.bt(bp.w_e), prev.G, prev.bn_p.y,
-                             prev.bn_p.acc_b, wpe, None, Min, bp.hidden, bp.cin, R=bp.G if bp.residual else None,
-                             X=prev.o, fin=prev.bn_p.fin_b, lz=bne.lz_b)
+                    # (h1 = BN_e's input is re-formed from the staged block input where the kernel can:
+                    # Cin <= 32, i.e. the 112x112 / 56x56 / 28x28 blocks)
+                    rc = (self.PW_BWD_RECOMPUTE and not self._fp8_layer(bp.cin)   # (bf16 forward GEMM)
+                          and K.pw_bwd_recompute_supported(Min, bp.hidden, bp.cin))
+                    K.pw_bwd(K.EPI_BWD_LIN, bne.g, None if rc else bne.y, bne.a, bne.b, bne.c, f.bt(bp.w_e), prev.G,
+                             prev.bn_p.y, prev.bn_p.acc_b, wpe, None, Min, bp.hidden, bp.cin,
+                             R=bp.G if bp.residual else None, X=prev.o, fin=prev.bn_p.fin_b, lz=bne.lz_b,
+                             We=f.b(bp.w_e) if rc else None)
                     Pe = K.pw_bwd_num_partials(Min, bp.hidden, bp.cin)
 
                     def exp_wgrad(ws, Pe=Pe, wpe=wpe, bp=bp):   # deferred: bind this layer's values

@@ -470,8 +470,13 @@ def pw_bwd_wgrad_workspace(M, Kg, Ng):
     return lib().pw_bwd_wgrad_workspace_floats(M, Kg, Ng)
 
 
+def pw_bwd_recompute_supported(M, Kg, Ng):
+    """True when pw_bwd can re-form Y = X We^T instead of reading it (expand convs, Cin <= 32)."""
+    return bool(lib().pw_bwd_recompute_supported(M, Kg, Ng))
+
+
 def pw_bwd(epi, G, Y, ca, cb, cc, WT, out, Yt, part, wpart, grad, M, Kg, Ng, es=None, et=None, R=None,
-           X=None, fin=None, lz=None):
+           X=None, fin=None, lz=None, We=None):
     """Fused 1x1-conv backward (one read of G, Y):
 
     dy = ca*G + cb*Y + cc                      [M, Kg]   (this conv's BN backward)
@@ -479,11 +484,22 @@ def pw_bwd(epi, G, Y, ca, cb, cc, WT, out, Yt, part, wpart, grad, M, Kg, Ng, es=
       EPI_BWD_RELU6: out *= 1[0 < Yt*es+et < 6];  EPI_BWD_LIN: out += R
     grad[Kg, Ng] = dy^T @ x,  x = relu6(Yt*es+et) (RELU6) or X (LIN)
     part <- BN partials (sum out, sum out*Yt) per workgroup.
+    ``We`` (EPI_BWD_LIN only; the forward weight [Kg, Ng]): Y is not read but re-formed as
+    bf16(X @ We^T) from the X tile the wgrad stages anyway (``Y`` may then be None).
     """
     if not pw_bwd_supported(M, Kg, Ng):
         raise ValueError(f"pw_bwd: unsupported shape M={M} Kg={Kg} Ng={Ng}")
     _chk(G, BF16, M * Kg, "G")
-    _chk(Y, BF16, M * Kg, "Y")
+    if We is not None:
+        if epi != EPI_BWD_LIN or not pw_bwd_recompute_supported(M, Kg, Ng):
+            raise ValueError(f"pw_bwd: no Y-recompute form for epi={epi} M={M} Kg={Kg} Ng={Ng}")
+        _chk(We, BF16, Kg * Ng, "We")
+        if Y is not None:
+            _chk(Y, BF16, M * Kg, "Y")
+    else:
+        if Y is None:
+            raise ValueError("pw_bwd: Y (or We for the recompute form) is required")
+        _chk(Y, BF16, M * Kg, "Y")
     _chk(WT, BF16, Ng * Kg, "WT")
     _chk(out, BF16, M * Ng, "out")
     _chk(Yt, BF16, M * Ng, "Yt")
@@ -503,7 +519,7 @@ def pw_bwd(epi, G, Y, ca, cb, cc, WT, out, Yt, part, wpart, grad, M, Kg, Ng, es=
     _arm(fin)
     _arm_lz(lz)
     lib().pw_bwd(int(epi), _p(G), _p(Y), _p(ca), _p(cb), _p(cc), _p(WT), _p(out), _p(Yt), _p(es), _p(et),
-                 _p(R), _p(X), _p(part), _p(wpart), _p(grad), M, Kg, Ng, _s())
+                 _p(R), _p(X), _p(We), _p(part), _p(wpart), _p(grad), M, Kg, Ng, _s())
 
 
 def wgrad_reduce(part, S, n, grad):

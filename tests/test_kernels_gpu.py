@@ -502,27 +502,35 @@ PW_BWD_CASES = [(70001, 96, 16, "lin", True), (66000, 24, 144, "relu6", False), 
                 (66001, 24, 96, "relu6", False), (401408, 32, 144, "relu6", False)]
 
 
-@pytest.mark.parametrize("M,Kg,Ng,mode,res", PW_BWD_CASES)
-def test_pw_bwd_fused(dev, M, Kg, Ng, mode, res):
+@pytest.mark.parametrize("M,Kg,Ng,mode,res,recompute", [c + (False,) for c in PW_BWD_CASES] + [
+    (70001, 96, 16, "lin", True, True), (65613, 144, 24, "lin", False, True), (100352, 192, 32, "lin", True, True),
+    (401408, 144, 24, "lin", True, True)])
+def test_pw_bwd_fused(dev, M, Kg, Ng, mode, res, recompute):
+    """recompute: the expand form that re-forms Y = bf16(X W^T) from the staged X tile (no Y
+    operand); the reference is computed from that Y."""
     assert K.pw_bwd_supported(M, Kg, Ng)
     G = bf(rnd(M, Kg, dev=dev, seed=1))
-    Y = bf(rnd(M, Kg, dev=dev, seed=2))
+    W = bf(rnd(Kg, Ng, dev=dev, seed=5) / math.sqrt(Kg))        # conv weight [Cout=Kg][Cin=Ng]
+    X = bf(rnd(M, Ng, dev=dev, seed=9)) if mode == "lin" else None
+    if recompute:
+        assert K.pw_bwd_recompute_supported(M, Kg, Ng)
+        Y = bf(X.float() @ W.float().t())
+    else:
+        Y = bf(rnd(M, Kg, dev=dev, seed=2))
     coef = torch.stack([torch.rand(Kg, device=dev) + 0.5, torch.rand(Kg, device=dev) - 0.5,
                         torch.rand(Kg, device=dev) - 0.5]).contiguous()
-    W = bf(rnd(Kg, Ng, dev=dev, seed=5) / math.sqrt(Kg))        # conv weight [Cout=Kg][Cin=Ng]
     WT = W.t().contiguous()
     Yt = bf(rnd(M, Ng, dev=dev, seed=6))
     es, et = bn_params(Ng, dev, 7)
     R = bf(rnd(M, Ng, dev=dev, seed=8)) if res else None
-    X = bf(rnd(M, Ng, dev=dev, seed=9)) if mode == "lin" else None
     out = torch.empty(M, Ng, dtype=torch.bfloat16, device=dev)
     P = K.pw_bwd_num_partials(M, Kg, Ng)
     part = torch.zeros(P * 2 * Ng, device=dev)
     wpart = torch.zeros(K.pw_bwd_wgrad_workspace(M, Kg, Ng), device=dev)
     grad = torch.empty(Kg * Ng, device=dev)
     epi = K.EPI_BWD_RELU6 if mode == "relu6" else K.EPI_BWD_LIN
-    K.pw_bwd(epi, G, Y, coef[0], coef[1], coef[2], WT, out, Yt, part, wpart, grad, M, Kg, Ng,
-             es=es, et=et, R=R, X=X)
+    K.pw_bwd(epi, G, None if recompute else Y, coef[0], coef[1], coef[2], WT, out, Yt, part, wpart, grad, M, Kg,
+             Ng, es=es, et=et, R=R, X=X, We=W if recompute else None)
     dy = bf(coef[0] * G.float() + coef[1] * Y.float() + coef[2]).float()
     ref = dy @ W.float()
     if mode == "relu6":
