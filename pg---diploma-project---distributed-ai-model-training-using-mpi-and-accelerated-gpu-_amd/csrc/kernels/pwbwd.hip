@@ -488,7 +488,7 @@ struct BwdGeom {
   int KP, BN, BM, nt, gx;
   bool ok;
 };
-BwdGeom bwd_geom(int M, int Kg, int Ng) {
+BwdGeom bwd_geom(int M, int Kg, int Ng, bool recomp = false) {
   BwdGeom g{};
   g.KP = (Kg + 31) / 32 * 32;
   // one N tile covering all of Ng where it is small enough (no re-read of G, Y per tile)
@@ -504,6 +504,9 @@ BwdGeom bwd_geom(int M, int Kg, int Ng) {
   // (G, Y) tile stays within 2 waves/SIMD of registers
   const int chunks = (g.KP > g.BN ? g.KP : g.BN) / 8;
   g.BM = g.KP >= 160 ? 32 : (chunks <= 4 ? 256 : (chunks <= 8 ? 128 : 64));
+  // the Y-recompute form loads no Y tile: twice the rows per tile keep the bytes in flight per
+  // workgroup (the loop is bound by one tile's load latency, not by its bytes)
+  if (recomp && g.BN == 32 && g.BM <= 64) g.BM *= 2;
   g.ok = M >= 65536 && g.KP <= 192 && Kg % 8 == 0 && Ng % 8 == 0 && Kg > 0 && Ng > 0;
   g.nt = (Ng + g.BN - 1) / g.BN;
   const int nmt = (M + g.BM - 1) / g.BM;
@@ -536,6 +539,9 @@ void launch_bwd_epi(const PwBwdArgs &a, const BwdGeom &g, hipStream_t st) {
   BWD_CASE(32, 48, 128) BWD_CASE(64, 48, 128) BWD_CASE(96, 48, 64) BWD_CASE(128, 48, 64)
   BWD_CASE(32, 64, 128) BWD_CASE(64, 64, 128) BWD_CASE(96, 64, 64) BWD_CASE(128, 64, 64)
   BWD_CASE(160, 32, 32) BWD_CASE(192, 32, 32) BWD_CASE(160, 64, 32) BWD_CASE(192, 64, 32)
+  if constexpr (EPI == EPI_BWD_LIN_) {   // Y-recompute geometries (twice the rows)
+    BWD_CASE(96, 32, 128) BWD_CASE(160, 32, 64) BWD_CASE(192, 32, 64)
+  }
   if constexpr (EPI != EPI_BWD_LIN_) {   // wide project tiles (RAWX): the project convs only
     BWD_CASE(32, 96, 64) BWD_CASE(32, 144, 64) BWD_CASE(32, 192, 64)
   }
@@ -560,7 +566,7 @@ void launch_pw_bwd(int epi, const bf16_t *G, const bf16_t *Y, const float *ca, c
                    const float *cc, const bf16_t *WT, bf16_t *out, const bf16_t *Yt, const float *es,
                    const float *et, const bf16_t *R, const bf16_t *X, const bf16_t *We, float *part,
                    float *wpart, float *grad, int M, int Kg, int Ng, hipStream_t st) {
-  const BwdGeom g = bwd_geom(M, Kg, Ng);
+  const BwdGeom g = bwd_geom(M, Kg, Ng, We != nullptr);
   const BnFin *fin = take_bn_fin();
   const BnFin *lz = take_bn_lz();
   if (!g.ok) return;
