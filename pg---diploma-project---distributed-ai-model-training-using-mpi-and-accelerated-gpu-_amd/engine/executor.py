@@ -562,20 +562,22 @@ class MobileNetV2Executor:
         for bp in self.blocks:
             Hin = bp.H
             Min = B * Hin * Hin
-            dwx_in = None
+            dwx_in = x_in = None
             if bp.expand:
                 if pend is not None:
                     self._consume_output(pend, f.b(bp.w_e), bp.bn_e.y, bp.bn_e.acc_f, Min, bp.hidden, bp.cin,
                                          fin=F(bp.bn_e), lz=L(pend[0]))
+                    x_in = pend[2]   # (materialised by that GEMM)
                 elif inp_t is None:
                     self._pw_fwd(K.ACT_BN_RELU6, inp_bn.y, bp.w_e, bp.bn_e.y, bp.bn_e.acc_f, Min, bp.hidden, bp.cin,
                                  pa=inp_bn.scale, pb=inp_bn.shift, fin=F(bp.bn_e), lz=L(inp_bn))
                 else:
                     self._pw_fwd(K.ACT_NONE, inp_t, bp.w_e, bp.bn_e.y, bp.bn_e.acc_f, Min, bp.hidden, bp.cin,
                                  fin=F(bp.bn_e))
-                    if (self.DWX_FWD and not self._fp8_layer(bp.cin)
-                            and K.dwx_fwd_supported(B, Hin, Hin, bp.hidden, bp.cin, bp.stride)):
-                        dwx_in = inp_t
+                    x_in = inp_t
+                if (x_in is not None and self.DWX_FWD and not self._fp8_layer(bp.cin)
+                        and K.dwx_fwd_supported(B, Hin, Hin, bp.hidden, bp.cin, bp.stride)):
+                    dwx_in = x_in
                 self._fin_fwd(bp.bn_e, K.pw_num_partials(Min, bp.hidden, bp.cin), train)
                 dw_in = bp.bn_e
             else:
