@@ -57,9 +57,6 @@ void conv_set_glds(int mode);
 int conv_get_glds();
 int dw_dgrad_num_partials(int, int, int, int, int);
 int dw_wgrad_num_partials(int, int, int, int, int);
-bool dwx_fwd_supported(int, int, int, int, int, int);
-void launch_dwx_fwd(const bf16_t *, int, const bf16_t *, const float *, const float *, const bf16_t *, bf16_t *,
-                    float *, int, int, int, int, int, hipStream_t);
 void launch_dw_fwd(const bf16_t *, const float *, const float *, int, const bf16_t *, bf16_t *,
                    float *, int, int, int, int, int, hipStream_t);
 void launch_dw_dgrad(const bf16_t *, const bf16_t *, const float *, const bf16_t *, const bf16_t *,
@@ -243,14 +240,6 @@ PYBIND11_MODULE(_pgdist_C, m) {
   m.def("bn_set_rep", &bn_set_rep, "set the replica rows (large = one row per workgroup: deterministic)");
   m.def("dw_dgrad_num_partials", &dw_dgrad_num_partials);
   m.def("dw_wgrad_num_partials", &dw_wgrad_num_partials);
-  m.def("dwx_fwd_supported", &dwx_fwd_supported);
-  m.def("dwx_fwd", [](P x, int cin, P we, P is, P it, P w, P y, P part, int B, int H, int W, int C, int stride,
-                      P s) {
-    pgdist_rt::run_op([=] {
-      launch_dwx_fwd(ptr<bf16_t>(x), cin, ptr<bf16_t>(we), ptr<float>(is), ptr<float>(it), ptr<bf16_t>(w),
-                     ptr<bf16_t>(y), ptr<float>(part), B, H, W, C, stride, S(s));
-    });
-  });
   m.def("dw_fwd", [](P x, P is, P it, int act, P w, P y, P part, int B, int H, int W, int C,
                      int stride, P s) {
     pgdist_rt::run_op([=] {

@@ -381,209 +381,6 @@ __global__ __launch_bounds__(256) void dw_fwd_lds_kernel(
   bn_fin_tail(g.fin);
 }
 
-// ---------------------------------------------------------------------------
-// Forward with the expand conv re-formed in the kernel (MobileNetV2 expand blocks whose input
-// has Cin <= 32 channels: the 112x112 / 56x56 / 28x28 blocks).  The depthwise input h1 = x We^T
-// (the block's hidden tensor, 3-6x the bytes of x) is NOT read from HBM: the ring streams rows
-// of the block input x (Cin channels, zero-padded to 32 in LDS), and one step ahead of the
-// depthwise row loop the workgroup forms that row's activation relu6(BN_e(bf16(x We^T))) for
-// its channel slab with 16x16x32 MFMAs (A = the W_e slab [channel][cin] staged once in LDS,
-// B = the x row [cin][pixel]; the transposed product gives each lane 4 consecutive channels of
-// one pixel, stored as one 8-B LDS write), so the BN + ReLU6 of the input is applied once per
-// element instead of once per tap read, and the tap reads come straight from the activation row.
-// Per step (one input row): 1 x-row DMA, <= 4 MFMAs per wave, 1 barrier, 1 store -- the same
-// ring discipline as dw_fwd_lds_kernel (counted vmcnt, no drains), one row deeper.
-// Same geometry (dw_geom kind 0) and statistics partials as the plain forward.
-// ---------------------------------------------------------------------------
-namespace {
-constexpr int kSlotX = 3072;            // x row segment: <= 48 columns x 32 channels x 2 B
-constexpr int kDwxMaxCC = 96;           // channel slab (<= 6 MFMA row tiles of 16)
-constexpr int kSlotAct = 7680;          // activation row: ncol x CC bf16 (<= 48 x 80, 21 x 96, ...)
-
-// One x row segment: ncol columns x 4 chunks of 8 channels (chunk t = col * 4 + part at byte
-// 16 t: the 64-B padded pixel rows the MFMA B operand reads); parts >= Cin/8 are out of range.
-struct XStream {
-  u32x4_t srd;
-  int H, W, cin, b, col0, lane_col, lane_part;
-  bool wave_used;
-  PG_DEVICE void init(const bf16_t *x, int B, int H_, int W_, int cin_, int b_, int col0_, int ncol) {
-    srd = make_srd(x, (uint32_t)B * H_ * W_ * cin_ * 2);
-    H = H_, W = W_, cin = cin_, b = b_, col0 = col0_;
-    const int t = threadIdx.x, nchunk = ncol * 4;
-    lane_col = t < nchunk ? t >> 2 : -1;
-    lane_part = t & 3;
-    wave_used = (t & ~63) < nchunk;
-  }
-  PG_DEVICE void issue(char *ring, int slot, int ih, char *dummy) const {
-    const int iw = col0 + lane_col;
-    const bool ok = wave_used && lane_col >= 0 && lane_part * 8 < cin && ih >= 0 && ih < H && iw >= 0 && iw < W;
-    const uint32_t off = ok ? (uint32_t)((((b * H + ih) * W + iw) * cin + lane_part * 8) * 2) : kOOB;
-    char *dst = wave_used ? ring + slot * kSlotX + (threadIdx.x & ~63) * 16 : dummy;
-    lds_dma16(srd, dst, off);
-  }
-};
-}  // namespace
-
-template <int S, int D = kDepth>
-__global__ __launch_bounds__(256) void dwx_fwd_kernel(
-    const bf16_t *__restrict__ x, const bf16_t *__restrict__ we, const float *__restrict__ in_s,
-    const float *__restrict__ in_t, const bf16_t *__restrict__ w, bf16_t *__restrict__ y,
-    float *__restrict__ part, DwGeom g, int cin) {
-  constexpr int kRing = D + 1;
-  constexpr int U = S == 1 ? 3 : 4;                 // window period in input rows
-  // x ring (the statistics reduction reuses it after the loop), two activation rows, W_e slab
-  __shared__ __attribute__((aligned(16))) char ring[kRing * kSlotX + 1024];
-  __shared__ __attribute__((aligned(16))) char actr[2 * kSlotAct];
-  __shared__ __attribute__((aligned(16))) bf16_t wes[kDwxMaxCC * 32];
-  char *dummy = ring + kRing * kSlotX;
-  float *red = reinterpret_cast<float *>(ring);
-  const int C4 = g.CC / CPT;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int c4 = tid % C4, col = tid / C4;
-  const Tile tl = tile_of(g);
-  const int cbase = tl.slab * g.CC;
-  const int c0 = cbase + c4 * CPT;
-  const int ow = tl.w0 + col;
-  const bool active = col < g.TWc && ow < g.Wo;
-  const int lcol = active ? col * S : 0;
-  const rsrc_t ry = make_rsrc(y, (uint32_t)g.B * g.Ho * g.Wo * g.C * 2);
-  const int oh_end = min(tl.r0 + g.R, g.Ho);
-  const int j0 = tl.r0 * S - 1;
-  const int nrows = (oh_end - 1) * S + 1 - j0 + 1;
-  const int iw0 = ow * S - 1;
-  const int ncol = (g.TWc - 1) * S + 3;             // x / activation columns of the segment
-  const int npg = (ncol + 15) >> 4, nct = (g.CC + 15) >> 4, ntile = npg * nct;
-  bool cok[3];
-#pragma unroll
-  for (int d = 0; d < 3; ++d) cok[d] = active && iw0 + d >= 0 && iw0 + d < g.W;
-  XStream sx;
-  sx.init(x, g.B, g.H, g.W, cin, tl.b, tl.w0 * S - 1, ncol);
-#pragma unroll
-  for (int q = 0; q < D; ++q) sx.issue(ring, q, j0 + q, dummy);
-  // W_e slab [CC][32] (zero past Cin / past the slab), BN_e scale / shift, depthwise weights
-  for (int i = tid; i < nct * 16 * 4; i += 256) {
-    const int r = i >> 2, p8 = (i & 3) * 8;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (r < g.CC && p8 < cin) v = ldg16(we + (size_t)(cbase + r) * cin + p8);
-    *reinterpret_cast<uint4 *>(wes + r * 32 + p8) = v;
-  }
-  float stats[2][CPT], wt[9][CPT];
-  uint2 wraw[9];
-#pragma unroll
-  for (int q = 0; q < 9; ++q) wraw[q] = ldg8(w + (size_t)q * g.C + c0);
-  if (g.lz != nullptr) {
-    lazy_stage(g, cbase, 2);
-  } else if (tid < g.CC) {
-    lzp[0][tid] = in_s[cbase + tid];
-    lzp[1][tid] = in_t[cbase + tid];
-  }
-#pragma unroll
-  for (int k = 0; k < CPT; ++k) stats[0][k] = stats[1][k] = 0.f;
-#pragma unroll
-  for (int q = 0; q < 9; ++q) unpack4(wraw[q], wt[q]);
-  params_landed();   // parameters and the first D x rows have landed
-  __syncthreads();
-  // activation row of input row j0 + r (x ring slot r % kRing) into activation slot r & 1
-  auto expand = [&](int r) {
-    const char *xs = ring + (r % kRing) * kSlotX;
-    char *as = actr + (r & 1) * kSlotAct;
-    for (int u = wave; u < ntile; u += 4) {
-      const int pg = u / nct, ct = u - pg * nct;
-      const s16x8_t a = *reinterpret_cast<const s16x8_t *>(wes + (ct * 16 + (lane & 15)) * 32 + 8 * (lane >> 4));
-      const s16x8_t bx = *reinterpret_cast<const s16x8_t *>(xs + (pg * 16 + (lane & 15)) * 64 + 16 * (lane >> 4));
-      const f32x4_t h = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a),
-                                                                __builtin_bit_cast(bf16x8_t, bx),
-                                                                f32x4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-      const int ch = ct * 16 + 4 * (lane >> 4), px = pg * 16 + (lane & 15);
-      const float4 sc = *reinterpret_cast<const float4 *>(&lzp[0][ch]);
-      const float4 sh = *reinterpret_cast<const float4 *>(&lzp[1][ch]);
-      float v[CPT];
-      // h1 as the expand forward stores it (bf16), then BN_e + ReLU6
-      v[0] = relu6f(fmaf(bf2f(f2bf(h[0])), sc.x, sh.x));
-      v[1] = relu6f(fmaf(bf2f(f2bf(h[1])), sc.y, sh.y));
-      v[2] = relu6f(fmaf(bf2f(f2bf(h[2])), sc.z, sh.z));
-      v[3] = relu6f(fmaf(bf2f(f2bf(h[3])), sc.w, sh.w));
-      if (px < ncol && ch < g.CC) *reinterpret_cast<uint2 *>(as + (px * g.CC + ch) * 2) = pack4(v);
-    }
-  };
-  expand(0);
-  float win[3][3][CPT];
-#pragma unroll
-  for (int r = 0; r < 3; ++r)
-#pragma unroll
-    for (int d = 0; d < 3; ++d) zero4(win[r][d]);
-  int ihl = j0 % g.Hi;
-  if (ihl < 0) ihl += g.Hi;
-  auto step = [&](int k, int into, bool emit, int ra, int rb, int rc) {
-    // x row k+1 has landed (D-2 DMAs issued after it), activation row k (formed by the previous
-    // step) is visible, and every read of the slots refilled below is done
-    ring_sync<D - 2>();
-    sx.issue(ring, (k + D) % kRing, j0 + k + D, dummy);
-    mem_fence_compiler();
-    expand(k + 1);
-    const char *sl = actr + (k & 1) * kSlotAct;
-    const int ih = j0 + k;
-    const bool rok = ih >= 0 && ih < g.H;
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-      float v[CPT];
-      unpack4(lds8(sl, lcol + d, g.CC, c4 * CPT), v);
-      const float m = (rok && cok[d]) ? 1.f : 0.f;
-#pragma unroll
-      for (int kk = 0; kk < CPT; ++kk) {
-        const float a = m * v[kk];
-        if (into == 0) win[0][d][kk] = a;
-        if (into == 1) win[1][d][kk] = a;
-        if (into == 2) win[2][d][kk] = a;
-      }
-    }
-    const int oh = S == 1 ? ih - 1 : (ih - 1) >> 1;
-    float m0 = 1.f, m2 = 1.f;
-    if constexpr (S == 1) {
-      const int ohl = ihl == 0 ? g.Hi - 1 : ihl - 1;
-      m0 = ohl != 0 ? 1.f : 0.f;
-      m2 = ohl != g.Hi - 1 ? 1.f : 0.f;
-      ihl = ihl + 1 == g.Hi ? 0 : ihl + 1;
-    }
-    float ar[3][CPT];
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      const int wr = r == 0 ? ra : r == 1 ? rb : rc;
-      zero4(ar[r]);
-#pragma unroll
-      for (int dw = 0; dw < 3; ++dw)
-#pragma unroll
-        for (int kk = 0; kk < CPT; ++kk) ar[r][kk] = fmaf(win[wr][dw][kk], wt[r * 3 + dw][kk], ar[r][kk]);
-    }
-    float acc[CPT];
-#pragma unroll
-    for (int kk = 0; kk < CPT; ++kk) acc[kk] = fmaf(m2, ar[2][kk], fmaf(m0, ar[0][kk], ar[1][kk]));
-    bst8(ry, (emit && active) ? nhwc_off(tl.b, g.Ho, g.Wo, g.C, oh, ow, c0) : kOOB, pack4(acc));
-    const float e = emit ? 1.f : 0.f;
-#pragma unroll
-    for (int kk = 0; kk < CPT; ++kk) {
-      stats[0][kk] = fmaf(e, acc[kk], stats[0][kk]);
-      stats[1][kk] = fmaf(e * acc[kk], acc[kk], stats[1][kk]);
-    }
-  };
-  for (int k = 0; k < nrows; k += U) {
-    if constexpr (S == 1) {
-      step(k, 0, k >= 2, 1, 2, 0);
-      if (k + 1 < nrows) step(k + 1, 1, k + 1 >= 2, 2, 0, 1);
-      if (k + 2 < nrows) step(k + 2, 2, true, 0, 1, 2);
-    } else {
-      step(k, 0, k > 0, 2, 1, 0);
-      if (k + 1 < nrows) step(k + 1, 1, false, 0, 1, 2);
-      if (k + 2 < nrows) step(k + 2, 2, true, 0, 1, 2);
-      if (k + 3 < nrows) step(k + 3, 1, false, 0, 1, 2);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may still target the ring
-  __syncthreads();
-  block_channel_partials<2>(stats, part, g.C, g.CC, cbase, g.TWc, red, tl.idx, dw_tiles(g), g.bn_rep);
-  bn_fin_tail(g.fin);
-}
-
 // dgrad (stride 1): thread = one INPUT column, strip of input rows.  Streams per step k: the dy
 // rows (g, y of this layer's BN backward, halo columns) of dy row r0-1+k and yprev (the
 // producer's pre-BN activation, own columns: ReLU6 mask + fused weight gradient) of input row
@@ -1284,28 +1081,6 @@ int dw_tall_rows() { return g_dw_tall; }
 int dw_fwd_num_partials(int B, int H, int W, int C, int stride) { return dw_grid_x(dw_geom(0, B, H, W, C, stride)); }
 int dw_dgrad_num_partials(int B, int H, int W, int C, int stride) { return dw_grid_x(dw_geom(1, B, H, W, C, stride)); }
 int dw_wgrad_num_partials(int B, int H, int W, int C, int stride) { return dw_grid_x(dw_geom(2, B, H, W, C, stride)); }
-
-// forward with the expand conv re-formed in the kernel (dwx_fwd_kernel): x is the block input
-// [B][H][W][cin], we the expand weight [C][cin] (bf16), in_s / in_t (or the armed lazy
-// descriptor) the expand BN's scale / shift
-bool dwx_fwd_supported(int B, int H, int W, int C, int cin, int stride) {
-  if (cin < 8 || cin > 32 || cin % 8 || C % 8 || (stride != 1 && stride != 2)) return false;
-  const DwGeom g = dw_geom(0, B, H, W, C, stride);
-  const int ncol = (g.TWc - 1) * stride + 3;
-  return g.CC <= kDwxMaxCC && ncol <= 48 && ncol * g.CC * 2 <= kSlotAct;
-}
-void launch_dwx_fwd(const bf16_t *x, int cin, const bf16_t *we, const float *in_s, const float *in_t,
-                    const bf16_t *w, bf16_t *y, float *part, int B, int H, int W, int C, int stride, hipStream_t st) {
-  DwGeom g = dw_geom(0, B, H, W, C, stride);
-  g.fin = take_bn_fin();
-  g.lz = take_bn_lz();
-  if (!dwx_fwd_supported(B, H, W, C, cin, stride)) return;   // (checked by the caller)
-  const dim3 grid(dw_grid_x(g) * (C / g.CC)), block(256);
-  if (stride == 1)
-    hipLaunchKernelGGL((dwx_fwd_kernel<1, 4>), grid, block, 0, st, x, we, in_s, in_t, w, y, part, g, cin);
-  else
-    hipLaunchKernelGGL((dwx_fwd_kernel<2, 4>), grid, block, 0, st, x, we, in_s, in_t, w, y, part, g, cin);
-}
 
 void launch_dw_fwd(const bf16_t *x, const float *in_s, const float *in_t, int act, const bf16_t *w,
                    bf16_t *y, float *part, int B, int H, int W, int C, int stride, hipStream_t st) {

@@ -187,8 +187,6 @@ class MobileNetV2Executor:
     # expand-conv backward re-forms its BN input h1 = x We^T from the staged block input instead of
     # reading it (pw_bwd ``We``), on the shapes that support it
     PW_BWD_RECOMPUTE = True
-    # depthwise forward of those blocks re-forms h1 from the block input too (dwx_fwd)
-    DWX_FWD = True
     # side-stream joins batched per this many weight gradients (1 / 2 / 3 / 4 / 6: 5.28 / 5.23 /
     # 5.15 / 5.22 / 5.21 ms/step, docs/PERF_NOTES.md round 2)
     SIDE_BATCH = 3
@@ -562,34 +560,23 @@ class MobileNetV2Executor:
         for bp in self.blocks:
             Hin = bp.H
             Min = B * Hin * Hin
-            dwx_in = x_in = None
             if bp.expand:
                 if pend is not None:
                     self._consume_output(pend, f.b(bp.w_e), bp.bn_e.y, bp.bn_e.acc_f, Min, bp.hidden, bp.cin,
                                          fin=F(bp.bn_e), lz=L(pend[0]))
-                    x_in = pend[2]   # (materialised by that GEMM)
                 elif inp_t is None:
                     self._pw_fwd(K.ACT_BN_RELU6, inp_bn.y, bp.w_e, bp.bn_e.y, bp.bn_e.acc_f, Min, bp.hidden, bp.cin,
                                  pa=inp_bn.scale, pb=inp_bn.shift, fin=F(bp.bn_e), lz=L(inp_bn))
                 else:
                     self._pw_fwd(K.ACT_NONE, inp_t, bp.w_e, bp.bn_e.y, bp.bn_e.acc_f, Min, bp.hidden, bp.cin,
                                  fin=F(bp.bn_e))
-                    x_in = inp_t
-                if (x_in is not None and self.DWX_FWD and not self._fp8_layer(bp.cin)
-                        and K.dwx_fwd_supported(B, Hin, Hin, bp.hidden, bp.cin, bp.stride)):
-                    dwx_in = x_in
                 self._fin_fwd(bp.bn_e, K.pw_num_partials(Min, bp.hidden, bp.cin), train)
                 dw_in = bp.bn_e
             else:
                 assert inp_t is None and pend is None, "t=1 block expects the (virtual) stem output"
                 dw_in = inp_bn
-            if dwx_in is not None:
-                # expand blocks with a narrow input: h1 re-formed from the block input in the kernel
-                K.dwx_fwd(dwx_in, bp.cin, f.b(bp.w_e), dw_in.scale, dw_in.shift, f.b(bp.w_d), bp.bn_d.y,
-                          bp.bn_d.acc_f, B, Hin, Hin, bp.hidden, bp.stride, fin=F(bp.bn_d), lz=L(dw_in))
-            else:
-                K.dw_fwd(dw_in.y, dw_in.scale, dw_in.shift, K.ACT_BN_RELU6, f.b(bp.w_d), bp.bn_d.y, bp.bn_d.acc_f, B,
-                         Hin, Hin, bp.hidden, bp.stride, fin=F(bp.bn_d), lz=L(dw_in))
+            K.dw_fwd(dw_in.y, dw_in.scale, dw_in.shift, K.ACT_BN_RELU6, f.b(bp.w_d), bp.bn_d.y, bp.bn_d.acc_f, B, Hin, Hin,
+                     bp.hidden, bp.stride, fin=F(bp.bn_d), lz=L(dw_in))
             self._fin_fwd(bp.bn_d, K.dw_num_partials("fwd", B, Hin, Hin, bp.hidden, bp.stride), train)
             Mout = B * bp.Ho * bp.Wo
             self._pw_fwd(K.ACT_BN_RELU6, bp.bn_d.y, bp.w_p, bp.bn_p.y, bp.bn_p.acc_f, Mout, bp.cout, bp.hidden,

@@ -288,33 +288,6 @@ def dw_fwd(x, in_s, in_t, act, w, y, part, B, H, W, C, stride, fin=None, lz=None
     lib().dw_fwd(_p(x), _p(in_s), _p(in_t), int(act), _p(w), _p(y), _p(part), B, H, W, C, stride, _s())
 
 
-def dwx_fwd_supported(B, H, W, C, cin, stride):
-    """True when dwx_fwd handles this expand block (Cin <= 32, slab / segment within its LDS)."""
-    return bool(lib().dwx_fwd_supported(B, H, W, C, cin, stride))
-
-
-def dwx_fwd(x, cin, we, in_s, in_t, w, y, part, B, H, W, C, stride, fin=None, lz=None):
-    """Depthwise forward of an expand block with the expand conv re-formed in the kernel:
-    y = dwconv3x3(relu6(BN_e(bf16(x @ we^T)))), x = the block input [B,H,W,cin], we = the expand
-    weight [C, cin]; BN_e from ``in_s`` / ``in_t`` or the lazy descriptor ``lz``.  Same outputs
-    and statistics partials as :func:`dw_fwd` on the stored expand output."""
-    _dw_check(B, H, W, C, stride)
-    if not dwx_fwd_supported(B, H, W, C, cin, stride):
-        raise ValueError(f"dwx_fwd: unsupported B={B} H={H} W={W} C={C} cin={cin} stride={stride}")
-    Ho, Wo = dw_out_hw(H, W, stride)
-    _chk(x, BF16, B * H * W * cin, "x")
-    _chk(we, BF16, C * cin, "we")
-    _chk(w, BF16, C * 9, "w")
-    _chk(y, BF16, B * Ho * Wo * C, "y")
-    _chk(part, F32, bn_rows(dw_num_partials("fwd", B, H, W, C, stride)) * 2 * C, "part")
-    if lz is None:
-        _chk(in_s, F32, C, "in_s")
-        _chk(in_t, F32, C, "in_t")
-    _arm(fin)
-    _arm_lz(lz)
-    lib().dwx_fwd(_p(x), int(cin), _p(we), _p(in_s), _p(in_t), _p(w), _p(y), _p(part), B, H, W, C, stride, _s())
-
-
 def dw_dgrad_wgrad_workspace(B, H, W, C, stride):
     """Floats of wpart a fused depthwise dgrad + wgrad needs ([P][9][C] + reduction rows)."""
     return lib().dw_dgrad_wgrad_workspace_floats(B, H, W, C, stride)
@@ -1133,7 +1106,7 @@ def _logged(fn):
 
 
 for _name in ("bn_fwd_finalize", "bn_bwd_finalize", "bn_apply", "bn_finalize_batch", "adam_flat", "f32_to_bf16",
-              "step_begin", "reduce_metrics", "dw_fwd", "dwx_fwd", "dw_dgrad", "dw_wgrad", "pw_gemm", "pw_gemm_f8", "w8_quant",
+              "step_begin", "reduce_metrics", "dw_fwd", "dw_dgrad", "dw_wgrad", "pw_gemm", "pw_gemm_f8", "w8_quant",
               "wt_transpose", "pw_bwd", "wgrad_reduce", "wgrad_reduce_flush", "pw_wgrad", "stem_fwd", "stem_wgrad",
               "head", "augment", "conv_fwd", "conv_dgrad", "conv_wgrad", "bn_mat", "conv_wt", "res_out", "maxpool_fwd",
               "maxpool_bwd", "avgpool", "head_bwd", "softmax_ce", "fc_gemm", "col_sum", "image_prep", "memset"):

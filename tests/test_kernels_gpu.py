@@ -159,40 +159,6 @@ def test_dw_fwd(dev, B, H, W, C, stride):
     assert rel(st[1], (r2 * r2).sum(0)) < 1e-3
 
 
-# depthwise forward with the expand conv re-formed in the kernel: (B, H, C, cin, stride); B = 128
-# cases take the production geometries (56x56 stride 1: 72-channel slabs of 14 columns)
-DWX_CASES = [(2, 112, 96, 16, 2), (2, 56, 144, 24, 2), (2, 28, 192, 32, 1),
-             (3, 28, 192, 32, 2), (1, 30, 96, 16, 1), (2, 13, 64, 8, 2), (128, 56, 144, 24, 1), (128, 112, 96, 16, 2), (128, 28, 192, 32, 2)]
-
-
-@pytest.mark.parametrize("B,H,C,cin,stride", DWX_CASES)
-def test_dwx_fwd(dev, B, H, C, cin, stride):
-    """dwx_fwd(x, We) against the fp32 reference of dwconv(relu6(BN(bf16(x We^T)))) (the kernel
-    rounds h1 and the activation to bf16 in LDS), and against dw_fwd on the stored expand output."""
-    assert K.dwx_fwd_supported(B, H, H, C, cin, stride)
-    x = bf(rnd(B, H, H, cin, dev=dev, seed=B + C))
-    We = bf(rnd(C, cin, dev=dev, seed=7) / math.sqrt(cin))
-    s, t = bn_params(C, dev)
-    w = bf(rnd(C, 1, 3, 3, dev=dev, seed=3) * 0.3)
-    Ho, Wo = K.dw_out_hw(H, H, stride)
-    y = torch.empty(B, Ho, Wo, C, dtype=torch.bfloat16, device=dev)
-    P = K.dw_num_partials("fwd", B, H, H, C, stride)
-    part = torch.zeros(P * 2 * C, device=dev)
-    K.dwx_fwd(x, cin, We, s, t, tapmajor(w), y, part, B, H, H, C, stride)
-    h1 = bf(x.float() @ We.float().t())
-    z = bf(relu6(h1.float() * s + t)).float().permute(0, 3, 1, 2)
-    ref = F.conv2d(z, w.float(), stride=stride, padding=1, groups=C).permute(0, 2, 3, 1)
-    assert rel(y, ref) < 8e-3
-    st = sum_parts(part, P, C)
-    r2 = ref.reshape(-1, C)
-    assert rel(st[0], r2.sum(0)) < 2e-3
-    assert rel(st[1], (r2 * r2).sum(0)) < 2e-3
-    y2 = torch.empty_like(y)
-    part2 = torch.zeros_like(part)
-    K.dw_fwd(h1, s, t, K.ACT_BN_RELU6, tapmajor(w), y2, part2, B, H, H, C, stride)
-    assert rel(y, y2) < 8e-3
-
-
 @pytest.mark.parametrize("B,H,W,C,stride", DW_CASES)
 def test_dw_dgrad_wgrad(dev, B, H, W, C, stride):
     yprev = bf(rnd(B, H, W, C, dev=dev, seed=11))
