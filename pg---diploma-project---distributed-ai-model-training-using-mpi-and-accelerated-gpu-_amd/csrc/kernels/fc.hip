@@ -7,8 +7,10 @@
 // native launches only (recordable into a launch plan).
 //
 // One strided kernel serves all three products:  C[m][n] = sum_k A(m,k) B(k,n) (+ bias[n]),
-// A(m,k) = A[m*sam + k*sak], B(k,n) = B[k*sbk + n*sbn].  Tiles of 32 x 32 outputs, 2 x 2 per
-// thread, operands staged through LDS with the unit-stride dimension mapped to consecutive
+// A(m,k) = A[m*sam + k*sak], B(k,n) = B[k*sbk + n*sbn].  Tiles of 64 x 64 outputs, 4 x 4 per
+// thread (two 16-B LDS reads per 16 FMAs; the former 32 x 32 tiles with 2 x 2 per thread
+// spent one LDS read per FMA and ran at 0.2-0.4 TB/s, 24-45 us per GEMM, round 4 roofline),
+// operands staged through LDS k-major with the unit-stride dimension mapped to consecutive
 // threads (coalesced whichever operand is transposed).  The shapes are small (0.5 GFLOP each),
 // so parallelism comes from splitting K: every split writes its partial tile to a workspace
 // and a second kernel sums the splits in a FIXED order (+ bias) -- deterministic, unlike
@@ -16,18 +18,18 @@
 #include "../common.h"
 
 namespace {
-constexpr int kTM = 32, kTN = 32, kTK = 32;
+constexpr int kTM = 64, kTN = 64, kTK = 16;
 
 __global__ __launch_bounds__(256) void fc_gemm_kernel(const float *__restrict__ A, long long sam, long long sak,
                                                       const float *__restrict__ B, long long sbk, long long sbn,
                                                       float *__restrict__ out, int M, int N, int K, int kchunk) {
-  __shared__ float As[kTK][kTM + 1];
-  __shared__ float Bs[kTK][kTN + 1];
+  __shared__ __attribute__((aligned(16))) float As[kTK][kTM + 4];
+  __shared__ __attribute__((aligned(16))) float Bs[kTK][kTN + 4];
   const int tid = threadIdx.x;
-  const int tx = tid % 16, ty = tid / 16;   // 2 x 2 outputs: rows ty*2.., cols tx*2..
+  const int tx = tid % 16, ty = tid / 16;   // 4 x 4 outputs: rows ty*4.., cols tx*4..
   const int n0 = blockIdx.x * kTN, m0 = blockIdx.y * kTM;
   const int kb = blockIdx.z * kchunk, ke = min(K, kb + kchunk);
-  float acc[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+  float acc[4][4] = {};
   for (int k0 = kb; k0 < ke; k0 += kTK) {
 #pragma unroll
     for (int i = 0; i < (kTM * kTK) / 256; ++i) {
@@ -48,25 +50,29 @@ __global__ __launch_bounds__(256) void fc_gemm_kernel(const float *__restrict__ 
       Bs[kk][nn] = (n < N && k < ke) ? B[(long long)k * sbk + (long long)n * sbn] : 0.f;
     }
     __syncthreads();
-#pragma unroll 8
+#pragma unroll
     for (int kk = 0; kk < kTK; ++kk) {
-      const float a0 = As[kk][ty * 2], a1 = As[kk][ty * 2 + 1];
-      const float b0 = Bs[kk][tx * 2], b1 = Bs[kk][tx * 2 + 1];
-      acc[0][0] = fmaf(a0, b0, acc[0][0]);
-      acc[0][1] = fmaf(a0, b1, acc[0][1]);
-      acc[1][0] = fmaf(a1, b0, acc[1][0]);
-      acc[1][1] = fmaf(a1, b1, acc[1][1]);
+      const float4 a = *reinterpret_cast<const float4 *>(&As[kk][ty * 4]);
+      const float4 b = *reinterpret_cast<const float4 *>(&Bs[kk][tx * 4]);
+      const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(av[i], bv[j], acc[i][j]);
     }
     __syncthreads();
   }
   float *dst = out + (size_t)blockIdx.z * M * N;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + ty * 4 + i;
+    if (m >= M) continue;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int m = m0 + ty * 2 + i, n = n0 + tx * 2 + j;
-      if (m < M && n < N) dst[(size_t)m * N + n] = acc[i][j];
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + tx * 4 + j;
+      if (n < N) dst[(size_t)m * N + n] = acc[i][j];
     }
+  }
 }
 
 // C[m][n] = (bias[n]) + sum_s P[s][m][n], splits summed in order s = 0..S-1
@@ -94,7 +100,7 @@ __global__ __launch_bounds__(256) void col_sum_kernel(const float *__restrict__ 
 int fc_gemm_splits(int M, int N, int K) {
   const long long tiles = (long long)((M + kTM - 1) / kTM) * ((N + kTN - 1) / kTN);
   int S = 1;
-  while (S < 16 && tiles * S < 512 && K / (S * 2) >= 2 * kTK) S *= 2;
+  while (S < 16 && tiles * S < 512 && K / (S * 2) >= 4 * kTK) S *= 2;
   return S;
 }
 long long fc_gemm_workspace_floats(int M, int N, int K) {
