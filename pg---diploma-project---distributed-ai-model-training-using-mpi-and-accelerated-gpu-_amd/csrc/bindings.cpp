@@ -55,9 +55,6 @@ std::string bn_fin_pack(float *, int *, int, int, float, int, const float *, con
 void bn_set_rep(int rep);
 void conv_set_glds(int mode);
 int conv_get_glds();
-void conv_set_halo(int on);
-int conv_get_halo();
-bool conv_halo_ok(int, int, int, int, int, int, int, int, int, int);
 int dw_dgrad_num_partials(int, int, int, int, int);
 int dw_wgrad_num_partials(int, int, int, int, int);
 void launch_dw_fwd(const bf16_t *, const float *, const float *, int, const bf16_t *, bf16_t *,
@@ -240,9 +237,6 @@ PYBIND11_MODULE(_pgdist_C, m) {
   });
   m.def("conv_set_glds", &conv_set_glds, "dense conv staging: 0 register-staged, 2/3 LDS-DMA buffers");
   m.def("conv_get_glds", &conv_get_glds);
-  m.def("conv_set_halo", &conv_set_halo, "3x3 stride-1 forward convs on the halo-tile kernel (1, default) or not (0)");
-  m.def("conv_get_halo", &conv_get_halo);
-  m.def("conv_halo_ok", &conv_halo_ok);
   m.def("bn_set_rep", &bn_set_rep, "set the replica rows (large = one row per workgroup: deterministic)");
   m.def("dw_dgrad_num_partials", &dw_dgrad_num_partials);
   m.def("dw_wgrad_num_partials", &dw_wgrad_num_partials);

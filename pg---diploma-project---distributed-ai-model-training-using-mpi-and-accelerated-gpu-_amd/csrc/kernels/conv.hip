@@ -687,185 +687,6 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs p) {
 }
 
 // ===========================================================================
-// 3x3 stride-1 forward convolution on a HALO tile (ResNet-50 conv2 of the stride-1 bottlenecks:
-// 56x56x64, 28x28x128, 14x14x256, 7x7x512, 13 of the 16 3x3 convs).  The implicit-GEMM kernels
-// above stream one A tile per (tap, 64-channel) k-step: every input pixel is DMA'd into LDS
-// nine times, with two barriers (or a ring) per k-step, and run at 13-26 % of the dense bf16
-// MFMA peak (profiles/r6_mfma_resnet50_bs128.txt, the 3x3 convs 45-60 us for 29.6 GFLOP).
-// Here a workgroup owns 224 output pixels = 224 / W whole rows of the batch seen as one tall
-// image ([Nb*H][W]), and per 64-channel chunk it DMAs the tile's input halo ONCE:
-// (224/W + 2) rows x (W + 2) columns x 128 B (<= 44 KiB, zero padding from the descriptor range
-// check, 16-B chunks XOR-swizzled by pixel so the fragment reads are conflict-free).  The nine
-// taps are then formed by addressing the halo at the tap's offset -- no LDS traffic for the
-// gather, one barrier per chunk, none per tap.  The weights (all taps x 64 output channels of
-// one N tile: L2-resident) go straight into registers, prefetched two taps ahead; 2 x 2 waves,
-// each wave 7 row tiles x 32 columns (28 MFMAs of 16x16x32 per tap and 32-channel step).  The
-// product is formed transposed (C^T = W . X^T), so a lane holds 4 consecutive channels of one
-// pixel: 8-B output stores, BN statistics reduced across the 16 pixel lanes by shuffles.
-// Image edges inside a tall tile: the dh = 0 / 2 taps of an image's first / last row are zeroed
-// per lane.  Requires Ci % 64 == 0, N % 64 == 0, 224 % W == 0.
-// ===========================================================================
-namespace {
-constexpr int kHxTM = 224;                 // output pixels per tile: 2 x 7 row tiles of 16
-constexpr int kHxChunks = 2816;            // halo 16-B chunks (352 pixels x 8): 11 DMA rounds
-struct HaloArgs {
-  const bf16_t *x;     // [rows][W][Ci], rows = Nb * H (materialised input)
-  const bf16_t *w;     // [N][3][3][Ci]
-  bf16_t *y;           // [rows][W][N]
-  float *part;         // BN partials [P][2][N] (replica rows)
-  int H, W, Ci, N, rows;
-  int nmt, ntn, P, bn_rep;
-};
-}  // namespace
-
-__global__ __launch_bounds__(256) void conv3x3_halo_kernel(HaloArgs p) {
-  __shared__ __attribute__((aligned(16))) char halo[kHxChunks * 16];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int W = p.W, Wp = W + 2, RT = kHxTM / W;
-  const int nchunk = (RT + 2) * Wp * 8;
-  int mt, nt;
-  {   // the N tiles of one M tile 8 workgroup ids apart (same XCD: the halo rows hit its L2)
-    const int L = blockIdx.x, NT = p.ntn, nmt = p.nmt, full = (nmt / 8) * 8 * NT;
-    if (L < full) {
-      mt = (L / (8 * NT)) * 8 + L % 8;
-      nt = (L / 8) % NT;
-    } else {
-      const int rem = nmt % 8, Lr = L - full;
-      mt = (nmt / 8) * 8 + Lr % rem;
-      nt = Lr / rem;
-    }
-  }
-  const int row0 = mt * RT;
-  const int n0 = nt * 64 + wn * 32;
-  // this lane's output pixel in each of its 7 row tiles: halo pixel of tap (0, 0), image-edge
-  // masks of the dh = 0 / dh = 2 taps, validity (rows past the batch: partial last tile)
-  int hb[7];
-  unsigned mup = 0, mdn = 0, mok = 0;
-#pragma unroll
-  for (int rt = 0; rt < 7; ++rt) {
-    const int m = (wm * 7 + rt) * 16 + (lane & 15);
-    const int r = m / W, c = m - r * W;
-    hb[rt] = r * Wp + c;
-    const int h = (row0 + r) % p.H;
-    if (h != 0) mup |= 1u << rt;
-    if (h != p.H - 1) mdn |= 1u << rt;
-    if (row0 + r < p.rows) mok |= 1u << rt;
-  }
-  const u32x4_t rx = make_srd(p.x, (uint32_t)((size_t)p.rows * W * p.Ci * 2));
-  // weight fragments: lane -> row n0 + 16 ct + (lane & 15), 8 channels at 8 (lane >> 4)
-  const int K9 = 9 * p.Ci;
-  const bf16_t *w0 = p.w + (size_t)(n0 + (lane & 15)) * K9 + 8 * (lane >> 4);
-  const bf16_t *w1 = w0 + (size_t)16 * K9;
-  const int nsteps = (p.Ci / 64) * 9;
-  uint4 bq[3][2][2];   // [step % 3][k half][column tile]
-  auto load_b = [&](int s, uint4 (&d)[2][2]) {
-    s = s < nsteps ? s : nsteps - 1;   // past the end: re-load the last step (unconditional)
-    const int ch = s / 9, tap = s - ch * 9;
-    const int off = tap * p.Ci + ch * 64;
-    d[0][0] = ldg16(w0 + off);
-    d[0][1] = ldg16(w1 + off);
-    d[1][0] = ldg16(w0 + off + 32);
-    d[1][1] = ldg16(w1 + off + 32);
-  };
-  f32x4_t acc[7][2];
-#pragma unroll
-  for (int rt = 0; rt < 7; ++rt) acc[rt][0] = acc[rt][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  load_b(0, bq[0]);
-  load_b(1, bq[1]);
-  for (int ck = 0; ck < p.Ci / 64; ++ck) {
-    __syncthreads();   // every wave is done with the previous chunk's halo
-    // halo DMA: chunk t -> pixel t >> 3 (row t / 8 / Wp, column t / 8 % Wp), LDS slot t & 7
-    // holding channel chunk (t & 7) ^ (pixel & 7)
-#pragma unroll
-    for (int it = 0; it < kHxChunks / 256; ++it) {
-      const int t = it * 256 + tid;
-      const int px = t >> 3, hr = px / Wp, hc = px - hr * Wp;
-      const int trow = row0 - 1 + hr, col = hc - 1;
-      const int kc = (t & 7) ^ (px & 7);
-      const bool ok = t < nchunk && trow >= 0 && trow < p.rows && col >= 0 && col < W;
-      const uint32_t off = ok ? (uint32_t)((((size_t)trow * W + col) * p.Ci + ck * 64 + kc * 8) * 2) : kOOB;
-      lds_dma16(rx, halo + (it * 256 + wave * 64) * 16, off);
-    }
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");   // (also lands bq of this chunk)
-    // one filter row (3 taps) per iteration: the weight ring slot of tap dw is dw (9 % 3 == 0)
-#pragma unroll 1
-    for (int dh = 0; dh < 3; ++dh) {
-      const bool edge = dh != 1;
-      const unsigned msk = dh == 0 ? mup : mdn;
-#pragma unroll
-      for (int dw = 0; dw < 3; ++dw) {
-        const int s = ck * 9 + dh * 3 + dw;
-        load_b(s + 2, bq[(dw + 2) % 3]);
-        const int toff = dh * Wp + dw;
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          const int kc = ks * 4 + (lane >> 4);
-#pragma unroll
-          for (int rt = 0; rt < 7; ++rt) {
-            const int px = hb[rt] + toff;
-            s16x8_t a = *reinterpret_cast<const s16x8_t *>(halo + px * 128 + ((kc ^ (px & 7)) << 4));
-            if (edge && !((msk >> rt) & 1)) a = s16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-            for (int ct = 0; ct < 2; ++ct)
-              acc[rt][ct] = mfma16(__builtin_bit_cast(s16x8_t, bq[dw][ks][ct]), a, acc[rt][ct]);
-          }
-        }
-      }
-    }
-  }
-  // epilogue: acc[rt][ct][j] = y[pixel (wm*7 + rt)*16 + (lane & 15)][n0 + 16 ct + 4 (lane >> 4) + j]
-  float s0[2][4], s1[2][4];
-#pragma unroll
-  for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) s0[ct][j] = s1[ct][j] = 0.f;
-  const rsrc_t ry = make_rsrc(p.y, (uint32_t)((size_t)p.rows * W * p.N * 2));
-#pragma unroll
-  for (int rt = 0; rt < 7; ++rt) {
-    const int m = (wm * 7 + rt) * 16 + (lane & 15);
-    const bool ok = (mok >> rt) & 1;
-    const size_t pix = (size_t)row0 * W + m;
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct) {
-      float v[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        v[j] = bf2f(f2bf(acc[rt][ct][j]));
-        const float e = ok ? 1.f : 0.f;
-        s0[ct][j] = fmaf(e, v[j], s0[ct][j]);
-        s1[ct][j] = fmaf(e * v[j], v[j], s1[ct][j]);
-      }
-      uint2 o;
-      o.x = pack2(v[0], v[1]);
-      o.y = pack2(v[2], v[3]);
-      bst8(ry, ok ? (uint32_t)((pix * p.N + n0 + ct * 16 + 4 * (lane >> 4)) * 2) : kOOB, o);
-    }
-  }
-  // per-channel sums over the 16 pixel lanes of each lane group, then one atomic per channel
-#pragma unroll
-  for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int o = 8; o > 0; o >>= 1) {
-        s0[ct][j] += __shfl_xor(s0[ct][j], o);
-        s1[ct][j] += __shfl_xor(s1[ct][j], o);
-      }
-  if ((lane & 15) == 0) {
-    const int prow = mt * p.ntn + nt;
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = n0 + ct * 16 + 4 * (lane >> 4) + j;
-        bn_part_add(p.part, prow, p.P, p.bn_rep, p.N, 0, n, s0[ct][j]);
-        bn_part_add(p.part, prow, p.P, p.bn_rep, p.N, 1, n, s1[ct][j]);
-      }
-  }
-}
-
-// ===========================================================================
 // BN materialisation for the LDS-DMA convs (operands without a prologue), [M][C] bf16:
 //   MODE 0: act = relu(Y*a + b)        (forward: the producer BN + ReLU, consumer input)
 //   MODE 1: dy  = a*G + b*Y + c        (backward: this layer's BN backward, dgrad + wgrad input)
@@ -1809,32 +1630,9 @@ int conv_dgrad_num_partials(int Nb, int H, int W, int N, int Cout, int R, int S,
 
 // forward conv.  x [Nb][H][W][Ci] (Ci % 8 == 0, or Ci == 4 for the stem), w [N][R][S][Ci]
 // pro: 0 none, 1 relu(x*pa+pb) of the producer BN
-// the halo-tiled 3x3 stride-1 forward (conv3x3_halo_kernel) for the shapes it supports
-int g_conv_halo = 1;
-void conv_set_halo(int on) { g_conv_halo = on; }
-int conv_get_halo() { return g_conv_halo; }
-bool conv_halo_ok(int pro, int Nb, int H, int W, int Ci, int N, int R, int S, int st, int pad) {
-  return g_conv_halo && pro == CP_NONE && R == 3 && S == 3 && st == 1 && pad == 1 && H == W && W > 0 &&
-         kHxTM % W == 0 && (kHxTM / W + 2) * (W + 2) * 8 <= kHxChunks && Ci % 64 == 0 && N % 64 == 0 &&
-         g_bn_rep <= kBnRep && (size_t)Nb * H * W * (Ci > N ? Ci : N) * 2 < (1ull << 31);
-}
-
 void launch_conv_fwd(int pro, const bf16_t *x, const float *pa, const float *pb, const bf16_t *w, bf16_t *y,
                      float *part, int Nb, int H, int W, int Ci, int N, int R, int S, int st, int pad,
                      hipStream_t stream) {
-  if (conv_halo_ok(pro, Nb, H, W, Ci, N, R, S, st, pad)) {
-    HaloArgs h{};
-    h.x = x; h.w = w; h.y = y; h.part = part;
-    h.H = H; h.W = W; h.Ci = Ci; h.N = N; h.rows = Nb * H;
-    h.nmt = (h.rows + kHxTM / W - 1) / (kHxTM / W);
-    h.ntn = N / 64;
-    // statistics rows: the accumulator is sized for the implicit-GEMM launch (min(its partial
-    // rows, bn_rep)); passing its row count keeps every atomic inside that allocation
-    h.P = igemm_geom(Nb * H * W, N, 9 * Ci, Ci, 1).nmt;
-    h.bn_rep = g_bn_rep;
-    hipLaunchKernelGGL(conv3x3_halo_kernel, dim3(h.nmt * h.ntn), dim3(256), 0, stream, h);
-    return;
-  }
   ConvArgs a{};
   a.A = x; a.pa = pa; a.pb = pb; a.W = w; a.out = y; a.part = part;
   a.Hi = H; a.Wi = W; a.Ci = Ci;

@@ -647,20 +647,6 @@ def conv_get_glds():
     return lib().conv_get_glds()
 
 
-def conv_set_halo(on):
-    """3x3 stride-1 forward convs (materialised input, Ci / Cout multiples of 64, 224 % W == 0) on
-    the halo-tile kernel (conv3x3_halo_kernel, default) or on the implicit-GEMM kernels (tests)."""
-    lib().conv_set_halo(int(bool(on)))
-
-
-def conv_get_halo():
-    return lib().conv_get_halo()
-
-
-def conv_halo_ok(pro, B, H, W, Ci, N, R, S, stride, pad):
-    return bool(lib().conv_halo_ok(int(pro), B, H, W, Ci, N, R, S, stride, pad))
-
-
 def conv_out_hw(H, W, R, S, stride, pad):
     return (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
 

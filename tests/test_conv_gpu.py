@@ -65,15 +65,6 @@ FWD_SHAPES = [
 
 
 @pytest.fixture
-def no_halo():
-    """the implicit-GEMM forward kernels on the shapes the halo kernel would take"""
-    old = K.conv_get_halo()
-    K.conv_set_halo(0)
-    yield
-    K.conv_set_halo(old)
-
-
-@pytest.fixture
 def glds_mode():
     """restores the dense-conv staging mode a test selects (ops.kernels.conv_set_glds)"""
     old = K.conv_get_glds()
@@ -83,9 +74,8 @@ def glds_mode():
 
 @pytest.mark.parametrize("shape", FWD_SHAPES)
 @pytest.mark.parametrize("pro,glds", [(K.CP_NONE, 0), (K.CP_NONE, 2), (K.CP_BN_RELU, 2)])
-def test_conv_fwd(dev, shape, pro, glds, glds_mode, no_halo):
-    """CP_NONE with Ci % 64 == 0 runs on the LDS-DMA kernel (2 or 3 LDS buffers) unless glds=0
-    (the halo kernel off: test_conv_fwd_halo covers it)."""
+def test_conv_fwd(dev, shape, pro, glds, glds_mode):
+    """CP_NONE with Ci % 64 == 0 runs on the LDS-DMA kernel (2 or 3 LDS buffers) unless glds=0."""
     glds_mode(glds)
     B, H, Ci, N, R, st, pad = shape
     x = bfr(rnd(B, H, H, Ci, dev=dev, seed=1))
@@ -99,33 +89,6 @@ def test_conv_fwd(dev, shape, pro, glds, glds_mode, no_halo):
     part = torch.zeros(P, 2, N, device=dev)   # replica rows are added to atomically (bn_part_add)
     K.conv_fwd(pro, x.to(torch.bfloat16).contiguous(), w_store(w), y, part, B, H, H, Ci, N, R, R, st, pad,
                pa=s if pro else None, pb=t if pro else None)
-    torch.cuda.synchronize()
-    assert rel(y, ref) < 1e-2, rel(y, ref)
-    yf = y.float().reshape(-1, N)
-    ps = part.sum(0)
-    assert torch.allclose(ps[0], yf.sum(0), rtol=1e-3, atol=1e-2)
-    assert torch.allclose(ps[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-2)
-
-
-# (B, H, Ci, N): the ResNet-50 stride-1 3x3 shapes, tiles crossing image edges (H = 14 / 7: 16 / 32
-# rows per tile), partial last tiles (B * H not a multiple of 224 / W), N = 192 (3 N tiles)
-HALO_SHAPES = [(2, 56, 64, 64), (2, 28, 128, 128), (8, 14, 256, 256), (32, 7, 512, 512), (3, 14, 128, 128),
-               (1, 7, 64, 64), (5, 28, 64, 192), (128, 56, 64, 64)]
-
-
-@pytest.mark.parametrize("shape", HALO_SHAPES)
-def test_conv_fwd_halo(dev, shape):
-    """The halo-tile 3x3 stride-1 forward (conv3x3_halo_kernel) against F.conv2d in fp32 on the
-    same bf16 values, and its BN partials against the output's column sums."""
-    B, H, Ci, N = shape
-    assert K.conv_get_halo() == 1 and K.conv_halo_ok(K.CP_NONE, B, H, H, Ci, N, 3, 3, 1, 1)
-    x = bfr(rnd(B, H, H, Ci, dev=dev, seed=1))
-    w = bfr(rnd(N, Ci, 3, 3, dev=dev, scale=(Ci * 9) ** -0.5, seed=2))
-    ref = nhwc(F.conv2d(nchw(x), w, stride=1, padding=1))
-    y = torch.empty(B, H, H, N, dtype=torch.bfloat16, device=dev)
-    P = K.conv_fwd_num_partials(B, H, H, N, 9 * Ci, Ci)
-    part = torch.zeros(P, 2, N, device=dev)
-    K.conv_fwd(K.CP_NONE, x.to(torch.bfloat16).contiguous(), w_store(w), y, part, B, H, H, Ci, N, 3, 3, 1, 1)
     torch.cuda.synchronize()
     assert rel(y, ref) < 1e-2, rel(y, ref)
     yf = y.float().reshape(-1, N)
