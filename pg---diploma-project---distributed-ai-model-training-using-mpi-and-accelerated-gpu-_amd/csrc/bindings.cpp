@@ -70,6 +70,7 @@ void pwt_trace_set(void *);
 void pwb_trace_set(void *);
 void pwg_trace_set(void *);
 bool pw_bwd_supported(int, int, int);
+void pw_bwd_set_min_m(int);
 int pw_bwd_num_partials(int, int, int);
 long long pw_bwd_wgrad_workspace_floats(int, int, int);
 void launch_pw_bwd(int, const bf16_t *, const bf16_t *, const float *, const float *, const float *,
@@ -298,6 +299,7 @@ PYBIND11_MODULE(_pgdist_C, m) {
     });
   });
   m.def("pw_bwd_supported", &pw_bwd_supported);
+  m.def("pw_bwd_set_min_m", &pw_bwd_set_min_m);
   m.def("pw_bwd_num_partials", &pw_bwd_num_partials);
   m.def("pw_bwd_wgrad_workspace_floats", &pw_bwd_wgrad_workspace_floats);
   m.def("pw_bwd_recompute_supported", &pw_bwd_recompute_supported);

@@ -483,6 +483,7 @@ void pwb_trace_set(void *ts) {   // nullptr: off; no-op unless built with PGDIST
 void launch_wgrad_reduce(float *part, int S, long long n, float *grad, hipStream_t st, bool stem36 = false);
 int colsum_rows(int R);
 
+int g_pwb_min_m = 65536;   // smallest M the fused dgrad + wgrad takes (pw_bwd_set_min_m)
 namespace {
 struct BwdGeom {
   int KP, BN, BM, nt, gx;
@@ -507,7 +508,12 @@ BwdGeom bwd_geom(int M, int Kg, int Ng, bool recomp = false) {
   // the Y-recompute form loads no Y tile: twice the rows per tile keep the bytes in flight per
   // workgroup (the loop is bound by one tile's load latency, not by its bytes)
   if (recomp && g.BN == 32 && g.BM <= 64) g.BM *= 2;
-  g.ok = M >= 65536 && g.KP <= 192 && Kg % 8 == 0 && Ng % 8 == 0 && Kg > 0 && Ng > 0;
+  // M >= 64k (the 112x112 .. 28x28 layers), or the narrow-K small maps (the 14x14 project convs
+  // at batch 128, Kg = 64 / 96): their weight gradient leaves the side stream, 4.198-4.213 vs
+  // 4.222-4.234 ms/step; the 7x7 project convs too (Kg = 160, M = 6272): 4.264-4.276, slower
+  // (docs/PERF_NOTES.md round 6)
+  g.ok = (M >= g_pwb_min_m || (M >= 16384 && g.KP <= 96)) && g.KP <= 192 && Kg % 8 == 0 && Ng % 8 == 0 &&
+         Kg > 0 && Ng > 0;
   g.nt = (Ng + g.BN - 1) / g.BN;
   const int nmt = (M + g.BM - 1) / g.BM;
   int gx = 512 / g.nt;   // grid target 512 (768 / 1024: slower, docs/PERF_NOTES.md round 2)
@@ -550,6 +556,7 @@ void launch_bwd_epi(const PwBwdArgs &a, const BwdGeom &g, hipStream_t st) {
 }  // namespace
 
 bool pw_bwd_supported(int M, int Kg, int Ng) { return bwd_geom(M, Kg, Ng).ok; }
+void pw_bwd_set_min_m(int m) { g_pwb_min_m = m; }
 // the expand-conv form that re-forms Y from X (pw_bwd with We): one 32-wide N tile
 bool pw_bwd_recompute_supported(int M, int Kg, int Ng) {
   const BwdGeom g = bwd_geom(M, Kg, Ng);

@@ -457,6 +457,11 @@ def wt_transpose(src, dst, tab, n):
     lib().wt_transpose(_p(src), _p(dst), _p(tab), int(n), _s())
 
 
+def pw_bwd_set_min_m(m):
+    """Smallest M (rows) the fused 1x1 dgrad + wgrad kernel takes (set before building an executor)."""
+    lib().pw_bwd_set_min_m(int(m))
+
+
 def pw_bwd_supported(M, Kg, Ng):
     """True when the fused dgrad+wgrad kernel handles this 1x1 conv backward (large M)."""
     return bool(lib().pw_bwd_supported(M, Kg, Ng))

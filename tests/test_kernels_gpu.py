@@ -499,7 +499,9 @@ def test_pw_wgrad(dev, M, Kf, Nf, xact):
 # fused dgrad + wgrad of a 1x1 conv (large M): (M, Kg = conv Cout, Ng = conv Cin, epilogue, residual)
 PW_BWD_CASES = [(70001, 96, 16, "lin", True), (66000, 24, 144, "relu6", False), (65600, 192, 32, "lin", False),
                 (70000, 32, 192, "relu6", False), (65613, 144, 24, "lin", True), (65540, 16, 32, "relu6", False),
-                (66001, 24, 96, "relu6", False), (401408, 32, 144, "relu6", False)]
+                (66001, 24, 96, "relu6", False), (401408, 32, 144, "relu6", False),
+                # small maps with a narrow K (the 14x14 project convs at batch 128): 6 / 9 N tiles
+                (25088, 64, 384, "relu6", False), (25088, 96, 576, "relu6", False)]
 
 
 @pytest.mark.parametrize("M,Kg,Ng,mode,res,recompute", [c + (False,) for c in PW_BWD_CASES] + [
