@@ -1316,27 +1316,40 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16_t *__restri
   const long long p0 = (long long)blockIdx.x * pix_per_wg;
   for (long long pix = p0 + pl; pix < min(total, p0 + pix_per_wg); pix += PPI) {
     const int w = (int)(pix % W), h = (int)((pix / W) % H), b = (int)(pix / ((long long)W * H));
+    // the (at most 2 x 2) windows (oh, ow) with oh*2-1 <= h <= oh*2+1: oh0 = h / 2, and oh0 + 1
+    // for odd h (same for w).  All four candidates are loaded unconditionally (an invalid one
+    // re-reads window (oh0, ow0) and is masked), so the loads of a pixel are in flight together
+    // instead of sitting behind data-dependent loop branches (vmcnt(0) at every join)
+    const int oh0 = h >> 1, ow0 = w >> 1;
+    const bool oh1ok = (h & 1) && oh0 + 1 < Ho, ow1ok = (w & 1) && ow0 + 1 < Wo;
+    uint2 u[4];
+    uint4 gq[4];
+    int tp[4];
+    bool ok[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int dy = q >> 1, dx = q & 1;
+      ok[q] = (dy == 0 || oh1ok) && (dx == 0 || ow1ok);
+      const int oh = ok[q] ? oh0 + dy : oh0, ow = ok[q] ? ow0 + dx : ow0;
+      tp[q] = (h - (oh * 2 - 1)) * 3 + (w - (ow * 2 - 1));
+      const size_t o = (((size_t)b * Ho + oh) * Wo + ow) * C + c0;
+      u[q] = *reinterpret_cast<const uint2 *>(idx + o);
+      gq[q] = ldg16(gp + o);
+    }
     float acc[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc[k] = 0.f;
-    // windows (oh, ow) with oh*2-1 <= h <= oh*2+1
-    const int oh_lo = h >= 1 ? (h - 1 + 1) / 2 : 0, oh_hi = min(Ho - 1, (h + 1) / 2);
-    const int ow_lo = w >= 1 ? (w - 1 + 1) / 2 : 0, ow_hi = min(Wo - 1, (w + 1) / 2);
-    for (int oh = oh_lo; oh <= oh_hi; ++oh)
-      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
-        const int tap = (h - (oh * 2 - 1)) * 3 + (w - (ow * 2 - 1));
-        if (tap < 0 || tap > 8) continue;
-        const size_t o = (((size_t)b * Ho + oh) * Wo + ow) * C + c0;
-        const uint2 u = *reinterpret_cast<const uint2 *>(idx + o);
-        float gv[8];
-        unpack8(ldg16(gp + o), gv);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const uint32_t word = k < 4 ? u.x : u.y;
-          const int ti = (word >> (8 * (k & 3))) & 0xff;
-          if (ti == tap) acc[k] += gv[k];
-        }
+    for (int q = 0; q < 4; ++q) {
+      float gv[8];
+      unpack8(gq[q], gv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t word = k < 4 ? u[q].x : u[q].y;
+        const int ti = (word >> (8 * (k & 3))) & 0xff;
+        acc[k] += (ok[q] && ti == tp[q]) ? gv[k] : 0.f;
       }
+    }
     float yv[8];
     const size_t io = pix * C + c0;
     unpack8(ldg16(y + io), yv);

@@ -90,8 +90,17 @@ __global__ __launch_bounds__(256) void fc_splits_kernel(const float *__restrict_
 __global__ __launch_bounds__(256) void col_sum_kernel(const float *__restrict__ X, int M, int N, float *__restrict__ out) {
   const int n = blockIdx.x * 256 + threadIdx.x;
   if (n >= N) return;
+  // 16 rows in flight per thread (the loads are independent; the sum stays in row order)
   float v = 0.f;
-  for (int m = 0; m < M; ++m) v += X[(size_t)m * N + n];
+  int m = 0;
+  for (; m + 16 <= M; m += 16) {
+    float x[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] = X[(size_t)(m + i) * N + n];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v += x[i];
+  }
+  for (; m < M; ++m) v += X[(size_t)m * N + n];
   out[n] = v;
 }
 }  // namespace

@@ -449,6 +449,13 @@ class ResNet50Executor:
         B = self.B
         if not self.__dict__.pop("arena_cleared", False):   # (else cleared by the step's step_begin)
             K.memset(self.bn_arena)   # every BN statistics accumulator of this step
+        # the dgrad weight transposes of a training step on the side stream, idle during the
+        # forward (as in the MobileNetV2 executor); the main stream joins it at the end of the forward
+        self._wt_pending = train and self.side is not None
+        if self._wt_pending:
+            K.stream_wait(self.side, torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self.side):
+                K.conv_wt(self.flat.shadow, self.flat.shadow_t, self.wt_tab, self.wt_tab.shape[0])
         if self.stem_s2d:
             st, H2 = self.stem, self.S // 2
             if not self.img_s2d_external:
@@ -485,11 +492,15 @@ class ResNet50Executor:
         K.fc_gemm(self.pooled, C, 1, self.fc_w, 1, C, self.logits, B, NC, C, bias=self.fc_b, ws=self.ws_fc)
         K.softmax_ce(self.logits, self.labels, self.loss, self.correct, self.dlogits if train else None,
                      scale=1.0 / B)
+        if self._wt_pending:   # join the side stream's weight transposes
+            K.stream_wait(torch.cuda.current_stream(self.device), self.side)
 
     # ------------------------------------------------------------------ backward
     def backward(self):
         f, B = self.flat, self.B
-        K.conv_wt(f.shadow, f.shadow_t, self.wt_tab, self.wt_tab.shape[0])
+        if not getattr(self, "_wt_pending", False):   # (else transposed on the side stream in the forward)
+            K.conv_wt(f.shadow, f.shadow_t, self.wt_tab, self.wt_tab.shape[0])
+        self._wt_pending = False
         # head: fc gradients (fp32 GEMMs) and the pooled gradient through the last ReLU
         C, NC = self.C_last, self.NC
         # fc_gw[j][c] = sum_b dlogits[b][j] * pooled[b][c];  fc_gb[j] = sum_b dlogits[b][j]
