@@ -210,8 +210,8 @@ class ResNet50Executor:
         for bn, o, nf, nb in spans:
             bn.acc_f = self.bn_arena[o:o + nf]
             bn.acc_b = self.bn_arena[o + nf:o + nf + nb]
-        # lazy BN finalize (opt-in outside deterministic mode, PGDIST_BN_LAZY=1; else a finalize launch
-        # after every producer): the consumers that support it -- max-pool, the bn_mat passes
+        # lazy BN finalize (outside deterministic mode; else a finalize launch after every
+        # producer): the consumers that support it -- max-pool, the bn_mat passes
         # (relu(BN(y)) forward, dy = a*G + b*Y + c backward) and the block output res_out --
         # compute the BN parameters they need from the replica rows in their prologue, so no
         # finalize launch sits between producer and consumer on the main stream.  The side
@@ -220,10 +220,15 @@ class ResNet50Executor:
         # batched finalizes on the weight-gradient side stream ahead of the gradient buckets.
         # A BN whose consumer needs materialised parameters (a conv with the BN+ReLU prologue, a
         # dgrad / wgrad with the BN-backward prologue) keeps its finalize launch.
-        # opt-in (PGDIST_BN_LAZY=1): measured on MI355X at bs128, 11.98 ms/step lazy vs 11.83 with
-        # the finalize launches (the bn_mat passes are 50 of the lazy consumers, and each of their
-        # workgroups re-reducing all C channels costs more than the ~3 us launch it replaces)
-        self.lazy_bn = not K.deterministic() and os.environ.get("PGDIST_BN_LAZY", "0") == "1"
+        # PGDIST_BN_LAZY: "act" (default) makes only bn1 / bn2 lazy where a forward relu(BN)
+        # materialisation (bn_mat) consumes them; "1" every consumer above; "0" none.  Measured on
+        # MI355X at bs128 (same box, profiles/r6_resnet50_lazy_act_ab.txt): act 11.256-11.267,
+        # off 11.275-11.306, all 11.393-11.422 ms/step.  Per kernel (rocprofv3 traces of both):
+        # a lazy backward bn_mat costs +9 us per launch against a 5 us finalize launch, a lazy
+        # max-pool / res_out +28 / +140 us in total, while the forward bn_mat saves ~2.6 us each.
+        lazy_mode = os.environ.get("PGDIST_BN_LAZY", "act")
+        self.lazy_bn = not K.deterministic() and lazy_mode in ("1", "act")
+        lazy_all = lazy_mode == "1"   # "act": only the forward BNs consumed by a bn_mat pass are lazy
         bns = self.all_bns()
         self.bn_ctr = torch.zeros(8 * len(bns) + 16, dtype=torch.int32, device=device)
         self._fin_tabs = {}
@@ -233,15 +238,16 @@ class ResNet50Executor:
             # forward: consumers bn0 -> max-pool, bn1 -> conv2 input, bn2 -> conv3 input, bn3 / bnd
             # -> res_out; backward: each BN's coefficients -> bn_mat of its conv's dy (the stem's
             # on the side stream, after its side finalize)
-            self.bn0.lz_f, self.bn0.lz_b = self.bn0.desc_f, self.bn0.desc_b
+            if lazy_all:
+                self.bn0.lz_f, self.bn0.lz_b = self.bn0.desc_f, self.bn0.desc_b
             for bp in self.blocks:
                 for bn, c_in, c_dy in ((bp.bn1, bp.c2, bp.c1), (bp.bn2, bp.c3, bp.c2), (bp.bn3, None, bp.c3),
                                        (bp.bnd, None, bp.cd)):
                     if bn is None:
                         continue
-                    if c_in is None or c_in.act:
+                    if (c_in is None and lazy_all) or (c_in is not None and c_in.act):
                         bn.lz_f = bn.desc_f
-                    if c_dy.dy is not None:
+                    if lazy_all and c_dy.dy is not None:
                         bn.lz_b = bn.desc_b
             self.fwd_lazy = [bn for bn in bns if bn.lz_f is not None]
             self.fwd_fin_tab = K.bn_desc_table([bn.desc_f for bn in self.fwd_lazy])
@@ -256,7 +262,7 @@ class ResNet50Executor:
         self.ws_wgrad_pool = [self.ws_wgrad] + [torch.zeros_like(self.ws_wgrad) for _ in range(nws - 1)]
         self.side = None
         self._side_pending = []
-        self.side_batch = 3   # side-stream joins per 3 weight gradients (neutral vs per conv here)
+        self.side_batch = 3   # side-stream joins per 3 weight gradients (2 / 5 / 8: within noise, round 6)
         if side_stream:
             self.side = K.side_stream(device)
             K.register_side_stream(self.side)

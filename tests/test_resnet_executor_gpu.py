@@ -195,14 +195,16 @@ def test_resnet_native_step_loss_decreases(dev):
     assert torch.isfinite(st.flat.master).all()
 
 
+@pytest.mark.parametrize("mode", ["1", "act"])
 @pytest.mark.parametrize("stem", ["s2d", "direct"])
-def test_resnet_lazy_bn_matches_launch(dev, monkeypatch, stem):
+def test_resnet_lazy_bn_matches_launch(dev, monkeypatch, stem, mode):
     """Lazy BN finalize (consumers compute the parameters from the replica rows; side outputs
     batched at the end of the forward / on the side stream) vs a finalize launch after every
     producer: after 4 replayed training steps the weights, Adam moments, BN running statistics
     and metrics agree within the float-atomic noise floor of the replica rows (both modes add the
     statistics atomically; estimated as the median pairwise spread of three launch-mode runs, and
-    the lazy run is compared with its closest launch-mode run)."""
+    the lazy run is compared with its closest launch-mode run).  mode "1": every consumer that
+    can is lazy; "act" (the default): only the forward relu(BN) materialisations."""
     from pgdist.engine.native_step import NativeTrainStep
     from pgdist.engine.resnet_executor import ResNet50Executor
     monkeypatch.setattr(ResNet50Executor, "STEM", stem)
@@ -210,12 +212,12 @@ def test_resnet_lazy_bn_matches_launch(dev, monkeypatch, stem):
                         generator=torch.Generator(device=dev).manual_seed(5))
     labels = torch.arange(16, device=dev) % 10
     out = []
-    for lazy in ("0", "0", "0", "1"):
+    for lazy in ("0", "0", "0", mode):
         monkeypatch.setenv("PGDIST_BN_LAZY", lazy)
         torch.manual_seed(0)
         st = NativeTrainStep(build_model("resnet50", num_classes=10), 8, dev, img_size=64, lr=1e-3,
                              use_graph=False)
-        assert st.exe.lazy_bn == (lazy == "1")
+        assert st.exe.lazy_bn == (lazy != "0")
         st.set_data(src, labels)
         losses = []
         for i in range(4):
