@@ -26,9 +26,9 @@ LDS-DMA convs (default, ``ops.kernels.conv_set_glds``): the operand tiles of a c
 streamed global -> LDS by buffer_load ... lds, which needs operands without a prologue.  So
 every backward conv first materialises its dy = a*G + b*Y + c once (``bn_mat``; read by both
 the dgrad and the side-stream wgrad, which then skip the BN-backward prologue), and the
-forward materialises relu(BN(y)) for the convs where the prologue costs more than the extra
-pass (``mat_dy_pays`` / ``mat_act_pays``, measured per layer with scripts/conv_bench.py; the
-class attributes RN_DY / RN_ACT = all|none|auto select the policy).
+forward materialises relu(BN(y)) of every conv2 / conv3 input (class attributes RN_DY / RN_ACT
+= all|none|auto select the policy; "auto" applies the per-layer rules ``mat_dy_pays`` /
+``mat_act_pays`` measured with scripts/conv_bench.py).
 
 Reference call stack for the model forward: SURVEY.md §3.3 (cuDNN conv / BN / ReLU
 launches per layer); this executor replaces all of them.
@@ -96,7 +96,11 @@ class ResNet50Executor:
     # which convs get a materialised dy / relu(BN(y)) (all | none | auto): every dy materialised
     # 12.48 -> 12.28 ms/step (all wgrads on the LDS-DMA kernel); activations per layer (auto)
     RN_DY = "all"
-    RN_ACT = "auto"
+    # relu(BN) of every conv2 / conv3 input materialised (LDS-DMA convs only): with those BNs
+    # finalized lazily by the bn_mat pass ("act" lazy mode) this beats the per-layer policy
+    # ("auto", which kept the register-prologue conv on the large 1x1 inputs): 11.093-11.141 vs
+    # 11.190-11.233 ms/step, same box (profiles/r6_resnet50_act_all_ab.txt)
+    RN_ACT = "all"
 
     def __init__(self, model: ResNet, batch: int, img_size: int, device: torch.device,
                  flat: Optional[FlatParams] = None, hyper: Optional[torch.Tensor] = None,
