@@ -113,6 +113,10 @@ int conv_fwd_num_partials(int, int, int, int, int, int);
 int conv_dgrad_num_partials(int, int, int, int, int, int, int, int);
 void launch_conv_fwd(int, const bf16_t *, const float *, const float *, const bf16_t *, bf16_t *, float *, int,
                      int, int, int, int, int, int, int, int, hipStream_t);
+void launch_conv_fold_w(const bf16_t *, const float *, const float *, const float *, const float *, bf16_t *, float *,
+                        int, int, hipStream_t);
+void launch_conv_dgrad_fold(const bf16_t *, const bf16_t *, const bf16_t *, const float *, bf16_t *, const bf16_t *,
+                            const float *, const float *, float *, int, int, int, int, int, hipStream_t);
 void launch_conv_dgrad(int, const bf16_t *, const bf16_t *, const float *, const float *, const float *,
                        const bf16_t *, bf16_t *, const bf16_t *, const float *, const float *, const bf16_t *,
                        const bf16_t *, const bf16_t *, float *, float *, int, int, int, int, int, int, int, int,
@@ -386,6 +390,20 @@ PYBIND11_MODULE(_pgdist_C, m) {
                         ptr<bf16_t>(wt), ptr<bf16_t>(dx), ptr<bf16_t>(Yt), ptr<float>(es), ptr<float>(et),
                         ptr<bf16_t>(Rg), ptr<bf16_t>(X), ptr<bf16_t>(Yt2), ptr<float>(part), ptr<float>(part2), Nb,
                         H, W, Cin, Cout, R, Sk, st, pad, ptr<uint8_t>(Xm), S(s));
+    });
+  });
+  m.def("conv_fold_w", [](P wt, P a, P b, P c, P mu, P w2, P fbias, int Cin, int Cout, P s) {
+    pgdist_rt::run_op([=] {
+      launch_conv_fold_w(ptr<bf16_t>(wt), ptr<float>(a), ptr<float>(b), ptr<float>(c), ptr<float>(mu),
+                         ptr<bf16_t>(w2), ptr<float>(fbias), Cin, Cout, S(s));
+    });
+  });
+  m.def("conv_dgrad_fold", [](P G, P Y, P w2, P fbias, P dx, P Yt, P es, P et, P part, int Nb, int H, int W, int Cin,
+                              int Cout, P s) {
+    pgdist_rt::run_op([=] {
+      launch_conv_dgrad_fold(ptr<bf16_t>(G), ptr<bf16_t>(Y), ptr<bf16_t>(w2), ptr<float>(fbias), ptr<bf16_t>(dx),
+                             ptr<bf16_t>(Yt), ptr<float>(es), ptr<float>(et), ptr<float>(part), Nb, H, W, Cin, Cout,
+                             S(s));
     });
   });
   m.def("conv_wgrad_workspace_floats", &conv_wgrad_workspace_floats);

@@ -68,6 +68,7 @@ struct ConvArgs {
   int bn_rep;           // BN-statistics replica rows (g_bn_rep): P = ncls * nmt partial rows are
                         // added atomically into min(P, bn_rep) rows of a zeroed accumulator;
                         // bn_rep >= P (deterministic mode): one plainly stored row per tile
+  const float *fbias;   // FOLD: per-output-channel bias added to the accumulators (conv_glds)
   int ntap[4];
   signed char tr[4][9], ts[4][9], tdh[4][9], tdw[4][9];
   int tapx[4][9];       // the same taps packed per dword (dh | dw << 8 | (tr * S + ts) << 16):
@@ -520,7 +521,10 @@ PG_DEVICE int glds_sw(int r) {
 // staged 128-B row belong to different filter taps, so each lane decodes its own chunk's tap
 // (an integer division per k-step) and the bounds check is per chunk.  Without MT the tap is
 // uniform per k-step (Ci % KS == 0).
-template <int MODE, int EPI, int BM, int BN, int NBUF, int KS = 64, bool MT = false>
+// FOLD (1x1 data gradient with this layer's BN backward folded into the GEMM, see
+// launch_conv_dgrad_fold): tap 0 streams G and tap 1 streams Y as the A operand (K = 2 Cout,
+// B = [a.W | b.W]), and the epilogue adds the per-channel term fbias.
+template <int MODE, int EPI, int BM, int BN, int NBUF, int KS = 64, bool MT = false, bool FOLD = false>
 __global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs p) {
   constexpr int ROWB = KS * 2;                        // staged row bytes
   constexpr int RPP = 1024 / ROWB, CPR = ROWB / 16;   // rows per 1-KiB piece, 16-B chunks per row
@@ -558,6 +562,7 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs p) {
   const int lch = (lane % CPR) ^ glds_sw<KS>(lrow);     // k-chunk this lane fetches (source swizzle)
   // raw descriptors for the inline-asm DMA (common.h lds_dma16)
   const u32x4_t ra = make_srd(p.A, (uint32_t)p.Nb * p.Hi * p.Wi * p.Ci * 2);
+  const u32x4_t ra2 = make_srd(FOLD ? p.A2 : p.A, (uint32_t)p.Nb * p.Hi * p.Wi * p.Ci * 2);
   const u32x4_t rw = make_srd(p.W, (uint32_t)p.N * p.Kw * 2);
 
   // A rows of this wave's pieces (fixed across k-steps): image, base h / w; rb < 0: past M
@@ -614,7 +619,8 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs p) {
       const int ih = rh[i] + dh, iw = rwc[i] + dw;
       const bool ok = rb[i] >= 0 && ih >= 0 && ih < p.Hi && iw >= 0 && iw < p.Wi;
       const uint32_t off = ok ? (uint32_t)((((rb[i] * p.Hi + ih) * p.Wi + iw) * p.Ci + ci) * 2) : kOOB;
-      lds_dma16(ra, abase + (wave * APW + i) * 1024, off);
+      if (FOLD && wt) lds_dma16(ra2, abase + (wave * APW + i) * 1024, off);   // (wt: wave-uniform)
+      else lds_dma16(ra, abase + (wave * APW + i) * 1024, off);
     }
     const uint32_t kb = (uint32_t)(wt * p.Ci + ci) * 2;
 #pragma unroll
@@ -682,6 +688,17 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs p) {
       nbuf = nbuf == NBUF - 1 ? 0 : nbuf + 1;
     }
     glds_wait_barrier<0>();             // every wave done reading before the C tile reuses LDS
+  }
+  if constexpr (FOLD) {   // acc[r][c][j] = C[m][n], n = n0 + wn*BN/2 + 16c + (lane & 15)
+#pragma unroll
+    for (int c = 0; c < CTW; ++c) {
+      const int n = n0 + wn * (BN / 2) + c * 16 + (lane & 15);
+      const float bv = n < p.N ? p.fbias[n] : 0.f;
+#pragma unroll
+      for (int r = 0; r < RT; ++r)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[r][c][j] += bv;
+    }
   }
   conv_epilogue<MODE, EPI, BM, BN>(p, acc, smem, m0, n0, mt, cls, ph, pw);
 }
@@ -1570,7 +1587,7 @@ void launch_geom(const ConvArgs &a, const Geom &g, hipStream_t st) {
 int g_conv_glds = 2;
 bool glds_ok(int Ci) { return g_conv_glds != 0 && Ci % 64 == 0; }
 
-template <int MODE, int EPI, int BM, int BN, int NBUF, int KS, bool MT = false>
+template <int MODE, int EPI, int BM, int BN, int NBUF, int KS, bool MT = false, bool FOLD = false>
 void launch_glds_t(const ConvArgs &a, const Geom &g, hipStream_t st) {
   // one k-step (K <= KS: the 1x1 convs on 64 channels, memory-bound): the kernel only ever fills
   // buffer 0, so one stage of LDS (the C tile sets the size) lets twice the workgroups per CU
@@ -1583,8 +1600,8 @@ void launch_glds_t(const ConvArgs &a, const Geom &g, hipStream_t st) {
   const size_t ctile = (size_t)BM * (BN + 8) * 2, red = (size_t)(256 / (BN / 8)) * BN * 4;
   if (ctile > lds) lds = ctile;
   if (red > lds) lds = red;
-  hipLaunchKernelGGL((conv_glds_kernel<MODE, EPI, BM, BN, NBUF, KS, MT>), dim3(g.nmt * g.nt, g.ncls), dim3(256), lds,
-                     st, a);
+  hipLaunchKernelGGL((conv_glds_kernel<MODE, EPI, BM, BN, NBUF, KS, MT, FOLD>), dim3(g.nmt * g.nt, g.ncls), dim3(256),
+                     lds, st, a);
 }
 
 
@@ -1713,6 +1730,82 @@ void launch_conv_dgrad(int epi, const bf16_t *G, const bf16_t *Y, const float *g
   else if (Rg && Xm && Yt && Yt2) launch_geom<CM_DGRAD, CP_BNBWD, CE_BWD_RXYYM, 8>(a, g, stream);
   else if (Rg && X && Yt && !Yt2) launch_geom<CM_DGRAD, CP_BNBWD, CE_BWD_RXY, 8>(a, g, stream);
   else if (Rg && X && Yt && Yt2) launch_geom<CM_DGRAD, CP_BNBWD, CE_BWD_RXYY, 8>(a, g, stream);
+}
+
+// ---- 1x1 data gradient with the BN backward folded into the GEMM
+// dy = a*G + b*Y + c (per output channel k of the conv)  =>  dx[m][n] = sum_k G[m][k] (a_k W[n][k])
+// + sum_k Y[m][k] (b_k W[n][k]) + sum_k c_k W[n][k]: one GEMM with K = 2 Cout over [G | Y] and the
+// per-step weights W2[n] = [a.W[n] | b.W[n]] (bf16), instead of materialising dy (a read of G and Y
+// and a write of dy) and reading it back.  The bias also carries the rounding of b.W against the
+// channel means: fbias[n] = sum_k c_k W[n][k] + sum_k mu_k (b_k W[n][k] - bf16(b_k W[n][k])), so the
+// bf16 rounding of b.W multiplies the centred Y - mu only (no error from the cancelling means).
+__global__ __launch_bounds__(256) void conv_fold_w_kernel(const bf16_t *__restrict__ wt, const float *__restrict__ a,
+                                                          const float *__restrict__ b, const float *__restrict__ c,
+                                                          const float *__restrict__ mu, bf16_t *__restrict__ w2,
+                                                          float *__restrict__ fbias, int K) {
+  __shared__ float red[256];
+  const int n = blockIdx.x, tid = threadIdx.x;
+  const bf16_t *wr = wt + (size_t)n * K;
+  bf16_t *o = w2 + (size_t)n * 2 * K;
+  float acc = 0.f;
+  for (int k = tid; k < K; k += 256) {
+    const float w = bf2f(wr[k]);
+    const float bw = b[k] * w;
+    const bf16_t q = f2bf(bw);
+    o[k] = f2bf(a[k] * w);
+    o[K + k] = q;
+    acc = fmaf(c[k], w, fmaf(mu[k], bw - bf2f(q), acc));
+  }
+  red[tid] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (tid < s) red[tid] += red[tid + s];
+    __syncthreads();
+  }
+  if (tid == 0) fbias[n] = red[0];
+}
+
+void launch_conv_fold_w(const bf16_t *wt, const float *a, const float *b, const float *c, const float *mu, bf16_t *w2,
+                        float *fbias, int Cin, int Cout, hipStream_t st) {
+  hipLaunchKernelGGL(conv_fold_w_kernel, dim3(Cin), dim3(256), 0, st, wt, a, b, c, mu, w2, fbias, Cout);
+}
+
+// dx = conv1x1^T(dy) with dy folded as above (w2 / fbias from launch_conv_fold_w), epilogue
+// CE_BWD_RELU: dx * 1[Yt*es + et > 0], BN partials (sum dx, sum dx*Yt).  Stride 1, Cout % 64 == 0.
+void launch_conv_dgrad_fold(const bf16_t *G, const bf16_t *Y, const bf16_t *w2, const float *fbias, bf16_t *dx,
+                            const bf16_t *Yt, const float *es, const float *et, float *part, int Nb, int H, int W,
+                            int Cin, int Cout, hipStream_t stream) {
+  ConvArgs a{};
+  a.A = G; a.A2 = Y; a.W = w2; a.out = dx; a.fbias = fbias;
+  a.Yt = Yt; a.es = es; a.et = et; a.part = part;
+  a.Hi = H; a.Wi = W; a.Ci = Cout;
+  a.Ho = H; a.Wo = W; a.N = Cin;
+  a.R = 1; a.S = 1; a.stride = 1; a.pad = 0;
+  a.Kw = 2 * Cout;
+  a.Hc = H; a.Wc = W;
+  a.Mc = Nb * H * W;
+  a.ntap[0] = 2;   // tap 0: G with a.W, tap 1: Y with b.W (same pixel)
+  a.tapx[0][0] = 0;
+  a.tapx[0][1] = 1 << 16;
+  a.tr[0][0] = a.tr[0][1] = 0;
+  a.ts[0][0] = 0; a.ts[0][1] = 1;
+  a.K = 2 * Cout;
+  // the BN partial rows must match conv_dgrad_num_partials of the unfolded 1x1 dgrad: same M
+  // tiles (igemm_geom picks the tile from M and N only, K decides the k-step alone)
+  const Geom g = igemm_geom(a.Mc, Cin, 2 * Cout, Cout, 1);
+  a.nmt = g.nmt;
+  a.Nb = Nb;
+  a.bn_rep = g_bn_rep;
+#define LG_FOLD(BM_, BN_)                                                                \
+  if (g.BM == BM_ && g.BN == BN_) {                                                      \
+    launch_glds_t<CM_DGRAD, CE_BWD_RELU, BM_, BN_, 2, 64, false, true>(a, g, stream);    \
+    return;                                                                              \
+  }
+  LG_FOLD(128, 128)
+  LG_FOLD(128, 64)
+  LG_FOLD(64, 128)
+  LG_FOLD(64, 64)
+#undef LG_FOLD
 }
 
 // ---- weight gradient

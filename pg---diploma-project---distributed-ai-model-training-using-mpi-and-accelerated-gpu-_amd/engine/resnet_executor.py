@@ -56,6 +56,8 @@ class ConvSpec:
     H: int          # input spatial size (square)
     dy: Optional[torch.Tensor] = None   # materialised BN-backward output gradient (bn_mat)
     act: bool = False                   # input relu(BN(y)) materialised for this conv (bn_mat)
+    w2: Optional[torch.Tensor] = None   # folded BN-backward dgrad: per-step [a.W | b.W] (conv_fold_w)
+    fbias: Optional[torch.Tensor] = None
 
     @property
     def Ho(self) -> int:
@@ -175,6 +177,11 @@ class ResNet50Executor:
         if self.mat:
             for bp in self.blocks:
                 for c in (bp.c1, bp.c2, bp.c3) + ((bp.cd,) if bp.cd else ()):
+                    if c is bp.c3 and self.fold_pays(c):
+                        # the BN backward folded into the data gradient's GEMM (no dy pass)
+                        c.w2 = torch.empty(2 * c.cin * c.cout, **bf16)
+                        c.fbias = torch.empty(c.cin, device=device, dtype=torch.float32)
+                        continue
                     if dy_mode == "all" or (dy_mode == "auto" and self.mat_dy_pays(c, B)):
                         c.dy = torch.empty(B * c.Ho * c.Ho, c.cout, **bf16)
                 for c, bn in ((bp.c2, bp.bn1), (bp.c3, bp.bn2)):
@@ -337,6 +344,19 @@ class ResNet50Executor:
     # expensive and one materialising pass pays; a 1x1 conv stages each element once per N tile,
     # so the extra pass pays only while the tensor is small (launch-bound maps).
     MAT_ELEMS = 16 * 2 ** 20
+
+    # conv3 data gradients with the BN backward folded into the GEMM (conv_dgrad_fold: K = 2 Cout
+    # over [G | Y], no materialised dy) where the GEMM output fits one N tile (Cin <= FOLD_MAX_CIN),
+    # so G and Y are each read once: the main stream drops the dy pass (read G, Y, write dy) and
+    # reads two tensors instead of one; the side-stream weight gradient applies the BN backward in
+    # its prologue (0: off)
+    # (measured: 128 -> 11.308-11.327, off 11.346-11.363, 256 11.391-11.423, 512 11.515-11.550 ms/step;
+    # profiles/r6_resnet50_fold_ab.txt)
+    FOLD_MAX_CIN = 128
+
+    @classmethod
+    def fold_pays(cls, c: ConvSpec) -> bool:
+        return c.k == 1 and c.stride == 1 and c.cin <= cls.FOLD_MAX_CIN and c.cout % 64 == 0
 
     @classmethod
     def mat_dy_pays(cls, c: ConvSpec, B: int) -> bool:
@@ -534,8 +554,13 @@ class ResNet50Executor:
             c1, c2, c3, cd = bp.c1, bp.c2, bp.c3, bp.cd
             # conv3 dgrad -> G2 (ReLU mask of BN2) + BN2 partials
             g3, y3 = self._dy(c3, bn3.g, bn3)
-            K.conv_dgrad(K.CE_BWD_RELU, g3, y3, bn3.a, bn3.b, bn3.c, f.bt(c3.name), bn2.g, bn2.acc_b, B, Ho, Ho,
-                         c3.cin, c3.cout, 1, 1, 1, 0, Yt=bn2.y, es=bn2.scale, et=bn2.shift)
+            if c3.w2 is not None:
+                K.conv_fold_w(f.bt(c3.name), bn3.a, bn3.b, bn3.c, bn3.mean, c3.w2, c3.fbias, c3.cin, c3.cout)
+                K.conv_dgrad_fold(g3, y3, c3.w2, c3.fbias, bn2.g, bn2.acc_b, B, Ho, Ho, c3.cin, c3.cout,
+                                  Yt=bn2.y, es=bn2.scale, et=bn2.shift)
+            else:
+                K.conv_dgrad(K.CE_BWD_RELU, g3, y3, bn3.a, bn3.b, bn3.c, f.bt(c3.name), bn2.g, bn2.acc_b, B, Ho,
+                             Ho, c3.cin, c3.cout, 1, 1, 1, 0, Yt=bn2.y, es=bn2.scale, et=bn2.shift)
             P2 = K.conv_dgrad_num_partials(B, Ho, Ho, c3.cin, c3.cout, 1, 1, 1)
             bn2.finalize_bwd(bn2.acc_b, P2)
             self._wgrad(lambda ws, bp=bp, g3=g3, y3=y3: K.conv_wgrad(

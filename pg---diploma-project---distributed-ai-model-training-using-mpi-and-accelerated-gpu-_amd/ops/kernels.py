@@ -692,6 +692,41 @@ def conv_fwd(pro, x, w, y, part, B, H, W, Ci, N, R, S, stride, pad, pa=None, pb=
                    _s())
 
 
+def conv_fold_w(wt, a, b, c, mu, w2, fbias, Cin, Cout):
+    """Per-step weights of :func:`conv_dgrad_fold`: w2 [Cin, 2, Cout] bf16 = [a*W | b*W] from the
+    transposed 1x1 weight wt [Cin, Cout] and this layer's BN-backward coefficients (a, b, c, fp32
+    [Cout]); fbias [Cin] fp32 = sum_k c_k W[n,k] + sum_k mu_k (b_k W[n,k] - bf16(b_k W[n,k]))."""
+    if Cout % 8:
+        raise ValueError("conv_fold_w: Cout % 8 == 0")
+    _chk(wt, BF16, Cin * Cout, "wt")
+    for t, nm in ((a, "a"), (b, "b"), (c, "c"), (mu, "mu")):
+        _chk(t, F32, Cout, nm)
+    _chk(w2, BF16, 2 * Cin * Cout, "w2")
+    _chk(fbias, F32, Cin, "fbias")
+    lib().conv_fold_w(_p(wt), _p(a), _p(b), _p(c), _p(mu), _p(w2), _p(fbias), Cin, Cout, _s())
+
+
+def conv_dgrad_fold(G, Y, w2, fbias, dx, part, B, H, W, Cin, Cout, Yt, es, et):
+    """1x1 stride-1 data gradient with this layer's BN backward folded into the GEMM:
+    dx = [G | Y] . w2^T + fbias (w2 / fbias from :func:`conv_fold_w`), i.e. conv^T(a*G + b*Y + c)
+    without materialising dy; epilogue CE_BWD_RELU (dx *= 1[Yt*es + et > 0], BN partials of dx
+    against Yt into part, the rows of the unfolded dgrad)."""
+    _conv_check(Cout, Cin, "conv_dgrad_fold")
+    if Cout % 64 or conv_get_glds() == 0:
+        raise ValueError("conv_dgrad_fold: Cout % 64 == 0 and the LDS-DMA kernel")
+    for t, nm in ((G, "G"), (Y, "Y")):
+        _chk(t, BF16, B * H * W * Cout, nm)
+    _chk(w2, BF16, 2 * Cin * Cout, "w2")
+    _chk(fbias, F32, Cin, "fbias")
+    for t, nm in ((dx, "dx"), (Yt, "Yt")):
+        _chk(t, BF16, B * H * W * Cin, nm)
+    _chk(es, F32, Cin, "es")
+    _chk(et, F32, Cin, "et")
+    _chk(part, F32, bn_rows(conv_dgrad_num_partials(B, H, W, Cin, Cout, 1, 1, 1)) * 2 * Cin, "part")
+    lib().conv_dgrad_fold(_p(G), _p(Y), _p(w2), _p(fbias), _p(dx), _p(Yt), _p(es), _p(et), _p(part), B, H, W, Cin,
+                          Cout, _s())
+
+
 def conv_dgrad(epi, G, Y, ga, gb, gc, wt, dx, part, B, H, W, Cin, Cout, R, S, stride, pad, Yt=None, es=None,
                et=None, Rg=None, X=None, Yt2=None, part2=None, Xm=None):
     """Data gradient of y = conv(x, w) with this layer's BN backward fused on the way in:

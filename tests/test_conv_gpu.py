@@ -211,6 +211,54 @@ def test_conv_dgrad(dev, shape, epi, mat):
             assert ((ps2[1] - s_ref[2]).abs() / (scale * 4)).max() < 2e-2
 
 
+@pytest.mark.parametrize("B,H,Cin,Cout", [(4, 14, 64, 256), (2, 28, 128, 512), (3, 9, 64, 128), (2, 7, 128, 64)])
+def test_conv_dgrad_fold(dev, B, H, Cin, Cout):
+    """1x1 data gradient with the BN backward folded into the GEMM (conv_fold_w + conv_dgrad_fold:
+    K = 2 Cout over [G | Y]) against the fp32 reference of conv^T(a*G + b*Y + c) with the ReLU-mask
+    epilogue, and its BN partials.  Y carries channel means 4x its spread and c cancels them (as in a
+    real BN backward), the case the mean-corrected bias is for."""
+    G = bfr(rnd(B, H, H, Cout, dev=dev, seed=5))
+    mu = (torch.rand(Cout, device=dev) * 8 - 4).contiguous()
+    Y = bfr(rnd(B, H, H, Cout, dev=dev, seed=6) + mu)
+    ga, gb = bn_params(Cout, dev, 7)
+    gc = (-gb * mu + 0.1 * bn_params(Cout, dev, 8)[1]).contiguous()
+    w = bfr(rnd(Cout, Cin, 1, 1, dev=dev, scale=Cout ** -0.5, seed=9))
+    dy = ga * G + gb * Y + gc                      # fp32, no rounding of dy
+    dx_ref = _dgrad_ref(dy, w, H, 1, 0, B, Cin)
+    wt = w.reshape(Cout, Cin).t().contiguous().to(torch.bfloat16)
+    w2 = torch.empty(2 * Cin * Cout, dtype=torch.bfloat16, device=dev)
+    fb = torch.empty(Cin, device=dev)
+    K.conv_fold_w(wt, ga, gb, gc, mu, w2, fb, Cin, Cout)
+    torch.cuda.synchronize()
+    wf = wt.float()
+    assert torch.equal(w2.view(Cin, 2, Cout)[:, 0], (ga * wf).to(torch.bfloat16))
+    assert torch.equal(w2.view(Cin, 2, Cout)[:, 1], (gb * wf).to(torch.bfloat16))
+    fb_ref = (gc * wf).sum(1) + (mu * (gb * wf - w2.view(Cin, 2, Cout)[:, 1].float())).sum(1)
+    assert rel(fb, fb_ref) < 1e-5
+    bf = lambda t: t.to(torch.bfloat16).contiguous()  # noqa: E731
+    Yt = bfr(rnd(B, H, H, Cin, dev=dev, seed=10))
+    es, et = bn_params(Cin, dev, 11)
+    dx = torch.empty(B, H, H, Cin, dtype=torch.bfloat16, device=dev)
+    P = K.conv_dgrad_num_partials(B, H, H, Cin, Cout, 1, 1, 1)
+    part = torch.zeros(P, 2, Cin, device=dev)
+    K.conv_dgrad_fold(bf(G), bf(Y), w2, fb, dx, part, B, H, H, Cin, Cout, Yt=bf(Yt), es=es, et=et)
+    torch.cuda.synchronize()
+    ref = dx_ref * ((Yt * es + et) > 0)
+    assert rel(dx, ref) < 1.5e-2, rel(dx, ref)
+    ref_b = bfr(ref)
+    ps = part.sum(0)
+    scale = ref_b.abs().reshape(-1, Cin).sum(0) + 1
+    assert ((ps[0] - ref_b.reshape(-1, Cin).sum(0)).abs() / scale).max() < 2e-2
+    assert ((ps[1] - (ref_b * Yt).reshape(-1, Cin).sum(0)).abs() / (scale * 4)).max() < 2e-2
+    # no worse than the materialised-dy path on the same operands
+    dx_m = torch.empty_like(dx)
+    part_m = torch.zeros_like(part)
+    K.conv_dgrad(K.CE_BWD_RELU, _mat_dy(G, Y, ga, gb, gc), None, ga, gb, gc, wt.view(-1), dx_m, part_m, B, H, H,
+                 Cin, Cout, 1, 1, 1, 0, Yt=bf(Yt), es=es, et=et)
+    torch.cuda.synchronize()
+    assert rel(dx, ref) < 2 * rel(dx_m, ref) + 1e-3, (rel(dx, ref), rel(dx_m, ref))
+
+
 # (B, H, Ci, N, R, stride, pad)
 WGRAD_SHAPES = [
     (2, 8, 64, 64, 3, 1, 1),

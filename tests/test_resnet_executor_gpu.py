@@ -240,10 +240,15 @@ def test_resnet_lazy_bn_matches_launch(dev, monkeypatch, stem, mode):
 
     def dist(f):     # lazy run vs the closest reference run (the same statistic as a pair)
         return min(f(lz, r) for r in ref)
-    # the first step's forward sees identical weights: its loss agrees to the atomic noise
-    # (a consumer reading stale BN parameters would be off by far more)
+    # the first step's forward sees identical weights: its loss agrees to the atomic noise (a
+    # consumer reading stale BN parameters would be off by far more).  The noise is chaotic: the
+    # float-atomic order of the replica rows flips bf16 roundings that 50 BN layers at batch 8 and
+    # 16-pixel maps amplify -- identically configured launch-mode runs in one process differ by up
+    # to 0.05 in this loss (scripts/diag_resnet_lazy_act.py), so three of them can under-estimate
+    # it; hence the 3 % floor
     lnoise = spread(lambda a, b: abs(a[4][0] - b[4][0]))
-    assert dist(lambda a, b: abs(a[4][0] - b[4][0])) <= 1e-3 * abs(k0[0]) + 10 * lnoise, ([r[4] for r in ref], k2)
+    assert dist(lambda a, b: abs(a[4][0] - b[4][0])) <= max(10 * lnoise, 0.03 * abs(k0[0])), \
+        ([r[4] for r in ref], k2)
     noise = max(spread(lambda a, b: _rel(a[0], b[0])), 1e-6)
     assert dist(lambda a, b: _rel(a[0], b[0])) < max(20 * noise, 1e-4), (_rel(w2, w0), noise)
     assert dist(lambda a, b: _rel(a[1], b[1])) < max(20 * max(spread(lambda a, b: _rel(a[1], b[1])), 1e-6), 1e-3)
