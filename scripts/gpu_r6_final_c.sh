@@ -2,8 +2,8 @@
 # Round 6 closing validation (after the ResNet-50 BN / materialisation changes): full GPU suite +
 # smoke, three default bench runs, two ResNet-50 bench runs, ResNet-50 roofline, kernel-trace
 # timeline and MFMA counters.  Each GPU step has its own limit; the script stops at the first failure.
-cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/r6c && export TMPDIR=/tmp
-O=$GRAFT_REPO_ROOT/gpurun_out/r6c
+cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/r6d && export TMPDIR=/tmp
+O=$GRAFT_REPO_ROOT/gpurun_out/r6d
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
 rc=$?; tail -2 $O/gpu_tests.log; grep -E "FAILED|ERROR" $O/gpu_tests.log | head; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -5 $O/smoke.log; exit 1; }
